@@ -1,0 +1,68 @@
+// Shared helpers for the acfe HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include "../../include/acfe.h"
+
+#define ACFE_API extern "C" __attribute__((visibility("default")))
+
+namespace acfe {
+
+void set_error(hipError_t e, const char* where);
+
+inline int hip_rc(hipError_t e, const char* where) {
+  if (e == hipSuccess) return ACFE_OK;
+  set_error(e, where);
+  return -(int)e;
+}
+
+// Check a kernel launch (hipGetLastError) and convert to an ABI code.
+inline int launch_rc(const char* where) { return hip_rc(hipGetLastError(), where); }
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// ---- bf16 helpers: bit-level, round-to-nearest-even (NaN kept NaN) ----------
+__device__ __forceinline__ float bf2f(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // plain cast lowers to v_cvt_pk_bf16_f32 on gfx950 (RNE, NaN preserving)
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sumd(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Counter-based RNG (splitmix-style hash) for dropout masks: deterministic in
+// (seed, index), so the backward regenerates the forward's mask.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+}  // namespace acfe

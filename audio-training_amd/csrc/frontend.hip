@@ -1,0 +1,707 @@
+// Feature front end: normalize, mix_up, STFT -> |X|^p -> banded mel, PCEN.
+// Reference: tfdataset.py:1916-1934 (normalize), :930-955 (mix_up),
+// :2007-2059 (raw_to_mel), predict_utils.py:163-239 (get_spect),
+// custommel.py:18-61 (mel_f, mel_spec), tfpcen.py:8-110 (EMA, PCEN, minmax).
+//
+// Design (gfx950): one 256-thread workgroup per (clip, group of frames).
+// The n_fft real FFT is computed as an n_fft/2-point complex FFT of
+// z[n] = x[2n] + i x[2n+1] with radix-8/4/2 Stockham passes: each thread
+// keeps its butterfly in VGPRs and exchanges through one LDS buffer
+// (16 KB at n_fft=4096); the first pass reads HBM/L2 directly (framing,
+// Hann window and optional per-clip normalisation fused into the load).
+// Only the bins covered by the mel filterbank are post-processed into power,
+// and the filterbank is applied as a banded sum (1839 taps at M=128 instead
+// of the reference's dense 128x2049 batch_dot).
+#include "common.h"
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace acfe;
+
+struct acfe_plan_s {
+  int sr, n_fft, hop, n_mels, n_bins;
+  int kmin, kmax;
+  float2* d_tw;   // W_{n_fft/2}^k, k < n_fft/2
+  float2* d_rtw;  // W_{n_fft}^k, k <= n_fft/2
+  float* d_win;   // periodic Hann [n_fft]
+  int* d_band;    // [n_mels][3]: start bin, length, offset into d_vals
+  float* d_vals;
+  int device;
+};
+
+// ------------------------------------------------------------ host: mel_f
+// custommel.py:18-54 restated in C (float64 math, float32 storage; numpy's
+// rfftfreq / linspace / in-place float32 *= float64 semantics reproduced).
+ACFE_API int acfe_mel_filterbank(int sr, int n_mels, double fmin, double fmax, int n_fft,
+                                 double break_freq, float* out) {
+  if (sr <= 0 || n_mels <= 0 || n_fft <= 0 || !out || break_freq <= 0) return ACFE_E_INVAL;
+  const int nb = 1 + n_fft / 2;
+  const int nm2 = n_mels + 2;
+  std::vector<double> ff(nb), mf(nm2);
+  const double d = 1.0 / sr;
+  const double val = 1.0 / (n_fft * d);  // numpy.fft.rfftfreq
+  for (int k = 0; k < nb; ++k) ff[k] = k * val;
+  const double lo = 2595.0 * std::log10(1.0 + fmin / break_freq);
+  const double hi = 2595.0 * std::log10(1.0 + fmax / break_freq);
+  const double step = (hi - lo) / (nm2 - 1);  // numpy.linspace
+  for (int i = 0; i < nm2; ++i) {
+    double m = (i == nm2 - 1) ? hi : i * step + lo;
+    mf[i] = break_freq * (std::pow(10.0, m / 2595.0) - 1.0);
+  }
+  for (int i = 0; i < n_mels; ++i) {
+    const double fd0 = mf[i + 1] - mf[i], fd1 = mf[i + 2] - mf[i + 1];
+    const double enorm = 2.0 / (mf[i + 2] - mf[i]);
+    for (int k = 0; k < nb; ++k) {
+      const double lower = -(mf[i] - ff[k]) / fd0;
+      const double upper = (mf[i + 2] - ff[k]) / fd1;
+      double w = std::fmin(lower, upper);
+      if (!(w > 0.0)) w = 0.0;
+      const float w32 = (float)w;
+      out[(size_t)i * nb + k] = (float)((double)w32 * enorm);
+    }
+  }
+  return ACFE_OK;
+}
+
+ACFE_API int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax,
+                              double break_freq, const float* w_host, acfe_plan_t* plan) {
+  if (!plan || n_fft < 256 || n_fft > 4096 || (n_fft & (n_fft - 1)) || hop <= 0 || n_mels <= 0 ||
+      n_mels > 1024)
+    return ACFE_E_INVAL;
+  const int nb = 1 + n_fft / 2, nc = n_fft / 2;
+  std::vector<float> w;
+  if (!w_host) {
+    w.resize((size_t)n_mels * nb);
+    int rc = acfe_mel_filterbank(sr, n_mels, fmin, fmax, n_fft, break_freq, w.data());
+    if (rc) return rc;
+    w_host = w.data();
+  }
+  std::vector<int> band(3 * n_mels);
+  std::vector<float> vals;
+  int kmin = nb, kmax = -1;
+  for (int m = 0; m < n_mels; ++m) {
+    int s = -1, e = -1;
+    for (int k = 0; k < nb; ++k)
+      if (w_host[(size_t)m * nb + k] != 0.f) {
+        if (s < 0) s = k;
+        e = k;
+      }
+    if (s < 0) {
+      band[3 * m] = 0;
+      band[3 * m + 1] = 0;
+      band[3 * m + 2] = (int)vals.size();
+      continue;
+    }
+    band[3 * m] = s;
+    band[3 * m + 1] = e - s + 1;
+    band[3 * m + 2] = (int)vals.size();
+    for (int k = s; k <= e; ++k) vals.push_back(w_host[(size_t)m * nb + k]);
+    kmin = s < kmin ? s : kmin;
+    kmax = e > kmax ? e : kmax;
+  }
+  if (kmax < 0) kmin = kmax = 0;
+  if (vals.empty()) vals.push_back(0.f);
+  std::vector<float2> tw(nc), rtw(nc + 1);
+  std::vector<float> win(n_fft);
+  for (int k = 0; k < nc; ++k) {
+    const double a = -2.0 * M_PI * (double)k / nc;
+    tw[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  for (int k = 0; k <= nc; ++k) {
+    const double a = -2.0 * M_PI * (double)k / n_fft;
+    rtw[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  for (int i = 0; i < n_fft; ++i) win[i] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * i / n_fft));
+
+  acfe_plan_s* p = new acfe_plan_s();
+  p->sr = sr; p->n_fft = n_fft; p->hop = hop; p->n_mels = n_mels; p->n_bins = nb;
+  p->kmin = kmin; p->kmax = kmax;
+  hipGetDevice(&p->device);
+  hipError_t e = hipSuccess;
+  e = e ? e : hipMalloc(&p->d_tw, sizeof(float2) * nc);
+  e = e ? e : hipMalloc(&p->d_rtw, sizeof(float2) * (nc + 1));
+  e = e ? e : hipMalloc(&p->d_win, sizeof(float) * n_fft);
+  e = e ? e : hipMalloc(&p->d_band, sizeof(int) * 3 * n_mels);
+  e = e ? e : hipMalloc(&p->d_vals, sizeof(float) * vals.size());
+  e = e ? e : hipMemcpy(p->d_tw, tw.data(), sizeof(float2) * nc, hipMemcpyHostToDevice);
+  e = e ? e : hipMemcpy(p->d_rtw, rtw.data(), sizeof(float2) * (nc + 1), hipMemcpyHostToDevice);
+  e = e ? e : hipMemcpy(p->d_win, win.data(), sizeof(float) * n_fft, hipMemcpyHostToDevice);
+  e = e ? e : hipMemcpy(p->d_band, band.data(), sizeof(int) * 3 * n_mels, hipMemcpyHostToDevice);
+  e = e ? e : hipMemcpy(p->d_vals, vals.data(), sizeof(float) * vals.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    acfe_plan_destroy(p);
+    return hip_rc(e, "acfe_plan_create");
+  }
+  *plan = p;
+  return ACFE_OK;
+}
+
+ACFE_API int acfe_plan_destroy(acfe_plan_t p) {
+  if (!p) return ACFE_E_INVAL;
+  hipFree(p->d_tw); hipFree(p->d_rtw); hipFree(p->d_win); hipFree(p->d_band); hipFree(p->d_vals);
+  delete p;
+  return ACFE_OK;
+}
+
+ACFE_API int acfe_plan_num_frames(acfe_plan_t p, int n, int pad_mode) {
+  if (!p || n <= 0) return ACFE_E_INVAL;
+  if (pad_mode == ACFE_PAD_END) return (n + p->hop - 1) / p->hop;
+  return 1 + n / p->hop;
+}
+
+// ------------------------------------------------------------ normalize
+__global__ void __launch_bounds__(256) k_norm_stats(const float* __restrict__ x, int64_t cs, int n,
+                                                    float* __restrict__ stats) {
+  const float* xb = x + (int64_t)blockIdx.x * cs;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float v = xb[i];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  __shared__ float smn[4], smx[4];
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[w] = mn; smx[w] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mn = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+    mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+    stats[2 * blockIdx.x] = mn;
+    stats[2 * blockIdx.x + 1] = mx - mn;  // == max(x - min) (fl is monotone)
+  }
+}
+
+__device__ __forceinline__ float norm1(float v, float mn, float rng) {
+  // tfdataset.py:1927-1931, float32, same order: -min, /max, +1e-6, -0.5, *2
+  float t = __fsub_rn(v, mn);
+  t = __fdiv_rn(t, rng);
+  t = __fadd_rn(t, 0.000001f);
+  t = __fsub_rn(t, 0.5f);
+  return __fmul_rn(t, 2.0f);
+}
+
+ACFE_API int acfe_normalize_stats(const float* x, int64_t cs, int batch, int n, float* stats,
+                                  void* stream) {
+  if (!x || !stats || batch < 0 || n <= 0) return ACFE_E_INVAL;
+  if (batch == 0) return ACFE_OK;
+  hipLaunchKernelGGL(k_norm_stats, dim3(batch), dim3(256), 0, S(stream), x, cs, n, stats);
+  return launch_rc("acfe_normalize_stats");
+}
+
+__global__ void k_norm_apply(const float* __restrict__ x, int64_t cs, int n,
+                             const float* __restrict__ stats, float* __restrict__ y) {
+  const int b = blockIdx.y;
+  const float mn = stats[2 * b], rng = stats[2 * b + 1];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    y[(int64_t)b * n + i] = norm1(x[(int64_t)b * cs + i], mn, rng);
+}
+
+ACFE_API int acfe_normalize_apply(const float* x, int64_t cs, int batch, int n, const float* stats,
+                                  float* y, void* stream) {
+  if (!x || !stats || !y || batch < 0 || n <= 0 || batch > 65535) return ACFE_E_INVAL;
+  if (batch == 0) return ACFE_OK;
+  hipLaunchKernelGGL(k_norm_apply, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, S(stream), x, cs,
+                     n, stats, y);
+  return launch_rc("acfe_normalize_apply");
+}
+
+__global__ void k_mixup(const float* __restrict__ x1, const float* __restrict__ s1,
+                        const float* __restrict__ x2, const float* __restrict__ s2,
+                        const float* __restrict__ lam, int n, float* __restrict__ y) {
+  const int b = blockIdx.y;
+  const float l = lam[b];
+  const float l1 = __fsub_rn(1.0f, l);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int64_t o = (int64_t)b * n + i;
+    float a = x1[o], c = x2[o];
+    if (s1) a = norm1(a, s1[2 * b], s1[2 * b + 1]);
+    if (s2) c = norm1(c, s2[2 * b], s2[2 * b + 1]);
+    y[o] = __fadd_rn(__fmul_rn(a, l), __fmul_rn(c, l1));  // tfdataset.py:950
+  }
+}
+
+ACFE_API int acfe_mixup(const float* x1, const float* s1, const float* x2, const float* s2,
+                        const float* lam, int batch, int n, float* y, void* stream) {
+  if (!x1 || !x2 || !lam || !y || batch < 0 || n <= 0 || batch > 65535) return ACFE_E_INVAL;
+  if (batch == 0) return ACFE_OK;
+  hipLaunchKernelGGL(k_mixup, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, S(stream), x1, s1, x2,
+                     s2, lam, n, y);
+  return launch_rc("acfe_mixup");
+}
+
+// ------------------------------------------------------------ FFT helpers
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
+
+template <int R>
+__device__ __forceinline__ void dft(float2* v);
+
+template <>
+__device__ __forceinline__ void dft<2>(float2* v) {
+  float2 a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+template <>
+__device__ __forceinline__ void dft<4>(float2* v) {
+  float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+  float2 t2 = cadd(v[1], v[3]), t3 = mul_mi(csub(v[1], v[3]));
+  v[0] = cadd(t0, t2);
+  v[2] = csub(t0, t2);
+  v[1] = cadd(t1, t3);
+  v[3] = csub(t1, t3);
+}
+template <>
+__device__ __forceinline__ void dft<8>(float2* v) {
+  float2 e[4] = {v[0], v[2], v[4], v[6]};
+  float2 o[4] = {v[1], v[3], v[5], v[7]};
+  dft<4>(e);
+  dft<4>(o);
+  const float c = 0.70710678118654752440f;
+  // W8^1 = c(1 - i), W8^2 = -i, W8^3 = -c(1 + i)
+  float2 o1 = make_float2(c * (o[1].x + o[1].y), c * (o[1].y - o[1].x));
+  float2 o2 = mul_mi(o[2]);
+  float2 o3 = make_float2(c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y));
+  v[0] = cadd(e[0], o[0]); v[4] = csub(e[0], o[0]);
+  v[1] = cadd(e[1], o1);   v[5] = csub(e[1], o1);
+  v[2] = cadd(e[2], o2);   v[6] = csub(e[2], o2);
+  v[3] = cadd(e[3], o3);   v[7] = csub(e[3], o3);
+}
+
+// One in-place Stockham pass (Govindaraju et al. formulation) over NC points
+// held in LDS `buf`, radix R, span Ns.  256 threads.
+template <int NC, int R>
+__device__ __forceinline__ void stockham_pass(float2* buf, int Ns, const float2* __restrict__ tw) {
+  constexpr int NB = NC / R;
+  constexpr int PER = (NB + 255) / 256;
+  float2 v[PER][R];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int j = threadIdx.x + 256 * p;
+    if (NB % 256 == 0 || j < NB) {
+      const int jm = j & (Ns - 1);
+      const int tstep = jm * (NC / (Ns * R));
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float2 a = buf[j + r * NB];
+        if (r) a = cmul(a, tw[r * tstep]);
+        v[p][r] = a;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int j = threadIdx.x + 256 * p;
+    if (NB % 256 == 0 || j < NB) {
+      dft<R>(v[p]);
+      const int idxD = (j / Ns) * Ns * R + (j & (Ns - 1));
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[idxD + r * Ns] = v[p][r];
+    }
+  }
+  __syncthreads();
+}
+
+// Fetch one (optionally normalised) sample of the framed signal.
+__device__ __forceinline__ float fetch(const float* __restrict__ xb, int n, int idx, int pad_mode,
+                                       bool do_norm, float mn, float rng) {
+  if (pad_mode == ACFE_PAD_CENTER_REFLECT) {
+    if (idx < 0) idx = -idx;
+    if (idx >= n) idx = 2 * (n - 1) - idx;
+  }
+  if (idx < 0 || idx >= n) return 0.f;
+  const float v = xb[idx];
+  return do_norm ? norm1(v, mn, rng) : v;
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int64_t cs, int n,
+                                             const float* __restrict__ stats, int pad_mode,
+                                             int power, int n_frames, int fpb, int hop,
+                                             const float2* __restrict__ tw,
+                                             const float2* __restrict__ rtw,
+                                             const float* __restrict__ win,
+                                             const int* __restrict__ band,
+                                             const float* __restrict__ vals, int n_mels, int kmin,
+                                             int kmax, float* __restrict__ out, int layout) {
+  constexpr int L = 2 * NC;
+  constexpr int NB0 = NC / 8;  // first pass butterflies
+  constexpr int PER0 = (NB0 + 255) / 256;
+  __shared__ float2 buf[NC];
+  __shared__ float pw[NC + 1];
+  const int b = blockIdx.y;
+  const float* xb = raw + (int64_t)b * cs;
+  const bool do_norm = stats != nullptr;
+  const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
+  const int nk = kmax - kmin + 1;
+  const int f0 = blockIdx.x * fpb;
+  for (int f = f0; f < f0 + fpb && f < n_frames; ++f) {
+    const int start = (pad_mode == ACFE_PAD_END) ? f * hop : f * hop - L / 2;
+    // ---- pass 1 (Ns = 1, radix 8) straight from memory: z[j + r*NB0]
+    {
+      float2 v[PER0][8];
+#pragma unroll
+      for (int p = 0; p < PER0; ++p) {
+        const int j = threadIdx.x + 256 * p;
+        if (NB0 % 256 == 0 || j < NB0) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int nn = j + r * NB0;
+            const float a = fetch(xb, n, start + 2 * nn, pad_mode, do_norm, mn, rng) * win[2 * nn];
+            const float c = fetch(xb, n, start + 2 * nn + 1, pad_mode, do_norm, mn, rng) * win[2 * nn + 1];
+            v[p][r] = make_float2(a, c);
+          }
+          dft<8>(v[p]);
+        }
+      }
+      __syncthreads();  // previous frame's readers of buf are done
+#pragma unroll
+      for (int p = 0; p < PER0; ++p) {
+        const int j = threadIdx.x + 256 * p;
+        if (NB0 % 256 == 0 || j < NB0) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) buf[j * 8 + r] = v[p][r];
+        }
+      }
+      __syncthreads();
+    }
+    int Ns = 8;
+    while (Ns * 8 <= NC) {
+      stockham_pass<NC, 8>(buf, Ns, tw);
+      Ns *= 8;
+    }
+    if (NC / Ns == 4) stockham_pass<NC, 4>(buf, Ns, tw);
+    else if (NC / Ns == 2) stockham_pass<NC, 2>(buf, Ns, tw);
+    // ---- real-FFT post-processing + power, only for bins in [kmin, kmax]
+    for (int i = threadIdx.x; i < nk; i += 256) {
+      const int k = kmin + i;
+      const float2 zk = buf[k & (NC - 1)];
+      const float2 zm = buf[(NC - k) & (NC - 1)];
+      // E = (zk + conj(zm))/2, O = (zk - conj(zm)) / (2i)
+      const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+      const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
+      const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
+      const float2 X = cadd(E, cmul(rtw[k], O));
+      const float p2 = X.x * X.x + X.y * X.y;
+      pw[i] = power == 2 ? p2 : sqrtf(p2);
+    }
+    __syncthreads();
+    // ---- banded mel
+    for (int m = threadIdx.x; m < n_mels; m += 256) {
+      const int s = band[3 * m], len = band[3 * m + 1], off = band[3 * m + 2];
+      float acc = 0.f;
+      for (int i = 0; i < len; ++i) acc += vals[off + i] * pw[s - kmin + i];
+      const size_t o = layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m
+                                                 : ((size_t)b * n_mels + m) * n_frames + f;
+      out[o] = acc;
+    }
+    // next frame's first __syncthreads protects buf/pw reuse
+  }
+}
+
+ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch, int n,
+                          const float* stats, int pad_mode, int power, float* out, int layout,
+                          void* stream) {
+  if (!p || !raw || !out || batch < 0 || n <= 0 || batch > 65535 || (power != 1 && power != 2) ||
+      pad_mode < 0 || pad_mode > 2 || (layout != 0 && layout != 1))
+    return ACFE_E_INVAL;
+  if (pad_mode == ACFE_PAD_CENTER_REFLECT && n <= p->n_fft / 2) return ACFE_E_INVAL;
+  if (batch == 0) return ACFE_OK;
+  const int T = acfe_plan_num_frames(p, n, pad_mode);
+  const int fpb = 4;
+  dim3 grid(cdiv(T, fpb), batch);
+#define LAUNCH_MEL(NC)                                                                          \
+  hipLaunchKernelGGL(k_mel<NC>, grid, dim3(256), 0, S(stream), raw, cs, n, stats, pad_mode,     \
+                     power, T, fpb, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,  \
+                     p->n_mels, p->kmin, p->kmax, out, layout)
+  switch (p->n_fft) {
+    case 4096: LAUNCH_MEL(2048); break;
+    case 2048: LAUNCH_MEL(1024); break;
+    case 1024: LAUNCH_MEL(512); break;
+    case 512: LAUNCH_MEL(256); break;
+    case 256: LAUNCH_MEL(128); break;
+    default: return ACFE_E_INVAL;
+  }
+#undef LAUNCH_MEL
+  return launch_rc("acfe_mel_fwd");
+}
+
+// ------------------------------------------------------------ PCEN
+// Thread per (b, m) row; the EMA recurrence runs sequentially over T (the
+// reference's tf.scan), reading mel [B][T][M] coalesced across threads.
+// Outputs go through an LDS tile so the [B][M][T] writes are row-contiguous.
+constexpr int PCEN_TCH = 32;
+
+ACFE_API int acfe_pcen_partials(int batch, int n_mels) { return cdiv((int64_t)batch * n_mels, 256); }
+
+struct PcenP {
+  float g, b, r, w, inv_r, bpow;
+};
+__device__ __forceinline__ PcenP pcen_params(const float* __restrict__ prm) {
+  PcenP p;
+  p.g = fminf(prm[0], 1.0f);
+  p.b = prm[1];
+  p.r = fmaxf(prm[2], 1.0f);
+  p.w = fminf(fmaxf(prm[3], 0.0f), 1.0f);
+  p.inv_r = 1.0f / p.r;
+  p.bpow = powf(p.b, p.inv_r);
+  return p;
+}
+
+// tfpcen.py:37: w * x + (1.0 - w) * a, float32, no contraction (so forward and
+// backward recompute identical values and the min/max tie test is exact).
+__device__ __forceinline__ float ema_step(float w, float x, float a) {
+  return __fadd_rn(__fmul_rn(w, x), __fmul_rn(__fsub_rn(1.0f, w), a));
+}
+
+__global__ void __launch_bounds__(256) k_pcen_fwd(const float* __restrict__ mel, int B, int T, int M,
+                                                  const float* __restrict__ prm, float eps,
+                                                  float* __restrict__ y, float* __restrict__ part) {
+  __shared__ float tile[256][PCEN_TCH + 1];
+  const PcenP P = pcen_params(prm);
+  const int64_t rows = (int64_t)B * M;
+  const int64_t row0 = (int64_t)blockIdx.x * 256;
+  const int64_t gr = row0 + threadIdx.x;
+  const bool valid = gr < rows;
+  const int bb = valid ? (int)(gr / M) : 0, m = valid ? (int)(gr % M) : 0;
+  const float* xr = mel + (int64_t)bb * T * M + m;
+  float a = valid ? xr[0] : 0.f;
+  float lmin = INFINITY, lmax = -INFINITY;
+  const int nrow = (int)((rows - row0) < 256 ? (rows - row0) : 256);
+  for (int t0 = 0; t0 < T; t0 += PCEN_TCH) {
+    const int tn = (T - t0) < PCEN_TCH ? (T - t0) : PCEN_TCH;
+    if (valid) {
+      for (int tt = 0; tt < tn; ++tt) {
+        const float x = xr[(int64_t)(t0 + tt) * M];
+        a = ema_step(P.w, x, a);
+        const float v = __fsub_rn(powf(__fadd_rn(__fdiv_rn(x, powf(__fadd_rn(eps, a), P.g)), P.b), P.inv_r), P.bpow);
+        tile[threadIdx.x][tt] = v;
+        lmin = fminf(lmin, v);
+        lmax = fmaxf(lmax, v);
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nrow * PCEN_TCH; i += 256) {
+      const int r = i / PCEN_TCH, tt = i % PCEN_TCH;
+      if (tt < tn) y[(row0 + r) * T + t0 + tt] = tile[r][tt];
+    }
+    __syncthreads();
+  }
+  __shared__ float smn[4], smx[4];
+  lmin = wave_min(lmin);
+  lmax = wave_max(lmax);
+  if ((threadIdx.x & 63) == 0) { smn[threadIdx.x >> 6] = lmin; smx[threadIdx.x >> 6] = lmax; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+    part[2 * blockIdx.x + 1] = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+  }
+}
+
+ACFE_API int acfe_pcen_fwd(const float* mel, int batch, int t, int m, const float* params, float eps,
+                           float* y, float* part, void* stream) {
+  if (!mel || !params || !y || !part || batch <= 0 || t <= 0 || m <= 0) return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_pcen_fwd, dim3(acfe_pcen_partials(batch, m)), dim3(256), 0, S(stream), mel,
+                     batch, t, m, params, eps, y, part);
+  return launch_rc("acfe_pcen_fwd");
+}
+
+__device__ __forceinline__ void reduce_minmax_partials(const float* __restrict__ part, int np,
+                                                       const float* __restrict__ scope, float& mn,
+                                                       float& mx) {
+  __shared__ float smn[4], smx[4];
+  if (scope) {
+    mn = scope[0];
+    mx = scope[1];
+    return;
+  }
+  float a = INFINITY, c = -INFINITY;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    a = fminf(a, part[2 * i]);
+    c = fmaxf(c, part[2 * i + 1]);
+  }
+  a = wave_min(a);
+  c = wave_max(c);
+  if ((threadIdx.x & 63) == 0) { smn[threadIdx.x >> 6] = a; smx[threadIdx.x >> 6] = c; }
+  __syncthreads();
+  mn = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+  mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+}
+
+__global__ void __launch_bounds__(256) k_pcen_norm(const float* __restrict__ y, int64_t count,
+                                                   const float* __restrict__ part, int np,
+                                                   const float* __restrict__ scope, void* out,
+                                                   int dtype, float* __restrict__ stats) {
+  float mn, mx;
+  reduce_minmax_partials(part, np, scope, mn, mx);
+  const float d = mx - mn;
+  float cmin = 0.f, cmax = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256) {
+    const float v = y[i];
+    cmin += (v == mn) ? 1.f : 0.f;
+    cmax += (v == mx) ? 1.f : 0.f;
+    const float o = 2.0f * ((v - mn) / d) - 1.0f;  // tfpcen.py:110
+    if (dtype == ACFE_DTYPE_BF16) reinterpret_cast<uint16_t*>(out)[i] = f2bf(o);
+    else reinterpret_cast<float*>(out)[i] = o;
+  }
+  cmin = wave_sum(cmin);
+  cmax = wave_sum(cmax);
+  if ((threadIdx.x & 63) == 0) {
+    if (cmin != 0.f) atomicAdd(&stats[2], cmin);
+    if (cmax != 0.f) atomicAdd(&stats[3], cmax);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    stats[0] = mn;
+    stats[1] = mx;
+  }
+}
+
+ACFE_API int acfe_pcen_normalize(const float* y, int64_t count, const float* part, int np,
+                                 const float* scope, void* out, int dtype, float* stats,
+                                 void* stream) {
+  if (!y || !out || !stats || count <= 0 || (!part && !scope) || (dtype != 0 && dtype != 1))
+    return ACFE_E_INVAL;
+  int rc = hip_rc(hipMemsetAsync(stats, 0, 4 * sizeof(float), S(stream)), "acfe_pcen_normalize");
+  if (rc) return rc;
+  int grid = cdiv(count, 256 * 8);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(k_pcen_norm, dim3(grid), dim3(256), 0, S(stream), y, count, part, np, scope,
+                     out, dtype, stats);
+  return launch_rc("acfe_pcen_normalize");
+}
+
+// Backward.  One pass: per row, recompute the EMA a_t, its forward-mode
+// derivative da_t/dw, y_t and the partials of y_t w.r.t. (g, b, r, w), and
+// accumulate (d = dL/dout):
+//   G_th  = sum d * dy/dth,  Smax_th = sum_{y == mx} dy/dth,
+//   Smin_th = sum_{y == mn} dy/dth,  S0 = sum d,  Sy = sum d * y.
+// The finaliser turns these into dL/dth through normalize_minmax (with the
+// TF reduce_max/min tie rule: gradient shared equally among tied extrema).
+constexpr int PCEN_NACC = 14;
+
+__global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel, int B, int T, int M,
+                                                  const float* __restrict__ prm, float eps,
+                                                  const float* __restrict__ st,
+                                                  const void* __restrict__ dout, int ddt,
+                                                  double* __restrict__ part) {
+  __shared__ float tile[256][PCEN_TCH + 1];
+  __shared__ double red[4][PCEN_NACC];
+  const PcenP P = pcen_params(prm);
+  const float mn = st[0], mx = st[1];
+  const int64_t rows = (int64_t)B * M;
+  const int64_t row0 = (int64_t)blockIdx.x * 256;
+  const int64_t gr = row0 + threadIdx.x;
+  const bool valid = gr < rows;
+  const int bb = valid ? (int)(gr / M) : 0, m = valid ? (int)(gr % M) : 0;
+  const float* xr = mel + (int64_t)bb * T * M + m;
+  const int nrow = (int)((rows - row0) < 256 ? (rows - row0) : 256);
+  float acc[PCEN_NACC];
+#pragma unroll
+  for (int i = 0; i < PCEN_NACC; ++i) acc[i] = 0.f;
+  float a = valid ? xr[0] : 0.f, da = 0.f;
+  const float lnb = logf(P.b);
+  for (int t0 = 0; t0 < T; t0 += PCEN_TCH) {
+    const int tn = (T - t0) < PCEN_TCH ? (T - t0) : PCEN_TCH;
+    for (int i = threadIdx.x; i < nrow * PCEN_TCH; i += 256) {
+      const int r = i / PCEN_TCH, tt = i % PCEN_TCH;
+      if (tt < tn) {
+        const int64_t o = (row0 + r) * T + t0 + tt;
+        tile[r][tt] = ddt == ACFE_DTYPE_BF16 ? bf2f(reinterpret_cast<const uint16_t*>(dout)[o])
+                                             : reinterpret_cast<const float*>(dout)[o];
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      for (int tt = 0; tt < tn; ++tt) {
+        const float x = xr[(int64_t)(t0 + tt) * M];
+        const float a_prev = a;
+        a = ema_step(P.w, x, a);                     // bit-identical to the forward
+        da = (x - a_prev) + (1.0f - P.w) * da;       // d a_t / d w
+        const float s = __fadd_rn(eps, a);
+        const float sg = powf(s, P.g);
+        const float q = __fdiv_rn(x, sg);
+        const float u = __fadd_rn(q, P.b);
+        const float ur = powf(u, P.inv_r);
+        const float y = __fsub_rn(ur, P.bpow);
+        const float dydu = P.inv_r * ur / u;
+        const float d_g = dydu * (-q * logf(s));
+        const float d_b = dydu - P.inv_r * P.bpow / P.b;
+        const float d_r = -(P.inv_r * P.inv_r) * (ur * logf(u) - P.bpow * lnb);
+        const float d_w = dydu * (-P.g * q / s) * da;
+        const float d = tile[threadIdx.x][tt];
+        acc[0] += d * d_g; acc[1] += d * d_b; acc[2] += d * d_r; acc[3] += d * d_w;
+        if (y == mx) { acc[4] += d_g; acc[5] += d_b; acc[6] += d_r; acc[7] += d_w; }
+        if (y == mn) { acc[8] += d_g; acc[9] += d_b; acc[10] += d_r; acc[11] += d_w; }
+        acc[12] += d;
+        acc[13] += d * y;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < PCEN_NACC; ++i) {
+    double v = wave_sumd((double)acc[i]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < PCEN_NACC)
+    part[(int64_t)blockIdx.x * 16 + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ void __launch_bounds__(64) k_pcen_bwd_fin(const double* __restrict__ part, int np,
+                                                     const float* __restrict__ prm,
+                                                     const float* __restrict__ st,
+                                                     float* __restrict__ dparams) {
+  __shared__ double tot[PCEN_NACC];
+  if (threadIdx.x < PCEN_NACC) {
+    double s = 0.0;
+    for (int i = 0; i < np; ++i) s += part[(int64_t)i * 16 + threadIdx.x];
+    tot[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double mn = st[0], mx = st[1], nmin = st[2], nmax = st[3];
+    const double D = mx - mn;
+    const double S0 = tot[12], Sy = tot[13];
+    const double S1 = (2.0 / D) * (Sy - mn * S0);  // sum d * (out + 1)
+    const double dmx = -S1 / D;
+    const double dmn = (S1 - 2.0 * S0) / D;
+    double g[4];
+    for (int k = 0; k < 4; ++k)
+      g[k] = (2.0 / D) * tot[k] + (nmax > 0 ? dmx / nmax * tot[4 + k] : 0.0) +
+             (nmin > 0 ? dmn / nmin * tot[8 + k] : 0.0);
+    // TF gradient masks: minimum(gain,1) -> gain <= 1; maximum(root,1) -> root >= 1;
+    // clip_by_value(smooth,0,1) -> 0 <= smooth <= 1.
+    dparams[0] = prm[0] <= 1.0f ? (float)g[0] : 0.f;
+    dparams[1] = (float)g[1];
+    dparams[2] = prm[2] >= 1.0f ? (float)g[2] : 0.f;
+    dparams[3] = (prm[3] >= 0.0f && prm[3] <= 1.0f) ? (float)g[3] : 0.f;
+  }
+}
+
+ACFE_API int acfe_pcen_bwd(const float* mel, int batch, int t, int m, const float* params, float eps,
+                           const float* stats, const void* dout, int ddt, float* ws, float* dparams,
+                           void* stream) {
+  if (!mel || !params || !stats || !dout || !ws || !dparams || batch <= 0 || t <= 0 || m <= 0 ||
+      (ddt != 0 && ddt != 1))
+    return ACFE_E_INVAL;
+  const int np = acfe_pcen_partials(batch, m);
+  double* part = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(k_pcen_bwd, dim3(np), dim3(256), 0, S(stream), mel, batch, t, m, params, eps,
+                     stats, dout, ddt, part);
+  int rc = launch_rc("acfe_pcen_bwd");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_pcen_bwd_fin, dim3(1), dim3(64), 0, S(stream), part, np, params, stats,
+                     dparams);
+  return launch_rc("acfe_pcen_bwd_fin");
+}

@@ -1,0 +1,130 @@
+/*
+ * acfe.h -- C ABI of the MI355X-native audio-classification front end + engine
+ * ("acfe") that replaces the hot path of TheCacophonyProject/audio-training.
+ *
+ * Conventions (every entry point):
+ *   - extern "C", plain pointers and sizes, no C++ / torch types.
+ *   - Return 0 on success; < 0 on error: ACFE_E_INVAL for bad arguments,
+ *     -(int)hipError_t for a HIP failure.  Nothing throws across the ABI.
+ *   - Every buffer argument is caller-owned DEVICE memory unless the name ends
+ *     in `_host`.  The library allocates only inside acfe_plan_create (twiddles,
+ *     window, banded mel filterbank), freed by acfe_plan_destroy.
+ *   - Every compute call takes the hipStream_t it is ordered on (passed as
+ *     void*; NULL = the default stream), is asynchronous and reentrant, and
+ *     never synchronises the device (graph-capturable).
+ *   - Tensor layouts: raw audio [B][N] fp32 with a clip stride (elements
+ *     between consecutive clips); features [B][T][M] ("BTM") or [B][M][T]
+ *     ("BMT" == NHWC with H=M, W=T, C=1, the model input of
+ *     resnet/wr_resnet*.py); activations NHWC; conv weights KRSC.
+ *
+ * Reference interfaces replaced (file:line in the reference repository):
+ *   acfe_mel_filterbank    custommel.py:18-54        mel_f(sr,n_mels,fmin,fmax,n_fft,break_freq)
+ *   acfe_plan_create       tfdataset.py:430-460      MEL_WEIGHTS / NFFT / HOP_LENGTH globals
+ *   acfe_normalize_stats   tfdataset.py:1916-1934    normalize (reductions)
+ *   acfe_normalize_apply   tfdataset.py:1916-1934    normalize (pointwise)
+ *   acfe_mixup             tfdataset.py:930-955      mix_up (x blend; lambda drawn by caller)
+ *   acfe_mel_fwd           tfdataset.py:2007-2059    raw_to_mel  (pad_end, power 2)
+ *                          predict_utils.py:163-239  get_spect   (center, power 2)
+ *                          tfdataset.py:1082-1090    spectrogram path (power 1)
+ *   acfe_pcen_fwd          tfpcen.py:33-39,89-99     ExponentialMovingAverage + PCEN.call
+ *   acfe_pcen_normalize    tfpcen.py:105-110         normalize_minmax (batch-global)
+ *   acfe_pcen_bwd          gradient of the three above w.r.t. gain/bias/root/smooth
+ */
+#ifndef ACFE_H
+#define ACFE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACFE_OK 0
+#define ACFE_E_INVAL (-1000)
+#define ACFE_E_NOMEM (-1001)
+
+/* Framing of acfe_mel_fwd. */
+#define ACFE_PAD_END 0            /* tf.signal.stft(pad_end=True): frames = ceil(N/hop)          */
+#define ACFE_PAD_CENTER_CONSTANT 1 /* librosa.stft(center=True, pad_mode="constant") (>=0.10)   */
+#define ACFE_PAD_CENTER_REFLECT 2  /* librosa.stft(center=True, pad_mode="reflect")  (<0.10)     */
+
+#define ACFE_LAYOUT_BTM 0
+#define ACFE_LAYOUT_BMT 1
+
+#define ACFE_DTYPE_F32 0
+#define ACFE_DTYPE_BF16 1
+
+typedef struct acfe_plan_s* acfe_plan_t;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int acfe_version(void);
+
+/* Last HIP error string (thread-local), for diagnostics. */
+const char* acfe_last_error(void);
+
+/* custommel.mel_f restated in C (float64 arithmetic, float32 result) into a
+ * caller-owned HOST array out_host[n_mels][1 + n_fft/2]. */
+int acfe_mel_filterbank(int sr, int n_mels, double fmin, double fmax, int n_fft,
+                        double break_freq, float* out_host);
+
+/* Create a front-end plan.  `mel_weights_host` is the dense [n_mels][1+n_fft/2]
+ * float32 filterbank (as custommel.mel_f returns it) or NULL to compute it
+ * with acfe_mel_filterbank(sr, n_mels, fmin, fmax, n_fft, break_freq).
+ * n_fft must be a power of two in [256, 4096].  Allocates device memory on
+ * the current device. */
+int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax,
+                     double break_freq, const float* mel_weights_host, acfe_plan_t* plan);
+int acfe_plan_destroy(acfe_plan_t plan);
+/* Number of frames the plan produces for an N-sample clip with pad_mode. */
+int acfe_plan_num_frames(acfe_plan_t plan, int n_samples, int pad_mode);
+
+/* Per-clip normalisation statistics: stats[b] = {min_b, max_b(x - min_b)}.
+ * Clip b is x[b*clip_stride .. b*clip_stride + n). */
+int acfe_normalize_stats(const float* x, int64_t clip_stride, int batch, int n,
+                         float* stats, void* stream);
+/* y[b][i] = ((x - min)/range + 1e-6 - 0.5) * 2, in that float32 order. */
+int acfe_normalize_apply(const float* x, int64_t clip_stride, int batch, int n,
+                         const float* stats, float* y, void* stream);
+/* mix_up on normalised inputs: y = norm(x1)*lam + norm(x2)*(1-lam), per row.
+ * stats1/stats2 may be NULL (inputs already normalised). */
+int acfe_mixup(const float* x1, const float* stats1, const float* x2, const float* stats2,
+               const float* lam, int batch, int n, float* y, void* stream);
+
+/* Fused framing -> periodic Hann -> n_fft real FFT (LDS radix-8/4 Stockham)
+ * -> |X|^power (power 1 or 2) -> banded mel, for every frame of every clip.
+ * If `stats` is non-NULL each clip is normalised on load (tfdataset.normalize).
+ * out: layout ACFE_LAYOUT_BTM -> [B][T][M], ACFE_LAYOUT_BMT -> [B][M][T], fp32. */
+int acfe_mel_fwd(acfe_plan_t plan, const float* raw, int64_t clip_stride, int batch, int n,
+                 const float* stats, int pad_mode, int power, float* out, int layout,
+                 void* stream);
+
+/* PCEN forward on mel [B][T][M] fp32 (tfpcen.py:89-95):
+ *   a_t = w x_t + (1-w) a_{t-1}, a_{-1} = x_0,  w = clip(smooth, 0, 1)
+ *   y   = (x/(eps + a)^min(gain,1) + bias)^(1/max(root,1)) - bias^(1/max(root,1))
+ * params: DEVICE float[4] = {gain, bias, root, smooth}; eps is a constant.
+ * y is written UN-normalised as [B][M][T] fp32 (model layout).
+ * minmax_partial: device float[2 * acfe_pcen_partials(batch, n_mels)]. */
+int acfe_pcen_partials(int batch, int n_mels);
+int acfe_pcen_fwd(const float* mel_btm, int batch, int t, int m, const float* params, float eps,
+                  float* y_bmt, float* minmax_partial, void* stream);
+/* normalize_minmax over the whole batch (tfpcen.py:105-110):
+ *   out = 2*((y - mn)/(mx - mn)) - 1 written as fp32 or bf16 (out_dtype).
+ * stats_out: device float[4] = {mn, mx, count(y==mn), count(y==mx)} (saved for
+ * the backward).  When `scope_minmax` is non-NULL it overrides the reduction
+ * with a caller-supplied {mn, mx} (e.g. all-reduced across replicas). */
+int acfe_pcen_normalize(const float* y_bmt, int64_t count, const float* minmax_partial,
+                        int n_partial, const float* scope_minmax, void* out, int out_dtype,
+                        float* stats_out, void* stream);
+/* Gradient of PCEN+normalize_minmax w.r.t. params {gain,bias,root,smooth}.
+ * dout: [B][M][T] gradient w.r.t. the normalised output (fp32 or bf16).
+ * workspace: device float[32 * acfe_pcen_partials(batch, n_mels)] (8-byte aligned).
+ * dparams: device float[4] (overwritten). */
+int acfe_pcen_bwd(const float* mel_btm, int batch, int t, int m, const float* params, float eps,
+                  const float* stats, const void* dout, int dout_dtype, float* workspace,
+                  float* dparams, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACFE_H */

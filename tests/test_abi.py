@@ -1,0 +1,38 @@
+"""The C-ABI library loads and exports every symbol include/acfe.h declares
+(no compute calls: this runs without a GPU)."""
+import re
+
+from conftest import ROOT
+
+
+def header_functions():
+    txt = (ROOT / "include" / "acfe.h").read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(acfe_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_api():
+    fns = header_functions()
+    assert "acfe_mel_fwd" in fns and "acfe_pcen_bwd" in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from acfe import _lib
+
+    missing = [f for f in header_functions() if not hasattr(_lib.lib, f)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    from acfe import _lib
+
+    assert sorted(_lib.SIGNATURES) == header_functions()
+
+
+def test_host_only_calls():
+    from acfe import _lib
+
+    assert _lib.lib.acfe_version() >= 100
+    assert _lib.lib.acfe_pcen_partials(512, 128) == 256
+    # invalid arguments are reported, not crashed on
+    assert _lib.lib.acfe_mel_filterbank(0, 128, 100.0, 11000.0, 4096, 1000.0, None) == _lib.E_INVAL

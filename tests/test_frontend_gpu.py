@@ -1,0 +1,140 @@
+"""GPU parity of the fused front end (HIP, via the C ABI) against the CPU oracle.
+
+Tolerances (fp32 kernels vs float64 oracle):
+  mel:   |gpu - ref| <= 2e-5 * max(ref) per clip  (fp32 FFT, 11 passes)
+  PCEN:  |gpu - ref| <= 5e-5 on the [-1, 1] output
+  dPCEN: relative 2e-3 on parameter gradients (fp32 accumulation over B*M*T)
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import synth_clips
+from oracle import frontend as of
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fe(cuda):
+    from acfe import frontend
+
+    return frontend
+
+
+def _plan(fe, **kw):
+    return fe.MelPlan(**kw)
+
+
+def _rel_close(gpu, ref, tol):
+    gpu = np.asarray(gpu, np.float64)
+    ref = np.asarray(ref, np.float64)
+    scale = np.abs(ref).reshape(ref.shape[0], -1).max(1).reshape((-1,) + (1,) * (ref.ndim - 1))
+    err = np.abs(gpu - ref) / scale
+    assert err.max() <= tol, f"max rel err {err.max():.3e} > {tol}"
+    return err.max()
+
+
+def test_normalize_and_mixup(fe, cuda):
+    x1 = torch.from_numpy(synth_clips(3, seed=11)).to(cuda)
+    x2 = torch.from_numpy(synth_clips(3, seed=21)).to(cuda)
+    y = fe.normalize(x1).cpu().numpy()
+    np.testing.assert_allclose(y, of.normalize(x1.cpu().numpy()), atol=2e-6)
+    lam = torch.tensor([0.0, 0.3, 0.9], device=cuda)
+    st1, st2 = fe.normalize_stats(x1), fe.normalize_stats(x2)
+    m = fe.mix_up(x1, x2, lam, st1, st2).cpu().numpy()
+    ref, _ = of.mix_up(of.normalize(x1.cpu().numpy()), np.zeros((3, 2)), of.normalize(x2.cpu().numpy()),
+                       np.zeros((3, 2)), lam.cpu().numpy())
+    np.testing.assert_allclose(m, ref, atol=4e-6)
+
+
+@pytest.mark.parametrize("n_mels,n_fft", [(128, 4096), (160, 4096), (96, 1024)])
+def test_mel_pad_end(fe, cuda, n_mels, n_fft):
+    raw = synth_clips(3, seed=5)
+    plan = _plan(fe, n_mels=n_mels, n_fft=n_fft)
+    x = torch.from_numpy(raw).to(cuda)
+    st = fe.normalize_stats(x)
+    out = plan.mel(x, st, pad_mode="end", layout="btm").cpu().numpy()
+    ref = of.raw_to_mel(of.normalize(raw), plan.weights, n_fft, 281).transpose(0, 2, 1)
+    assert out.shape == ref.shape == (3, 513, n_mels)
+    _rel_close(out, ref, 2e-5)
+    bmt = plan.mel(x, st, pad_mode="end", layout="bmt").cpu().numpy()
+    np.testing.assert_array_equal(bmt, out.transpose(0, 2, 1))
+
+
+@pytest.mark.parametrize("pad_mode", ["constant", "reflect"])
+def test_mel_center_predict_path(fe, cuda, pad_mode):
+    raw = synth_clips(2, seed=7)
+    plan = _plan(fe, n_mels=160)
+    x = torch.from_numpy(raw).to(cuda)
+    out = plan.mel(x, fe.normalize_stats(x), pad_mode=pad_mode, layout="bmt").cpu().numpy()
+    ref = of.get_spect(of.normalize(raw), plan.weights, 4096, 281, 2, pad_mode)
+    _rel_close(out, ref, 2e-5)
+
+
+def test_mel_power1_no_norm(fe, cuda):
+    raw = synth_clips(2, seed=8) * 0.5
+    plan = _plan(fe)
+    out = plan.mel(torch.from_numpy(raw).to(cuda), None, power=1, layout="bmt").cpu().numpy()
+    ref = of.raw_to_mel(raw, plan.weights, 4096, 281, power=1)
+    _rel_close(out, ref, 2e-5)
+
+
+def test_mel_streaming_windows(fe, cuda):
+    """Overlapping 3 s windows at a 1.5 s hop of one recording (clip_stride < n)."""
+    rec = synth_clips(1, n=48000 * 9, seed=9)[0]
+    plan = _plan(fe)
+    x = torch.from_numpy(rec).to(cuda)
+    nwin = 1 + (len(rec) - 144000) // 72000
+    st = fe.normalize_stats(x, n=144000, clip_stride=72000, batch=nwin)
+    out = plan.mel(x, st, pad_mode="constant", layout="bmt", n=144000, clip_stride=72000, batch=nwin).cpu().numpy()
+    wins = np.stack([rec[i * 72000: i * 72000 + 144000] for i in range(nwin)])
+    ref = of.get_spect(of.normalize(wins), plan.weights, 4096, 281, 2, "constant")
+    _rel_close(out, ref, 2e-5)
+
+
+def test_mel_short_and_empty(fe, cuda):
+    plan = _plan(fe)
+    raw = synth_clips(2, n=5000, seed=10)
+    x = torch.from_numpy(raw).to(cuda)
+    out = plan.mel(x, fe.normalize_stats(x)).cpu().numpy()
+    ref = of.raw_to_mel(of.normalize(raw), plan.weights).transpose(0, 2, 1)
+    assert out.shape[1] == -(-5000 // 281)
+    _rel_close(out, ref, 2e-5)
+    e = plan.mel(torch.zeros((0, 144000), device=cuda))
+    assert e.shape == (0, 513, 128)
+
+
+def _mel_batch(fe, cuda, b, seed):
+    raw = synth_clips(b, seed=seed)
+    plan = _plan(fe)
+    x = torch.from_numpy(raw).to(cuda)
+    return plan.mel(x, fe.normalize_stats(x), layout="btm")
+
+
+def test_pcen_forward(fe, cuda):
+    mel = _mel_batch(fe, cuda, 2, 12)
+    p = torch.tensor([0.98, 2.0, 2.0, 0.04], device=cuda)
+    out = fe.pcen(mel, p).cpu().numpy()
+    ref = of.pcen(mel.cpu().numpy().astype(np.float64)).transpose(0, 2, 1)
+    assert out.shape == (2, 128, 513)
+    assert np.abs(out - ref).max() <= 5e-5
+    assert out.min() == -1.0 and out.max() == 1.0
+    ob = fe.pcen(mel, p, out_dtype=torch.bfloat16).float().cpu().numpy()
+    assert np.abs(ob - ref).max() <= 8e-3
+
+
+@pytest.mark.parametrize("params", [(0.98, 2.0, 2.0, 0.04), (0.5, 1.5, 3.0, 0.2)])
+def test_pcen_backward(fe, cuda, params):
+    from oracle.torch_ref import pcen_torch
+
+    mel = _mel_batch(fe, cuda, 2, 13)
+    g = torch.randn((2, 128, 513), generator=torch.Generator().manual_seed(0), dtype=torch.float64)
+    p = torch.tensor(params, device=cuda, requires_grad=True)
+    out = fe.pcen(mel, p)
+    (out * g.float().to(cuda)).sum().backward()
+    pr = torch.tensor(params, dtype=torch.float64, requires_grad=True)
+    ref = pcen_torch(mel.cpu().double(), pr)
+    (ref * g).sum().backward()
+    gg, gr = p.grad.cpu().double().numpy(), pr.grad.numpy()
+    np.testing.assert_allclose(gg, gr, rtol=2e-3, atol=2e-3 * np.abs(gr).max())
