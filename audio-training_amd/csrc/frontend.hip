@@ -186,6 +186,7 @@ __device__ __forceinline__ float norm1(float v, float mn, float rng) {
 
 ACFE_API int acfe_normalize_stats(const float* x, int64_t cs, int batch, int n, float* stats,
                                   void* stream) {
+  if (batch == 0 && n > 0) return ACFE_OK;
   if (!x || !stats || batch < 0 || n <= 0) return ACFE_E_INVAL;
   if (batch == 0) return ACFE_OK;
   hipLaunchKernelGGL(k_norm_stats, dim3(batch), dim3(256), 0, S(stream), x, cs, n, stats);
@@ -411,6 +412,7 @@ __global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int6
 ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch, int n,
                           const float* stats, int pad_mode, int power, float* out, int layout,
                           void* stream) {
+  if (batch == 0 && p && n > 0) return ACFE_OK;
   if (!p || !raw || !out || batch < 0 || n <= 0 || batch > 65535 || (power != 1 && power != 2) ||
       pad_mode < 0 || pad_mode > 2 || (layout != 0 && layout != 1))
     return ACFE_E_INVAL;
