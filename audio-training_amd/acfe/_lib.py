@@ -34,8 +34,43 @@ SIGNATURES: dict[str, list] = {
     "acfe_pcen_fwd": [P, I32, I32, I32, P, F32, P, P, P],
     "acfe_pcen_normalize": [P, I64, P, I32, P, P, I32, P, P],
     "acfe_pcen_bwd": [P, I32, I32, I32, P, F32, P, P, I32, P, P, P],
+    "acfe_conv2d_packed_shape": [I32, I32, I32, I32, I32, I32, P, P],
+    "acfe_conv2d_pack_weights": [P, I32, I32, I32, I32, I32, I32, P, P],
+    "acfe_conv2d_stats_rows": [I64, I32],
+    "acfe_conv2d_fwd": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P, P],
+    "acfe_conv2d_dgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P],
+    "acfe_conv2d_wgrad_workspace": [I32, I32, I32, I32, I32, I32, I32, I32, I32],
+    "acfe_conv2d_wgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, I32, P, P],
+    "acfe_stem_blocks": [I32, I32, I32],
+    "acfe_stem_fold_weights": [P, I32, I32, I32, I32, P, P],
+    "acfe_stem_fwd": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, I32, P, P],
+    "acfe_stem_dgrad": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P],
+    "acfe_stem_wgrad": [P, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, P, P],
+    "acfe_reduce_blocks": [I64],
+    "acfe_bn_stats": [P, I64, I32, I32, P, P],
+    "acfe_bn_finalize": [P, I32, I32, I32, F64, P, P, F32, F32, P, P, I32, P, P, P, P, P],
+    "acfe_bn_apply": [P, I32, I64, I32, P, P, I32, P, I32, P],
+    "acfe_bn_bwd_reduce": [P, I32, P, I32, I64, I32, P, P, P, P, I32, P, P],
+    "acfe_bn_bwd_finalize": [P, I32, I32, F64, P, P, P, P, P, P, P],
+    "acfe_bn_bwd_apply": [P, I32, P, I32, I64, I32, P, P, I32, P, P, P, I32, P],
+    "acfe_channel_sum": [P, I64, I32, I32, P, P, F32, P],
+    "acfe_add": [P, P, I64, I32, P, I32, P],
+    "acfe_relu_bwd": [P, P, I64, P, I32, P],
+    "acfe_dropout": [P, I64, F32, C.c_uint64, P, I32, P],
+    "acfe_cast": [P, I32, I64, P, I32, P],
+    "acfe_sigmoid": [P, I64, P, P],
+    "acfe_maxpool2d": [P, I32, I32, I32, I32, I32, I32, P, I32, P],
+    "acfe_maxpool2d_bwd": [P, P, I32, I32, I32, I32, I32, I32, P, I32, P],
+    "acfe_avgpool2d": [P, I32, I32, I32, I32, I32, P, I32, P],
+    "acfe_avgpool2d_bwd": [P, I32, I32, I32, I32, I32, P, I32, P],
+    "acfe_axis_pool": [P, I32, I64, I32, I32, F32, I32, P, P],
+    "acfe_axis_pool_bwd": [P, I32, P, I64, I32, I32, F32, I32, P, P],
+    "acfe_dense_fwd": [P, P, P, I32, I32, I32, P, P],
+    "acfe_dense_bwd": [P, P, P, I32, I32, I32, P, P, P, P],
+    "acfe_loss": [P, P, I32, I32, I32, F32, P, P, P, P],
+    "acfe_adam_step": [P, P, P, P, I64, F32, F32, F32, F32, F32, P],
 }
-_RESTYPES = {"acfe_last_error": C.c_char_p}
+_RESTYPES = {"acfe_last_error": C.c_char_p, "acfe_conv2d_wgrad_workspace": I64}
 
 PAD_END, PAD_CENTER_CONSTANT, PAD_CENTER_REFLECT = 0, 1, 2
 LAYOUT_BTM, LAYOUT_BMT = 0, 1

@@ -1,0 +1,140 @@
+"""Keras-layer equivalents (tf.keras.layers.Conv2D / BatchNormalization / Dense)
+as torch Modules running on the acfe kernels.  Parameter names and layouts:
+conv kernel KRSC fp32 (Keras stores RSCK; see to_keras/from_keras), Dense
+kernel [in][out] as in Keras, BN gamma/beta/moving_mean/moving_variance."""
+from __future__ import annotations
+
+import math
+import zlib
+
+import torch
+from torch import nn
+
+from . import ops
+
+
+def _pair(k):
+    return (k, k) if isinstance(k, int) else tuple(k)
+
+
+def glorot_uniform(shape, fan_in, fan_out, seed):
+    """tf.keras.initializers.GlorotUniform: U(-l, l), l = sqrt(6/(fan_in+fan_out))."""
+    g = torch.Generator().manual_seed(int(seed))
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    return (torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1).mul_(lim).to(torch.float32)
+
+
+def _seed(name, base=0):
+    return (zlib.crc32(name.encode()) + base) & 0x7FFFFFFF
+
+
+class Conv2D(nn.Module):
+    """tf.keras.layers.Conv2D(filters, kernel_size, strides, padding, use_bias=True)."""
+
+    def __init__(self, cin, filters, kernel_size, strides=1, padding="same", use_bias=True, name="conv2d", seed=0):
+        super().__init__()
+        kh, kw = _pair(kernel_size)
+        self.strides, self.padding, self.name = int(strides), padding, name
+        self.weight = nn.Parameter(glorot_uniform((filters, kh, kw, cin), kh * kw * cin, kh * kw * filters,
+                                                  _seed(name, seed)))
+        self.bias = nn.Parameter(torch.zeros(filters)) if use_bias else None
+
+    def forward(self, x, want_stats=False):
+        y, st = ops.conv2d(x, self.weight, self.bias, self.strides, self.padding, want_stats)
+        return (y, st) if want_stats else y
+
+
+class StemConv2D(Conv2D):
+    """First Conv2D of both WRN variants.  Its input has `cin` identical channels
+    (tfdataset.py:2053 repeats the mel image 3x); the kernel keeps the Keras
+    parameter shape [16, R, S, cin] but runs on the single folded channel."""
+
+    def __init__(self, cin, filters, kernel_size, name="conv1_1", seed=0, out_dtype=torch.bfloat16):
+        super().__init__(cin, filters, kernel_size, 1, "same", True, name, seed)
+        if filters != 16:
+            raise ValueError("the stem kernel is specialised to 16 output channels")
+        self.out_dtype = out_dtype
+
+    def forward(self, x, want_stats=False):
+        y, st = ops.stem_conv(x, self.weight, self.bias, self.out_dtype, want_stats)
+        return (y, st) if want_stats else y
+
+
+class BatchNormalization(nn.Module):
+    """tf.keras.layers.BatchNormalization(axis=3): eps 1e-3, momentum 0.99."""
+
+    def __init__(self, channels, name="batch_normalization", eps=1e-3, momentum=0.99):
+        super().__init__()
+        self.name, self.eps, self.momentum = name, eps, momentum
+        self.gamma = nn.Parameter(torch.ones(channels))
+        self.beta = nn.Parameter(torch.zeros(channels))
+        self.register_buffer("moving_mean", torch.zeros(channels))
+        self.register_buffer("moving_variance", torch.ones(channels))
+
+    def forward(self, x, relu=False, stats=None):
+        return ops.batch_norm(x, self.gamma, self.beta, self.moving_mean, self.moving_variance, self.training,
+                              relu, stats, self.eps, self.momentum)
+
+
+class Dense(nn.Module):
+    """tf.keras.layers.Dense(units) logits; the sigmoid of the reference's
+    Dense(activation="sigmoid") is applied by predict()/the loss."""
+
+    def __init__(self, cin, units, name="dense", seed=0):
+        super().__init__()
+        self.name = name
+        self.kernel = nn.Parameter(glorot_uniform((cin, units), cin, units, _seed(name, seed)))
+        self.bias = nn.Parameter(torch.zeros(units))
+
+    def forward(self, x):
+        return ops.dense(x, self.kernel, self.bias)
+
+
+class ParamArena:
+    """All trainable parameters of a module as views of ONE flat fp32 buffer,
+    with gradients as views of one flat gradient buffer: the data-parallel
+    all-reduce is a single (bucketable) collective and Adam one kernel launch."""
+
+    def __init__(self, module: nn.Module, device):
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        self.numel = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        o = 0
+        self.offsets = []
+        with torch.no_grad():
+            for p in self.params:
+                n = p.numel()
+                self.flat[o:o + n].copy_(p.detach().reshape(-1).to(device))
+                p.data = self.flat[o:o + n].view(p.shape)
+                p.grad = self.grad[o:o + n].view(p.shape)
+                self.offsets.append((o, n))
+                o += n
+
+    def zero_grad(self):
+        self.grad.zero_()
+        for p, (o, n) in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:].data_ptr():
+                p.grad = self.grad[o:o + n].view(p.shape)
+
+
+class Adam:
+    """tf.keras.optimizers.Adam(learning_rate=lr) (audiomodel.py:1226-1240):
+    beta_1 0.9, beta_2 0.999, epsilon 1e-7, one fused kernel over the arena."""
+
+    def __init__(self, arena: ParamArena, lr=0.01, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+        self.arena, self.lr, self.b1, self.b2, self.eps = arena, lr, beta_1, beta_2, epsilon
+        self.m = torch.zeros_like(arena.flat)
+        self.v = torch.zeros_like(arena.flat)
+        self.iterations = 0
+
+    def step(self, grad_scale=1.0):
+        from ._lib import call
+        from ._torch import ptr, stream
+
+        self.iterations += 1
+        t = self.iterations
+        alpha = self.lr * math.sqrt(1.0 - self.b2 ** t) / (1.0 - self.b1 ** t)
+        a = self.arena
+        call("acfe_adam_step", ptr(a.flat), ptr(a.grad), ptr(self.m), ptr(self.v), a.numel, float(grad_scale),
+             self.b1, self.b2, self.eps, float(alpha), stream())

@@ -1,0 +1,454 @@
+"""Autograd operators over the acfe model kernels (csrc/conv.hip, csrc/nn.hip).
+
+Every forward/backward here is one or more calls through the C ABI; torch is
+used only for device memory (torch.empty), streams and autograd bookkeeping.
+Layouts: activations NHWC (bf16 for training, fp32 for inference), weights
+fp32 KRSC master copies packed to the compute dtype on every forward.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+
+from ._lib import call, lib
+from ._torch import dtype_code, ptr, stream
+
+F32, F64 = torch.float32, torch.float64
+
+
+def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
+    """TF/Keras padding="same": out = ceil(n/s), pad_before = total//2."""
+    out = -(-n // s)
+    total = max((out - 1) * s + k - n, 0)
+    return out, total // 2
+
+
+def valid_out(n: int, k: int, s: int) -> int:
+    return (n - k) // s + 1
+
+
+def _empty(shape, dtype, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+def packed_shape(K, R, S, C, dt, flip):
+    import ctypes as C_
+
+    rp, cp = C_.c_int(), C_.c_int()
+    call("acfe_conv2d_packed_shape", K, R, S, C, dt, flip, C_.byref(rp), C_.byref(cp))
+    return rp.value, cp.value
+
+
+def pack_weights(w: torch.Tensor, dtype: torch.dtype, flip: bool) -> torch.Tensor:
+    K, R, S, C = w.shape
+    dt = dtype_code(dtype)
+    rp, cp = packed_shape(K, R, S, C, dt, int(flip))
+    out = _empty((rp, cp), dtype, w.device)
+    call("acfe_conv2d_pack_weights", ptr(w), K, R, S, C, dt, int(flip), ptr(out), stream())
+    return out
+
+
+def _no_stats(dev):
+    return torch.empty(0, dtype=F64, device=dev)
+
+
+# ------------------------------------------------------------------ conv
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pt, pl, P, Q, want_stats):
+        N, H, W, C = x.shape
+        K, R, S, Cw = w.shape
+        assert Cw == C, (Cw, C)
+        dt = dtype_code(x.dtype)
+        wp = pack_weights(w, x.dtype, False)
+        y = _empty((N, P, Q, K), x.dtype, x.device)
+        stats = _no_stats(x.device)
+        if want_stats:
+            rows = lib.acfe_conv2d_stats_rows(N * P * Q, K)
+            stats = _empty((rows, 2, wp.shape[0]), F64, x.device)
+        call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, stride, pt, pl, P, Q, ptr(b), ptr(y), dt,
+             ptr(stats) if want_stats else None, stream())
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, pt, pl, P, Q, b is not None)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        x, w = ctx.saved_tensors
+        stride, pt, pl, P, Q, has_b = ctx.conf
+        N, H, W, C = x.shape
+        K, R, S, _ = w.shape
+        dt = dtype_code(x.dtype)
+        dy = dy.contiguous()
+        dx = dw = db = None
+        s = stream()
+        if ctx.needs_input_grad[0]:
+            wf = pack_weights(w, x.dtype, True)
+            dx = _empty(x.shape, x.dtype, x.device)
+            ws = None
+            if stride > 1:
+                ws = _empty((N * ((P - 1) * stride + 1) * ((Q - 1) * stride + 1) * K,), x.dtype, x.device)
+            call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
+                 ptr(ws), s)
+        if ctx.needs_input_grad[1]:
+            dw = _empty(w.shape, F32, w.device)
+            nws = lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, P, Q)
+            ws = _empty((nws,), F32, x.device)
+            call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, stride, pt, pl, P, Q, ptr(dw), 0.0,
+                 dt, ptr(ws), s)
+        if has_b and ctx.needs_input_grad[2]:
+            db = channel_sum(dy, K)
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def channel_sum(x: torch.Tensor, C: int) -> torch.Tensor:
+    rows = x.numel() // C
+    out = _empty((C,), F32, x.device)
+    part = _empty((lib.acfe_reduce_blocks(rows) * 2 * C,), F64, x.device)
+    call("acfe_channel_sum", ptr(x), rows, C, dtype_code(x.dtype), ptr(part), ptr(out), 0.0, stream())
+    return out
+
+
+def conv2d(x, w, b=None, stride=1, padding="same", want_stats=False):
+    """Keras Conv2D on NHWC x with KRSC weights. Returns (y, stats_partial)."""
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    if padding == "same":
+        P, pt = same_padding(H, R, stride)
+        Q, pl = same_padding(W, S, stride)
+    elif padding == "valid":
+        P, Q, pt, pl = valid_out(H, R, stride), valid_out(W, S, stride), 0, 0
+    else:
+        raise ValueError(padding)
+    return _Conv2dFn.apply(x, w, b, stride, pt, pl, P, Q, want_stats)
+
+
+# ------------------------------------------------------------------ stem (folded C=1)
+class _StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, pt, pl, out_dtype, want_stats):
+        # x: [N, H, W] (one folded channel); w: [16, R, S, Crep] fp32
+        N, H, W = x.shape
+        K, R, S, rep = w.shape
+        weff = _empty((K, R, S), F32, x.device)
+        s = stream()
+        call("acfe_stem_fold_weights", ptr(w), K, R, S, rep, ptr(weff), s)
+        y = _empty((N, H, W, K), out_dtype, x.device)
+        stats = _no_stats(x.device)
+        if want_stats:
+            stats = _empty((lib.acfe_stem_blocks(N, H, W), 2, K), F64, x.device)
+        call("acfe_stem_fwd", ptr(x), dtype_code(x.dtype), N, H, W, R, S, pt, pl, ptr(weff), ptr(b), ptr(y),
+             dtype_code(out_dtype), ptr(stats) if want_stats else None, s)
+        ctx.save_for_backward(x, w, weff)
+        ctx.conf = (pt, pl, b is not None)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _ds):
+        x, w, weff = ctx.saved_tensors
+        pt, pl, has_b = ctx.conf
+        N, H, W = x.shape
+        K, R, S, rep = w.shape
+        dy = dy.contiguous()
+        s = stream()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty(x.shape, x.dtype, x.device)
+            call("acfe_stem_dgrad", ptr(dy), dtype_code(dy.dtype), N, H, W, R, S, pt, pl, ptr(weff), ptr(dx),
+                 dtype_code(x.dtype), s)
+        if ctx.needs_input_grad[1]:
+            dw = _empty(w.shape, F32, w.device)
+            ws = _empty((lib.acfe_stem_blocks(N, H, W) * K * R * S,), F64, x.device)
+            call("acfe_stem_wgrad", ptr(x), dtype_code(x.dtype), ptr(dy), dtype_code(dy.dtype), N, H, W, R, S, pt,
+                 pl, rep, ptr(dw), 0.0, ptr(ws), s)
+        if has_b and ctx.needs_input_grad[2]:
+            db = channel_sum(dy, K)
+        return dx, dw, db, None, None, None, None
+
+
+def stem_conv(x, w, b, out_dtype, want_stats=False):
+    """'same' stride-1 conv of a one-channel map x [N,H,W] whose Cin copies are folded."""
+    N, H, W = x.shape
+    _, R, S, _ = w.shape
+    _, pt = same_padding(H, R, 1)
+    _, pl = same_padding(W, S, 1)
+    return _StemFn.apply(x, w, b, pt, pl, out_dtype, want_stats)
+
+
+# ------------------------------------------------------------------ batch norm
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype):
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dt = dtype_code(x.dtype)
+        dev = x.device
+        s = stream()
+        scale, shift, mean, invstd = (_empty((C,), F32, dev) for _ in range(4))
+        if training:
+            if stats is None or stats.numel() == 0:
+                nrows = lib.acfe_reduce_blocks(rows)
+                part = _empty((nrows * 2 * C,), F64, dev)
+                call("acfe_bn_stats", ptr(x), rows, C, dt, ptr(part), s)
+                ld = C
+            else:
+                part = stats
+                ld = stats.shape[-1]
+                nrows = stats.numel() // (2 * ld)
+            call("acfe_bn_finalize", ptr(part), nrows, ld, C, float(rows), ptr(gamma), ptr(beta), eps, momentum,
+                 ptr(mmean), ptr(mvar), 1, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
+        else:
+            call("acfe_bn_finalize", None, 0, C, C, 0.0, ptr(gamma), ptr(beta), eps, momentum, ptr(mmean), ptr(mvar),
+                 0, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
+        y = _empty(x.shape, out_dtype, dev)
+        call("acfe_bn_apply", ptr(x), dt, rows, C, ptr(scale), ptr(shift), int(relu), ptr(y), dtype_code(out_dtype), s)
+        ctx.save_for_backward(x, scale, shift, mean, invstd)
+        ctx.conf = (relu, training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, scale, shift, mean, invstd = ctx.saved_tensors
+        relu, training = ctx.conf
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dev = x.device
+        s = stream()
+        dy = dy.contiguous()
+        nrows = lib.acfe_reduce_blocks(rows)
+        part = _empty((nrows * 2 * C,), F64, dev)
+        call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+             ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
+        dgamma, dbeta = _empty((C,), F32, dev), _empty((C,), F32, dev)
+        coef = _empty((3 * C,), F32, dev)
+        # eval mode: statistics are constants -> count -> inf removes the mean terms
+        count = float(rows) if training else 1e300
+        call("acfe_bn_bwd_finalize", ptr(part), nrows, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
+             ptr(dbeta), ptr(coef), s)
+        dx = _empty(x.shape, x.dtype, dev)
+        call("acfe_bn_bwd_apply", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+             ptr(shift), int(relu), ptr(coef), None, ptr(dx), dtype_code(x.dtype), s)
+        return dx, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+
+def batch_norm(x, gamma, beta, mmean, mvar, training, relu=False, stats=None, eps=1e-3, momentum=0.99):
+    return _BNFn.apply(x, gamma, beta, stats, mmean, mvar, bool(training), bool(relu), float(eps),
+                       float(momentum), x.dtype)
+
+
+# ------------------------------------------------------------------ elementwise / pooling
+class _AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, relu):
+        z = torch.empty_like(a)
+        call("acfe_add", ptr(a), ptr(b), a.numel(), int(relu), ptr(z), dtype_code(a.dtype), stream())
+        ctx.relu = relu
+        if relu:
+            ctx.save_for_backward(z)
+        return z
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        if ctx.relu:
+            (z,) = ctx.saved_tensors
+            d = torch.empty_like(g)
+            call("acfe_relu_bwd", ptr(g), ptr(z), g.numel(), ptr(d), dtype_code(g.dtype), stream())
+            g = d
+        return g, g, None
+
+
+def add(a, b, relu=False):
+    return _AddFn.apply(a.contiguous(), b.contiguous(), bool(relu))
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rate, seed):
+        y = torch.empty_like(x)
+        call("acfe_dropout", ptr(x), x.numel(), rate, seed, ptr(y), dtype_code(x.dtype), stream())
+        ctx.conf = (rate, seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        rate, seed = ctx.conf
+        g = g.contiguous()
+        d = torch.empty_like(g)
+        call("acfe_dropout", ptr(g), g.numel(), rate, seed, ptr(d), dtype_code(g.dtype), stream())
+        return d, None, None
+
+
+_seed_counter = itertools.count(1)
+
+
+def dropout(x, rate, training, seed=None):
+    if not training or rate == 0.0:
+        return x
+    if seed is None:
+        seed = (0x5EED << 32) + next(_seed_counter)
+    return _DropoutFn.apply(x, float(rate), int(seed))
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kh, kw):
+        N, H, W, C = x.shape
+        y = _empty((N, H // kh, W // kw, C), x.dtype, x.device)
+        call("acfe_maxpool2d", ptr(x), N, H, W, C, kh, kw, ptr(y), dtype_code(x.dtype), stream())
+        ctx.save_for_backward(x)
+        ctx.k = (kh, kw)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        kh, kw = ctx.k
+        N, H, W, C = x.shape
+        g = g.contiguous()
+        dx = torch.empty_like(x)
+        call("acfe_maxpool2d_bwd", ptr(x), ptr(g), N, H, W, C, kh, kw, ptr(dx), dtype_code(x.dtype), stream())
+        return dx, None, None
+
+
+def max_pool(x, kh, kw):
+    return _MaxPoolFn.apply(x, kh, kw)
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        N, H, W, C = x.shape
+        y = _empty((N, -(-H // k), -(-W // k), C), x.dtype, x.device)
+        call("acfe_avgpool2d", ptr(x), N, H, W, C, k, ptr(y), dtype_code(x.dtype), stream())
+        ctx.shape, ctx.k = x.shape, k
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        N, H, W, C = ctx.shape
+        g = g.contiguous()
+        dx = _empty(ctx.shape, g.dtype, g.device)
+        call("acfe_avgpool2d_bwd", ptr(g), N, H, W, C, ctx.k, ptr(dx), dtype_code(g.dtype), stream())
+        return dx, None
+
+
+def avg_pool_same(x, k):
+    return _AvgPoolFn.apply(x, k)
+
+
+class _AxisPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, outer, L, inner, sharp, mode):
+        y = _empty((outer, inner), F32, x.device)
+        call("acfe_axis_pool", ptr(x), dtype_code(x.dtype), outer, L, inner, sharp, mode, ptr(y), stream())
+        ctx.save_for_backward(x)
+        ctx.conf = (outer, L, inner, sharp, mode)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        outer, L, inner, sharp, mode = ctx.conf
+        g = g.contiguous().to(F32)
+        dx = torch.empty_like(x)
+        call("acfe_axis_pool_bwd", ptr(x), dtype_code(x.dtype), ptr(g), outer, L, inner, sharp, mode, ptr(dx),
+             stream())
+        return dx, None, None, None, None, None
+
+
+def logmeanexp(x: torch.Tensor, axis: int, sharpness: float = 5.0) -> torch.Tensor:
+    """wr_resnet_bird.logmeanexp (wr_resnet_bird.py:83-87), keepdims=False, fp32 out."""
+    shp = list(x.shape)
+    outer = 1
+    for d in shp[:axis]:
+        outer *= d
+    inner = 1
+    for d in shp[axis + 1:]:
+        inner *= d
+    y = _AxisPoolFn.apply(x.contiguous(), outer, shp[axis], inner, float(sharpness), 0)
+    return y.view(shp[:axis] + shp[axis + 1:])
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """GlobalAveragePooling2D on NHWC -> [N, C] fp32."""
+    N, H, W, C = x.shape
+    return _AxisPoolFn.apply(x.contiguous(), N, H * W, C, 1.0, 1)
+
+
+class _DenseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        B, I = x.shape
+        O = w.shape[1]
+        z = _empty((B, O), F32, x.device)
+        call("acfe_dense_fwd", ptr(x), ptr(w), ptr(b), B, I, O, ptr(z), stream())
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, w = ctx.saved_tensors
+        B, I = x.shape
+        O = w.shape[1]
+        dz = dz.contiguous()
+        dx = _empty((B, I), F32, x.device) if ctx.needs_input_grad[0] else None
+        dw = _empty((I, O), F32, x.device)
+        db = _empty((O,), F32, x.device) if ctx.has_b else None
+        call("acfe_dense_bwd", ptr(x), ptr(w), ptr(dz), B, I, O, ptr(dx), ptr(dw), ptr(db), stream())
+        return dx, dw, db
+
+
+def dense(x, w, b=None):
+    """Dense logits (the sigmoid is applied by sigmoid()/the loss)."""
+    return _DenseFn.apply(x.contiguous().to(F32), w, b)
+
+
+def sigmoid(z: torch.Tensor) -> torch.Tensor:
+    p = torch.empty_like(z)
+    call("acfe_sigmoid", ptr(z), z.numel(), ptr(p), stream())
+    return p
+
+
+LOSS_MODES = {"bce": 0, "binary": 0, "cce": 1, "categorical": 1}
+
+
+def loss_and_grad(logits: torch.Tensor, target: torch.Tensor, mode: str = "cce", grad_scale: float | None = None):
+    """Keras loss (audiomodel.loss, :1206-1223) on sigmoid(logits): returns
+    (loss[1] fp32 device tensor, dL/dlogits).  grad_scale defaults to 1/B
+    (the batch mean)."""
+    B, L = logits.shape
+    loss = _empty((1,), F32, logits.device)
+    dz = torch.empty_like(logits)
+    ws = _empty((B,), F32, logits.device)
+    gs = 1.0 / B if grad_scale is None else grad_scale
+    call("acfe_loss", ptr(logits.contiguous()), ptr(target.contiguous().to(F32)), B, L, LOSS_MODES[mode], gs, ptr(loss),
+         ptr(dz), ptr(ws), stream())
+    return loss, dz
+
+
+def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    if x.dtype == dtype:
+        return x
+    y = _empty(x.shape, dtype, x.device)
+    call("acfe_cast", ptr(x.contiguous()), dtype_code(x.dtype), x.numel(), ptr(y), dtype_code(dtype), stream())
+    return y
+
+
+class _CastFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return cast(x.contiguous(), dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return cast(g.contiguous(), ctx.src), None
+
+
+def cast_grad(x, dtype):
+    return x if x.dtype == dtype else _CastFn.apply(x, dtype)

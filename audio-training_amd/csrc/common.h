@@ -20,7 +20,7 @@ inline int hip_rc(hipError_t e, const char* where) {
 // Check a kernel launch (hipGetLastError) and convert to an ABI code.
 inline int launch_rc(const char* where) { return hip_rc(hipGetLastError(), where); }
 
-inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline hipStream_t strm(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 

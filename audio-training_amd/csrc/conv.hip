@@ -1,0 +1,1003 @@
+// Convolution engine for resnet/wr_resnet.py and resnet/wr_resnet_bird.py
+// (Keras Conv2D, NHWC, "same"/"valid", bias, KRSC weights).
+//
+//  * k_conv_fwd   implicit-im2col GEMM on MFMA: M = N*P*Q output pixels,
+//                 N = K output channels, reduction = R*S*C.  bf16 operands on
+//                 v_mfma_f32_16x16x32_bf16, or exact fp32 on v_mfma_f32_16x16x4_f32.
+//                 256 threads = 4 waves, BM=128 pixel rows x BN channels per tile,
+//                 register-staged double-buffered LDS (rows padded by 16 B so the
+//                 ds_read_b128 fragment reads are conflict-free), persistent loop
+//                 over M tiles.  Epilogue: +bias, round to the storage type,
+//                 per-channel sum / sum-of-squares of the ROUNDED outputs (the
+//                 training-mode BatchNormalization statistics of the next layer)
+//                 accumulated in double per block, tile staged in LDS and written
+//                 as 16-byte rows.
+//  * dgrad        stride 1: the same kernel on flipped/transposed weights
+//                 (W'[c][r'][s'][k] = W[k][R-1-r'][S-1-s'][c], pad' = R-1-pad);
+//                 stride > 1: zero-insert dY, then the same.
+//  * k_conv_wgrad split-K GEMM dW[k][rsc] = sum_m dY[m][k] * im2col(X)[m][rsc]
+//                 with both operands staged m-major and fed to the MFMA through
+//                 ds_read_b64_tr_b16 (bf16) -- per-split fp32 slabs, then a
+//                 deterministic reduction.
+//  * stem         C = 1 direct kernels (the 3 identical input channels of
+//                 tfdataset.py:2053 are folded into one by summing the stem
+//                 weights over Cin; exact up to fp reassociation).
+#include "common.h"
+
+using namespace acfe;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+
+struct ConvGeom {
+  int N, H, W, C;    // input
+  int K, P, Q;       // output
+  int R, S, st, pt, pl;
+  int Kd, Kdp, Kp;   // R*S*C, padded to BK, K padded to BN
+  int ldy;           // output row stride (elements)
+  long long M;       // N*P*Q
+};
+
+template <typename T> struct TT;
+template <> struct TT<uint16_t> { static constexpr int GR = 8, BK = 64; };
+template <> struct TT<float> { static constexpr int GR = 4, BK = 32; };
+
+__device__ __forceinline__ void mma(f4& acc, const uint4& a, const uint4& b, uint16_t) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), acc,
+                                                0, 0, 0);
+}
+__device__ __forceinline__ void mma(f4& acc, const uint4& a, const uint4& b, float) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+}
+__device__ __forceinline__ uint16_t cvt_out(float v, uint16_t) { return f2bf(v); }
+__device__ __forceinline__ float cvt_out(float v, float) { return v; }
+__device__ __forceinline__ float to_f(uint16_t v) { return bf2f(v); }
+__device__ __forceinline__ float to_f(float v) { return v; }
+
+template <typename T, int BM, int BN>
+constexpr int conv_smem() {
+  constexpr int LR = TT<T>::BK + TT<T>::GR;
+  constexpr int a = 2 * (BM + BN) * LR * (int)sizeof(T);
+  constexpr int b = BM * (BN + TT<T>::GR) * (int)sizeof(T);
+  constexpr int c = 2 * 2 * BN * 8;
+  return a > b ? (a > c ? a : c) : (b > c ? b : c);
+}
+
+// ------------------------------------------------------------------ forward
+template <typename T, int BM, int BN, int WM, int WN, bool FAST_A>
+__global__ void __launch_bounds__(256)
+k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const float* __restrict__ bias,
+           T* __restrict__ Y, double* __restrict__ stats, int tiles_m) {
+  constexpr int GR = TT<T>::GR, BK = TT<T>::BK, LR = BK + GR, LC = BN + GR;
+  constexpr int RA = BM / 32, RB = BN / 32;
+  constexpr int TWM = BM / WM, TWN = BN / WN, FM = TWM / 16, FN = TWN / 16;
+  constexpr int KF = 4 * GR;
+  static_assert(WM * WN == 4 && BN >= 32 && FM >= 1 && FN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[conv_smem<T, BM, BN>()];
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + 2 * BM * LR;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int gc = tid & 7, rr = tid >> 3;
+  const int n0 = blockIdx.y * BN;
+  const int nkt = g.Kdp / BK;
+  const long long PQ = (long long)g.P * g.Q;
+  double s1d[FN], s2d[FN];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) s1d[i] = s2d[i] = 0.0;
+
+  for (int tm = blockIdx.x; tm < tiles_m; tm += gridDim.x) {
+    const long long m0 = (long long)tm * BM;
+    const T* rowp[RA];
+    int h0[RA], w0[RA];
+    bool mv[RA];
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const long long m = m0 + rr + 32 * i;
+      mv[i] = m < g.M;
+      const long long mm = mv[i] ? m : 0;
+      const int n = (int)(mm / PQ);
+      const int rem = (int)(mm - (long long)n * PQ);
+      const int p = rem / g.Q, q = rem - (rem / g.Q) * g.Q;
+      h0[i] = p * g.st - g.pt;
+      w0[i] = q * g.st - g.pl;
+      rowp[i] = X + (((long long)n * g.H + h0[i]) * g.W + w0[i]) * g.C;
+    }
+    int kk0 = gc * GR, c0, r, s;
+    {
+      const int rs = kk0 / g.C;
+      c0 = kk0 - rs * g.C;
+      r = rs / g.S;
+      s = rs - r * g.S;
+    }
+    uint4 ra[RA], rb[RB];
+    auto gload = [&](int kt) {
+      if constexpr (FAST_A) {
+        const bool kv = kk0 < g.Kd;
+        const int off = (r * g.W + s) * g.C + c0;
+#pragma unroll
+        for (int i = 0; i < RA; ++i) {
+          const int h = h0[i] + r, w = w0[i] + s;
+          const bool ok = kv && mv[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+          const T* src = ok ? rowp[i] + off : X;
+          const uint4 v = *reinterpret_cast<const uint4*>(src);
+          ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < RA; ++i) {
+          T e[GR];
+#pragma unroll
+          for (int j = 0; j < GR; ++j) {
+            const int kk = kk0 + j;
+            bool ok = mv[i] && kk < g.Kd;
+            const int rs = kk / g.C, c = kk - rs * g.C, rq = rs / g.S, sq = rs - rq * g.S;
+            const int h = h0[i] + rq, w = w0[i] + sq;
+            ok = ok && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+            const T* src = ok ? rowp[i] + (rq * g.W + sq) * g.C + c : X;
+            const T v = *src;
+            e[j] = ok ? v : (T)0;
+          }
+          ra[i] = *reinterpret_cast<const uint4*>(e);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+        rb[i] = *reinterpret_cast<const uint4*>(Wp + (long long)(n0 + rr + 32 * i) * g.Kdp + kt * BK + gc * GR);
+    };
+    auto advance = [&]() {
+      kk0 += BK;
+      if constexpr (FAST_A) {
+        c0 += BK;
+        while (c0 >= g.C) {
+          c0 -= g.C;
+          if (++s == g.S) { s = 0; ++r; }
+        }
+      }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+      for (int i = 0; i < RA; ++i)
+        *reinterpret_cast<uint4*>(As + (buf * BM + rr + 32 * i) * LR + gc * GR) = ra[i];
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+        *reinterpret_cast<uint4*>(Bs + (buf * BN + rr + 32 * i) * LR + gc * GR) = rb[i];
+    };
+    f4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+    gload(0);
+    advance();
+    sstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const bool more = kt + 1 < nkt;
+      if (more) {
+        gload(kt + 1);
+        advance();
+      }
+      const int buf = kt & 1;
+#pragma unroll
+      for (int kk = 0; kk < BK / KF; ++kk) {
+        uint4 af[FM], bfr[FN];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          af[fm] = *reinterpret_cast<const uint4*>(
+              As + (buf * BM + wm * TWM + fm * 16 + (lane & 15)) * LR + kk * KF + (lane >> 4) * GR);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          bfr[fn] = *reinterpret_cast<const uint4*>(
+              Bs + (buf * BN + wn * TWN + fn * 16 + (lane & 15)) * LR + kk * KF + (lane >> 4) * GR);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], af[fm], bfr[fn], T());
+      }
+      if (more) sstore(buf ^ 1);
+      __syncthreads();
+    }
+    // ---- epilogue
+    T* Cs = As;
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int col = wn * TWN + fn * 16 + (lane & 15);
+      const int gcn = n0 + col;
+      const float bv = (bias && gcn < g.K) ? bias[gcn] : 0.f;
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = wm * TWM + fm * 16 + (lane >> 4) * 4 + j;
+          const T tv = cvt_out(acc[fm][fn][j] + bv, T());
+          Cs[row * LC + col] = tv;
+          if (m0 + row < g.M) {
+            const float f = to_f(tv);
+            t1 += f;
+            t2 += f * f;
+          }
+        }
+      s1d[fn] += t1;
+      s2d[fn] += t2;
+    }
+    __syncthreads();
+    constexpr int GPR = BN / GR;
+    if (n0 + BN <= g.K && (g.ldy % GR) == 0) {
+      for (int idx = tid; idx < BM * GPR; idx += 256) {
+        const int row = idx / GPR, cg = idx - (idx / GPR) * GPR;
+        const long long m = m0 + row;
+        if (m < g.M)
+          *reinterpret_cast<uint4*>(Y + m * g.ldy + n0 + cg * GR) =
+              *reinterpret_cast<const uint4*>(Cs + row * LC + cg * GR);
+      }
+    } else {
+      for (int idx = tid; idx < BM * BN; idx += 256) {
+        const int row = idx / BN, col = idx - (idx / BN) * BN;
+        const long long m = m0 + row;
+        if (m < g.M && n0 + col < g.K) Y[m * g.ldy + n0 + col] = Cs[row * LC + col];
+      }
+    }
+    __syncthreads();
+  }
+  if (stats) {
+    double* red = reinterpret_cast<double*>(smem);  // [WM][2][BN]
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      double a = s1d[fn], b = s2d[fn];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (lane < 16) {
+        const int col = wn * TWN + fn * 16 + lane;
+        red[(wm * 2 + 0) * BN + col] = a;
+        red[(wm * 2 + 1) * BN + col] = b;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        a += red[(w * 2 + 0) * BN + c];
+        b += red[(w * 2 + 1) * BN + c];
+      }
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + n0 + c] = a;
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + n0 + c] = b;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ weight packing
+// forward:  out[k][(r*S+s)*C + c] = w[k][r][s][c]      (KRSC, zero-padded to [Kp][Kdp])
+// flipped:  out[c][(r*S+s)*K + k] = w[k][R-1-r][S-1-s][c]   (dgrad operand)
+template <typename T>
+__global__ void k_pack_w(const float* __restrict__ w, int K, int R, int S, int C, int flip, int rows_p,
+                         int cols_p, T* __restrict__ out) {
+  const long long total = (long long)rows_p * cols_p;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int row = (int)(i / cols_p), col = (int)(i - (i / cols_p) * cols_p);
+    float v = 0.f;
+    if (!flip) {
+      if (row < K && col < R * S * C) v = w[(long long)row * R * S * C + col];
+    } else {
+      if (row < C && col < R * S * K) {
+        const int k = col % K, rs = col / K, r = rs / S, s = rs % S;
+        v = w[(((long long)k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + row];
+      }
+    }
+    out[i] = cvt_out(v, T());
+  }
+}
+
+// ------------------------------------------------------------------ zero insertion (strided dgrad)
+template <typename T>
+__global__ void k_zero_insert(const T* __restrict__ dy, int N, int P, int Q, int K, int st, int Hu, int Wu,
+                              T* __restrict__ out) {
+  const long long total = (long long)N * Hu * Wu * K;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int k = (int)(i % K);
+    long long t = i / K;
+    const int w = (int)(t % Wu);
+    t /= Wu;
+    const int h = (int)(t % Hu);
+    const int n = (int)(t / Hu);
+    T v = (T)0;
+    if (h % st == 0 && w % st == 0 && h / st < P && w / st < Q)
+      v = dy[(((long long)n * P + h / st) * Q + w / st) * K + k];
+    out[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------ wgrad
+// Block: 256 threads; output tile BMW (k rows) x 128 (rsc cols); reduction over
+// a contiguous chunk of m in steps of 32.  LDS images are m-major:
+// Ds[32][BMW + 16], Xs[32][128 + 16].
+template <typename T, int BMW, bool FAST_D, bool FAST_X>
+__global__ void __launch_bounds__(256)
+k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, float* __restrict__ ws,
+             long long chunk) {
+  constexpr int GR = TT<T>::GR, BNW = 128, BR = 32;
+  constexpr int LDD = BMW + 16, LDX = BNW + 16;
+  constexpr int WM = BMW >= 64 ? 2 : 1, WN = 4 / WM;
+  constexpr int TWM = BMW / WM, TWN = BNW / WN, FM = TWM / 16, FN = TWN / 16;
+  constexpr int DG = BR * BMW / GR, XG = BR * BNW / GR;  // granules per stage
+  constexpr int DPT = (DG + 255) / 256, XPT = XG / 256;
+  static_assert(XG % 256 == 0, "x tile");
+  __shared__ __attribute__((aligned(16))) T Ds[2][BR * LDD];
+  __shared__ __attribute__((aligned(16))) T Xs[2][BR * LDX];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int k0 = blockIdx.y * BMW, c0blk = blockIdx.x * BNW;
+  const long long mbeg = (long long)blockIdx.z * chunk;
+  long long mend = mbeg + chunk;
+  if (mend > g.M) mend = g.M;
+  const int nsteps = mbeg < mend ? (int)((mend - mbeg + BR - 1) / BR) : 0;
+  const long long PQ = (long long)g.P * g.Q;
+
+  // X loader: thread -> XPT (row, col-granule) pairs; fixed col granule, rows advance by 32
+  constexpr int XGPR = BNW / GR;
+  int xrow[XPT], xr[XPT], xs[XPT], xc[XPT], xn[XPT], xp[XPT], xq[XPT];
+  bool xkv[XPT];
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int idx = tid + 256 * i;
+    xrow[i] = idx / XGPR;
+    const int cg = idx - xrow[i] * XGPR;
+    const int kk = c0blk + cg * GR;
+    xkv[i] = kk < g.Kd;
+    const int kkc = xkv[i] ? kk : 0;
+    const int rs = kkc / g.C;
+    xc[i] = kkc - rs * g.C;
+    xr[i] = rs / g.S;
+    xs[i] = rs - xr[i] * g.S;
+    const long long m = mbeg + xrow[i];
+    const int n = (int)(m / PQ);
+    const int rem = (int)(m - (long long)n * PQ);
+    xn[i] = n;
+    xp[i] = rem / g.Q;
+    xq[i] = rem - xp[i] * g.Q;
+  }
+  constexpr int DGPR = BMW / GR;
+  uint4 rd[DPT], rx[XPT];
+  auto gload = [&](int step) {
+    const long long mb = mbeg + (long long)step * BR;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / DGPR, cg = idx - (idx / DGPR) * DGPR;
+      const long long m = mb + row;
+      const bool ok = idx < DG && m < mend;
+      if constexpr (FAST_D) {
+        const bool okk = ok && (k0 + cg * GR) < g.K;
+        const T* src = okk ? dY + m * g.ldy + k0 + cg * GR : dY;
+        const uint4 v = *reinterpret_cast<const uint4*>(src);
+        rd[i] = okk ? v : make_uint4(0, 0, 0, 0);
+      } else {
+        T e[GR];
+#pragma unroll
+        for (int j = 0; j < GR; ++j) {
+          const int k = k0 + cg * GR + j;
+          const bool okk = ok && k < g.K;
+          const T v = *(okk ? dY + m * g.ldy + k : dY);
+          e[j] = okk ? v : (T)0;
+        }
+        rd[i] = *reinterpret_cast<const uint4*>(e);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const long long m = mb + xrow[i];
+      const int h = xp[i] * g.st - g.pt + xr[i], w = xq[i] * g.st - g.pl + xs[i];
+      const bool ok = xkv[i] && m < mend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      if constexpr (FAST_X) {
+        const T* src = ok ? X + (((long long)xn[i] * g.H + h) * g.W + w) * g.C + xc[i] : X;
+        const uint4 v = *reinterpret_cast<const uint4*>(src);
+        rx[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      } else {
+        T e[GR];
+        const int cg = (tid + 256 * i) - xrow[i] * XGPR;
+#pragma unroll
+        for (int j = 0; j < GR; ++j) {
+          const int kk = c0blk + cg * GR + j;
+          bool okj = kk < g.Kd && m < mend;
+          const int rs = kk / g.C, c = kk - rs * g.C, rq = rs / g.S, sq = rs - rq * g.S;
+          const int hh = xp[i] * g.st - g.pt + rq, ww = xq[i] * g.st - g.pl + sq;
+          okj = okj && (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+          const T v = *(okj ? X + (((long long)xn[i] * g.H + hh) * g.W + ww) * g.C + c : X);
+          e[j] = okj ? v : (T)0;
+        }
+        rx[i] = *reinterpret_cast<const uint4*>(e);
+      }
+    }
+  };
+  auto advance = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      xq[i] += BR;
+      while (xq[i] >= g.Q) {
+        xq[i] -= g.Q;
+        if (++xp[i] == g.P) { xp[i] = 0; ++xn[i]; }
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < DG) {
+        const int row = idx / DGPR, cg = idx - (idx / DGPR) * DGPR;
+        *reinterpret_cast<uint4*>(&Ds[buf][row * LDD + cg * GR]) = rd[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 256 * i;
+      const int cg = idx - xrow[i] * XGPR;
+      *reinterpret_cast<uint4*>(&Xs[buf][xrow[i] * LDX + cg * GR]) = rx[i];
+    }
+  };
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  if (nsteps > 0) {
+    gload(0);
+    advance();
+    sstore(0);
+  }
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const bool more = step + 1 < nsteps;
+    if (more) {
+      gload(step + 1);
+      advance();
+    }
+    const int buf = step & 1;
+    if constexpr (sizeof(T) == 2) {
+      // MFMA k-slot (g = lane>>4, j) <-> m: j<4: 4g+j, j>=4: 16+4g+(j-4)
+      const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+      bf8 af[FM], bfr[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int col = wm * TWM + fm * 16 + 4 * p;
+        typedef __attribute__((address_space(3))) bf4* lp;
+        const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(&Ds[buf][(4 * grp + q) * LDD + col])));
+        const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(&Ds[buf][(16 + 4 * grp + q) * LDD + col])));
+        af[fm] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int col = wn * TWN + fn * 16 + 4 * p;
+        typedef __attribute__((address_space(3))) bf4* lp;
+        const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(&Xs[buf][(4 * grp + q) * LDX + col])));
+        const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(&Xs[buf][(16 + 4 * grp + q) * LDX + col])));
+        bfr[fn] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int k4 = 0; k4 < BR / 4; ++k4) {
+        const int mrow = k4 * 4 + (lane >> 4);
+        float a[FM], b[FN];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          a[fm] = reinterpret_cast<const float*>(Ds[buf])[mrow * LDD + wm * TWM + fm * 16 + (lane & 15)];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          b[fn] = reinterpret_cast<const float*>(Xs[buf])[mrow * LDX + wn * TWN + fn * 16 + (lane & 15)];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn)
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
+      }
+    }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  // partial slab: ws[z][k][kk] (k < K, kk < Kd)
+  float* out = ws + (long long)blockIdx.z * g.K * g.Kd;
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + wm * TWM + fm * 16 + (lane >> 4) * 4 + j;
+        const int kk = c0blk + wn * TWN + fn * 16 + (lane & 15);
+        if (k < g.K && kk < g.Kd) out[(long long)k * g.Kd + kk] = acc[fm][fn][j];
+      }
+}
+
+// sum of split slabs -> dW (optionally accumulated, optionally replicated over
+// `rep` input channels for the folded stem)
+__global__ void k_wgrad_reduce(const float* __restrict__ ws, int nsplit, long long n, float beta,
+                               float* __restrict__ dw) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < nsplit; ++z) s += ws[(long long)z * n + i];
+    dw[i] = beta != 0.f ? dw[i] * beta + s : s;
+  }
+}
+
+// ------------------------------------------------------------------ host side
+static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int st, int pt, int pl, int P,
+                          int Q, int BK, int BN) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.P = P; g.Q = Q;
+  g.R = R; g.S = S; g.st = st; g.pt = pt; g.pl = pl;
+  g.Kd = R * S * C;
+  g.Kdp = (g.Kd + BK - 1) / BK * BK;
+  g.Kp = (K + BN - 1) / BN * BN;
+  g.ldy = K;
+  g.M = (long long)N * P * Q;
+  return g;
+}
+
+static int pick_bn(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
+
+template <typename T, int BN, int WM, int WN>
+static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
+                        double* stats, int grid_m, hipStream_t s) {
+  const int tiles_m = (int)((g.M + 127) / 128);
+  dim3 grid(grid_m, g.Kp / BN);
+  if (g.C % TT<T>::GR == 0)
+    hipLaunchKernelGGL((k_conv_fwd<T, 128, BN, WM, WN, true>), grid, dim3(256), 0, s, g, (const T*)x,
+                       (const T*)wp, bias, (T*)y, stats, tiles_m);
+  else
+    hipLaunchKernelGGL((k_conv_fwd<T, 128, BN, WM, WN, false>), grid, dim3(256), 0, s, g, (const T*)x,
+                       (const T*)wp, bias, (T*)y, stats, tiles_m);
+  return launch_rc("acfe_conv2d_fwd");
+}
+
+template <typename T>
+static int launch_fwd(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
+                      double* stats, int grid_m, hipStream_t s) {
+  const int bn = pick_bn(g.K);
+  if (bn == 32) return launch_fwd_t<T, 32, 4, 1>(g, x, wp, bias, y, stats, grid_m, s);
+  if (bn == 64) return launch_fwd_t<T, 64, 2, 2>(g, x, wp, bias, y, stats, grid_m, s);
+  return launch_fwd_t<T, 128, 2, 2>(g, x, wp, bias, y, stats, grid_m, s);
+}
+
+static int grid_m_for(long long M, int ny) {
+  const long long tiles = (M + 127) / 128;
+  long long gm = 2048 / ny;
+  if (gm < 1) gm = 1;
+  return (int)(tiles < gm ? tiles : gm);
+}
+
+// Packed-weight geometry so callers can size buffers: rows_p x cols_p.
+ACFE_API int acfe_conv2d_packed_shape(int K, int R, int S, int C, int dtype, int flip, int* rows_p,
+                                      int* cols_p) {
+  if (K <= 0 || R <= 0 || S <= 0 || C <= 0 || !rows_p || !cols_p || (dtype != 0 && dtype != 1))
+    return ACFE_E_INVAL;
+  const int BK = dtype == ACFE_DTYPE_BF16 ? 64 : 32;
+  const int outc = flip ? C : K, red = R * S * (flip ? K : C);
+  const int bn = pick_bn(outc);
+  *rows_p = (outc + bn - 1) / bn * bn;
+  *cols_p = (red + BK - 1) / BK * BK;
+  return ACFE_OK;
+}
+
+ACFE_API int acfe_conv2d_pack_weights(const float* w, int K, int R, int S, int C, int dtype, int flip,
+                                      void* out, void* stream) {
+  int rp, cp;
+  int rc = acfe_conv2d_packed_shape(K, R, S, C, dtype, flip, &rp, &cp);
+  if (rc) return rc;
+  if (!w || !out) return ACFE_E_INVAL;
+  const long long total = (long long)rp * cp;
+  int grid = cdiv(total, 256);
+  if (grid > 4096) grid = 4096;
+  if (dtype == ACFE_DTYPE_BF16)
+    hipLaunchKernelGGL(k_pack_w<uint16_t>, dim3(grid), dim3(256), 0, strm(stream), w, K, R, S, C, flip, rp, cp,
+                       (uint16_t*)out);
+  else
+    hipLaunchKernelGGL(k_pack_w<float>, dim3(grid), dim3(256), 0, strm(stream), w, K, R, S, C, flip, rp, cp,
+                       (float*)out);
+  return launch_rc("acfe_conv2d_pack_weights");
+}
+
+ACFE_API int acfe_conv2d_stats_rows(long long M, int K) {
+  return grid_m_for(M, (K + pick_bn(K) - 1) / pick_bn(K));
+}
+
+ACFE_API int acfe_conv2d_fwd(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R,
+                             int S, int stride, int pad_top, int pad_left, int P, int Q,
+                             const float* bias, void* y, int dtype, double* stats_partial,
+                             void* stream) {
+  if (!x || !wpacked || !y || N < 0 || H <= 0 || W <= 0 || C <= 0 || K <= 0 || R <= 0 || S <= 0 ||
+      stride <= 0 || P <= 0 || Q <= 0 || (dtype != 0 && dtype != 1))
+    return ACFE_E_INVAL;
+  if (N == 0) return ACFE_OK;
+  const int BK = dtype == ACFE_DTYPE_BF16 ? 64 : 32;
+  const int bn = pick_bn(K);
+  ConvGeom g = make_geom(N, H, W, C, K, R, S, stride, pad_top, pad_left, P, Q, BK, bn);
+  const int gm = grid_m_for(g.M, g.Kp / bn);
+  if (dtype == ACFE_DTYPE_BF16) return launch_fwd<uint16_t>(g, x, wpacked, bias, y, stats_partial, gm, strm(stream));
+  return launch_fwd<float>(g, x, wpacked, bias, y, stats_partial, gm, strm(stream));
+}
+
+// dX = conv^T(dY, W).  wflip = acfe_conv2d_pack_weights(..., flip=1).
+// workspace: for stride > 1, device buffer of N*Hu*Wu*K elements of dtype with
+// Hu = (P-1)*stride + 1, Wu = (Q-1)*stride + 1 (NULL allowed for stride 1).
+ACFE_API int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R,
+                               int S, int stride, int pad_top, int pad_left, int H, int W, void* dx,
+                               int dtype, void* workspace, void* stream) {
+  if (!dy || !wflip || !dx || N < 0 || P <= 0 || Q <= 0 || K <= 0 || C <= 0 || stride <= 0 ||
+      (dtype != 0 && dtype != 1))
+    return ACFE_E_INVAL;
+  if (N == 0) return ACFE_OK;
+  const void* src = dy;
+  int Hs = P, Ws = Q;
+  if (stride > 1) {
+    if (!workspace) return ACFE_E_INVAL;
+    const int Hu = (P - 1) * stride + 1, Wu = (Q - 1) * stride + 1;
+    const long long total = (long long)N * Hu * Wu * K;
+    int grid = cdiv(total, 256);
+    if (grid > 8192) grid = 8192;
+    if (dtype == ACFE_DTYPE_BF16)
+      hipLaunchKernelGGL(k_zero_insert<uint16_t>, dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)dy, N, P,
+                         Q, K, stride, Hu, Wu, (uint16_t*)workspace);
+    else
+      hipLaunchKernelGGL(k_zero_insert<float>, dim3(grid), dim3(256), 0, strm(stream), (const float*)dy, N, P, Q, K,
+                         stride, Hu, Wu, (float*)workspace);
+    int rc = launch_rc("acfe_conv2d_dgrad(zero_insert)");
+    if (rc) return rc;
+    src = workspace;
+    Hs = Hu;
+    Ws = Wu;
+  }
+  // stride-1 conv of (upsampled) dY with flipped weights: input channels K, output C
+  return acfe_conv2d_fwd(src, N, Hs, Ws, K, wflip, C, R, S, 1, R - 1 - pad_top, S - 1 - pad_left, H, W,
+                         nullptr, dx, dtype, nullptr, stream);
+}
+
+ACFE_API long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q) {
+  const long long M = (long long)N * P * Q;
+  const int kd = R * S * C;
+  const int bmw = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
+  const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
+  long long splits = (1024 + tiles - 1) / tiles;
+  long long chunk = (M + splits - 1) / splits;
+  chunk = (chunk + 31) / 32 * 32;
+  if (chunk < 512) chunk = 512;
+  splits = (M + chunk - 1) / chunk;
+  if (splits < 1) splits = 1;
+  return splits * K * kd;  // floats
+}
+
+template <typename T, int BMW>
+static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, float* ws, long long chunk,
+                          int splits, hipStream_t s) {
+  dim3 grid((g.Kd + 127) / 128, (g.K + BMW - 1) / BMW, splits);
+  const bool fd = g.K % TT<T>::GR == 0, fx = g.C % TT<T>::GR == 0;
+#define WG(FD, FX)                                                                                       \
+  hipLaunchKernelGGL((k_conv_wgrad<T, BMW, FD, FX>), grid, dim3(256), 0, s, g, (const T*)x, (const T*)dy, \
+                     ws, chunk)
+  if (fd && fx) WG(true, true);
+  else if (fd) WG(true, false);
+  else if (fx) WG(false, true);
+  else WG(false, false);
+#undef WG
+  return launch_rc("acfe_conv2d_wgrad");
+}
+
+// dW[k][r][s][c] (fp32, KRSC) = sum over pixels.  beta: dW = beta*dW + grad.
+ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy, int K, int R, int S,
+                               int stride, int pad_top, int pad_left, int P, int Q, float* dw, float beta,
+                               int dtype, float* workspace, void* stream) {
+  if (!x || !dy || !dw || !workspace || N < 0 || C <= 0 || K <= 0 || (dtype != 0 && dtype != 1))
+    return ACFE_E_INVAL;
+  const long long M = (long long)N * P * Q;
+  const int kd = R * S * C;
+  if (N == 0) return hip_rc(hipMemsetAsync(dw, 0, sizeof(float) * K * kd, strm(stream)), "wgrad");
+  const int bmw = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
+  const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
+  long long splits = (1024 + tiles - 1) / tiles;
+  long long chunk = (M + splits - 1) / splits;
+  chunk = (chunk + 31) / 32 * 32;
+  if (chunk < 512) chunk = 512;
+  splits = (M + chunk - 1) / chunk;
+  if (splits < 1) splits = 1;
+  ConvGeom g = make_geom(N, H, W, C, K, R, S, stride, pad_top, pad_left, P, Q, 64, 128);
+  g.ldy = K;
+  int rc;
+  if (dtype == ACFE_DTYPE_BF16) {
+    if (bmw == 32) rc = launch_wgrad_t<uint16_t, 32>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+    else if (bmw == 64) rc = launch_wgrad_t<uint16_t, 64>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+    else rc = launch_wgrad_t<uint16_t, 128>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+  } else {
+    if (bmw == 32) rc = launch_wgrad_t<float, 32>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+    else if (bmw == 64) rc = launch_wgrad_t<float, 64>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+    else rc = launch_wgrad_t<float, 128>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+  }
+  if (rc) return rc;
+  const long long n = (long long)K * kd;
+  int grid = cdiv(n, 256);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, strm(stream), workspace, (int)splits, n, beta, dw);
+  return launch_rc("acfe_conv2d_wgrad(reduce)");
+}
+
+// ------------------------------------------------------------------ stem (C = 1)
+// y[n,h,w,k] = sum_{r,s} x[n, h - pt + r, w - pl + s] * weff[k][r][s] + b[k]
+// (stride 1, P = H, Q = W).  Tile: 8 rows x 64 cols per block iteration.
+constexpr int STEM_TH = 8, STEM_TW = 64, STEM_K = 16, STEM_MAXR = 7;
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int R, int S, int pt, int pl,
+           const float* __restrict__ weff, const float* __restrict__ bias, TO* __restrict__ y,
+           double* __restrict__ stats, int tiles_h, int tiles_w) {
+  __shared__ float xs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1)];
+  __shared__ float wsm[STEM_K * STEM_MAXR * STEM_MAXR];
+  __shared__ double red[4][2][STEM_K];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < STEM_K * R * S; i += 256) wsm[i] = weff[i];
+  const int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1;
+  const long long ntiles = (long long)N * tiles_h * tiles_w;
+  double s1[2] = {0, 0}, s2[2] = {0, 0};  // thread owns channels (tid & 7) and (tid & 7) + 8
+  const int kq = tid & 7;
+  float b0 = bias ? bias[kq] : 0.f, b1 = bias ? bias[kq + 8] : 0.f;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tw = (int)(t % tiles_w);
+    const int th = (int)((t / tiles_w) % tiles_h);
+    const int n = (int)(t / ((long long)tiles_w * tiles_h));
+    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+    __syncthreads();
+    for (int i = tid; i < XH * XW; i += 256) {
+      const int yy = i / XW, xx = i - (i / XW) * XW;
+      const int h = h0 - pt + yy, w = w0 - pl + xx;
+      float v = 0.f;
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = to_f(x[((long long)n * H + h) * W + w]);
+      xs[i] = v;
+    }
+    __syncthreads();
+    // thread -> pixel pix = tid >> 3 + 32*j (j < 16), channels kq, kq+8
+    for (int j = 0; j < STEM_TH * STEM_TW / 32; ++j) {
+      const int pix = (tid >> 3) + 32 * j;
+      const int py = pix / STEM_TW, px = pix - (pix / STEM_TW) * STEM_TW;
+      const int h = h0 + py, w = w0 + px;
+      float a0 = 0.f, a1 = 0.f;
+      for (int r = 0; r < R; ++r)
+        for (int s = 0; s < S; ++s) {
+          const float xv = xs[(py + r) * XW + px + s];
+          a0 += xv * wsm[(kq * R + r) * S + s];
+          a1 += xv * wsm[((kq + 8) * R + r) * S + s];
+        }
+      if (h < H && w < W) {
+        const TO o0 = cvt_out(a0 + b0, TO()), o1 = cvt_out(a1 + b1, TO());
+        TO* dst = y + (((long long)n * H + h) * W + w) * STEM_K;
+        dst[kq] = o0;
+        dst[kq + 8] = o1;
+        const float f0 = to_f(o0), f1 = to_f(o1);
+        s1[0] += f0; s2[0] += (double)f0 * f0;
+        s1[1] += f1; s2[1] += (double)f1 * f1;
+      }
+    }
+  }
+  if (stats) {
+    // reduce over the 8 lanes-groups sharing kq within each wave, then waves
+    for (int o = 8; o < 64; o <<= 1) {
+      s1[0] += __shfl_xor(s1[0], o, 64); s1[1] += __shfl_xor(s1[1], o, 64);
+      s2[0] += __shfl_xor(s2[0], o, 64); s2[1] += __shfl_xor(s2[1], o, 64);
+    }
+    const int lane = tid & 63, wid = tid >> 6;
+    if (lane < 8) {
+      red[wid][0][lane] = s1[0]; red[wid][0][lane + 8] = s1[1];
+      red[wid][1][lane] = s2[0]; red[wid][1][lane + 8] = s2[1];
+    }
+    __syncthreads();
+    if (tid < 2 * STEM_K) {
+      const int which = tid / STEM_K, k = tid % STEM_K;
+      stats[((long long)blockIdx.x * 2 + which) * STEM_K + k] =
+          red[0][which][k] + red[1][which][k] + red[2][which][k] + red[3][which][k];
+    }
+  }
+}
+
+// dx[n,h,w] = sum_{k,r,s} dy[n, h + pt - r, w + pl - s, k] * weff[k][r][s]
+template <typename TG, typename TO>
+__global__ void __launch_bounds__(256)
+k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int R, int S, int pt, int pl,
+             const float* __restrict__ weff, TO* __restrict__ dx, int tiles_h, int tiles_w) {
+  __shared__ float gs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1) * STEM_K];
+  __shared__ float wsm[STEM_K * STEM_MAXR * STEM_MAXR];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < STEM_K * R * S; i += 256) wsm[i] = weff[i];
+  const int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1;
+  const long long ntiles = (long long)N * tiles_h * tiles_w;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tw = (int)(t % tiles_w);
+    const int th = (int)((t / tiles_w) % tiles_h);
+    const int n = (int)(t / ((long long)tiles_w * tiles_h));
+    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+    // gs covers dy rows h0 - (R-1-pt) .. , cols w0 - (S-1-pl) ..
+    const int gh0 = h0 - (R - 1 - pt), gw0 = w0 - (S - 1 - pl);
+    __syncthreads();
+    for (int i = tid; i < XH * XW * STEM_K; i += 256) {
+      const int k = i % STEM_K, pos = i / STEM_K;
+      const int yy = pos / XW, xx = pos - (pos / XW) * XW;
+      const int h = gh0 + yy, w = gw0 + xx;
+      float v = 0.f;
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+        v = to_f(dy[(((long long)n * H + h) * W + w) * STEM_K + k]);
+      gs[i] = v;
+    }
+    __syncthreads();
+    for (int pix = tid; pix < STEM_TH * STEM_TW; pix += 256) {
+      const int py = pix / STEM_TW, px = pix - (pix / STEM_TW) * STEM_TW;
+      const int h = h0 + py, w = w0 + px;
+      float a = 0.f;
+      // dy row = h + pt - r  -> gs row = py + (R-1-pt) + pt - r = py + R-1-r
+      for (int r = 0; r < R; ++r)
+        for (int s = 0; s < S; ++s) {
+          const float* gp = &gs[((py + R - 1 - r) * XW + px + S - 1 - s) * STEM_K];
+#pragma unroll
+          for (int k = 0; k < STEM_K; ++k) a += gp[k] * wsm[(k * R + r) * S + s];
+        }
+      if (h < H && w < W) dx[((long long)n * H + h) * W + w] = cvt_out(a, TO());
+    }
+  }
+}
+
+// dweff[k][r][s] partials per block: thread -> (k = tid & 15, pixel group = tid >> 4)
+template <typename TI, typename TG>
+__global__ void __launch_bounds__(256)
+k_stem_wgrad(const TI* __restrict__ x, const TG* __restrict__ dy, int N, int H, int W, int R, int S, int pt,
+             int pl, double* __restrict__ part, int tiles_h, int tiles_w) {
+  __shared__ float xs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1)];
+  __shared__ float red[16][STEM_K * STEM_MAXR * STEM_MAXR + 1];
+  const int tid = threadIdx.x, k = tid & 15, pg = tid >> 4;
+  const int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1;
+  float acc[STEM_MAXR * STEM_MAXR];
+  for (int i = 0; i < R * S; ++i) acc[i] = 0.f;
+  double accd[STEM_MAXR * STEM_MAXR];
+  for (int i = 0; i < R * S; ++i) accd[i] = 0.0;
+  const long long ntiles = (long long)N * tiles_h * tiles_w;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tw = (int)(t % tiles_w);
+    const int th = (int)((t / tiles_w) % tiles_h);
+    const int n = (int)(t / ((long long)tiles_w * tiles_h));
+    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+    __syncthreads();
+    for (int i = tid; i < XH * XW; i += 256) {
+      const int yy = i / XW, xx = i - (i / XW) * XW;
+      const int h = h0 - pt + yy, w = w0 - pl + xx;
+      float v = 0.f;
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = to_f(x[((long long)n * H + h) * W + w]);
+      xs[i] = v;
+    }
+    __syncthreads();
+    for (int pix = pg; pix < STEM_TH * STEM_TW; pix += 16) {
+      const int py = pix / STEM_TW, px = pix - (pix / STEM_TW) * STEM_TW;
+      const int h = h0 + py, w = w0 + px;
+      if (h >= H || w >= W) continue;
+      const float g = to_f(dy[(((long long)n * H + h) * W + w) * STEM_K + k]);
+      for (int r = 0; r < R; ++r)
+        for (int s = 0; s < S; ++s) acc[r * S + s] += g * xs[(py + r) * XW + px + s];
+    }
+    for (int i = 0; i < R * S; ++i) {
+      accd[i] += acc[i];
+      acc[i] = 0.f;
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < R * S; ++i) red[pg][k * R * S + i] = (float)accd[i];
+  __syncthreads();
+  for (int i = tid; i < STEM_K * R * S; i += 256) {
+    double s = 0.0;
+    for (int j = 0; j < 16; ++j) s += red[j][i];
+    part[(long long)blockIdx.x * STEM_K * R * S + i] = s;
+  }
+}
+
+__global__ void k_stem_wgrad_reduce(const double* __restrict__ part, int np, int n, int rep, float beta,
+                                    float* __restrict__ dw) {
+  // dw layout [K][R][S][rep] (KRSC with C = rep copies of the folded channel)
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    double s = 0.0;
+    for (int j = 0; j < np; ++j) s += part[(long long)j * n + i];
+    for (int c = 0; c < rep; ++c) {
+      float* d = dw + (long long)i * rep + c;
+      *d = beta != 0.f ? *d * beta + (float)s : (float)s;
+    }
+  }
+}
+
+__global__ void k_stem_fold(const float* __restrict__ w, int n, int rep, float* __restrict__ weff) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    float s = 0.f;
+    for (int c = 0; c < rep; ++c) s += w[(long long)i * rep + c];
+    weff[i] = s;
+  }
+}
+
+ACFE_API int acfe_stem_blocks(int N, int H, int W) {
+  const long long t = (long long)N * ((H + STEM_TH - 1) / STEM_TH) * ((W + STEM_TW - 1) / STEM_TW);
+  return (int)(t < 2048 ? t : 2048);
+}
+
+// weff[k][r][s] = sum_c w[k][r][s][c]  (folds the identical input channels)
+ACFE_API int acfe_stem_fold_weights(const float* w, int K, int R, int S, int C, float* weff, void* stream) {
+  if (!w || !weff || K != STEM_K || R > STEM_MAXR || S > STEM_MAXR || C <= 0) return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_stem_fold, dim3(cdiv(K * R * S, 256)), dim3(256), 0, strm(stream), w, K * R * S, C, weff);
+  return launch_rc("acfe_stem_fold_weights");
+}
+
+ACFE_API int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int R, int S, int pad_top,
+                           int pad_left, const float* weff, const float* bias, void* y, int y_dtype,
+                           double* stats_partial, void* stream) {
+  if (!x || !weff || !y || N < 0 || H <= 0 || W <= 0 || R > STEM_MAXR || S > STEM_MAXR || R <= 0 || S <= 0)
+    return ACFE_E_INVAL;
+  if (N == 0) return ACFE_OK;
+  const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
+  const int grid = acfe_stem_blocks(N, H, W);
+#define SF(TI, TO)                                                                                          \
+  hipLaunchKernelGGL((k_stem_fwd<TI, TO>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x, N, H, W, R, S, \
+                     pad_top, pad_left, weff, bias, (TO*)y, stats_partial, th, tw)
+  if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16) SF(uint16_t, uint16_t);
+  else if (x_dtype == ACFE_DTYPE_BF16) SF(uint16_t, float);
+  else if (y_dtype == ACFE_DTYPE_BF16) SF(float, uint16_t);
+  else SF(float, float);
+#undef SF
+  return launch_rc("acfe_stem_fwd");
+}
+
+ACFE_API int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, int R, int S, int pad_top,
+                             int pad_left, const float* weff, void* dx, int dx_dtype, void* stream) {
+  if (!dy || !weff || !dx || N < 0 || R > STEM_MAXR || S > STEM_MAXR) return ACFE_E_INVAL;
+  if (N == 0) return ACFE_OK;
+  const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
+  const int grid = acfe_stem_blocks(N, H, W);
+#define SD(TG, TO)                                                                                           \
+  hipLaunchKernelGGL((k_stem_dgrad<TG, TO>), dim3(grid), dim3(256), 0, strm(stream), (const TG*)dy, N, H, W, R, S, \
+                     pad_top, pad_left, weff, (TO*)dx, th, tw)
+  if (dy_dtype == ACFE_DTYPE_BF16 && dx_dtype == ACFE_DTYPE_BF16) SD(uint16_t, uint16_t);
+  else if (dy_dtype == ACFE_DTYPE_BF16) SD(uint16_t, float);
+  else if (dx_dtype == ACFE_DTYPE_BF16) SD(float, uint16_t);
+  else SD(float, float);
+#undef SD
+  return launch_rc("acfe_stem_dgrad");
+}
+
+// workspace: double[acfe_stem_blocks(N,H,W) * 16 * R * S]
+ACFE_API int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, int N, int H, int W,
+                             int R, int S, int pad_top, int pad_left, int rep, float* dw, float beta,
+                             double* workspace, void* stream) {
+  if (!x || !dy || !dw || !workspace || N <= 0 || R > STEM_MAXR || S > STEM_MAXR || rep <= 0)
+    return ACFE_E_INVAL;
+  const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
+  const int grid = acfe_stem_blocks(N, H, W);
+#define SW(TI, TG)                                                                                          \
+  hipLaunchKernelGGL((k_stem_wgrad<TI, TG>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x, (const TG*)dy, \
+                     N, H, W, R, S, pad_top, pad_left, workspace, th, tw)
+  if (x_dtype == ACFE_DTYPE_BF16 && dy_dtype == ACFE_DTYPE_BF16) SW(uint16_t, uint16_t);
+  else if (x_dtype == ACFE_DTYPE_BF16) SW(uint16_t, float);
+  else if (dy_dtype == ACFE_DTYPE_BF16) SW(float, uint16_t);
+  else SW(float, float);
+#undef SW
+  int rc = launch_rc("acfe_stem_wgrad");
+  if (rc) return rc;
+  const int n = STEM_K * R * S;
+  hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3(cdiv(n, 256)), dim3(256), 0, strm(stream), workspace, grid, n, rep,
+                     beta, dw);
+  return launch_rc("acfe_stem_wgrad(reduce)");
+}

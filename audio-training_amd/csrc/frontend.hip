@@ -118,7 +118,7 @@ ACFE_API int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmi
   acfe_plan_s* p = new acfe_plan_s();
   p->sr = sr; p->n_fft = n_fft; p->hop = hop; p->n_mels = n_mels; p->n_bins = nb;
   p->kmin = kmin; p->kmax = kmax;
-  hipGetDevice(&p->device);
+  (void)hipGetDevice(&p->device);
   hipError_t e = hipSuccess;
   e = e ? e : hipMalloc(&p->d_tw, sizeof(float2) * nc);
   e = e ? e : hipMalloc(&p->d_rtw, sizeof(float2) * (nc + 1));
@@ -140,7 +140,7 @@ ACFE_API int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmi
 
 ACFE_API int acfe_plan_destroy(acfe_plan_t p) {
   if (!p) return ACFE_E_INVAL;
-  hipFree(p->d_tw); hipFree(p->d_rtw); hipFree(p->d_win); hipFree(p->d_band); hipFree(p->d_vals);
+  (void)hipFree(p->d_tw); (void)hipFree(p->d_rtw); (void)hipFree(p->d_win); (void)hipFree(p->d_band); (void)hipFree(p->d_vals);
   delete p;
   return ACFE_OK;
 }
@@ -189,7 +189,7 @@ ACFE_API int acfe_normalize_stats(const float* x, int64_t cs, int batch, int n, 
   if (batch == 0 && n > 0) return ACFE_OK;
   if (!x || !stats || batch < 0 || n <= 0) return ACFE_E_INVAL;
   if (batch == 0) return ACFE_OK;
-  hipLaunchKernelGGL(k_norm_stats, dim3(batch), dim3(256), 0, S(stream), x, cs, n, stats);
+  hipLaunchKernelGGL(k_norm_stats, dim3(batch), dim3(256), 0, strm(stream), x, cs, n, stats);
   return launch_rc("acfe_normalize_stats");
 }
 
@@ -205,7 +205,7 @@ ACFE_API int acfe_normalize_apply(const float* x, int64_t cs, int batch, int n, 
                                   float* y, void* stream) {
   if (!x || !stats || !y || batch < 0 || n <= 0 || batch > 65535) return ACFE_E_INVAL;
   if (batch == 0) return ACFE_OK;
-  hipLaunchKernelGGL(k_norm_apply, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, S(stream), x, cs,
+  hipLaunchKernelGGL(k_norm_apply, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, strm(stream), x, cs,
                      n, stats, y);
   return launch_rc("acfe_normalize_apply");
 }
@@ -229,7 +229,7 @@ ACFE_API int acfe_mixup(const float* x1, const float* s1, const float* x2, const
                         const float* lam, int batch, int n, float* y, void* stream) {
   if (!x1 || !x2 || !lam || !y || batch < 0 || n <= 0 || batch > 65535) return ACFE_E_INVAL;
   if (batch == 0) return ACFE_OK;
-  hipLaunchKernelGGL(k_mixup, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, S(stream), x1, s1, x2,
+  hipLaunchKernelGGL(k_mixup, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, strm(stream), x1, s1, x2,
                      s2, lam, n, y);
   return launch_rc("acfe_mixup");
 }
@@ -422,7 +422,7 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   const int fpb = 4;
   dim3 grid(cdiv(T, fpb), batch);
 #define LAUNCH_MEL(NC)                                                                          \
-  hipLaunchKernelGGL(k_mel<NC>, grid, dim3(256), 0, S(stream), raw, cs, n, stats, pad_mode,     \
+  hipLaunchKernelGGL(k_mel<NC>, grid, dim3(256), 0, strm(stream), raw, cs, n, stats, pad_mode,     \
                      power, T, fpb, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,  \
                      p->n_mels, p->kmin, p->kmax, out, layout)
   switch (p->n_fft) {
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(256) k_pcen_fwd(const float* __restrict__ mel,
 ACFE_API int acfe_pcen_fwd(const float* mel, int batch, int t, int m, const float* params, float eps,
                            float* y, float* part, void* stream) {
   if (!mel || !params || !y || !part || batch <= 0 || t <= 0 || m <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_pcen_fwd, dim3(acfe_pcen_partials(batch, m)), dim3(256), 0, S(stream), mel,
+  hipLaunchKernelGGL(k_pcen_fwd, dim3(acfe_pcen_partials(batch, m)), dim3(256), 0, strm(stream), mel,
                      batch, t, m, params, eps, y, part);
   return launch_rc("acfe_pcen_fwd");
 }
@@ -572,11 +572,11 @@ ACFE_API int acfe_pcen_normalize(const float* y, int64_t count, const float* par
                                  void* stream) {
   if (!y || !out || !stats || count <= 0 || (!part && !scope) || (dtype != 0 && dtype != 1))
     return ACFE_E_INVAL;
-  int rc = hip_rc(hipMemsetAsync(stats, 0, 4 * sizeof(float), S(stream)), "acfe_pcen_normalize");
+  int rc = hip_rc(hipMemsetAsync(stats, 0, 4 * sizeof(float), strm(stream)), "acfe_pcen_normalize");
   if (rc) return rc;
   int grid = cdiv(count, 256 * 8);
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(k_pcen_norm, dim3(grid), dim3(256), 0, S(stream), y, count, part, np, scope,
+  hipLaunchKernelGGL(k_pcen_norm, dim3(grid), dim3(256), 0, strm(stream), y, count, part, np, scope,
                      out, dtype, stats);
   return launch_rc("acfe_pcen_normalize");
 }
@@ -699,11 +699,11 @@ ACFE_API int acfe_pcen_bwd(const float* mel, int batch, int t, int m, const floa
     return ACFE_E_INVAL;
   const int np = acfe_pcen_partials(batch, m);
   double* part = reinterpret_cast<double*>(ws);
-  hipLaunchKernelGGL(k_pcen_bwd, dim3(np), dim3(256), 0, S(stream), mel, batch, t, m, params, eps,
+  hipLaunchKernelGGL(k_pcen_bwd, dim3(np), dim3(256), 0, strm(stream), mel, batch, t, m, params, eps,
                      stats, dout, ddt, part);
   int rc = launch_rc("acfe_pcen_bwd");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_pcen_bwd_fin, dim3(1), dim3(64), 0, S(stream), part, np, params, stats,
+  hipLaunchKernelGGL(k_pcen_bwd_fin, dim3(1), dim3(64), 0, strm(stream), part, np, params, stats,
                      dparams);
   return launch_rc("acfe_pcen_bwd_fin");
 }

@@ -1,0 +1,743 @@
+// Layer kernels around the convolutions of resnet/wr_resnet*.py:
+//   BatchNormalization (Keras: axis=3, eps 1e-3, momentum 0.99, batch stats in
+//   training, biased variance), ReLU, Add, Dropout, MaxPool2D, AveragePooling2D,
+//   log-mean-exp pooling (wr_resnet_bird.py:83-87), GlobalAveragePooling2D,
+//   Dense(+sigmoid), BCE / CCE losses (audiomodel.py:1206-1223) and Adam
+//   (audiomodel.py:1226-1240, Keras defaults b1 .9, b2 .999, eps 1e-7).
+// Activations are NHWC, bf16 or fp32 ("dtype" codes of acfe.h); per-channel
+// parameters and statistics are fp32; cross-block reductions go through
+// double-precision partial slabs reduced in a fixed order (deterministic).
+#include "common.h"
+
+using namespace acfe;
+
+template <typename T> __device__ __forceinline__ float ld(const T* p, long long i);
+template <> __device__ __forceinline__ float ld<uint16_t>(const uint16_t* p, long long i) { return bf2f(p[i]); }
+template <> __device__ __forceinline__ float ld<float>(const float* p, long long i) { return p[i]; }
+template <typename T> __device__ __forceinline__ void st(T* p, long long i, float v);
+template <> __device__ __forceinline__ void st<uint16_t>(uint16_t* p, long long i, float v) { p[i] = f2bf(v); }
+template <> __device__ __forceinline__ void st<float>(float* p, long long i, float v) { p[i] = v; }
+
+#define DISPATCH1(dt, T, ...)                                   \
+  do {                                                          \
+    if ((dt) == ACFE_DTYPE_BF16) { typedef uint16_t T; __VA_ARGS__; } \
+    else { typedef float T; __VA_ARGS__; }                      \
+  } while (0)
+
+static int grid_for(long long n, int per = 256, int cap = 8192) {
+  long long g = (n + per - 1) / per;
+  if (g < 1) g = 1;
+  return (int)(g < cap ? g : cap);
+}
+
+// Partial-slab row count used by every per-channel reduction below.
+static int red_blocks(long long rows) {
+  long long b = (rows + 255) / 256;
+  return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
+}
+ACFE_API int acfe_reduce_blocks(long long rows) { return red_blocks(rows); }
+
+// ---------------------------------------------------------------- BN statistics
+// part[blk][2][C] = {sum x, sum x^2} over the block's rows (double)
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_stats(const T* __restrict__ x, long long rows, int C,
+                                                  double* __restrict__ part) {
+  extern __shared__ double red[];  // [2][C]
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+  __syncthreads();
+  // thread -> channel c = tid % C' chunks; rows strided
+  const long long r0 = (long long)blockIdx.x * ((rows + gridDim.x - 1) / gridDim.x);
+  long long r1 = r0 + (rows + gridDim.x - 1) / gridDim.x;
+  if (r1 > rows) r1 = rows;
+  const int tpr = C < 256 ? C : 256;  // threads per row slice
+  const int rpp = 256 / tpr;          // rows per pass
+  const int c_base = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  if (rsub < rpp) {
+    for (int c = c_base; c < C; c += tpr) {
+      double s1 = 0.0, s2 = 0.0;
+      float f1 = 0.f, f2 = 0.f;
+      int cnt = 0;
+      for (long long r = r0 + rsub; r < r1; r += rpp) {
+        const float v = ld(x, r * C + c);
+        f1 += v;
+        f2 += v * v;
+        if (++cnt == 256) { s1 += f1; s2 += f2; f1 = f2 = 0.f; cnt = 0; }
+      }
+      s1 += f1;
+      s2 += f2;
+      atomicAdd(&red[c], s1);
+      atomicAdd(&red[C + c], s2);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
+}
+
+ACFE_API int acfe_bn_stats(const void* x, long long rows, int C, int dtype, double* part, void* stream) {
+  if (!x || !part || rows <= 0 || C <= 0 || C > 2048) return ACFE_E_INVAL;
+  const int nb = red_blocks(rows);
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_bn_stats<T>, dim3(nb), dim3(256), 2 * C * sizeof(double),
+                                         strm(stream), (const T*)x, rows, C, part));
+  return launch_rc("acfe_bn_stats");
+}
+
+// part: [nrows][2][ld] (ld >= C; conv epilogues use the padded K as ld)
+// out (each fp32[C], any may be NULL except scale/shift):
+//   scale = gamma * invstd, shift = beta - mean * scale, mean, invstd
+// training: batch statistics + moving-average update (momentum); else moving stats.
+__global__ void k_bn_finalize(const double* __restrict__ part, int nrows, int ld, int C, double count,
+                              const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                              float momentum, float* __restrict__ mmean, float* __restrict__ mvar, int training,
+                              float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_o,
+                              float* __restrict__ invstd_o) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  double mean, var;
+  if (training) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int r = 0; r < nrows; ++r) {
+      s1 += part[((long long)r * 2 + 0) * ld + c];
+      s2 += part[((long long)r * 2 + 1) * ld + c];
+    }
+    mean = s1 / count;
+    var = s2 / count - mean * mean;
+    if (var < 0) var = 0;
+    if (mmean) mmean[c] = (float)(mmean[c] * (double)momentum + mean * (1.0 - momentum));
+    if (mvar) mvar[c] = (float)(mvar[c] * (double)momentum + var * (1.0 - momentum));
+  } else {
+    mean = mmean[c];
+    var = mvar[c];
+  }
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  const double g = gamma ? gamma[c] : 1.0, b = beta ? beta[c] : 0.0;
+  const double sc = g * inv;
+  scale[c] = (float)sc;
+  shift[c] = (float)(b - mean * sc);
+  if (mean_o) mean_o[c] = (float)mean;
+  if (invstd_o) invstd_o[c] = (float)inv;
+}
+
+ACFE_API int acfe_bn_finalize(const double* part, int nrows, int ld, int C, double count, const float* gamma,
+                              const float* beta, float eps, float momentum, float* moving_mean,
+                              float* moving_var, int training, float* scale, float* shift, float* mean,
+                              float* invstd, void* stream) {
+  if (!scale || !shift || C <= 0 || (training && (!part || nrows <= 0 || count <= 0)) ||
+      (!training && (!moving_mean || !moving_var)))
+    return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 64)), dim3(64), 0, strm(stream), part, nrows, ld, C, count, gamma,
+                     beta, eps, momentum, moving_mean, moving_var, training, scale, shift, mean, invstd);
+  return launch_rc("acfe_bn_finalize");
+}
+
+// y = x*scale[c] + shift[c] (+ReLU)
+template <typename TI, typename TO>
+__global__ void k_bn_apply(const TI* __restrict__ x, long long n, int C, const float* __restrict__ scale,
+                           const float* __restrict__ shift, int relu, TO* __restrict__ y) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    float v = ld(x, i) * scale[c] + shift[c];
+    if (relu) v = fmaxf(v, 0.f);
+    st(y, i, v);
+  }
+}
+
+ACFE_API int acfe_bn_apply(const void* x, int x_dtype, long long rows, int C, const float* scale,
+                           const float* shift, int relu, void* y, int y_dtype, void* stream) {
+  if (!x || !y || !scale || !shift || rows < 0 || C <= 0) return ACFE_E_INVAL;
+  const long long n = rows * C;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(x_dtype, TI, DISPATCH1(y_dtype, TO,
+      hipLaunchKernelGGL((k_bn_apply<TI, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream), (const TI*)x, n, C,
+                         scale, shift, relu, (TO*)y)));
+  return launch_rc("acfe_bn_apply");
+}
+
+// Backward reduce: g = dy * (relu ? [x*scale+shift > 0] : 1); xhat = (x-mean)*invstd
+// part[blk][2][C] = {sum g, sum g*xhat}
+template <typename TG, typename TX>
+__global__ void __launch_bounds__(256) k_bn_bwd_reduce(const TG* __restrict__ dy, const TX* __restrict__ x,
+                                                       long long rows, int C, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, int relu,
+                                                       double* __restrict__ part) {
+  extern __shared__ double red[];
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+  __syncthreads();
+  const long long per = (rows + gridDim.x - 1) / gridDim.x;
+  const long long r0 = (long long)blockIdx.x * per;
+  long long r1 = r0 + per;
+  if (r1 > rows) r1 = rows;
+  const int tpr = C < 256 ? C : 256;
+  const int rpp = 256 / tpr;
+  const int c_base = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  if (rsub < rpp) {
+    for (int c = c_base; c < C; c += tpr) {
+      const float sc = scale[c], sh = shift[c], mu = mean[c], is = invstd[c];
+      double s1 = 0.0, s2 = 0.0;
+      float f1 = 0.f, f2 = 0.f;
+      int cnt = 0;
+      for (long long r = r0 + rsub; r < r1; r += rpp) {
+        const float xv = ld(x, r * C + c);
+        float g = ld(dy, r * C + c);
+        if (relu && !(xv * sc + sh > 0.f)) g = 0.f;
+        f1 += g;
+        f2 += g * ((xv - mu) * is);
+        if (++cnt == 256) { s1 += f1; s2 += f2; f1 = f2 = 0.f; cnt = 0; }
+      }
+      s1 += f1;
+      s2 += f2;
+      atomicAdd(&red[c], s1);
+      atomicAdd(&red[C + c], s2);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
+}
+
+ACFE_API int acfe_bn_bwd_reduce(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                                const float* scale, const float* shift, const float* mean, const float* invstd,
+                                int relu, double* part, void* stream) {
+  if (!dy || !x || !scale || !shift || !mean || !invstd || !part || rows <= 0 || C <= 0 || C > 2048)
+    return ACFE_E_INVAL;
+  const int nb = red_blocks(rows);
+  DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX,
+      hipLaunchKernelGGL((k_bn_bwd_reduce<TG, TX>), dim3(nb), dim3(256), 2 * C * sizeof(double), strm(stream),
+                         (const TG*)dy, (const TX*)x, rows, C, scale, shift, mean, invstd, relu, part)));
+  return launch_rc("acfe_bn_bwd_reduce");
+}
+
+// coef[3][C] = {a, b, c} with dx = a*g + b*x + c; dgamma = sum g xhat, dbeta = sum g
+__global__ void k_bn_bwd_finalize(const double* __restrict__ part, int nrows, int C, double count,
+                                  const float* __restrict__ scale, const float* __restrict__ mean,
+                                  const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                  float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int r = 0; r < nrows; ++r) {
+    sg += part[((long long)r * 2 + 0) * C + c];
+    sgx += part[((long long)r * 2 + 1) * C + c];
+  }
+  if (dgamma) dgamma[c] = (float)sgx;
+  if (dbeta) dbeta[c] = (float)sg;
+  const double sc = scale[c], is = invstd[c], mu = mean[c];
+  const double mg = sg / count, mgx = sgx / count;
+  coef[c] = (float)sc;
+  coef[C + c] = (float)(-sc * mgx * is);
+  coef[2 * C + c] = (float)(-sc * mg + sc * mgx * is * mu);
+}
+
+ACFE_API int acfe_bn_bwd_finalize(const double* part, int nrows, int C, double count, const float* scale,
+                                  const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                  float* coef, void* stream) {
+  if (!part || !scale || !mean || !invstd || !coef || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(64), 0, strm(stream), part, nrows, C, count, scale,
+                     mean, invstd, dgamma, dbeta, coef);
+  return launch_rc("acfe_bn_bwd_finalize");
+}
+
+// dx = a*g + b*x + c  (+ add[i] if add != NULL); g relu-masked as in the reduce
+template <typename TG, typename TX, typename TO>
+__global__ void k_bn_bwd_apply(const TG* __restrict__ dy, const TX* __restrict__ x, long long n, int C,
+                               const float* __restrict__ scale, const float* __restrict__ shift, int relu,
+                               const float* __restrict__ coef, const TO* __restrict__ add, TO* __restrict__ dx) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const float xv = ld(x, i);
+    float g = ld(dy, i);
+    if (relu && !(xv * scale[c] + shift[c] > 0.f)) g = 0.f;
+    float v = coef[c] * g + coef[C + c] * xv + coef[2 * C + c];
+    if (add) v += ld(add, i);
+    st(dx, i, v);
+  }
+}
+
+ACFE_API int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                               const float* scale, const float* shift, int relu, const float* coef,
+                               const void* add, void* dx, int dx_dtype, void* stream) {
+  if (!dy || !x || !scale || !shift || !coef || !dx || rows < 0 || C <= 0) return ACFE_E_INVAL;
+  const long long n = rows * C;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
+      hipLaunchKernelGGL((k_bn_bwd_apply<TG, TX, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                         (const TG*)dy, (const TX*)x, n, C, scale, shift, relu, coef, (const TO*)add, (TO*)dx))));
+  return launch_rc("acfe_bn_bwd_apply");
+}
+
+// ---------------------------------------------------------------- elementwise
+// z = a + b (+ReLU)
+template <typename T>
+__global__ void k_add(const T* __restrict__ a, const T* __restrict__ b, long long n, int relu, T* __restrict__ z) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float v = ld(a, i) + ld(b, i);
+    if (relu) v = fmaxf(v, 0.f);
+    st(z, i, v);
+  }
+}
+ACFE_API int acfe_add(const void* a, const void* b, long long n, int relu, void* z, int dtype, void* stream) {
+  if (!a || !b || !z || n < 0) return ACFE_E_INVAL;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_add<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream), (const T*)a,
+                                         (const T*)b, n, relu, (T*)z));
+  return launch_rc("acfe_add");
+}
+
+// dx = dy * [y > 0]
+template <typename T>
+__global__ void k_relu_bwd(const T* __restrict__ dy, const T* __restrict__ y, long long n, T* __restrict__ dx) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    st(dx, i, ld(y, i) > 0.f ? ld(dy, i) : 0.f);
+}
+ACFE_API int acfe_relu_bwd(const void* dy, const void* y, long long n, void* dx, int dtype, void* stream) {
+  if (!dy || !y || !dx || n < 0) return ACFE_E_INVAL;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_relu_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                         (const T*)dy, (const T*)y, n, (T*)dx));
+  return launch_rc("acfe_relu_bwd");
+}
+
+// Dropout (tf.keras.layers.Dropout: keep with prob 1-rate, scale 1/(1-rate)).
+// Mask = hash(seed, i) >= rate * 2^32, regenerated in the backward.
+template <typename T>
+__global__ void k_dropout(const T* __restrict__ x, long long n, float rate, unsigned long long seed,
+                          T* __restrict__ y) {
+  const uint32_t thr = (uint32_t)fminf(rate * 4294967296.0f, 4294967295.0f);
+  const float scl = 1.0f / (1.0f - rate);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const bool keep = hash_u32(seed, (uint64_t)i) >= thr;
+    st(y, i, keep ? ld(x, i) * scl : 0.f);
+  }
+}
+ACFE_API int acfe_dropout(const void* x, long long n, float rate, unsigned long long seed, void* y, int dtype,
+                          void* stream) {
+  if (!x || !y || n < 0 || rate < 0.f || rate >= 1.f) return ACFE_E_INVAL;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_dropout<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                         (const T*)x, n, rate, seed, (T*)y));
+  return launch_rc("acfe_dropout");
+}
+
+// ---------------------------------------------------------------- pooling (NHWC)
+// MaxPool2D(pool=(kh,kw), strides=pool, padding="valid")
+template <typename T>
+__global__ void k_maxpool(const T* __restrict__ x, int N, int H, int W, int C, int kh, int kw, int P, int Q,
+                          T* __restrict__ y) {
+  const long long n_out = (long long)N * P * Q * C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_out; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float m = -INFINITY;
+    for (int a = 0; a < kh; ++a)
+      for (int b = 0; b < kw; ++b)
+        m = fmaxf(m, ld(x, (((long long)n * H + p * kh + a) * W + q * kw + b) * C + c));
+    st(y, i, m);
+  }
+}
+// gradient to the FIRST maximum of each window (row-major), 0 elsewhere
+template <typename T>
+__global__ void k_maxpool_bwd(const T* __restrict__ x, const T* __restrict__ dy, int N, int H, int W, int C, int kh,
+                              int kw, int P, int Q, T* __restrict__ dx) {
+  const long long n_in = (long long)N * H * W * C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_in; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    const int p = h / kh, q = w / kw;
+    float g = 0.f;
+    if (p < P && q < Q) {
+      float m = -INFINITY;
+      int am = 0;
+      for (int a = 0; a < kh; ++a)
+        for (int b = 0; b < kw; ++b) {
+          const float v = ld(x, (((long long)n * H + p * kh + a) * W + q * kw + b) * C + c);
+          if (v > m) { m = v; am = a * kw + b; }
+        }
+      if (am == (h - p * kh) * kw + (w - q * kw)) g = ld(dy, (((long long)n * P + p) * Q + q) * C + c);
+    }
+    st(dx, i, g);
+  }
+}
+ACFE_API int acfe_maxpool2d(const void* x, int N, int H, int W, int C, int kh, int kw, void* y, int dtype,
+                            void* stream) {
+  if (!x || !y || N < 0 || kh <= 0 || kw <= 0 || H < kh || W < kw) return ACFE_E_INVAL;
+  const int P = H / kh, Q = W / kw;
+  const long long n = (long long)N * P * Q * C;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_maxpool<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream), (const T*)x,
+                                         N, H, W, C, kh, kw, P, Q, (T*)y));
+  return launch_rc("acfe_maxpool2d");
+}
+ACFE_API int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int W, int C, int kh, int kw,
+                                void* dx, int dtype, void* stream) {
+  if (!x || !dy || !dx || N < 0 || kh <= 0 || kw <= 0) return ACFE_E_INVAL;
+  const int P = H / kh, Q = W / kw;
+  const long long n = (long long)N * H * W * C;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_maxpool_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                         (const T*)x, (const T*)dy, N, H, W, C, kh, kw, P, Q, (T*)dx));
+  return launch_rc("acfe_maxpool2d_bwd");
+}
+
+// AveragePooling2D(pool=k, strides=k, padding="same"): P = ceil(H/k); TF pads
+// (total = (P-1)*k + k - H) with pad_top = total/2 and averages over the
+// in-bounds elements only.
+template <typename T>
+__global__ void k_avgpool(const T* __restrict__ x, int N, int H, int W, int C, int k, int P, int Q, int pt, int pl,
+                          T* __restrict__ y) {
+  const long long n_out = (long long)N * P * Q * C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_out; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float s = 0.f;
+    int cnt = 0;
+    for (int a = 0; a < k; ++a)
+      for (int b = 0; b < k; ++b) {
+        const int h = p * k - pt + a, w = q * k - pl + b;
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+          s += ld(x, (((long long)n * H + h) * W + w) * C + c);
+          ++cnt;
+        }
+      }
+    st(y, i, s / (float)cnt);
+  }
+}
+template <typename T>
+__global__ void k_avgpool_bwd(const T* __restrict__ dy, int N, int H, int W, int C, int k, int P, int Q, int pt,
+                              int pl, T* __restrict__ dx) {
+  const long long n_in = (long long)N * H * W * C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_in; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    const int p = (h + pt) / k, q = (w + pl) / k;
+    float g = 0.f;
+    if (p < P && q < Q) {
+      int cnt = 0;
+      for (int a = 0; a < k; ++a)
+        for (int b = 0; b < k; ++b) {
+          const int hh = p * k - pt + a, ww = q * k - pl + b;
+          cnt += ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) ? 1 : 0;
+        }
+      g = ld(dy, (((long long)n * P + p) * Q + q) * C + c) / (float)cnt;
+    }
+    st(dx, i, g);
+  }
+}
+ACFE_API int acfe_avgpool2d(const void* x, int N, int H, int W, int C, int k, void* y, int dtype, void* stream) {
+  if (!x || !y || N < 0 || k <= 0) return ACFE_E_INVAL;
+  const int P = (H + k - 1) / k, Q = (W + k - 1) / k;
+  const int pt = ((P - 1) * k + k - H) / 2, pl = ((Q - 1) * k + k - W) / 2;
+  const long long n = (long long)N * P * Q * C;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_avgpool<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream), (const T*)x,
+                                         N, H, W, C, k, P, Q, pt, pl, (T*)y));
+  return launch_rc("acfe_avgpool2d");
+}
+ACFE_API int acfe_avgpool2d_bwd(const void* dy, int N, int H, int W, int C, int k, void* dx, int dtype,
+                                void* stream) {
+  if (!dy || !dx || N < 0 || k <= 0) return ACFE_E_INVAL;
+  const int P = (H + k - 1) / k, Q = (W + k - 1) / k;
+  const int pt = ((P - 1) * k + k - H) / 2, pl = ((Q - 1) * k + k - W) / 2;
+  const long long n = (long long)N * H * W * C;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_avgpool_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                         (const T*)dy, N, H, W, C, k, P, Q, pt, pl, (T*)dx));
+  return launch_rc("acfe_avgpool2d_bwd");
+}
+
+// ---------------------------------------------------------------- log-mean-exp / mean pooling
+// x viewed as [outer][L][inner] -> y [outer][inner] fp32:
+//   mode 0 (LME, wr_resnet_bird.py:83-87): (logsumexp(s*x) - log L) / s
+//   mode 1 (mean, GlobalAveragePooling2D per axis): sum x / L
+template <typename T>
+__global__ void k_axis_pool(const T* __restrict__ x, long long outer, int L, int inner, float s, int mode,
+                            float* __restrict__ y) {
+  const long long n = outer * inner;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long o = i / inner;
+    const int in = (int)(i % inner);
+    const T* xp = x + o * (long long)L * inner + in;
+    if (mode == 0) {
+      float m = -INFINITY;
+      for (int l = 0; l < L; ++l) m = fmaxf(m, s * ld(xp, (long long)l * inner));
+      float acc = 0.f;
+      for (int l = 0; l < L; ++l) acc += expf(s * ld(xp, (long long)l * inner) - m);
+      y[i] = (m + logf(acc) - logf((float)L)) / s;
+    } else {
+      float acc = 0.f;
+      for (int l = 0; l < L; ++l) acc += ld(xp, (long long)l * inner);
+      y[i] = acc / (float)L;
+    }
+  }
+}
+// dx = dy * softmax(s*x) along L (LME) or dy / L (mean)
+template <typename T>
+__global__ void k_axis_pool_bwd(const T* __restrict__ x, const float* __restrict__ dy, long long outer, int L,
+                                int inner, float s, int mode, T* __restrict__ dx) {
+  const long long n = outer * inner;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long o = i / inner;
+    const int in = (int)(i % inner);
+    const long long base = o * (long long)L * inner + in;
+    const float g = dy[i];
+    if (mode == 0) {
+      float m = -INFINITY;
+      for (int l = 0; l < L; ++l) m = fmaxf(m, s * ld(x, base + (long long)l * inner));
+      float acc = 0.f;
+      for (int l = 0; l < L; ++l) acc += expf(s * ld(x, base + (long long)l * inner) - m);
+      const float inv = 1.f / acc;
+      for (int l = 0; l < L; ++l) {
+        const long long j = base + (long long)l * inner;
+        st(dx, j, g * expf(s * ld(x, j) - m) * inv);
+      }
+    } else {
+      for (int l = 0; l < L; ++l) st(dx, base + (long long)l * inner, g / (float)L);
+    }
+  }
+}
+ACFE_API int acfe_axis_pool(const void* x, int x_dtype, long long outer, int L, int inner, float sharpness,
+                            int mode, float* y, void* stream) {
+  if (!x || !y || outer < 0 || L <= 0 || inner <= 0 || (mode == 0 && sharpness == 0.f)) return ACFE_E_INVAL;
+  const long long n = outer * inner;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(x_dtype, T, hipLaunchKernelGGL(k_axis_pool<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                           (const T*)x, outer, L, inner, sharpness, mode, y));
+  return launch_rc("acfe_axis_pool");
+}
+ACFE_API int acfe_axis_pool_bwd(const void* x, int x_dtype, const float* dy, long long outer, int L, int inner,
+                                float sharpness, int mode, void* dx, void* stream) {
+  if (!x || !dy || !dx || outer < 0 || L <= 0 || inner <= 0) return ACFE_E_INVAL;
+  const long long n = outer * inner;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(x_dtype, T, hipLaunchKernelGGL(k_axis_pool_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                           (const T*)x, dy, outer, L, inner, sharpness, mode, (T*)dx));
+  return launch_rc("acfe_axis_pool_bwd");
+}
+
+// ---------------------------------------------------------------- Dense (+sigmoid) and losses
+// z[b][o] = sum_i x[b][i] * w[i][o] + bias[o]   (Keras kernel layout [in][out])
+__global__ void k_dense(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                        int B, int I, int O, float* __restrict__ z) {
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < B * O; t += gridDim.x * 256) {
+    const int b = t / O, o = t % O;
+    float acc = bias ? bias[o] : 0.f;
+    for (int i = 0; i < I; ++i) acc += x[(long long)b * I + i] * w[(long long)i * O + o];
+    z[t] = acc;
+  }
+}
+ACFE_API int acfe_dense_fwd(const float* x, const float* w, const float* bias, int B, int I, int O, float* z,
+                            void* stream) {
+  if (!x || !w || !z || B < 0 || I <= 0 || O <= 0) return ACFE_E_INVAL;
+  if (B == 0) return ACFE_OK;
+  hipLaunchKernelGGL(k_dense, dim3(grid_for((long long)B * O)), dim3(256), 0, strm(stream), x, w, bias, B, I, O, z);
+  return launch_rc("acfe_dense_fwd");
+}
+// dx = dz w^T ; dw = x^T dz ; db = sum_b dz   (dw/db overwritten)
+__global__ void k_dense_bwd_x(const float* __restrict__ dz, const float* __restrict__ w, int B, int I, int O,
+                              float* __restrict__ dx) {
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < B * I; t += gridDim.x * 256) {
+    const int b = t / I, i = t % I;
+    float acc = 0.f;
+    for (int o = 0; o < O; ++o) acc += dz[(long long)b * O + o] * w[(long long)i * O + o];
+    dx[t] = acc;
+  }
+}
+__global__ void k_dense_bwd_w(const float* __restrict__ x, const float* __restrict__ dz, int B, int I, int O,
+                              float* __restrict__ dw, float* __restrict__ db) {
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < (I + 1) * O; t += gridDim.x * 256) {
+    const int i = t / O, o = t % O;
+    double acc = 0.0;
+    if (i < I) {
+      for (int b = 0; b < B; ++b) acc += (double)x[(long long)b * I + i] * dz[(long long)b * O + o];
+      dw[t] = (float)acc;
+    } else if (db) {
+      for (int b = 0; b < B; ++b) acc += dz[(long long)b * O + o];
+      db[o] = (float)acc;
+    }
+  }
+}
+ACFE_API int acfe_dense_bwd(const float* x, const float* w, const float* dz, int B, int I, int O, float* dx,
+                            float* dw, float* db, void* stream) {
+  if (!x || !w || !dz || !dw || B < 0 || I <= 0 || O <= 0) return ACFE_E_INVAL;
+  if (dx && B > 0)
+    hipLaunchKernelGGL(k_dense_bwd_x, dim3(grid_for((long long)B * I)), dim3(256), 0, strm(stream), dz, w, B, I, O,
+                       dx);
+  hipLaunchKernelGGL(k_dense_bwd_w, dim3(grid_for((long long)(I + 1) * O)), dim3(256), 0, strm(stream), x, dz, B, I,
+                     O, dw, db);
+  return launch_rc("acfe_dense_bwd");
+}
+
+// Loss on Dense(sigmoid) outputs; z = logits [B][L], y = targets.
+//  mode 0 BCE (tf.keras.losses.BinaryCrossentropy on a sigmoid output, computed
+//         from the logits: max(z,0) - z*y + log1p(exp(-|z|)), mean over L then B)
+//  mode 1 CCE (tf.keras.losses.CategoricalCrossentropy, from_logits=False:
+//         q = p / sum p, clip to [1e-7, 1-1e-7], -sum y log q, mean over B)
+// Writes loss[0] (mean over the batch) and dz = dL/dz.  One block per row.
+__global__ void __launch_bounds__(256) k_loss(const float* __restrict__ z, const float* __restrict__ y, int B,
+                                              int L, int mode, float inv_scale, float* __restrict__ row_loss,
+                                              float* __restrict__ dz) {
+  const int b = blockIdx.x;
+  __shared__ float red[4];
+  __shared__ float sh[2];
+  const float* zr = z + (long long)b * L;
+  const float* yr = y + (long long)b * L;
+  float* dr = dz + (long long)b * L;
+  if (mode == 0) {
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < L; i += 256) {
+      const float zz = zr[i], yy = yr[i];
+      acc += fmaxf(zz, 0.f) - zz * yy + log1pf(expf(-fabsf(zz)));
+      const float p = 1.f / (1.f + expf(-zz));
+      dr[i] = (p - yy) / (float)L * inv_scale;
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) row_loss[b] = (red[0] + red[1] + red[2] + red[3]) / (float)L;
+  } else {
+    float sp = 0.f;
+    for (int i = threadIdx.x; i < L; i += 256) sp += 1.f / (1.f + expf(-zr[i]));
+    sp = wave_sum(sp);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sp;
+    __syncthreads();
+    const float S = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    const float lo = 1e-7f, hi = 1.f - 1e-7f;
+    float acc = 0.f, gq = 0.f;
+    for (int i = threadIdx.x; i < L; i += 256) {
+      const float p = 1.f / (1.f + expf(-zr[i]));
+      const float q = p / S;
+      const float qc = fminf(fmaxf(q, lo), hi);
+      acc += -yr[i] * logf(qc);
+      const float g = (q >= lo && q <= hi) ? -yr[i] / qc : 0.f;  // dL/dq
+      gq += g * q;
+    }
+    acc = wave_sum(acc);
+    gq = wave_sum(gq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) sh[0] = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = gq;
+    __syncthreads();
+    if (threadIdx.x == 0) sh[1] = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    const float sgq = sh[1];
+    for (int i = threadIdx.x; i < L; i += 256) {
+      const float p = 1.f / (1.f + expf(-zr[i]));
+      const float q = p / S;
+      const float qc = fminf(fmaxf(q, lo), hi);
+      const float g = (q >= lo && q <= hi) ? -yr[i] / qc : 0.f;
+      const float dp = (g - sgq) / S;  // dL/dp_j = (g_j - sum_i g_i q_i) / S
+      dr[i] = dp * p * (1.f - p) * inv_scale;
+    }
+    if (threadIdx.x == 0) row_loss[b] = sh[0];
+  }
+}
+__global__ void k_mean(const float* __restrict__ v, int n, float* __restrict__ out) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += v[i];
+  acc = wave_sumd(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (float)((red[0] + red[1] + red[2] + red[3]) / n);
+}
+// workspace: float[B]; grad_scale multiplies dz (e.g. 1/B for a batch mean)
+ACFE_API int acfe_loss(const float* z, const float* y, int B, int L, int mode, float grad_scale, float* loss,
+                       float* dz, float* workspace, void* stream) {
+  if (!z || !y || !loss || !dz || !workspace || B <= 0 || L <= 0 || (mode != 0 && mode != 1))
+    return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_loss, dim3(B), dim3(256), 0, strm(stream), z, y, B, L, mode, grad_scale, workspace, dz);
+  int rc = launch_rc("acfe_loss");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_mean, dim3(1), dim3(256), 0, strm(stream), workspace, B, loss);
+  return launch_rc("acfe_loss(mean)");
+}
+
+__global__ void k_sigmoid(const float* __restrict__ z, long long n, float* __restrict__ p) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    p[i] = 1.f / (1.f + expf(-z[i]));
+}
+ACFE_API int acfe_sigmoid(const float* z, long long n, float* p, void* stream) {
+  if (!z || !p || n < 0) return ACFE_E_INVAL;
+  if (n == 0) return ACFE_OK;
+  hipLaunchKernelGGL(k_sigmoid, dim3(grid_for(n)), dim3(256), 0, strm(stream), z, n, p);
+  return launch_rc("acfe_sigmoid");
+}
+
+// ---------------------------------------------------------------- Adam (Keras 3)
+// m += (g - m)(1-b1); v += (g^2 - v)(1-b2); p -= alpha * m / (sqrt(v) + eps),
+// alpha = lr * sqrt(1 - b2^t) / (1 - b1^t) computed by the caller; g is scaled
+// by grad_scale first (e.g. 1/world_size after a sum all-reduce).
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, long long n, float grad_scale, float b1, float b2, float eps,
+                       float alpha) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float gi = g[i] * grad_scale;
+    float mi = m[i], vi = v[i];
+    mi += (gi - mi) * (1.f - b1);
+    vi += (gi * gi - vi) * (1.f - b2);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= alpha * mi / (sqrtf(vi) + eps);
+  }
+}
+ACFE_API int acfe_adam_step(float* params, const float* grads, float* m, float* v, long long n, float grad_scale,
+                            float beta1, float beta2, float eps, float alpha, void* stream) {
+  if (!params || !grads || !m || !v || n < 0) return ACFE_E_INVAL;
+  if (n == 0) return ACFE_OK;
+  hipLaunchKernelGGL(k_adam, dim3(grid_for(n, 256, 4096)), dim3(256), 0, strm(stream), params, grads, m, v, n,
+                     grad_scale, beta1, beta2, eps, alpha);
+  return launch_rc("acfe_adam_step");
+}
+
+// dst[i] = src[i] cast (bf16 <-> fp32), for packing model inputs / outputs
+template <typename TI, typename TO>
+__global__ void k_cast(const TI* __restrict__ x, long long n, TO* __restrict__ y) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    st(y, i, ld(x, i));
+}
+ACFE_API int acfe_cast(const void* x, int x_dtype, long long n, void* y, int y_dtype, void* stream) {
+  if (!x || !y || n < 0) return ACFE_E_INVAL;
+  if (n == 0) return ACFE_OK;
+  DISPATCH1(x_dtype, TI, DISPATCH1(y_dtype, TO,
+      hipLaunchKernelGGL((k_cast<TI, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream), (const TI*)x, n,
+                         (TO*)y)));
+  return launch_rc("acfe_cast");
+}
+
+// out[c] = beta*out[c] + sum_rows x[r][c]  (bias gradients); part: bn_stats slab
+__global__ void k_chan_sum_fin(const double* __restrict__ part, int nrows, int C, float beta,
+                               float* __restrict__ out) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int r = 0; r < nrows; ++r) s += part[((long long)r * 2) * C + c];
+  out[c] = beta != 0.f ? out[c] * beta + (float)s : (float)s;
+}
+ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* part, float* out,
+                              float beta, void* stream) {
+  if (!out || C <= 0) return ACFE_E_INVAL;
+  if (rows == 0) return hip_rc(hipMemsetAsync(out, 0, sizeof(float) * C, strm(stream)), "acfe_channel_sum");
+  int rc = acfe_bn_stats(x, rows, C, dtype, part, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 64)), dim3(64), 0, strm(stream), part, red_blocks(rows), C, beta,
+                     out);
+  return launch_rc("acfe_channel_sum");
+}

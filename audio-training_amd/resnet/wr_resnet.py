@@ -1,0 +1,80 @@
+"""Wide ResNet WRN-22-4 (reference: resnet/wr_resnet.py:5-90) on the acfe kernels.
+
+Pre-activation basic blocks (BN-ReLU-Conv3x3(stride)-Dropout-BN-ReLU-Conv3x3
++ identity or 1x1 strided "valid" shortcut, ReLU after the Add); stage strides
+1, 2, 3 (wr_resnet.py:21-23); BN-ReLU-GlobalAveragePooling-Dense(sigmoid) head.
+Input: the mel image as ONE channel [N, H, W] (the 3 identical channels of
+tfdataset.py:2053 are folded into the stem kernel)."""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from acfe import ops
+from acfe.layers import BatchNormalization, Conv2D, Dense, StemConv2D
+
+
+class BasicBlock(nn.Module):
+    """wr_resnet.basic_block (:46-90)."""
+
+    def __init__(self, cin, filters, stage, block, stride, dropout=0.1, seed=0):
+        super().__init__()
+        F1, F2 = filters
+        cb, bb = f"res{stage}{block}_branch", f"bn{stage}{block}_branch"
+        self.stride, self.dropout = stride, dropout
+        self.bn2a = BatchNormalization(cin, bb + "2a")
+        self.conv2a = Conv2D(cin, F1, (3, 3), stride, "same", name=cb + "2a", seed=seed)
+        self.bn2b = BatchNormalization(F1, bb + "2b")
+        self.conv2b = Conv2D(F1, F2, (3, 3), 1, "same", name=cb + "2b", seed=seed)
+        self.shortcut = None
+        if cin != F2:
+            # Keras default padding "valid", default (unseeded) GlorotUniform
+            self.shortcut = Conv2D(cin, F2, 1, stride, "valid", name=f"conv2d_shortcut_{stage}{block}", seed=seed + 1)
+        self.out_channels = F2
+
+    def forward(self, x):
+        y = self.bn2a(x, relu=True)
+        y = self.conv2a(y)
+        y = ops.dropout(y, self.dropout, self.training)
+        y = self.bn2b(y, relu=True)
+        y = self.conv2b(y)
+        sc = x if self.shortcut is None else self.shortcut(x)
+        return ops.add(y, sc, relu=True)
+
+
+class WRResNet(nn.Module):
+    """WRResNet(input_shape, classes, depth=22, k=4) of wr_resnet.py:5-33."""
+
+    def __init__(self, input_shape=(128, 512, 1), classes=6, depth=22, k=4, dtype=torch.bfloat16, dropout=0.1,
+                 seed=0):
+        super().__init__()
+        H, W, cin = input_shape
+        self.input_shape, self.classes, self.dtype, self.dropout = tuple(input_shape), classes, dtype, dropout
+        filters = [16, 16 * k, 32 * k, 64 * k]
+        n = int((depth - 4) / 6)
+        self.conv1_1 = StemConv2D(cin, filters[0], (3, 3), name="conv1_1", seed=seed, out_dtype=dtype)
+        c = filters[0]
+        blocks = []
+        for stage in range(1, len(filters)):
+            f = filters[stage]
+            for d in range(n):
+                stride = stage if d == 0 else 1
+                blk = BasicBlock(c, (f, f), stage + 1, f"b{d}", stride, dropout, seed)
+                blocks.append(blk)
+                c = blk.out_channels
+        self.blocks = nn.ModuleList(blocks)
+        self.final_bn = BatchNormalization(c, "final_bn")
+        self.prediction = Dense(c, classes, name="prediction", seed=seed)
+
+    def forward(self, x):
+        if x.dim() == 4:
+            x = x[..., 0]
+        y = self.conv1_1(x)
+        for blk in self.blocks:
+            y = blk(y)
+        y = self.final_bn(y, relu=True)
+        y = ops.global_avg_pool(y)
+        return self.prediction(y)
+
+    def predict(self, x):
+        return ops.sigmoid(self.forward(x))

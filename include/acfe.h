@@ -124,6 +124,119 @@ int acfe_pcen_bwd(const float* mel_btm, int batch, int t, int m, const float* pa
                   const float* stats, const void* dout, int dout_dtype, float* workspace,
                   float* dparams, void* stream);
 
+/* ===================================================================== model
+ * Replaces the Keras layers of resnet/wr_resnet.py:5-90 and
+ * resnet/wr_resnet_bird.py:7-179 (Conv2D, BatchNormalization, ReLU, Add,
+ * Dropout, MaxPool2D, AveragePooling2D, logmeanexp, GlobalAveragePooling2D,
+ * Dense) and the loss / optimizer of audiomodel.py:1206-1240.
+ * Activations NHWC (dtype ACFE_DTYPE_*), weights fp32 KRSC master copies. */
+
+/* Packed-weight shape [rows_p][cols_p] for acfe_conv2d_pack_weights:
+ * flip=0 -> forward operand [K pad][R*S*C pad]; flip=1 -> dgrad operand
+ * [C pad][R*S*K pad] with the kernel rotated by 180 degrees. */
+int acfe_conv2d_packed_shape(int K, int R, int S, int C, int dtype, int flip, int* rows_p, int* cols_p);
+int acfe_conv2d_pack_weights(const float* w_krsc, int K, int R, int S, int C, int dtype, int flip,
+                             void* out, void* stream);
+/* Rows of the per-channel statistics slab written by acfe_conv2d_fwd
+ * (stats_partial: double[rows][2][rows_p of the forward packing]). */
+int acfe_conv2d_stats_rows(long long M, int K);
+/* Keras Conv2D forward (tf.keras.layers.Conv2D, NHWC): y[n,p,q,k] =
+ * sum_{r,s,c} x[n, p*stride - pad_top + r, q*stride - pad_left + s, c] w[k,r,s,c] + bias[k].
+ * Out-of-range taps read zero, so "same" needs only the top/left pads
+ * (TF: pad_total = max((P-1)*stride + R - H, 0), pad_top = pad_total/2).
+ * Optionally writes per-block {sum y, sum y^2} of the ROUNDED outputs for the
+ * next BatchNormalization (stats_partial, may be NULL). */
+int acfe_conv2d_fwd(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R, int S,
+                    int stride, int pad_top, int pad_left, int P, int Q, const float* bias, void* y,
+                    int dtype, double* stats_partial, void* stream);
+/* dX of the convolution above (wflip = flip=1 packing).  workspace: for
+ * stride > 1, N*((P-1)*stride+1)*((Q-1)*stride+1)*K elements of dtype. */
+int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R, int S,
+                      int stride, int pad_top, int pad_left, int H, int W, void* dx, int dtype,
+                      void* workspace, void* stream);
+/* float count of the wgrad split-K workspace. */
+long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q);
+/* dW (fp32 KRSC) = beta*dW + sum_pixels dY (x) im2col(X). */
+int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy, int K, int R, int S,
+                      int stride, int pad_top, int pad_left, int P, int Q, float* dw, float beta, int dtype,
+                      float* workspace, void* stream);
+
+/* Stem convolution with one (folded) input channel and 16 outputs: the three
+ * identical channels of tfdataset.py:2053 are folded by weff = sum_c w[...,c]. */
+int acfe_stem_blocks(int N, int H, int W);
+int acfe_stem_fold_weights(const float* w_krsc, int K, int R, int S, int C, float* weff, void* stream);
+int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int R, int S, int pad_top, int pad_left,
+                  const float* weff, const float* bias, void* y, int y_dtype, double* stats_partial,
+                  void* stream);
+int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, int R, int S, int pad_top,
+                    int pad_left, const float* weff, void* dx, int dx_dtype, void* stream);
+/* workspace: double[acfe_stem_blocks(N,H,W) * 16 * R * S]; dw is [16][R][S][rep]. */
+int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, int N, int H, int W, int R,
+                    int S, int pad_top, int pad_left, int rep, float* dw, float beta, double* workspace,
+                    void* stream);
+
+/* BatchNormalization(axis=3) (Keras: eps 1e-3, momentum 0.99, biased variance).
+ * Partial slabs are double[acfe_reduce_blocks(rows)][2][C]. */
+int acfe_reduce_blocks(long long rows);
+int acfe_bn_stats(const void* x, long long rows, int C, int dtype, double* partial, void* stream);
+int acfe_bn_finalize(const double* partial, int nrows, int ld, int C, double count, const float* gamma,
+                     const float* beta, float eps, float momentum, float* moving_mean, float* moving_var,
+                     int training, float* scale, float* shift, float* mean, float* invstd, void* stream);
+int acfe_bn_apply(const void* x, int x_dtype, long long rows, int C, const float* scale, const float* shift,
+                  int relu, void* y, int y_dtype, void* stream);
+int acfe_bn_bwd_reduce(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                       const float* scale, const float* shift, const float* mean, const float* invstd,
+                       int relu, double* partial, void* stream);
+/* coef: float[3][C] for dx = a*g + b*x + c; dgamma/dbeta overwritten (nullable). */
+int acfe_bn_bwd_finalize(const double* partial, int nrows, int C, double count, const float* scale,
+                         const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
+                         void* stream);
+int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                      const float* scale, const float* shift, int relu, const float* coef, const void* add,
+                      void* dx, int dx_dtype, void* stream);
+
+/* out[c] = beta*out[c] + sum_rows x[r][c] (bias gradients); partial as acfe_bn_stats. */
+int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* partial, float* out, float beta,
+                     void* stream);
+
+/* Elementwise. */
+int acfe_add(const void* a, const void* b, long long n, int relu, void* z, int dtype, void* stream);
+int acfe_relu_bwd(const void* dy, const void* y, long long n, void* dx, int dtype, void* stream);
+int acfe_dropout(const void* x, long long n, float rate, unsigned long long seed, void* y, int dtype,
+                 void* stream);
+int acfe_cast(const void* x, int x_dtype, long long n, void* y, int y_dtype, void* stream);
+int acfe_sigmoid(const float* z, long long n, float* p, void* stream);
+
+/* Pooling (NHWC). MaxPool2D valid (gradient to the first maximum);
+ * AveragePooling2D "same" with strides == pool (in-bounds averaging). */
+int acfe_maxpool2d(const void* x, int N, int H, int W, int C, int kh, int kw, void* y, int dtype,
+                   void* stream);
+int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int W, int C, int kh, int kw, void* dx,
+                       int dtype, void* stream);
+int acfe_avgpool2d(const void* x, int N, int H, int W, int C, int k, void* y, int dtype, void* stream);
+int acfe_avgpool2d_bwd(const void* dy, int N, int H, int W, int C, int k, void* dx, int dtype, void* stream);
+/* Reduce the middle axis of [outer][L][inner] to fp32 [outer][inner]:
+ * mode 0 = log-mean-exp with sharpness (wr_resnet_bird.py:83-87), 1 = mean. */
+int acfe_axis_pool(const void* x, int x_dtype, long long outer, int L, int inner, float sharpness, int mode,
+                   float* y, void* stream);
+int acfe_axis_pool_bwd(const void* x, int x_dtype, const float* dy, long long outer, int L, int inner,
+                       float sharpness, int mode, void* dx, void* stream);
+
+/* Dense (Keras kernel layout [in][out]) and losses on its sigmoid output:
+ * mode 0 BinaryCrossentropy, 1 CategoricalCrossentropy (audiomodel.py:1206-1223).
+ * workspace: float[B]. */
+int acfe_dense_fwd(const float* x, const float* w, const float* bias, int B, int I, int O, float* z,
+                   void* stream);
+int acfe_dense_bwd(const float* x, const float* w, const float* dz, int B, int I, int O, float* dx, float* dw,
+                   float* db, void* stream);
+int acfe_loss(const float* z, const float* y, int B, int L, int mode, float grad_scale, float* loss, float* dz,
+              float* workspace, void* stream);
+
+/* Adam (tf.keras.optimizers.Adam, audiomodel.py:1226-1240) over a flat fp32
+ * parameter arena; alpha = lr*sqrt(1-b2^t)/(1-b1^t). */
+int acfe_adam_step(float* params, const float* grads, float* m, float* v, long long n, float grad_scale,
+                   float beta1, float beta2, float eps, float alpha, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

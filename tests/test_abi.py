@@ -36,3 +36,21 @@ def test_host_only_calls():
     assert _lib.lib.acfe_pcen_partials(512, 128) == 256
     # invalid arguments are reported, not crashed on
     assert _lib.lib.acfe_mel_filterbank(0, 128, 100.0, 11000.0, 4096, 1000.0, None) == _lib.E_INVAL
+
+
+def header_param_counts():
+    txt = (ROOT / "include" / "acfe.h").read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(acfe_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_binding_arity_matches_header():
+    from acfe import _lib
+
+    counts = header_param_counts()
+    bad = {k: (len(v), counts[k]) for k, v in _lib.SIGNATURES.items() if len(v) != counts[k]}
+    assert not bad, bad
