@@ -60,7 +60,7 @@ class MelPlan:
 
     def mel(self, raw: torch.Tensor, stats: torch.Tensor | None = None, pad_mode="end", power=2,
             layout="btm", n: int | None = None, clip_stride: int | None = None, batch: int | None = None,
-            out: torch.Tensor | None = None) -> torch.Tensor:
+            out: torch.Tensor | None = None, timer: list | None = None) -> torch.Tensor:
         """raw [B, N] fp32 (or a 1-D recording with explicit n / clip_stride / batch
         for overlapping windows) -> mel [B,T,M] ("btm") or [B,M,T] ("bmt")."""
         require_cuda(raw, stats)
@@ -78,9 +78,17 @@ class MelPlan:
             out = torch.empty(shape, dtype=torch.float32, device=raw.device)
         elif tuple(out.shape) != shape or out.dtype != torch.float32 or not out.is_contiguous():
             raise ValueError("bad out tensor")
+        e0 = None
+        if timer is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         call("acfe_mel_fwd", self._h, ptr(raw), int(clip_stride), int(batch), int(n), ptr(stats),
              PAD_MODES[pad_mode], int(power), ptr(out), _lib.LAYOUT_BTM if layout == "btm" else _lib.LAYOUT_BMT,
              stream())
+        if timer is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            timer.append(("mel", e0, e1))
         return out
 
 

@@ -53,6 +53,36 @@ def _no_stats(dev):
     return torch.empty(0, dtype=F64, device=dev)
 
 
+# Live kernel timing for bench.py: weight data_ptr -> list of (kind, ev0, ev1).
+# Events are recorded on the current torch stream, the stream every acfe
+# kernel is launched on.
+_WATCH: dict[int, list] = {}
+
+
+def watch_conv(weight: torch.Tensor, store: list | None):
+    if store is None:
+        _WATCH.pop(weight.data_ptr(), None)
+    else:
+        _WATCH[weight.data_ptr()] = store
+
+
+class _Timed:
+    def __init__(self, w, kind):
+        self.store = _WATCH.get(w.data_ptr()) if _WATCH else None
+        self.kind = kind
+
+    def __enter__(self):
+        if self.store is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+
+    def __exit__(self, *a):
+        if self.store is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.store.append((self.kind, self.e0, e1))
+
+
 # ------------------------------------------------------------------ conv
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
@@ -67,8 +97,9 @@ class _Conv2dFn(torch.autograd.Function):
         if want_stats:
             rows = lib.acfe_conv2d_stats_rows(N * P * Q, K)
             stats = _empty((rows, 2, wp.shape[0]), F64, x.device)
-        call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, stride, pt, pl, P, Q, ptr(b), ptr(y), dt,
-             ptr(stats) if want_stats else None, stream())
+        with _Timed(w, "fwd"):
+            call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, stride, pt, pl, P, Q, ptr(b), ptr(y), dt,
+                 ptr(stats) if want_stats else None, stream())
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pt, pl, P, Q, b is not None)
         ctx.mark_non_differentiable(stats)
@@ -90,14 +121,16 @@ class _Conv2dFn(torch.autograd.Function):
             ws = None
             if stride > 1:
                 ws = _empty((N * ((P - 1) * stride + 1) * ((Q - 1) * stride + 1) * K,), x.dtype, x.device)
-            call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
-                 ptr(ws), s)
+            with _Timed(w, "dgrad"):
+                call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
+                     ptr(ws), s)
         if ctx.needs_input_grad[1]:
             dw = _empty(w.shape, F32, w.device)
             nws = lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, P, Q)
             ws = _empty((nws,), F32, x.device)
-            call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, stride, pt, pl, P, Q, ptr(dw), 0.0,
-                 dt, ptr(ws), s)
+            with _Timed(w, "wgrad"):
+                call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, stride, pt, pl, P, Q, ptr(dw), 0.0,
+                     dt, ptr(ws), s)
         if has_b and ctx.needs_input_grad[2]:
             db = channel_sum(dy, K)
         return dx, dw, db, None, None, None, None, None, None

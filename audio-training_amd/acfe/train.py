@@ -1,0 +1,99 @@
+"""One data-parallel training step of the hot path, MI355X-native.
+
+raw 3 s @ 48 kHz clips --(normalize, mix_up, normalize)--> STFT -> |X|^2 ->
+mel (tfdataset.py:913-915, :474-481, :2007-2059) --> PCEN (tfpcen.py) -->
+wr_resnet / wr_resnet_bird forward + backward --> loss (audiomodel.loss) -->
+gradient all-reduce (RCCL, one collective over the flat gradient arena) -->
+Adam (audiomodel.optimizer).  Every compute stage is a HIP kernel behind
+include/acfe.h; torch provides memory, streams, autograd bookkeeping and
+torch.distributed.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import frontend as fe
+from . import ops
+from .layers import Adam, ParamArena
+
+
+class FrontEnd(nn.Module):
+    """Device feature extractor: raw [B, N] fp32 -> model input [B, M, T] (dtype).
+
+    With `pcen=True` the mel energies go through trainable PCEN +
+    normalize_minmax (tfpcen.py:42-110); otherwise the mel power itself is
+    the feature, as in the reference's raw_to_mel output (tfdataset.py:2049-2053)."""
+
+    def __init__(self, n_mels=128, n_fft=4096, hop=281, sr=48000, fmin=100, fmax=11000, break_freq=1000,
+                 pcen=True, dtype=torch.bfloat16, device=None, weights=None):
+        super().__init__()
+        self.plan = fe.MelPlan(sr, n_fft, hop, n_mels, fmin, fmax, break_freq, weights=weights, device=device)
+        self.pcen = fe.PCEN(out_dtype=dtype) if pcen else None
+        self.dtype = dtype
+        self.timer = None  # bench.py: list receiving ("mel", ev0, ev1)
+
+    def forward(self, x1, x2=None, lam=None, pad_mode="end", scope_minmax=None):
+        st1 = fe.normalize_stats(x1)
+        if x2 is not None:
+            st2 = fe.normalize_stats(x2)
+            src = fe.mix_up(x1, x2, lam, st1, st2)
+            st = fe.normalize_stats(src)
+        else:
+            src, st = x1, st1
+        if self.pcen is not None:
+            mel = self.plan.mel(src, st, pad_mode=pad_mode, layout="btm", timer=self.timer)
+            return self.pcen(mel, scope_minmax)
+        mel = self.plan.mel(src, st, pad_mode=pad_mode, layout="bmt", timer=self.timer)
+        return ops.cast(mel, self.dtype)
+
+
+def mix_labels(y1: torch.Tensor, y2: torch.Tensor, lam: torch.Tensor, single_label=True) -> torch.Tensor:
+    """Label half of tfdataset.mix_up (:946-954): hard lambda > 0.5 for single-label."""
+    lw = (lam > 0.5).float() if single_label else lam
+    lw = lw.reshape(-1, 1).to(y1.device)
+    return y1 * lw + y2 * (1 - lw)
+
+
+class Trainer:
+    """Holds the front end, the model, one flat parameter arena for both, and
+    Keras-Adam; `step` runs one full training iteration on device tensors."""
+
+    def __init__(self, model: nn.Module, frontend: FrontEnd, lr=0.01, loss="cce", process_group=None,
+                 device=None):
+        self.model, self.frontend, self.loss_mode = model, frontend, loss
+        self.device = device or next(model.parameters()).device
+        self.holder = nn.ModuleList([frontend, model])
+        self.arena = ParamArena(self.holder, self.device)
+        self.opt = Adam(self.arena, lr=lr)
+        self.pg = process_group
+        import torch.distributed as dist
+
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+
+    def train(self, mode=True):
+        self.holder.train(mode)
+        return self
+
+    def step(self, x1, y, x2=None, lam=None):
+        feats = self.frontend(x1, x2, lam)
+        z = self.model(feats)
+        loss, dz = ops.loss_and_grad(z, y, self.loss_mode)
+        self.arena.zero_grad()
+        z.backward(dz)
+        scale = 1.0
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(self.arena.grad, group=self.pg)
+            scale = 1.0 / self.world
+        self.opt.step(grad_scale=scale)
+        return loss, z
+
+    @torch.no_grad()
+    def predict(self, x, pad_mode="end"):
+        self.holder.eval()
+        try:
+            return ops.sigmoid(self.model(self.frontend(x, pad_mode=pad_mode)))
+        finally:
+            self.holder.train()

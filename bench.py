@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: clips/s of data-parallel TRAINING on synthetic
+3 s @ 48 kHz clips (BASELINE.json configs[2]/[3]: wr_resnet_bird, 50 classes,
+bf16, batch 512 per GPU, Adam), plus the mel-pipeline GB/s of the fused
+front-end kernel.
+
+A step = one pass of the hot path over one batch resident in HBM:
+normalize x2 -> mix_up -> normalize -> STFT/|X|^2/mel -> PCEN -> WRN forward
+-> loss -> backward -> gradient all-reduce (N > 1) -> Adam.
+
+  python bench.py [--gpus N --steps K --warmup W]      (N > 1 under torch.distributed.run)
+
+Prints ONE JSON line on rank 0.  `roofline` is measured live with HIP events
+around the dominant kernel (the forward of the stage-1 block-0 3x3 128->128
+convolution, 57 % of the model FLOPs) on the stream it runs on; the rocprofv3
+summaries under profiles/ are the cross-check.  `cpu_baseline` times the CPU
+restatement of the same step (oracle/, torch-CPU + numpy) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT / "audio-training_amd"), str(ROOT)]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+MI355X_PEAK_BF16_TFLOPS = 2500.0  # dense MFMA (MI355X_MICROARCH.md)
+MI355X_PEAK_FP32_TFLOPS = 157.3
+MI355X_PEAK_HBM_GBS = 8000.0
+N_SAMPLES = 144000
+FRONTEND_BYTES_PER_CLIP = 144000 * 4 + 128 * 513 * 4  # SURVEY.md 6 / BASELINE.md 2
+
+
+def synth_bank(n_clips, seed=20260227, sr=48000, n=N_SAMPLES):
+    """SURVEY.md 8(d) synthetic clips: 1-3 linear chirps + white noise, clipped."""
+    t = np.arange(n) / sr
+    out = np.zeros((n_clips, n), np.float32)
+    for i in range(n_clips):
+        rng = np.random.default_rng(seed + i)
+        x = rng.normal(0, rng.uniform(0.002, 0.02), n)
+        if i % 8 != 0:
+            for _ in range(rng.integers(1, 4)):
+                f0, f1 = rng.uniform(500, 10000, 2)
+                amp, on = rng.uniform(0.05, 0.5), rng.uniform(0, 2.0)
+                dur = rng.uniform(0.3, 3.0 - on)
+                m = (t >= on) & (t < on + dur)
+                tt = t[m] - on
+                x[m] += amp * np.sin(2 * np.pi * (f0 * tt + 0.5 * (f1 - f0) / dur * tt * tt))
+        out[i] = np.clip(x, -1, 1)
+    return out
+
+
+def make_batches(batch, classes, device, n_sets=2, seed=0):
+    """n_sets (x1, x2, lam, y) tuples resident in HBM; clips are circular
+    shifts of a 64-clip synthetic bank (distinct per row)."""
+    bank = torch.from_numpy(synth_bank(64, seed=20260227 + seed)).to(device)
+    g = torch.Generator().manual_seed(seed)
+    from acfe.frontend import sample_mixup_lambda
+    from acfe.train import mix_labels
+
+    sets = []
+    for s in range(n_sets):
+        xs, ys = [], []
+        for _ in range(2):
+            idx = torch.randint(0, 64, (batch,), generator=g)
+            shift = torch.randint(0, N_SAMPLES, (batch,), generator=g)
+            x = torch.empty((batch, N_SAMPLES), device=device)
+            for i in range(batch):
+                x[i] = torch.roll(bank[int(idx[i])], int(shift[i]))
+            lab = torch.randint(0, classes, (batch,), generator=g)
+            y = torch.zeros((batch, classes), device=device)
+            y[torch.arange(batch), lab.to(device)] = 1
+            xs.append(x)
+            ys.append(y)
+        torch.manual_seed(seed * 1000 + s)
+        lam = sample_mixup_lambda(batch, 0.5, 0.25, device=device)
+        sets.append((xs[0], xs[1], lam, mix_labels(ys[0], ys[1], lam)))
+    return sets
+
+
+def cpu_baseline(batch=2, steps=2, model="bird", classes=50):
+    """Reference algorithm on the host (oracle/: numpy STFT + the reference's
+    DENSE batch_dot mel, sequential PCEN scan, torch-CPU WRN fwd/bwd + Adam)."""
+    from oracle import frontend as of
+    from oracle import models as om
+    from oracle.torch_ref import pcen_torch
+
+    if model == "bird":
+        from resnet.wr_resnet_bird import WRResNet
+        fwd = om.wr_resnet_bird
+    else:
+        from resnet.wr_resnet import WRResNet
+        fwd = om.wr_resnet
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    m = WRResNet(input_shape=(128, 513, 3), classes=classes, dropout=0.0)
+    params = {k: v.detach().clone().requires_grad_("moving" not in k) for k, v in m.state_dict().items()}
+    trainable = [v for k, v in params.items() if "moving" not in k]
+    state = {k: v for k, v in params.items() if "moving" in k}
+    mvec = [torch.zeros_like(p) for p in trainable]
+    vvec = [torch.zeros_like(p) for p in trainable]
+    w = of.mel_f(48000, 128, 100, 11000, 4096, 1000).astype(np.float32)
+    raw = synth_bank(batch * 2, seed=777)
+    lam = np.full(batch, 0.3)
+    y = np.zeros((batch, classes), np.float32)
+    y[np.arange(batch), np.arange(batch) % classes] = 1
+    pc = torch.tensor([0.98, 2.0, 2.0, 0.04], dtype=torch.float32, requires_grad=True)
+
+    def one_step(t):
+        a, b = of.normalize(raw[:batch]), of.normalize(raw[batch:])
+        x, _ = of.mix_up(a, y, b, y, lam)
+        x = of.normalize(x).astype(np.float32)
+        spec = np.abs(of.stft_pad_end(x, 4096, 281)).astype(np.float32) ** 2      # [B, T, F]
+        mel = np.einsum("mf,btf->bmt", w, spec, optimize=True).astype(np.float32)   # dense mel (K5)
+        feats = pcen_torch(torch.from_numpy(mel).transpose(1, 2).contiguous(), pc)  # [B, M, T]
+        z = fwd(feats[:, None].repeat(1, 3, 1, 1).float(), params, True, state)
+        loss = om.keras_loss(z, torch.from_numpy(y), "cce")
+        loss.backward()
+        with torch.no_grad():
+            new, _, _ = om.keras_adam([p.detach() for p in trainable], [p.grad for p in trainable], mvec, vvec, t)
+            for p, q in zip(trainable, new):
+                p.copy_(q)
+                p.grad = None
+
+    one_step(1)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one_step(i + 2)
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * steps / dt, 4), "unit": "clips/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} timed training steps x {batch} clips (after 1 warm-up) of the CPU restatement: "
+                      f"numpy STFT + dense mel batch_dot, sequential PCEN scan, torch-CPU {model} fwd/bwd "
+                      f"(fp32, {cores} threads) + Keras Adam; {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=512, help="clips per GPU")
+    ap.add_argument("--classes", type=int, default=50)
+    ap.add_argument("--model", choices=["bird", "wrn"], default="bird")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from acfe import ops
+    from acfe.train import FrontEnd, Trainer
+
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    if a.model == "bird":
+        from resnet.wr_resnet_bird import WRResNet, flops_per_clip
+    else:
+        from resnet.wr_resnet import WRResNet
+        flops_per_clip = None
+    torch.manual_seed(1234 + rank)
+    model = WRResNet(input_shape=(128, 513, 3), classes=a.classes, dtype=dtype).to(dev)
+    if world > 1:  # replicas start from rank 0's weights
+        with torch.no_grad():
+            for t in list(model.parameters()) + list(model.buffers()):
+                dist.broadcast(t.data, 0)
+    frontend = FrontEnd(n_mels=128, dtype=dtype, device=dev).to(dev)
+    trainer = Trainer(model, frontend, lr=0.01, loss="cce", device=dev)
+    sets = make_batches(a.batch, a.classes, dev, n_sets=2, seed=rank)
+
+    # dominant kernel: stage-1 block-0 3x3 conv (128 -> 128 ch at 128 x 256)
+    target = model.blocks[0].conv21 if a.model == "bird" else model.blocks[1].conv2a
+    K, R, S, C = target.weight.shape
+    events: list = []
+    mel_events: list = []
+
+    def step(i):
+        x1, x2, lam, y = sets[i % len(sets)]
+        return trainer.step(x1, y, x2, lam)
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ops.watch_conv(target.weight, events)
+    frontend.timer = mel_events
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss, _ = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.watch_conv(target.weight, None)
+    frontend.timer = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_v = float(loss.item())
+
+    def avg_ms(kind, evs):
+        d = [e0.elapsed_time(e1) for k, e0, e1 in evs if k == kind]
+        return float(np.mean(d)) if d else float("nan")
+
+    fwd_ms, dgrad_ms, wgrad_ms = avg_ms("fwd", events), avg_ms("dgrad", events), avg_ms("wgrad", events)
+    mel_ms = avg_ms("mel", mel_events)
+    H_t = 128
+    W_t = 256 if a.model == "bird" else 513
+    flops_launch = 2.0 * a.batch * H_t * W_t * K * R * S * C
+    peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
+    ach = flops_launch / (fwd_ms * 1e-3) / 1e12
+    traffic = None
+    pmc = ROOT / "profiles" / "pmc_dominant_r01.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    clips = world * a.batch * a.steps
+    value = clips / elapsed
+    out = {
+        "metric": "clips/sec training (3s@48kHz, wr_resnet) at 1/2/4/8 GPU; mel pipeline GB/s",
+        "value": round(value, 2),
+        "unit": "clips/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+        "data": "synthetic (SURVEY 8d chirps+noise, resident in HBM; random-init weights)",
+        "config": {
+            "workload": f"T1 training step: normalize/mix_up/STFT-mel/PCEN + {'wr_resnet_bird' if a.model == 'bird' else 'wr_resnet'} fwd/bwd + Adam",
+            "model": "wr_resnet_bird" if a.model == "bird" else "wr_resnet",
+            "input": [128, 513, 3], "classes": a.classes, "global_batch": world * a.batch,
+            "batch_per_gpu": a.batch, "seq_len": 513, "parallelism": f"dp{world}",
+            "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
+        },
+        "roofline": {
+            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv_fwd<bf16,128,128>)",
+            "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": traffic,
+            "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
+            "dgrad_ms": round(dgrad_ms, 4), "wgrad_ms": round(wgrad_ms, 4),
+            "dgrad_tflops": round(flops_launch / (dgrad_ms * 1e-3) / 1e12, 2),
+            "wgrad_tflops": round(flops_launch / (wgrad_ms * 1e-3) / 1e12, 2),
+        },
+        "mel_pipeline": {
+            "kernel": "k_mel<2048> (frame+Hann+4096 rFFT+|X|^2+banded mel)",
+            "avg_launch_ms": round(mel_ms, 4),
+            "GBps": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2),
+            "hbm_frac": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9 / MI355X_PEAK_HBM_GBS, 4),
+            "bytes_per_clip": FRONTEND_BYTES_PER_CLIP,
+        },
+        "model_tflops_fwd_bwd": round(3 * (flops_per_clip(model) if flops_per_clip else 64.956e9) * value / 1e12, 2),
+        "final_loss": round(loss_v, 5),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps, a.model, a.classes)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
