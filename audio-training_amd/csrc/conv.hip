@@ -741,9 +741,9 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
 // (stride 1, P = H, Q = W).  Tile: 8 rows x 64 cols per block iteration.
 constexpr int STEM_TH = 8, STEM_TW = 64, STEM_K = 16, STEM_MAXR = 7;
 
-template <typename TI, typename TO>
+template <typename TI, typename TO, int R, int S>
 __global__ void __launch_bounds__(256)
-k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int R, int S, int pt, int pl,
+k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int pt, int pl,
            const float* __restrict__ weff, const float* __restrict__ bias, TO* __restrict__ y,
            double* __restrict__ stats, int tiles_h, int tiles_w) {
   __shared__ float xs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1)];
@@ -776,7 +776,9 @@ k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int R, int S, int pt, 
       const int py = pix / STEM_TW, px = pix - (pix / STEM_TW) * STEM_TW;
       const int h = h0 + py, w = w0 + px;
       float a0 = 0.f, a1 = 0.f;
+#pragma unroll
       for (int r = 0; r < R; ++r)
+#pragma unroll
         for (int s = 0; s < S; ++s) {
           const float xv = xs[(py + r) * XW + px + s];
           a0 += xv * wsm[(kq * R + r) * S + s];
@@ -814,9 +816,9 @@ k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int R, int S, int pt, 
 }
 
 // dx[n,h,w] = sum_{k,r,s} dy[n, h + pt - r, w + pl - s, k] * weff[k][r][s]
-template <typename TG, typename TO>
+template <typename TG, typename TO, int R, int S>
 __global__ void __launch_bounds__(256)
-k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int R, int S, int pt, int pl,
+k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int pt, int pl,
              const float* __restrict__ weff, TO* __restrict__ dx, int tiles_h, int tiles_w) {
   __shared__ float gs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1) * STEM_K];
   __shared__ float wsm[STEM_K * STEM_MAXR * STEM_MAXR];
@@ -847,7 +849,9 @@ k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int R, int S, int p
       const int h = h0 + py, w = w0 + px;
       float a = 0.f;
       // dy row = h + pt - r  -> gs row = py + (R-1-pt) + pt - r = py + R-1-r
+#pragma unroll
       for (int r = 0; r < R; ++r)
+#pragma unroll
         for (int s = 0; s < S; ++s) {
           const float* gp = &gs[((py + R - 1 - r) * XW + px + S - 1 - s) * STEM_K];
 #pragma unroll
@@ -859,18 +863,18 @@ k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int R, int S, int p
 }
 
 // dweff[k][r][s] partials per block: thread -> (k = tid & 15, pixel group = tid >> 4)
-template <typename TI, typename TG>
+template <typename TI, typename TG, int R, int S>
 __global__ void __launch_bounds__(256)
-k_stem_wgrad(const TI* __restrict__ x, const TG* __restrict__ dy, int N, int H, int W, int R, int S, int pt,
+k_stem_wgrad(const TI* __restrict__ x, const TG* __restrict__ dy, int N, int H, int W, int pt,
              int pl, double* __restrict__ part, int tiles_h, int tiles_w) {
   __shared__ float xs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1)];
   __shared__ float red[16][STEM_K * STEM_MAXR * STEM_MAXR + 1];
   const int tid = threadIdx.x, k = tid & 15, pg = tid >> 4;
   const int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1;
-  float acc[STEM_MAXR * STEM_MAXR];
-  for (int i = 0; i < R * S; ++i) acc[i] = 0.f;
-  double accd[STEM_MAXR * STEM_MAXR];
-  for (int i = 0; i < R * S; ++i) accd[i] = 0.0;
+  float acc[R * S];
+  double accd[R * S];
+#pragma unroll
+  for (int i = 0; i < R * S; ++i) acc[i] = 0.f, accd[i] = 0.0;
   const long long ntiles = (long long)N * tiles_h * tiles_w;
   for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int tw = (int)(t % tiles_w);
@@ -891,15 +895,19 @@ k_stem_wgrad(const TI* __restrict__ x, const TG* __restrict__ dy, int N, int H, 
       const int h = h0 + py, w = w0 + px;
       if (h >= H || w >= W) continue;
       const float g = to_f(dy[(((long long)n * H + h) * W + w) * STEM_K + k]);
+#pragma unroll
       for (int r = 0; r < R; ++r)
+#pragma unroll
         for (int s = 0; s < S; ++s) acc[r * S + s] += g * xs[(py + r) * XW + px + s];
     }
+#pragma unroll
     for (int i = 0; i < R * S; ++i) {
       accd[i] += acc[i];
       acc[i] = 0.f;
     }
   }
   __syncthreads();
+#pragma unroll
   for (int i = 0; i < R * S; ++i) red[pg][k * R * S + i] = (float)accd[i];
   __syncthreads();
   for (int i = tid; i < STEM_K * R * S; i += 256) {
@@ -945,14 +953,14 @@ ACFE_API int acfe_stem_fold_weights(const float* w, int K, int R, int S, int C, 
 ACFE_API int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int R, int S, int pad_top,
                            int pad_left, const float* weff, const float* bias, void* y, int y_dtype,
                            double* stats_partial, void* stream) {
-  if (!x || !weff || !y || N < 0 || H <= 0 || W <= 0 || R > STEM_MAXR || S > STEM_MAXR || R <= 0 || S <= 0)
-    return ACFE_E_INVAL;
+  if (!x || !weff || !y || N < 0 || H <= 0 || W <= 0 || R != S || (R != 5 && R != 3)) return ACFE_E_INVAL;
   if (N == 0) return ACFE_OK;
   const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
   const int grid = acfe_stem_blocks(N, H, W);
-#define SF(TI, TO)                                                                                          \
-  hipLaunchKernelGGL((k_stem_fwd<TI, TO>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x, N, H, W, R, S, \
+#define SF1(TI, TO, RR)                                                                                      \
+  hipLaunchKernelGGL((k_stem_fwd<TI, TO, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x, N, H, W, \
                      pad_top, pad_left, weff, bias, (TO*)y, stats_partial, th, tw)
+#define SF(TI, TO) if (R == 5) SF1(TI, TO, 5); else SF1(TI, TO, 3)
   if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16) SF(uint16_t, uint16_t);
   else if (x_dtype == ACFE_DTYPE_BF16) SF(uint16_t, float);
   else if (y_dtype == ACFE_DTYPE_BF16) SF(float, uint16_t);
@@ -963,13 +971,14 @@ ACFE_API int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int 
 
 ACFE_API int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, int R, int S, int pad_top,
                              int pad_left, const float* weff, void* dx, int dx_dtype, void* stream) {
-  if (!dy || !weff || !dx || N < 0 || R > STEM_MAXR || S > STEM_MAXR) return ACFE_E_INVAL;
+  if (!dy || !weff || !dx || N < 0 || R != S || (R != 5 && R != 3)) return ACFE_E_INVAL;
   if (N == 0) return ACFE_OK;
   const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
   const int grid = acfe_stem_blocks(N, H, W);
-#define SD(TG, TO)                                                                                           \
-  hipLaunchKernelGGL((k_stem_dgrad<TG, TO>), dim3(grid), dim3(256), 0, strm(stream), (const TG*)dy, N, H, W, R, S, \
-                     pad_top, pad_left, weff, (TO*)dx, th, tw)
+#define SD1(TG, TO, RR)                                                                                      \
+  hipLaunchKernelGGL((k_stem_dgrad<TG, TO, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TG*)dy, N, H, \
+                     W, pad_top, pad_left, weff, (TO*)dx, th, tw)
+#define SD(TG, TO) if (R == 5) SD1(TG, TO, 5); else SD1(TG, TO, 3)
   if (dy_dtype == ACFE_DTYPE_BF16 && dx_dtype == ACFE_DTYPE_BF16) SD(uint16_t, uint16_t);
   else if (dy_dtype == ACFE_DTYPE_BF16) SD(uint16_t, float);
   else if (dx_dtype == ACFE_DTYPE_BF16) SD(float, uint16_t);
@@ -982,13 +991,13 @@ ACFE_API int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, 
 ACFE_API int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, int N, int H, int W,
                              int R, int S, int pad_top, int pad_left, int rep, float* dw, float beta,
                              double* workspace, void* stream) {
-  if (!x || !dy || !dw || !workspace || N <= 0 || R > STEM_MAXR || S > STEM_MAXR || rep <= 0)
-    return ACFE_E_INVAL;
+  if (!x || !dy || !dw || !workspace || N <= 0 || R != S || (R != 5 && R != 3) || rep <= 0) return ACFE_E_INVAL;
   const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
   const int grid = acfe_stem_blocks(N, H, W);
-#define SW(TI, TG)                                                                                          \
-  hipLaunchKernelGGL((k_stem_wgrad<TI, TG>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x, (const TG*)dy, \
-                     N, H, W, R, S, pad_top, pad_left, workspace, th, tw)
+#define SW1(TI, TG, RR)                                                                                      \
+  hipLaunchKernelGGL((k_stem_wgrad<TI, TG, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x,        \
+                     (const TG*)dy, N, H, W, pad_top, pad_left, workspace, th, tw)
+#define SW(TI, TG) if (R == 5) SW1(TI, TG, 5); else SW1(TI, TG, 3)
   if (x_dtype == ACFE_DTYPE_BF16 && dy_dtype == ACFE_DTYPE_BF16) SW(uint16_t, uint16_t);
   else if (x_dtype == ACFE_DTYPE_BF16) SW(uint16_t, float);
   else if (dy_dtype == ACFE_DTYPE_BF16) SW(float, uint16_t);

@@ -37,6 +37,72 @@ static int red_blocks(long long rows) {
 }
 ACFE_API int acfe_reduce_blocks(long long rows) { return red_blocks(rows); }
 
+// ---------------------------------------------------------------- 8-wide access
+// Channel-contiguous NHWC tensors are processed 8 elements per thread (16 B of
+// bf16 / 32 B of fp32) when C % 8 == 0 and the buffers are 16-B aligned;
+// scalar kernels remain as the fallback.
+__device__ __forceinline__ void ld8(const uint16_t* p, float* f) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(w[j] << 16);
+    f[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void ld8(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void st8(uint16_t* p, const float* f) {
+  uint4 v;
+  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
+  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  *reinterpret_cast<uint4*>(p) = v;
+}
+__device__ __forceinline__ void st8(float* p, const float* f) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+static bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static bool vec_ok(long long n, int C, const void* a, const void* b = nullptr, const void* c = nullptr,
+                   const void* d = nullptr) {
+  return C % 8 == 0 && n % 8 == 0 && n / 8 < 0xFFFFFFFFll && al16(a) && al16(b) && al16(c) && al16(d);
+}
+static int vgrid(long long nvec) { return grid_for(nvec, 256, 16384); }
+
+// Sum a [nrows][2][ld] double slab over rows for the 32 channels of this block
+// (8 row groups x 32 channels, fixed order): s[j][cl] for j in {0, 1}.
+__device__ __forceinline__ void slab_sum32(const double* __restrict__ part, int nrows, int ld, int C,
+                                           double (*s)[32]) {
+  __shared__ double tmp[8][2][32];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int r = rg; r < nrows; r += 8) {
+      a += part[((long long)r * 2 + 0) * ld + c];
+      b += part[((long long)r * 2 + 1) * ld + c];
+    }
+  tmp[rg][0][cl] = a;
+  tmp[rg][1][cl] = b;
+  __syncthreads();
+  if (rg == 0) {
+    double x = 0.0, y = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      x += tmp[i][0][cl];
+      y += tmp[i][1][cl];
+    }
+    s[0][cl] = x;
+    s[1][cl] = y;
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------- BN statistics
 // part[blk][2][C] = {sum x, sum x^2} over the block's rows (double)
 template <typename T>
@@ -45,12 +111,12 @@ __global__ void __launch_bounds__(256) k_bn_stats(const T* __restrict__ x, long 
   extern __shared__ double red[];  // [2][C]
   for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
   __syncthreads();
-  // thread -> channel c = tid % C' chunks; rows strided
-  const long long r0 = (long long)blockIdx.x * ((rows + gridDim.x - 1) / gridDim.x);
-  long long r1 = r0 + (rows + gridDim.x - 1) / gridDim.x;
+  const long long per = (rows + gridDim.x - 1) / gridDim.x;
+  const long long r0 = (long long)blockIdx.x * per;
+  long long r1 = r0 + per;
   if (r1 > rows) r1 = rows;
-  const int tpr = C < 256 ? C : 256;  // threads per row slice
-  const int rpp = 256 / tpr;          // rows per pass
+  const int tpr = C < 256 ? C : 256;
+  const int rpp = 256 / tpr;
   const int c_base = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
   if (rsub < rpp) {
     for (int c = c_base; c < C; c += tpr) {
@@ -63,10 +129,54 @@ __global__ void __launch_bounds__(256) k_bn_stats(const T* __restrict__ x, long 
         f2 += v * v;
         if (++cnt == 256) { s1 += f1; s2 += f2; f1 = f2 = 0.f; cnt = 0; }
       }
-      s1 += f1;
-      s2 += f2;
-      atomicAdd(&red[c], s1);
-      atomicAdd(&red[C + c], s2);
+      atomicAdd(&red[c], s1 + f1);
+      atomicAdd(&red[C + c], s2 + f2);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_stats8(const T* __restrict__ x, long long rows, int C,
+                                                   double* __restrict__ part) {
+  extern __shared__ double red[];  // [2][C]
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+  __syncthreads();
+  const long long per = (rows + gridDim.x - 1) / gridDim.x;
+  const long long r0 = (long long)blockIdx.x * per;
+  long long r1 = r0 + per;
+  if (r1 > rows) r1 = rows;
+  const int CV = C >> 3;
+  const int tpr = CV < 256 ? CV : 256;
+  const int rpp = 256 / tpr;
+  const int cvb = threadIdx.x % tpr, rs = threadIdx.x / tpr;
+  if (rs < rpp) {
+    for (int cv = cvb; cv < CV; cv += tpr) {
+      float a[8], b[8];
+      double da[8], db[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f, da[j] = db[j] = 0.0;
+      int cnt = 0;
+      for (long long r = r0 + rs; r < r1; r += rpp) {
+        float f[8];
+        ld8(x + r * C + cv * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[j] += f[j];
+          b[j] += f[j] * f[j];
+        }
+        if (++cnt == 64) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) da[j] += a[j], db[j] += b[j], a[j] = b[j] = 0.f;
+          cnt = 0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        atomicAdd(&red[cv * 8 + j], da[j] + a[j]);
+        atomicAdd(&red[C + cv * 8 + j], db[j] + b[j]);
+      }
     }
   }
   __syncthreads();
@@ -76,8 +186,13 @@ __global__ void __launch_bounds__(256) k_bn_stats(const T* __restrict__ x, long 
 ACFE_API int acfe_bn_stats(const void* x, long long rows, int C, int dtype, double* part, void* stream) {
   if (!x || !part || rows <= 0 || C <= 0 || C > 2048) return ACFE_E_INVAL;
   const int nb = red_blocks(rows);
-  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_bn_stats<T>, dim3(nb), dim3(256), 2 * C * sizeof(double),
-                                         strm(stream), (const T*)x, rows, C, part));
+  if (vec_ok(rows * C, C, x)) {
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_bn_stats8<T>, dim3(nb), dim3(256), 2 * C * sizeof(double),
+                                           strm(stream), (const T*)x, rows, C, part));
+  } else {
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_bn_stats<T>, dim3(nb), dim3(256), 2 * C * sizeof(double),
+                                           strm(stream), (const T*)x, rows, C, part));
+  }
   return launch_rc("acfe_bn_stats");
 }
 
@@ -85,22 +200,21 @@ ACFE_API int acfe_bn_stats(const void* x, long long rows, int C, int dtype, doub
 // out (each fp32[C], any may be NULL except scale/shift):
 //   scale = gamma * invstd, shift = beta - mean * scale, mean, invstd
 // training: batch statistics + moving-average update (momentum); else moving stats.
-__global__ void k_bn_finalize(const double* __restrict__ part, int nrows, int ld, int C, double count,
-                              const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                              float momentum, float* __restrict__ mmean, float* __restrict__ mvar, int training,
-                              float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_o,
-                              float* __restrict__ invstd_o) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= C) return;
+__global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ part, int nrows, int ld, int C,
+                                                     double count, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps, float momentum,
+                                                     float* __restrict__ mmean, float* __restrict__ mvar,
+                                                     int training, float* __restrict__ scale,
+                                                     float* __restrict__ shift, float* __restrict__ mean_o,
+                                                     float* __restrict__ invstd_o) {
+  __shared__ double s[2][32];
+  if (training) slab_sum32(part, nrows, ld, C, s);
+  const int c = blockIdx.x * 32 + threadIdx.x;
+  if (threadIdx.x >= 32 || c >= C) return;
   double mean, var;
   if (training) {
-    double s1 = 0.0, s2 = 0.0;
-    for (int r = 0; r < nrows; ++r) {
-      s1 += part[((long long)r * 2 + 0) * ld + c];
-      s2 += part[((long long)r * 2 + 1) * ld + c];
-    }
-    mean = s1 / count;
-    var = s2 / count - mean * mean;
+    mean = s[0][threadIdx.x] / count;
+    var = s[1][threadIdx.x] / count - mean * mean;
     if (var < 0) var = 0;
     if (mmean) mmean[c] = (float)(mmean[c] * (double)momentum + mean * (1.0 - momentum));
     if (mvar) mvar[c] = (float)(mvar[c] * (double)momentum + var * (1.0 - momentum));
@@ -124,8 +238,8 @@ ACFE_API int acfe_bn_finalize(const double* part, int nrows, int ld, int C, doub
   if (!scale || !shift || C <= 0 || (training && (!part || nrows <= 0 || count <= 0)) ||
       (!training && (!moving_mean || !moving_var)))
     return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 64)), dim3(64), 0, strm(stream), part, nrows, ld, C, count, gamma,
-                     beta, eps, momentum, moving_mean, moving_var, training, scale, shift, mean, invstd);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, nrows, ld, C, count,
+                     gamma, beta, eps, momentum, moving_mean, moving_var, training, scale, shift, mean, invstd);
   return launch_rc("acfe_bn_finalize");
 }
 
@@ -140,15 +254,41 @@ __global__ void k_bn_apply(const TI* __restrict__ x, long long n, int C, const f
     st(y, i, v);
   }
 }
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) k_bn_apply8(const TI* __restrict__ x, unsigned nvec, int C,
+                                                   const float* __restrict__ scale, const float* __restrict__ shift,
+                                                   int relu, TO* __restrict__ y) {
+  extern __shared__ float sm[];
+  for (int i = threadIdx.x; i < C; i += 256) sm[i] = scale[i], sm[C + i] = shift[i];
+  __syncthreads();
+  const unsigned CV = C >> 3;
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    const int c0 = (int)(v % CV) * 8;
+    float f[8];
+    ld8(x + (size_t)v * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] = f[j] * sm[c0 + j] + sm[C + c0 + j];
+      if (relu) f[j] = fmaxf(f[j], 0.f);
+    }
+    st8(y + (size_t)v * 8, f);
+  }
+}
 
 ACFE_API int acfe_bn_apply(const void* x, int x_dtype, long long rows, int C, const float* scale,
                            const float* shift, int relu, void* y, int y_dtype, void* stream) {
   if (!x || !y || !scale || !shift || rows < 0 || C <= 0) return ACFE_E_INVAL;
   const long long n = rows * C;
   if (n == 0) return ACFE_OK;
-  DISPATCH1(x_dtype, TI, DISPATCH1(y_dtype, TO,
-      hipLaunchKernelGGL((k_bn_apply<TI, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream), (const TI*)x, n, C,
-                         scale, shift, relu, (TO*)y)));
+  if (vec_ok(n, C, x, y) && C <= 4096) {
+    DISPATCH1(x_dtype, TI, DISPATCH1(y_dtype, TO,
+        hipLaunchKernelGGL((k_bn_apply8<TI, TO>), dim3(vgrid(n / 8)), dim3(256), 2 * C * sizeof(float),
+                           strm(stream), (const TI*)x, (unsigned)(n / 8), C, scale, shift, relu, (TO*)y)));
+  } else {
+    DISPATCH1(x_dtype, TI, DISPATCH1(y_dtype, TO,
+        hipLaunchKernelGGL((k_bn_apply<TI, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream), (const TI*)x, n,
+                           C, scale, shift, relu, (TO*)y)));
+  }
   return launch_rc("acfe_bn_apply");
 }
 
@@ -185,10 +325,63 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(const TG* __restrict__ dy
         f2 += g * ((xv - mu) * is);
         if (++cnt == 256) { s1 += f1; s2 += f2; f1 = f2 = 0.f; cnt = 0; }
       }
-      s1 += f1;
-      s2 += f2;
-      atomicAdd(&red[c], s1);
-      atomicAdd(&red[C + c], s2);
+      atomicAdd(&red[c], s1 + f1);
+      atomicAdd(&red[C + c], s2 + f2);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
+}
+template <typename TG, typename TX>
+__global__ void __launch_bounds__(256) k_bn_bwd_reduce8(const TG* __restrict__ dy, const TX* __restrict__ x,
+                                                        long long rows, int C, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, int relu,
+                                                        double* __restrict__ part) {
+  extern __shared__ double red[];
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+  __syncthreads();
+  const long long per = (rows + gridDim.x - 1) / gridDim.x;
+  const long long r0 = (long long)blockIdx.x * per;
+  long long r1 = r0 + per;
+  if (r1 > rows) r1 = rows;
+  const int CV = C >> 3;
+  const int tpr = CV < 256 ? CV : 256;
+  const int rpp = 256 / tpr;
+  const int cvb = threadIdx.x % tpr, rs = threadIdx.x / tpr;
+  if (rs < rpp) {
+    for (int cv = cvb; cv < CV; cv += tpr) {
+      float sc[8], sh[8], mu[8], is[8], a[8], b[8];
+      double da[8], db[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = cv * 8 + j;
+        sc[j] = scale[c], sh[j] = shift[c], mu[j] = mean[c], is[j] = invstd[c];
+        a[j] = b[j] = 0.f, da[j] = db[j] = 0.0;
+      }
+      int cnt = 0;
+      for (long long r = r0 + rs; r < r1; r += rpp) {
+        float g[8], xv[8];
+        ld8(dy + r * C + cv * 8, g);
+        ld8(x + r * C + cv * 8, xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gj = (relu && !(xv[j] * sc[j] + sh[j] > 0.f)) ? 0.f : g[j];
+          a[j] += gj;
+          b[j] += gj * ((xv[j] - mu[j]) * is[j]);
+        }
+        if (++cnt == 64) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) da[j] += a[j], db[j] += b[j], a[j] = b[j] = 0.f;
+          cnt = 0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        atomicAdd(&red[cv * 8 + j], da[j] + a[j]);
+        atomicAdd(&red[C + cv * 8 + j], db[j] + b[j]);
+      }
     }
   }
   __syncthreads();
@@ -201,24 +394,30 @@ ACFE_API int acfe_bn_bwd_reduce(const void* dy, int dy_dtype, const void* x, int
   if (!dy || !x || !scale || !shift || !mean || !invstd || !part || rows <= 0 || C <= 0 || C > 2048)
     return ACFE_E_INVAL;
   const int nb = red_blocks(rows);
-  DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX,
-      hipLaunchKernelGGL((k_bn_bwd_reduce<TG, TX>), dim3(nb), dim3(256), 2 * C * sizeof(double), strm(stream),
-                         (const TG*)dy, (const TX*)x, rows, C, scale, shift, mean, invstd, relu, part)));
+  if (vec_ok(rows * C, C, dy, x)) {
+    DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX,
+        hipLaunchKernelGGL((k_bn_bwd_reduce8<TG, TX>), dim3(nb), dim3(256), 2 * C * sizeof(double), strm(stream),
+                           (const TG*)dy, (const TX*)x, rows, C, scale, shift, mean, invstd, relu, part)));
+  } else {
+    DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX,
+        hipLaunchKernelGGL((k_bn_bwd_reduce<TG, TX>), dim3(nb), dim3(256), 2 * C * sizeof(double), strm(stream),
+                           (const TG*)dy, (const TX*)x, rows, C, scale, shift, mean, invstd, relu, part)));
+  }
   return launch_rc("acfe_bn_bwd_reduce");
 }
 
 // coef[3][C] = {a, b, c} with dx = a*g + b*x + c; dgamma = sum g xhat, dbeta = sum g
-__global__ void k_bn_bwd_finalize(const double* __restrict__ part, int nrows, int C, double count,
-                                  const float* __restrict__ scale, const float* __restrict__ mean,
-                                  const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                  float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= C) return;
-  double sg = 0.0, sgx = 0.0;
-  for (int r = 0; r < nrows; ++r) {
-    sg += part[((long long)r * 2 + 0) * C + c];
-    sgx += part[((long long)r * 2 + 1) * C + c];
-  }
+__global__ void __launch_bounds__(256) k_bn_bwd_finalize(const double* __restrict__ part, int nrows, int C,
+                                                         double count, const float* __restrict__ scale,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         float* __restrict__ coef) {
+  __shared__ double s[2][32];
+  slab_sum32(part, nrows, C, C, s);
+  const int c = blockIdx.x * 32 + threadIdx.x;
+  if (threadIdx.x >= 32 || c >= C) return;
+  const double sg = s[0][threadIdx.x], sgx = s[1][threadIdx.x];
   if (dgamma) dgamma[c] = (float)sgx;
   if (dbeta) dbeta[c] = (float)sg;
   const double sc = scale[c], is = invstd[c], mu = mean[c];
@@ -232,7 +431,7 @@ ACFE_API int acfe_bn_bwd_finalize(const double* part, int nrows, int C, double c
                                   const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                   float* coef, void* stream) {
   if (!part || !scale || !mean || !invstd || !coef || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(64), 0, strm(stream), part, nrows, C, count, scale,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, nrows, C, count, scale,
                      mean, invstd, dgamma, dbeta, coef);
   return launch_rc("acfe_bn_bwd_finalize");
 }
@@ -252,6 +451,38 @@ __global__ void k_bn_bwd_apply(const TG* __restrict__ dy, const TX* __restrict__
     st(dx, i, v);
   }
 }
+template <typename TG, typename TX, typename TO>
+__global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy, const TX* __restrict__ x,
+                                                       unsigned nvec, int C, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int relu,
+                                                       const float* __restrict__ coef, const TO* __restrict__ add,
+                                                       TO* __restrict__ dx) {
+  extern __shared__ float sm[];  // scale, shift, a, b, c
+  for (int i = threadIdx.x; i < C; i += 256) {
+    sm[i] = scale[i];
+    sm[C + i] = shift[i];
+    sm[2 * C + i] = coef[i];
+    sm[3 * C + i] = coef[C + i];
+    sm[4 * C + i] = coef[2 * C + i];
+  }
+  __syncthreads();
+  const unsigned CV = C >> 3;
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    const int c0 = (int)(v % CV) * 8;
+    float g[8], xv[8], o[8];
+    ld8(dy + (size_t)v * 8, g);
+    ld8(x + (size_t)v * 8, xv);
+    if (add) ld8(add + (size_t)v * 8, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float gj = (relu && !(xv[j] * sm[c] + sm[C + c] > 0.f)) ? 0.f : g[j];
+      const float r = sm[2 * C + c] * gj + sm[3 * C + c] * xv[j] + sm[4 * C + c];
+      o[j] = add ? o[j] + r : r;
+    }
+    st8(dx + (size_t)v * 8, o);
+  }
+}
 
 ACFE_API int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                                const float* scale, const float* shift, int relu, const float* coef,
@@ -259,9 +490,16 @@ ACFE_API int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int 
   if (!dy || !x || !scale || !shift || !coef || !dx || rows < 0 || C <= 0) return ACFE_E_INVAL;
   const long long n = rows * C;
   if (n == 0) return ACFE_OK;
-  DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
-      hipLaunchKernelGGL((k_bn_bwd_apply<TG, TX, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream),
-                         (const TG*)dy, (const TX*)x, n, C, scale, shift, relu, coef, (const TO*)add, (TO*)dx))));
+  if (vec_ok(n, C, dy, x, add, dx) && C <= 2048) {
+    DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
+        hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(vgrid(n / 8)), dim3(256), 5 * C * sizeof(float),
+                           strm(stream), (const TG*)dy, (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu,
+                           coef, (const TO*)add, (TO*)dx))));
+  } else {
+    DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
+        hipLaunchKernelGGL((k_bn_bwd_apply<TG, TX, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                           (const TG*)dy, (const TX*)x, n, C, scale, shift, relu, coef, (const TO*)add, (TO*)dx))));
+  }
   return launch_rc("acfe_bn_bwd_apply");
 }
 
@@ -275,11 +513,27 @@ __global__ void k_add(const T* __restrict__ a, const T* __restrict__ b, long lon
     st(z, i, v);
   }
 }
+template <typename T>
+__global__ void k_add8(const T* __restrict__ a, const T* __restrict__ b, unsigned nvec, int relu,
+                       T* __restrict__ z) {
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    float x[8], y[8];
+    ld8(a + (size_t)v * 8, x);
+    ld8(b + (size_t)v * 8, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = relu ? fmaxf(x[j] + y[j], 0.f) : x[j] + y[j];
+    st8(z + (size_t)v * 8, x);
+  }
+}
 ACFE_API int acfe_add(const void* a, const void* b, long long n, int relu, void* z, int dtype, void* stream) {
   if (!a || !b || !z || n < 0) return ACFE_E_INVAL;
   if (n == 0) return ACFE_OK;
-  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_add<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream), (const T*)a,
-                                         (const T*)b, n, relu, (T*)z));
+  if (vec_ok(n, 8, a, b, z))
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_add8<T>, dim3(vgrid(n / 8)), dim3(256), 0, strm(stream), (const T*)a,
+                                           (const T*)b, (unsigned)(n / 8), relu, (T*)z));
+  else
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_add<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream), (const T*)a,
+                                           (const T*)b, n, relu, (T*)z));
   return launch_rc("acfe_add");
 }
 
@@ -289,11 +543,26 @@ __global__ void k_relu_bwd(const T* __restrict__ dy, const T* __restrict__ y, lo
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     st(dx, i, ld(y, i) > 0.f ? ld(dy, i) : 0.f);
 }
+template <typename T>
+__global__ void k_relu_bwd8(const T* __restrict__ dy, const T* __restrict__ y, unsigned nvec, T* __restrict__ dx) {
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    float g[8], yy[8];
+    ld8(dy + (size_t)v * 8, g);
+    ld8(y + (size_t)v * 8, yy);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+    st8(dx + (size_t)v * 8, g);
+  }
+}
 ACFE_API int acfe_relu_bwd(const void* dy, const void* y, long long n, void* dx, int dtype, void* stream) {
   if (!dy || !y || !dx || n < 0) return ACFE_E_INVAL;
   if (n == 0) return ACFE_OK;
-  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_relu_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
-                                         (const T*)dy, (const T*)y, n, (T*)dx));
+  if (vec_ok(n, 8, dy, y, dx))
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_relu_bwd8<T>, dim3(vgrid(n / 8)), dim3(256), 0, strm(stream),
+                                           (const T*)dy, (const T*)y, (unsigned)(n / 8), (T*)dx));
+  else
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_relu_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                           (const T*)dy, (const T*)y, n, (T*)dx));
   return launch_rc("acfe_relu_bwd");
 }
 
@@ -309,12 +578,29 @@ __global__ void k_dropout(const T* __restrict__ x, long long n, float rate, unsi
     st(y, i, keep ? ld(x, i) * scl : 0.f);
   }
 }
+template <typename T>
+__global__ void k_dropout8(const T* __restrict__ x, unsigned nvec, float rate, unsigned long long seed,
+                           T* __restrict__ y) {
+  const uint32_t thr = (uint32_t)fminf(rate * 4294967296.0f, 4294967295.0f);
+  const float scl = 1.0f / (1.0f - rate);
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    float f[8];
+    ld8(x + (size_t)v * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = hash_u32(seed, (uint64_t)v * 8 + j) >= thr ? f[j] * scl : 0.f;
+    st8(y + (size_t)v * 8, f);
+  }
+}
 ACFE_API int acfe_dropout(const void* x, long long n, float rate, unsigned long long seed, void* y, int dtype,
                           void* stream) {
   if (!x || !y || n < 0 || rate < 0.f || rate >= 1.f) return ACFE_E_INVAL;
   if (n == 0) return ACFE_OK;
-  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_dropout<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
-                                         (const T*)x, n, rate, seed, (T*)y));
+  if (vec_ok(n, 8, x, y))
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_dropout8<T>, dim3(vgrid(n / 8)), dim3(256), 0, strm(stream),
+                                           (const T*)x, (unsigned)(n / 8), rate, seed, (T*)y));
+  else
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_dropout<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
+                                           (const T*)x, n, rate, seed, (T*)y));
   return launch_rc("acfe_dropout");
 }
 
@@ -365,12 +651,100 @@ __global__ void k_maxpool_bwd(const T* __restrict__ x, const T* __restrict__ dy,
     st(dx, i, g);
   }
 }
+// vectorised: one thread per (output window, 8 channels)
+template <typename T, int KH, int KW>
+__global__ void __launch_bounds__(256) k_maxpool8(const T* __restrict__ x, int N, int H, int W, int C, int P, int Q,
+                                                  T* __restrict__ y) {
+  const int CV = C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < total; v += gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    unsigned t = v / CV;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < KH; ++a)
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
+        float f[8];
+        ld8(x + (((size_t)n * H + p * KH + a) * W + q * KW + b) * C + cv * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], f[j]);
+      }
+    st8(y + (size_t)v * 8, m);
+  }
+}
+template <typename T, int KH, int KW>
+__global__ void __launch_bounds__(256) k_maxpool_bwd8(const T* __restrict__ x, const T* __restrict__ dy, int N,
+                                                      int H, int W, int C, int P, int Q, T* __restrict__ dx) {
+  const int CV = C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < total; v += gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    unsigned t = v / CV;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float f[KH * KW][8], m[8], g[8];
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY, am[j] = 0;
+#pragma unroll
+    for (int a = 0; a < KH; ++a)
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
+        ld8(x + (((size_t)n * H + p * KH + a) * W + q * KW + b) * C + cv * 8, f[a * KW + b]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[a * KW + b][j] > m[j]) m[j] = f[a * KW + b][j], am[j] = a * KW + b;
+      }
+    ld8(dy + (size_t)v * 8, g);
+#pragma unroll
+    for (int a = 0; a < KH; ++a)
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = am[j] == a * KW + b ? g[j] : 0.f;
+        st8(dx + (((size_t)n * H + p * KH + a) * W + q * KW + b) * C + cv * 8, o);
+      }
+    // leftover columns / rows of a non-divisible input receive zero gradient
+    const float z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q == Q - 1)
+      for (int a = 0; a < KH; ++a)
+        for (int w = Q * KW; w < W; ++w) st8(dx + (((size_t)n * H + p * KH + a) * W + w) * C + cv * 8, z);
+    if (p == P - 1)
+      for (int h = P * KH; h < H; ++h) {
+        for (int w = q * KW; w < q * KW + KW; ++w) st8(dx + (((size_t)n * H + h) * W + w) * C + cv * 8, z);
+        if (q == Q - 1)
+          for (int w = Q * KW; w < W; ++w) st8(dx + (((size_t)n * H + h) * W + w) * C + cv * 8, z);
+      }
+  }
+}
+#define MAXPOOL_SHAPES(X) X(1, 2) X(2, 2) X(3, 3)
+
 ACFE_API int acfe_maxpool2d(const void* x, int N, int H, int W, int C, int kh, int kw, void* y, int dtype,
                             void* stream) {
   if (!x || !y || N < 0 || kh <= 0 || kw <= 0 || H < kh || W < kw) return ACFE_E_INVAL;
   const int P = H / kh, Q = W / kw;
   const long long n = (long long)N * P * Q * C;
   if (n == 0) return ACFE_OK;
+  if (vec_ok((long long)N * H * W * C, C, x, y) && (long long)N * P * Q * (C / 8) < 0xFFFFFFFFll) {
+#define MP(A, B)                                                                                             \
+  if (kh == A && kw == B) {                                                                                  \
+    DISPATCH1(dtype, T, hipLaunchKernelGGL((k_maxpool8<T, A, B>), dim3(vgrid(n / 8)), dim3(256), 0,          \
+                                           strm(stream), (const T*)x, N, H, W, C, P, Q, (T*)y));             \
+    return launch_rc("acfe_maxpool2d");                                                                      \
+  }
+    MAXPOOL_SHAPES(MP)
+#undef MP
+  }
   DISPATCH1(dtype, T, hipLaunchKernelGGL(k_maxpool<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream), (const T*)x,
                                          N, H, W, C, kh, kw, P, Q, (T*)y));
   return launch_rc("acfe_maxpool2d");
@@ -381,6 +755,17 @@ ACFE_API int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int
   const int P = H / kh, Q = W / kw;
   const long long n = (long long)N * H * W * C;
   if (n == 0) return ACFE_OK;
+  if (vec_ok(n, C, x, dy, dx) && (long long)N * P * Q * (C / 8) < 0xFFFFFFFFll && P > 0 && Q > 0) {
+    const long long nw = (long long)N * P * Q * (C / 8);
+#define MPB(A, B)                                                                                           \
+  if (kh == A && kw == B) {                                                                                 \
+    DISPATCH1(dtype, T, hipLaunchKernelGGL((k_maxpool_bwd8<T, A, B>), dim3(vgrid(nw)), dim3(256), 0,        \
+                                           strm(stream), (const T*)x, (const T*)dy, N, H, W, C, P, Q, (T*)dx)); \
+    return launch_rc("acfe_maxpool2d_bwd");                                                                 \
+  }
+    MAXPOOL_SHAPES(MPB)
+#undef MPB
+  }
   DISPATCH1(dtype, T, hipLaunchKernelGGL(k_maxpool_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
                                          (const T*)x, (const T*)dy, N, H, W, C, kh, kw, P, Q, (T*)dx));
   return launch_rc("acfe_maxpool2d_bwd");
@@ -713,9 +1098,23 @@ __global__ void k_cast(const TI* __restrict__ x, long long n, TO* __restrict__ y
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     st(y, i, ld(x, i));
 }
+template <typename TI, typename TO>
+__global__ void k_cast8(const TI* __restrict__ x, unsigned nvec, TO* __restrict__ y) {
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    float f[8];
+    ld8(x + (size_t)v * 8, f);
+    st8(y + (size_t)v * 8, f);
+  }
+}
 ACFE_API int acfe_cast(const void* x, int x_dtype, long long n, void* y, int y_dtype, void* stream) {
   if (!x || !y || n < 0) return ACFE_E_INVAL;
   if (n == 0) return ACFE_OK;
+  if (vec_ok(n, 8, x, y)) {
+    DISPATCH1(x_dtype, TI, DISPATCH1(y_dtype, TO,
+        hipLaunchKernelGGL((k_cast8<TI, TO>), dim3(vgrid(n / 8)), dim3(256), 0, strm(stream), (const TI*)x,
+                           (unsigned)(n / 8), (TO*)y)));
+    return launch_rc("acfe_cast");
+  }
   DISPATCH1(x_dtype, TI, DISPATCH1(y_dtype, TO,
       hipLaunchKernelGGL((k_cast<TI, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream), (const TI*)x, n,
                          (TO*)y)));
@@ -723,13 +1122,13 @@ ACFE_API int acfe_cast(const void* x, int x_dtype, long long n, void* y, int y_d
 }
 
 // out[c] = beta*out[c] + sum_rows x[r][c]  (bias gradients); part: bn_stats slab
-__global__ void k_chan_sum_fin(const double* __restrict__ part, int nrows, int C, float beta,
-                               float* __restrict__ out) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int r = 0; r < nrows; ++r) s += part[((long long)r * 2) * C + c];
-  out[c] = beta != 0.f ? out[c] * beta + (float)s : (float)s;
+__global__ void __launch_bounds__(256) k_chan_sum_fin(const double* __restrict__ part, int nrows, int C, float beta,
+                                                      float* __restrict__ out) {
+  __shared__ double s[2][32];
+  slab_sum32(part, nrows, C, C, s);
+  const int c = blockIdx.x * 32 + threadIdx.x;
+  if (threadIdx.x >= 32 || c >= C) return;
+  out[c] = beta != 0.f ? out[c] * beta + (float)s[0][threadIdx.x] : (float)s[0][threadIdx.x];
 }
 ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* part, float* out,
                               float beta, void* stream) {
@@ -737,7 +1136,7 @@ ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, d
   if (rows == 0) return hip_rc(hipMemsetAsync(out, 0, sizeof(float) * C, strm(stream)), "acfe_channel_sum");
   int rc = acfe_bn_stats(x, rows, C, dtype, part, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 64)), dim3(64), 0, strm(stream), part, red_blocks(rows), C, beta,
+  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, red_blocks(rows), C, beta,
                      out);
   return launch_rc("acfe_channel_sum");
 }

@@ -161,8 +161,9 @@ int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy,
                       int stride, int pad_top, int pad_left, int P, int Q, float* dw, float beta, int dtype,
                       float* workspace, void* stream);
 
-/* Stem convolution with one (folded) input channel and 16 outputs: the three
- * identical channels of tfdataset.py:2053 are folded by weff = sum_c w[...,c]. */
+/* Stem convolution with one (folded) input channel and 16 outputs ("same",
+ * stride 1, R = S = 5 (wr_resnet_bird) or 3 (wr_resnet)): the three identical
+ * channels of tfdataset.py:2053 are folded by weff = sum_c w[...,c]. */
 int acfe_stem_blocks(int N, int H, int W);
 int acfe_stem_fold_weights(const float* w_krsc, int K, int R, int S, int C, float* weff, void* stream);
 int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int R, int S, int pad_top, int pad_left,
