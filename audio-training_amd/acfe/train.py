@@ -55,6 +55,21 @@ def mix_labels(y1: torch.Tensor, y2: torch.Tensor, lam: torch.Tensor, single_lab
     return y1 * lw + y2 * (1 - lw)
 
 
+def allreduce_mean_(flat: torch.Tensor, group=None) -> float:
+    """Sum-all-reduce the flat gradient arena in place (RCCL on the GPU, gloo in
+    the CPU tests); returns the factor (1/world) that turns the sum into the
+    mean of the replicas' batch-mean gradients, applied inside the Adam kernel."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1.0
+    world = dist.get_world_size(group)
+    if world == 1:
+        return 1.0
+    dist.all_reduce(flat, group=group)
+    return 1.0 / world
+
+
 class Trainer:
     """Holds the front end, the model, one flat parameter arena for both, and
     Keras-Adam; `step` runs one full training iteration on device tensors."""
@@ -81,12 +96,7 @@ class Trainer:
         loss, dz = ops.loss_and_grad(z, y, self.loss_mode)
         self.arena.zero_grad()
         z.backward(dz)
-        scale = 1.0
-        if self.world > 1:
-            import torch.distributed as dist
-
-            dist.all_reduce(self.arena.grad, group=self.pg)
-            scale = 1.0 / self.world
+        scale = allreduce_mean_(self.arena.grad, self.pg)
         self.opt.step(grad_scale=scale)
         return loss, z
 

@@ -39,6 +39,11 @@ struct ConvGeom {
   long long M;       // N*P*Q
 };
 
+// 64 bytes of zeros in global memory: im2col taps that fall into the padding
+// (or past the last pixel) load from here, so every load is unconditional
+// (no branch around the load, no select after it).
+__device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
+
 template <typename T> struct TT;
 template <> struct TT<uint16_t> { static constexpr int GR = 8, BK = 64; };
 template <> struct TT<float> { static constexpr int GR = 4, BK = 32; };
@@ -86,9 +91,10 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
   const int n0 = blockIdx.y * BN;
   const int nkt = g.Kdp / BK;
   const long long PQ = (long long)g.P * g.Q;
-  double s1d[FN], s2d[FN];
-#pragma unroll
-  for (int i = 0; i < FN; ++i) s1d[i] = s2d[i] = 0.0;
+  __shared__ double sstat[2][BN];  // per-block BN statistics (sum, sum of squares)
+  if (stats)
+    for (int i = tid; i < 2 * BN; i += 256) (&sstat[0][0])[i] = 0.0;
+  const T* zp = reinterpret_cast<const T*>(g_zero_page);
 
   for (int tm = blockIdx.x; tm < tiles_m; tm += gridDim.x) {
     const long long m0 = (long long)tm * BM;
@@ -115,7 +121,7 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
       s = rs - r * g.S;
     }
     uint4 ra[RA], rb[RB];
-    auto gload = [&](int kt) {
+    auto gload = [&](int kt) __attribute__((always_inline)) {
       if constexpr (FAST_A) {
         const bool kv = kk0 < g.Kd;
         const int off = (r * g.W + s) * g.C + c0;
@@ -123,9 +129,7 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
         for (int i = 0; i < RA; ++i) {
           const int h = h0[i] + r, w = w0[i] + s;
           const bool ok = kv && mv[i] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-          const T* src = ok ? rowp[i] + off : X;
-          const uint4 v = *reinterpret_cast<const uint4*>(src);
-          ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
+          ra[i] = *reinterpret_cast<const uint4*>(ok ? rowp[i] + off : zp);
         }
       } else {
 #pragma unroll
@@ -149,7 +153,7 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
       for (int i = 0; i < RB; ++i)
         rb[i] = *reinterpret_cast<const uint4*>(Wp + (long long)(n0 + rr + 32 * i) * g.Kdp + kt * BK + gc * GR);
     };
-    auto advance = [&]() {
+    auto advance = [&]() __attribute__((always_inline)) {
       kk0 += BK;
       if constexpr (FAST_A) {
         c0 += BK;
@@ -159,7 +163,7 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
         }
       }
     };
-    auto sstore = [&](int buf) {
+    auto sstore = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < RA; ++i)
         *reinterpret_cast<uint4*>(As + (buf * BM + rr + 32 * i) * LR + gc * GR) = ra[i];
@@ -224,8 +228,16 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
             t2 += f * f;
           }
         }
-      s1d[fn] += t1;
-      s2d[fn] += t2;
+      if (stats) {
+        t1 += __shfl_xor(t1, 16, 64);
+        t1 += __shfl_xor(t1, 32, 64);
+        t2 += __shfl_xor(t2, 16, 64);
+        t2 += __shfl_xor(t2, 32, 64);
+        if (lane < 16) {
+          atomicAdd(&sstat[0][col], (double)t1);
+          atomicAdd(&sstat[1][col], (double)t2);
+        }
+      }
     }
     __syncthreads();
     constexpr int GPR = BN / GR;
@@ -247,30 +259,201 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
     __syncthreads();
   }
   if (stats) {
-    double* red = reinterpret_cast<double*>(smem);  // [WM][2][BN]
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + n0 + c] = sstat[0][c];
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + n0 + c] = sstat[1][c];
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------ forward, LDS-DMA staged
+// C % GR == 0 path.  Each K-tile (BK elements = 128 B per row) of the im2col A
+// tile and of the packed weight tile is copied HBM/L2 -> LDS by
+// global_load_lds_dwordx4 (no staging VGPRs, no ds_write).  One wave
+// instruction fills 8 rows x 128 B lane-linearly; lane l holds row l>>3, LDS
+// slot l&7, and fetches global granule (l&7) ^ (row&7): the XOR swizzle lives on
+// the source address, so the 16-lane ds_read_b128 fragment reads (granule g of
+// row r at slot g ^ (r&7)) are bank-conflict free.  Two LDS buffers, prefetch
+// of tile t+1 issued before the MFMAs of tile t, one vmcnt(0)+barrier per tile.
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+template <typename T, int BM, int BN>
+constexpr int conv_g_smem() {
+  constexpr int a = 2 * (BM + BN) * 128;
+  constexpr int b = BM * (BN + TT<T>::GR) * (int)sizeof(T);
+  return a > b ? a : b;
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256)
+k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const float* __restrict__ bias,
+             T* __restrict__ Y, double* __restrict__ stats, int tiles_m) {
+  constexpr int GR = TT<T>::GR, BK = TT<T>::BK, LC = BN + GR;
+  static_assert(BK * (int)sizeof(T) == 128, "128-byte K rows");
+  constexpr int AJ = BM / 32, BJ = BN / 32;
+  constexpr int TWM = BM / WM, TWN = BN / WN, FM = TWM / 16, FN = TWN / 16;
+  constexpr int KF = 4 * GR;
+  static_assert(WM * WN == 4 && BN >= 32 && FM >= 1 && FN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[conv_g_smem<T, BM, BN>()];
+  __shared__ double sstat[2][BN];
+  unsigned char* As = smem;                   // [2][BM][128 B]
+  unsigned char* Bs = smem + 2 * BM * 128;    // [2][BN][128 B]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int lrow = lane >> 3;                       // row within an 8-row wave piece
+  const int gsw = (lane & 7) ^ (lrow & 7);          // granule column this lane fetches
+  const int n0 = blockIdx.y * BN;
+  const int nkt = g.Kdp / BK;
+  const long long PQ = (long long)g.P * g.Q;
+  const T* zp = reinterpret_cast<const T*>(g_zero_page);
+  if (stats)
+    for (int i = tid; i < 2 * BN; i += 256) (&sstat[0][0])[i] = 0.0;
+  const T* wrow[BJ];
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) wrow[j] = Wp + (long long)(n0 + (wid * BJ + j) * 8 + lrow) * g.Kdp + gsw * GR;
+
+  for (int tm = blockIdx.x; tm < tiles_m; tm += gridDim.x) {
+    const long long m0 = (long long)tm * BM;
+    const T* rowp[AJ];
+    int h0[AJ], w0[AJ];
+    bool mv[AJ];
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const long long m = m0 + (wid * AJ + j) * 8 + lrow;
+      mv[j] = m < g.M;
+      const long long mm = mv[j] ? m : 0;
+      const int n = (int)(mm / PQ);
+      const int rem = (int)(mm - (long long)n * PQ);
+      const int p = rem / g.Q, q = rem - (rem / g.Q) * g.Q;
+      h0[j] = p * g.st - g.pt;
+      w0[j] = q * g.st - g.pl;
+      rowp[j] = X + (((long long)n * g.H + h0[j]) * g.W + w0[j]) * g.C;
+    }
+    int kk0 = gsw * GR, c0, r, s;
+    {
+      const int rs = kk0 / g.C;
+      c0 = kk0 - rs * g.C;
+      r = rs / g.S;
+      s = rs - r * g.S;
+    }
+#define CONV_G_ISSUE(KT, BUF)                                                                     \
+    {                                                                                             \
+      const bool kv = kk0 < g.Kd;                                                                 \
+      const int off = (r * g.W + s) * g.C + c0;                                                   \
+      _Pragma("unroll") for (int j = 0; j < AJ; ++j) {                                            \
+        const int h = h0[j] + r, w = w0[j] + s;                                                   \
+        const bool ok = kv && mv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W; \
+        glds16(ok ? (const void*)(rowp[j] + off) : (const void*)zp,                              \
+               As + ((BUF) * BM + (wid * AJ + j) * 8) * 128);                                     \
+      }                                                                                           \
+      _Pragma("unroll") for (int j = 0; j < BJ; ++j)                                              \
+        glds16(wrow[j] + (KT) * BK, Bs + ((BUF) * BN + (wid * BJ + j) * 8) * 128);                \
+      kk0 += BK;                                                                                  \
+      c0 += BK;                                                                                   \
+      while (c0 >= g.C) {                                                                         \
+        c0 -= g.C;                                                                                \
+        if (++s == g.S) { s = 0; ++r; }                                                           \
+      }                                                                                           \
+    }
+    f4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    CONV_G_ISSUE(0, 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nkt) CONV_G_ISSUE(kt + 1, buf ^ 1)
+      const unsigned char* Ab = As + buf * BM * 128;
+      const unsigned char* Bb = Bs + buf * BN * 128;
+#pragma unroll
+      for (int kk = 0; kk < BK / KF; ++kk) {
+        const int gi = kk * 4 + (lane >> 4);
+        uint4 af[FM], bfr[FN];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int row = wm * TWM + fm * 16 + (lane & 15);
+          af[fm] = *reinterpret_cast<const uint4*>(Ab + row * 128 + ((gi ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int row = wn * TWN + fn * 16 + (lane & 15);
+          bfr[fn] = *reinterpret_cast<const uint4*>(Bb + row * 128 + ((gi ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], af[fm], bfr[fn], T());
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+#undef CONV_G_ISSUE
+    // ---- epilogue: +bias, round, BN statistics of the rounded values, LDS-staged 16-B row stores
+    T* Cs = reinterpret_cast<T*>(smem);
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      double a = s1d[fn], b = s2d[fn];
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      b += __shfl_xor(b, 16, 64);
-      b += __shfl_xor(b, 32, 64);
-      if (lane < 16) {
-        const int col = wn * TWN + fn * 16 + lane;
-        red[(wm * 2 + 0) * BN + col] = a;
-        red[(wm * 2 + 1) * BN + col] = b;
+      const int col = wn * TWN + fn * 16 + (lane & 15);
+      const int gcn = n0 + col;
+      const float bv = (bias && gcn < g.K) ? bias[gcn] : 0.f;
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = wm * TWM + fm * 16 + (lane >> 4) * 4 + j;
+          const T tv = cvt_out(acc[fm][fn][j] + bv, T());
+          Cs[row * LC + col] = tv;
+          if (m0 + row < g.M) {
+            const float f = to_f(tv);
+            t1 += f;
+            t2 += f * f;
+          }
+        }
+      if (stats) {
+        t1 += __shfl_xor(t1, 16, 64);
+        t1 += __shfl_xor(t1, 32, 64);
+        t2 += __shfl_xor(t2, 16, 64);
+        t2 += __shfl_xor(t2, 32, 64);
+        if (lane < 16) {
+          atomicAdd(&sstat[0][col], (double)t1);
+          atomicAdd(&sstat[1][col], (double)t2);
+        }
       }
     }
     __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        a += red[(w * 2 + 0) * BN + c];
-        b += red[(w * 2 + 1) * BN + c];
+    constexpr int GPR = BN / GR;
+    if (n0 + BN <= g.K && (g.ldy % GR) == 0) {
+      for (int idx = tid; idx < BM * GPR; idx += 256) {
+        const int row = idx / GPR, cg = idx - (idx / GPR) * GPR;
+        const long long m = m0 + row;
+        if (m < g.M)
+          *reinterpret_cast<uint4*>(Y + m * g.ldy + n0 + cg * GR) =
+              *reinterpret_cast<const uint4*>(Cs + row * LC + cg * GR);
       }
-      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + n0 + c] = a;
-      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + n0 + c] = b;
+    } else {
+      for (int idx = tid; idx < BM * BN; idx += 256) {
+        const int row = idx / BN, col = idx - (idx / BN) * BN;
+        const long long m = m0 + row;
+        if (m < g.M && n0 + col < g.K) Y[m * g.ldy + n0 + col] = Cs[row * LC + col];
+      }
+    }
+    __syncthreads();
+  }
+  if (stats) {
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + n0 + c] = sstat[0][c];
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + n0 + c] = sstat[1][c];
     }
   }
 }
@@ -367,7 +550,7 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
   }
   constexpr int DGPR = BMW / GR;
   uint4 rd[DPT], rx[XPT];
-  auto gload = [&](int step) {
+  auto gload = [&](int step) __attribute__((always_inline)) {
     const long long mb = mbeg + (long long)step * BR;
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
@@ -377,9 +560,8 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
       const bool ok = idx < DG && m < mend;
       if constexpr (FAST_D) {
         const bool okk = ok && (k0 + cg * GR) < g.K;
-        const T* src = okk ? dY + m * g.ldy + k0 + cg * GR : dY;
-        const uint4 v = *reinterpret_cast<const uint4*>(src);
-        rd[i] = okk ? v : make_uint4(0, 0, 0, 0);
+        rd[i] = *reinterpret_cast<const uint4*>(okk ? dY + m * g.ldy + k0 + cg * GR
+                                                    : reinterpret_cast<const T*>(g_zero_page));
       } else {
         T e[GR];
 #pragma unroll
@@ -398,9 +580,8 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
       const int h = xp[i] * g.st - g.pt + xr[i], w = xq[i] * g.st - g.pl + xs[i];
       const bool ok = xkv[i] && m < mend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       if constexpr (FAST_X) {
-        const T* src = ok ? X + (((long long)xn[i] * g.H + h) * g.W + w) * g.C + xc[i] : X;
-        const uint4 v = *reinterpret_cast<const uint4*>(src);
-        rx[i] = ok ? v : make_uint4(0, 0, 0, 0);
+        rx[i] = *reinterpret_cast<const uint4*>(ok ? X + (((long long)xn[i] * g.H + h) * g.W + w) * g.C + xc[i]
+                                                   : reinterpret_cast<const T*>(g_zero_page));
       } else {
         T e[GR];
         const int cg = (tid + 256 * i) - xrow[i] * XGPR;
@@ -418,7 +599,7 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
       }
     }
   };
-  auto advance = [&]() {
+  auto advance = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       xq[i] += BR;
@@ -428,7 +609,7 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
       }
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
       const int idx = tid + 256 * i;
@@ -559,7 +740,7 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
   const int tiles_m = (int)((g.M + 127) / 128);
   dim3 grid(grid_m, g.Kp / BN);
   if (g.C % TT<T>::GR == 0)
-    hipLaunchKernelGGL((k_conv_fwd<T, 128, BN, WM, WN, true>), grid, dim3(256), 0, s, g, (const T*)x,
+    hipLaunchKernelGGL((k_conv_fwd_g<T, 128, BN, WM, WN>), grid, dim3(256), 0, s, g, (const T*)x,
                        (const T*)wp, bias, (T*)y, stats, tiles_m);
   else
     hipLaunchKernelGGL((k_conv_fwd<T, 128, BN, WM, WN, false>), grid, dim3(256), 0, s, g, (const T*)x,
@@ -816,22 +997,23 @@ k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int pt, int pl,
 }
 
 // dx[n,h,w] = sum_{k,r,s} dy[n, h + pt - r, w + pl - s, k] * weff[k][r][s]
+// LDS image channel-major (gs[k][pos]) so the 64 lanes of a wave, which own
+// consecutive pixels, read consecutive words for every (k, r, s).
 template <typename TG, typename TO, int R, int S>
 __global__ void __launch_bounds__(256)
 k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int pt, int pl,
              const float* __restrict__ weff, TO* __restrict__ dx, int tiles_h, int tiles_w) {
-  __shared__ float gs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1) * STEM_K];
-  __shared__ float wsm[STEM_K * STEM_MAXR * STEM_MAXR];
+  constexpr int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1, XP = XH * XW + 1;
+  __shared__ float gs[STEM_K * XP];
+  __shared__ float wsm[STEM_K * R * S];
   const int tid = threadIdx.x;
   for (int i = tid; i < STEM_K * R * S; i += 256) wsm[i] = weff[i];
-  const int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1;
   const long long ntiles = (long long)N * tiles_h * tiles_w;
   for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int tw = (int)(t % tiles_w);
     const int th = (int)((t / tiles_w) % tiles_h);
     const int n = (int)(t / ((long long)tiles_w * tiles_h));
     const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
-    // gs covers dy rows h0 - (R-1-pt) .. , cols w0 - (S-1-pl) ..
     const int gh0 = h0 - (R - 1 - pt), gw0 = w0 - (S - 1 - pl);
     __syncthreads();
     for (int i = tid; i < XH * XW * STEM_K; i += 256) {
@@ -841,7 +1023,7 @@ k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int pt, int pl,
       float v = 0.f;
       if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
         v = to_f(dy[(((long long)n * H + h) * W + w) * STEM_K + k]);
-      gs[i] = v;
+      gs[k * XP + pos] = v;
     }
     __syncthreads();
     for (int pix = tid; pix < STEM_TH * STEM_TW; pix += 256) {
@@ -852,10 +1034,10 @@ k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int pt, int pl,
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const float* gp = &gs[((py + R - 1 - r) * XW + px + S - 1 - s) * STEM_K];
+        for (int s2 = 0; s2 < S; ++s2) {
+          const int pos = (py + R - 1 - r) * XW + px + S - 1 - s2;
 #pragma unroll
-          for (int k = 0; k < STEM_K; ++k) a += gp[k] * wsm[(k * R + r) * S + s];
+          for (int k = 0; k < STEM_K; ++k) a += gs[k * XP + pos] * wsm[(k * R + r) * S + s2];
         }
       if (h < H && w < W) dx[((long long)n * H + h) * W + w] = cvt_out(a, TO());
     }
