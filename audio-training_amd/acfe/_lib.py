@@ -22,6 +22,7 @@ F64 = C.c_double
 SIGNATURES: dict[str, list] = {
     "acfe_version": [],
     "acfe_last_error": [],
+    "acfe_crc32c": [P, C.c_size_t, C.c_uint32],
     "acfe_mel_filterbank": [I32, I32, F64, F64, I32, F64, P],
     "acfe_plan_create": [I32, I32, I32, I32, F64, F64, F64, P, P],
     "acfe_plan_destroy": [P],
@@ -70,7 +71,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_loss": [P, P, I32, I32, I32, F32, P, P, P, P],
     "acfe_adam_step": [P, P, P, P, I64, F32, F32, F32, F32, F32, P],
 }
-_RESTYPES = {"acfe_last_error": C.c_char_p, "acfe_conv2d_wgrad_workspace": I64}
+_RESTYPES = {"acfe_last_error": C.c_char_p, "acfe_conv2d_wgrad_workspace": I64, "acfe_crc32c": C.c_uint32}
 
 PAD_END, PAD_CENTER_CONSTANT, PAD_CENTER_REFLECT = 0, 1, 2
 LAYOUT_BTM, LAYOUT_BMT = 0, 1

@@ -29,6 +29,9 @@ using namespace acfe;
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+// Native 16-byte vector for register staging (HIP's uint4 struct-with-union
+// defeats SROA: arrays of it were demoted to scratch).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvGeom {
   int N, H, W, C;    // input
@@ -501,13 +504,16 @@ __global__ void k_zero_insert(const T* __restrict__ dy, int N, int P, int Q, int
 
 // ------------------------------------------------------------------ wgrad
 // Block: 256 threads; output tile BMW (k rows) x 128 (rsc cols); reduction over
-// a contiguous chunk of m in steps of 32.  LDS images are m-major:
-// Ds[32][BMW + 16], Xs[32][128 + 16].
+// a contiguous chunk of pixels m in steps of BR (64 for bf16 = two MFMA
+// k-chunks per barrier, 32 for fp32).  LDS images are m-major:
+// Ds[BR][BMW + 16], Xs[BR][128 + 16]; register staging (straight-line code:
+// no closures, so the staging arrays stay in VGPRs), zero-page loads for
+// padding taps and tails.
 template <typename T, int BMW, bool FAST_D, bool FAST_X>
 __global__ void __launch_bounds__(256)
 k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, float* __restrict__ ws,
              long long chunk) {
-  constexpr int GR = TT<T>::GR, BNW = 128, BR = 32;
+  constexpr int GR = TT<T>::GR, BNW = 128, BR = sizeof(T) == 2 ? 64 : 32;
   constexpr int LDD = BMW + 16, LDX = BNW + 16;
   constexpr int WM = BMW >= 64 ? 2 : 1, WN = 4 / WM;
   constexpr int TWM = BMW / WM, TWN = BNW / WN, FM = TWM / 16, FN = TWN / 16;
@@ -524,9 +530,9 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
   if (mend > g.M) mend = g.M;
   const int nsteps = mbeg < mend ? (int)((mend - mbeg + BR - 1) / BR) : 0;
   const long long PQ = (long long)g.P * g.Q;
+  const T* zp = reinterpret_cast<const T*>(g_zero_page);
 
-  // X loader: thread -> XPT (row, col-granule) pairs; fixed col granule, rows advance by 32
-  constexpr int XGPR = BNW / GR;
+  constexpr int XGPR = BNW / GR, DGPR = BMW / GR;
   int xrow[XPT], xr[XPT], xs[XPT], xc[XPT], xn[XPT], xp[XPT], xq[XPT];
   bool xkv[XPT];
 #pragma unroll
@@ -548,10 +554,18 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
     xp[i] = rem / g.Q;
     xq[i] = rem - xp[i] * g.Q;
   }
-  constexpr int DGPR = BMW / GR;
-  uint4 rd[DPT], rx[XPT];
-  auto gload = [&](int step) __attribute__((always_inline)) {
-    const long long mb = mbeg + (long long)step * BR;
+  u32x4 rd[DPT], rx[XPT];
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  if (nsteps > 0) {
+#define STEPV 0
+#define BUFV 0
+
+  {
+    const long long mb = mbeg + (long long)(STEPV) * BR;
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
       const int idx = tid + 256 * i;
@@ -560,18 +574,16 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
       const bool ok = idx < DG && m < mend;
       if constexpr (FAST_D) {
         const bool okk = ok && (k0 + cg * GR) < g.K;
-        rd[i] = *reinterpret_cast<const uint4*>(okk ? dY + m * g.ldy + k0 + cg * GR
-                                                    : reinterpret_cast<const T*>(g_zero_page));
+        rd[i] = *reinterpret_cast<const u32x4*>(okk ? dY + m * g.ldy + k0 + cg * GR : zp);
       } else {
         T e[GR];
 #pragma unroll
         for (int j = 0; j < GR; ++j) {
           const int k = k0 + cg * GR + j;
           const bool okk = ok && k < g.K;
-          const T v = *(okk ? dY + m * g.ldy + k : dY);
-          e[j] = okk ? v : (T)0;
+          e[j] = *(okk ? dY + m * g.ldy + k : zp);
         }
-        rd[i] = *reinterpret_cast<const uint4*>(e);
+        rd[i] = *reinterpret_cast<const u32x4*>(e);
       }
     }
 #pragma unroll
@@ -580,8 +592,7 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
       const int h = xp[i] * g.st - g.pt + xr[i], w = xq[i] * g.st - g.pl + xs[i];
       const bool ok = xkv[i] && m < mend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       if constexpr (FAST_X) {
-        rx[i] = *reinterpret_cast<const uint4*>(ok ? X + (((long long)xn[i] * g.H + h) * g.W + w) * g.C + xc[i]
-                                                   : reinterpret_cast<const T*>(g_zero_page));
+        rx[i] = *reinterpret_cast<const u32x4*>(ok ? X + (((long long)xn[i] * g.H + h) * g.W + w) * g.C + xc[i] : zp);
       } else {
         T e[GR];
         const int cg = (tid + 256 * i) - xrow[i] * XGPR;
@@ -592,14 +603,11 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
           const int rs = kk / g.C, c = kk - rs * g.C, rq = rs / g.S, sq = rs - rq * g.S;
           const int hh = xp[i] * g.st - g.pt + rq, ww = xq[i] * g.st - g.pl + sq;
           okj = okj && (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
-          const T v = *(okj ? X + (((long long)xn[i] * g.H + hh) * g.W + ww) * g.C + c : X);
-          e[j] = okj ? v : (T)0;
+          e[j] = *(okj ? X + (((long long)xn[i] * g.H + hh) * g.W + ww) * g.C + c : zp);
         }
-        rx[i] = *reinterpret_cast<const uint4*>(e);
+        rx[i] = *reinterpret_cast<const u32x4*>(e);
       }
     }
-  };
-  auto advance = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       xq[i] += BR;
@@ -608,89 +616,163 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
         if (++xp[i] == g.P) { xp[i] = 0; ++xn[i]; }
       }
     }
-  };
-  auto sstore = [&](int buf) __attribute__((always_inline)) {
+  }
+
+  {
 #pragma unroll
     for (int i = 0; i < DPT; ++i) {
       const int idx = tid + 256 * i;
       if (idx < DG) {
         const int row = idx / DGPR, cg = idx - (idx / DGPR) * DGPR;
-        *reinterpret_cast<uint4*>(&Ds[buf][row * LDD + cg * GR]) = rd[i];
+        *reinterpret_cast<u32x4*>(&Ds[BUFV][row * LDD + cg * GR]) = rd[i];
       }
     }
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + 256 * i;
       const int cg = idx - xrow[i] * XGPR;
-      *reinterpret_cast<uint4*>(&Xs[buf][xrow[i] * LDX + cg * GR]) = rx[i];
+      *reinterpret_cast<u32x4*>(&Xs[BUFV][xrow[i] * LDX + cg * GR]) = rx[i];
     }
-  };
-  f4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  if (nsteps > 0) {
-    gload(0);
-    advance();
-    sstore(0);
+  }
+
+#undef STEPV
+#undef BUFV
   }
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
     const bool more = step + 1 < nsteps;
     if (more) {
-      gload(step + 1);
-      advance();
+#define STEPV (step + 1)
+
+  {
+    const long long mb = mbeg + (long long)(STEPV) * BR;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / DGPR, cg = idx - (idx / DGPR) * DGPR;
+      const long long m = mb + row;
+      const bool ok = idx < DG && m < mend;
+      if constexpr (FAST_D) {
+        const bool okk = ok && (k0 + cg * GR) < g.K;
+        rd[i] = *reinterpret_cast<const u32x4*>(okk ? dY + m * g.ldy + k0 + cg * GR : zp);
+      } else {
+        T e[GR];
+#pragma unroll
+        for (int j = 0; j < GR; ++j) {
+          const int k = k0 + cg * GR + j;
+          const bool okk = ok && k < g.K;
+          e[j] = *(okk ? dY + m * g.ldy + k : zp);
+        }
+        rd[i] = *reinterpret_cast<const u32x4*>(e);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const long long m = mb + xrow[i];
+      const int h = xp[i] * g.st - g.pt + xr[i], w = xq[i] * g.st - g.pl + xs[i];
+      const bool ok = xkv[i] && m < mend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      if constexpr (FAST_X) {
+        rx[i] = *reinterpret_cast<const u32x4*>(ok ? X + (((long long)xn[i] * g.H + h) * g.W + w) * g.C + xc[i] : zp);
+      } else {
+        T e[GR];
+        const int cg = (tid + 256 * i) - xrow[i] * XGPR;
+#pragma unroll
+        for (int j = 0; j < GR; ++j) {
+          const int kk = c0blk + cg * GR + j;
+          bool okj = kk < g.Kd && m < mend;
+          const int rs = kk / g.C, c = kk - rs * g.C, rq = rs / g.S, sq = rs - rq * g.S;
+          const int hh = xp[i] * g.st - g.pt + rq, ww = xq[i] * g.st - g.pl + sq;
+          okj = okj && (unsigned)hh < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+          e[j] = *(okj ? X + (((long long)xn[i] * g.H + hh) * g.W + ww) * g.C + c : zp);
+        }
+        rx[i] = *reinterpret_cast<const u32x4*>(e);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      xq[i] += BR;
+      while (xq[i] >= g.Q) {
+        xq[i] -= g.Q;
+        if (++xp[i] == g.P) { xp[i] = 0; ++xn[i]; }
+      }
+    }
+  }
+
+#undef STEPV
     }
     const int buf = step & 1;
-    if constexpr (sizeof(T) == 2) {
-      // MFMA k-slot (g = lane>>4, j) <-> m: j<4: 4g+j, j>=4: 16+4g+(j-4)
-      const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-      bf8 af[FM], bfr[FN];
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const int col = wm * TWM + fm * 16 + 4 * p;
+    for (int kc = 0; kc < BR / 32; ++kc) {
+      if constexpr (sizeof(T) == 2) {
+        // MFMA k-slot (g = lane>>4, j) <-> m: j<4: 4g+j, j>=4: 16+4g+(j-4)  (within this 32-row chunk)
+        const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+        const int rb = kc * 32;
         typedef __attribute__((address_space(3))) bf4* lp;
-        const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lp)(reinterpret_cast<const __bf16*>(&Ds[buf][(4 * grp + q) * LDD + col])));
-        const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lp)(reinterpret_cast<const __bf16*>(&Ds[buf][(16 + 4 * grp + q) * LDD + col])));
-        af[fm] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
+        bf8 af[FM], bfr[FN];
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int col = wn * TWN + fn * 16 + 4 * p;
-        typedef __attribute__((address_space(3))) bf4* lp;
-        const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lp)(reinterpret_cast<const __bf16*>(&Xs[buf][(4 * grp + q) * LDX + col])));
-        const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lp)(reinterpret_cast<const __bf16*>(&Xs[buf][(16 + 4 * grp + q) * LDX + col])));
-        bfr[fn] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
+        for (int fm = 0; fm < FM; ++fm) {
+          const int col = wm * TWM + fm * 16 + 4 * p;
+          const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(&Ds[buf][(rb + 4 * grp + q) * LDD + col])));
+          const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(&Ds[buf][(rb + 16 + 4 * grp + q) * LDD + col])));
+          af[fm] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int k4 = 0; k4 < BR / 4; ++k4) {
-        const int mrow = k4 * 4 + (lane >> 4);
-        float a[FM], b[FN];
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-          a[fm] = reinterpret_cast<const float*>(Ds[buf])[mrow * LDD + wm * TWM + fm * 16 + (lane & 15)];
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          b[fn] = reinterpret_cast<const float*>(Xs[buf])[mrow * LDX + wn * TWN + fn * 16 + (lane & 15)];
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = wn * TWN + fn * 16 + 4 * p;
+          const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(&Xs[buf][(rb + 4 * grp + q) * LDX + col])));
+          const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(&Xs[buf][(rb + 16 + 4 * grp + q) * LDX + col])));
+          bfr[fn] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
           for (int fn = 0; fn < FN; ++fn)
-            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int k4 = 0; k4 < 8; ++k4) {
+          const int mrow = kc * 32 + k4 * 4 + (lane >> 4);
+          float a[FM], b[FN];
+#pragma unroll
+          for (int fm = 0; fm < FM; ++fm)
+            a[fm] = reinterpret_cast<const float*>(Ds[buf])[mrow * LDD + wm * TWM + fm * 16 + (lane & 15)];
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn)
+            b[fn] = reinterpret_cast<const float*>(Xs[buf])[mrow * LDX + wn * TWN + fn * 16 + (lane & 15)];
+#pragma unroll
+          for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+              acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
+        }
       }
     }
-    if (more) sstore(buf ^ 1);
+    if (more) {
+#define BUFV (buf ^ 1)
+
+  {
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < DG) {
+        const int row = idx / DGPR, cg = idx - (idx / DGPR) * DGPR;
+        *reinterpret_cast<u32x4*>(&Ds[BUFV][row * LDD + cg * GR]) = rd[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 256 * i;
+      const int cg = idx - xrow[i] * XGPR;
+      *reinterpret_cast<u32x4*>(&Xs[BUFV][xrow[i] * LDX + cg * GR]) = rx[i];
+    }
+  }
+
+#undef BUFV
+    }
     __syncthreads();
   }
   // partial slab: ws[z][k][kk] (k < K, kk < Kd)
@@ -857,7 +939,7 @@ ACFE_API long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K
   const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
   long long splits = (1024 + tiles - 1) / tiles;
   long long chunk = (M + splits - 1) / splits;
-  chunk = (chunk + 31) / 32 * 32;
+  chunk = (chunk + 63) / 64 * 64;
   if (chunk < 512) chunk = 512;
   splits = (M + chunk - 1) / chunk;
   if (splits < 1) splits = 1;
@@ -893,7 +975,7 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
   long long splits = (1024 + tiles - 1) / tiles;
   long long chunk = (M + splits - 1) / splits;
-  chunk = (chunk + 31) / 32 * 32;
+  chunk = (chunk + 63) / 64 * 64;
   if (chunk < 512) chunk = 512;
   splits = (M + chunk - 1) / chunk;
   if (splits < 1) splits = 1;

@@ -63,6 +63,12 @@ int acfe_version(void);
 /* Last HIP error string (thread-local), for diagnostics. */
 const char* acfe_last_error(void);
 
+/* Host CRC-32C (Castagnoli) of n bytes continuing from `crc` (0 to start):
+ * the checksum of the TFRecord framing written by tf.io.TFRecordWriter
+ * (audiowriter.py:259-277) and read by tf.data.TFRecordDataset
+ * (tfdataset.py:212-214).  No GPU involved. */
+uint32_t acfe_crc32c(const void* data, size_t n, uint32_t crc);
+
 /* custommel.mel_f restated in C (float64 arithmetic, float32 result) into a
  * caller-owned HOST array out_host[n_mels][1 + n_fft/2]. */
 int acfe_mel_filterbank(int sr, int n_mels, double fmin, double fmax, int n_fft,

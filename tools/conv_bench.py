@@ -42,22 +42,36 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
+    from acfe._lib import call, lib
+    from acfe._torch import ptr, stream
+
     dev = torch.device("cuda", 0)
     for name, H, W, C, K, R, S in LAYERS:
         N = a.batch
-        x = (torch.randn((N, H, W, C), device=dev) * 0.5).to(torch.bfloat16).requires_grad_(True)
-        w = (torch.randn((K, R, S, C), device=dev) / (R * S * C) ** 0.5).requires_grad_(True)
-        b = torch.zeros(K, device=dev, requires_grad=True)
+        x = (torch.randn((N, H, W, C), device=dev) * 0.5).to(torch.bfloat16)
+        w = torch.randn((K, R, S, C), device=dev) / (R * S * C) ** 0.5
+        b = torch.zeros(K, device=dev)
+        P, pt = ops.same_padding(H, R, 1)
+        Q, pl = ops.same_padding(W, S, 1)
+        wp, wf = ops.pack_weights(w, torch.bfloat16, False), ops.pack_weights(w, torch.bfloat16, True)
+        y = torch.empty((N, P, Q, K), dtype=torch.bfloat16, device=dev)
+        dy = (torch.randn((N, P, Q, K), device=dev)).to(torch.bfloat16)
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(w)
+        rows = lib.acfe_conv2d_stats_rows(N * P * Q, K)
+        st = torch.empty((rows, 2, wp.shape[0]), dtype=torch.float64, device=dev)
+        wsz = lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, P, Q)
+        ws = torch.empty((wsz,), dtype=torch.float32, device=dev)
         flops = 2.0 * N * H * W * K * R * S * C
-        y, _ = ops.conv2d(x, w, b, 1, "same", want_stats=True)
-        gy = torch.randn_like(y)
-        t_f = timeit(lambda: ops.conv2d(x, w, b, 1, "same", want_stats=True), a.iters)
-        fn_b = lambda: torch.autograd.grad(ops.conv2d(x, w, b, 1, "same")[0], (x, w), gy)  # noqa: E731
-        t_fb = timeit(fn_b, a.iters)
-        t_b = t_fb - timeit(lambda: ops.conv2d(x, w, b, 1, "same"), a.iters)
-        print(f"{name:28s} fwd {t_f:8.3f} ms {flops / t_f / 1e9:8.1f} TF | bwd(dgrad+wgrad+db) {t_b:8.3f} ms "
-              f"{2 * flops / t_b / 1e9:8.1f} TF", flush=True)
-        del x, w, b, y, gy
+        t_f = timeit(lambda: call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, 1, pt, pl, P, Q, ptr(b),
+                                  ptr(y), 1, ptr(st), stream()), a.iters)
+        t_d = timeit(lambda: call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, 1, pt, pl, H, W,
+                                  ptr(dx), 1, None, stream()), a.iters)
+        t_w = timeit(lambda: call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, 1, pt, pl, P, Q,
+                                  ptr(dw), 0.0, 1, ptr(ws), stream()), a.iters)
+        print(f"{name:28s} fwd {t_f:7.3f} ms {flops / t_f / 1e9:7.1f} TF | dgrad {t_d:7.3f} ms "
+              f"{flops / t_d / 1e9:7.1f} TF | wgrad {t_w:7.3f} ms {flops / t_w / 1e9:7.1f} TF", flush=True)
+        del x, w, y, dy, dx, dw, ws, st
         torch.cuda.empty_cache()
 
 
