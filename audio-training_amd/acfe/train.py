@@ -48,6 +48,20 @@ class FrontEnd(nn.Module):
         return ops.cast(mel, self.dtype)
 
 
+    def forward_windows(self, rec, first, count, n=144000, hop=72000, pad_mode="constant", scope_minmax=None):
+        """Features of `count` overlapping windows of one device recording `rec`
+        (1-D fp32): window w covers rec[(first + w) * hop : ... + n].  The
+        streaming predict path (predict_utils.load_samples :53-148 slides 3 s
+        windows; here the windows are read in place via the clip stride)."""
+        view = rec[first * hop:]
+        st = fe.normalize_stats(view, n=n, clip_stride=hop, batch=count)
+        if self.pcen is not None:
+            mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="btm", n=n, clip_stride=hop, batch=count)
+            return self.pcen(mel, scope_minmax)
+        mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="bmt", n=n, clip_stride=hop, batch=count)
+        return ops.cast(mel, self.dtype)
+
+
 def mix_labels(y1: torch.Tensor, y2: torch.Tensor, lam: torch.Tensor, single_label=True) -> torch.Tensor:
     """Label half of tfdataset.mix_up (:946-954): hard lambda > 0.5 for single-label."""
     lw = (lam > 0.5).float() if single_label else lam

@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Training driver of the acfe path (reference audiomodel.py:117-567, CLI :2238-2414).
+
+  python audiomodel.py RUN_NAME -d DATA_DIR [--model-name wr-resnet-bird|wr-resnet]
+         [--epochs E] [--batch-size B] [--n_mels 128] [--multi-label false] [--lr 0.01]
+  multi-GPU:  python -m torch.distributed.run --nproc-per-node 8 audiomodel.py ...
+
+DATA_DIR is the directory holding training-data/ (build.py output):
+training-meta.json gives the labels; train/ and validation/ hold the GZIP
+TFRecord shards.  The reference flow (load_datasets -> build_model -> compile
+-> fit with checkpoints -> save metadata) becomes: tfdataset.get_dataset
+(raw audio batches, mix_up pairs when augmenting) -> acfe.train.FrontEnd (GPU
+normalize / mix_up / STFT / mel / PCEN) + resnet WRResNet -> acfe.train.Trainer
+(loss, backward, RCCL all-reduce, Adam) -> checkpoints/<run>/ {model.pt,
+metadata.txt}.  Dataset curation options of the reference (taxonomy remaps,
+cross-fold, rf/embeddings models) are out of scope.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
+
+import torch  # noqa: E402
+
+
+def str2bool(v):
+    if isinstance(v, bool):
+        return v
+    return str(v).lower() in ("yes", "true", "t", "y", "1")
+
+
+MODEL_NAMES = {"wr-resnet": "wr_resnet", "wr-resnet-bird": "wr_resnet_bird", "wr_resnet": "wr_resnet",
+               "wr_resnet_bird": "wr_resnet_bird"}
+
+
+def build_model(model_name, input_shape, classes, dtype, dropout=0.1):
+    """AudioModel.build_model for the wr-resnet branches (audiomodel.py:776-780)."""
+    kind = MODEL_NAMES[model_name]
+    if kind == "wr_resnet_bird":
+        from resnet.wr_resnet_bird import WRResNet
+    else:
+        from resnet.wr_resnet import WRResNet
+    return WRResNet(input_shape=input_shape, classes=classes, dtype=dtype, dropout=dropout)
+
+
+def load_meta(data_dir):
+    base = Path(data_dir)
+    for cand in (base / "training-meta.json", base / "training-data" / "training-meta.json"):
+        if cand.exists():
+            return json.loads(cand.read_text()), cand.parent
+    raise FileNotFoundError(f"training-meta.json not found under {data_dir}")
+
+
+def save_checkpoint(out_dir: Path, trainer, meta: dict, history: dict | None = None):
+    out_dir.mkdir(parents=True, exist_ok=True)
+    torch.save({k: v.detach().cpu() for k, v in trainer.holder.state_dict().items()}, out_dir / "model.pt")
+    m = dict(meta)
+    if history:
+        m["history"] = history
+    (out_dir / "metadata.txt").write_text(json.dumps(m, indent=2))
+
+
+def evaluate(trainer, dataset, multi_label):
+    """Validation loss / accuracy (Keras categorical or binary accuracy)."""
+    from acfe import ops
+
+    trainer.holder.eval()
+    n, loss_sum, correct = 0, 0.0, 0.0
+    with torch.no_grad():
+        for x, y in dataset:
+            z = trainer.model(trainer.frontend(x))
+            loss, _ = ops.loss_and_grad(z, y, trainer.loss_mode)
+            b = x.shape[0]
+            loss_sum += float(loss) * b
+            if multi_label:
+                correct += float(((z > 0).float() == y).float().mean(1).sum())
+            else:
+                correct += float((z.argmax(1) == y.argmax(1)).float().sum())
+            n += b
+    trainer.holder.train()
+    return (loss_sum / max(n, 1), correct / max(n, 1)) if n else (float("nan"), float("nan"))
+
+
+def train_model(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import tfdataset
+    from acfe.frontend import sample_mixup_lambda
+    from acfe.train import FrontEnd, Trainer, mix_labels
+
+    meta, td = load_meta(args.dataset_dir)
+    labels = list(meta["labels"])
+    n_mels = args.n_mels or meta.get("n_mels", 160)
+    fmin = args.fmin if args.fmin is not None else 100
+    fmax = args.fmax if args.fmax is not None else 11000
+    n_fft = args.n_fft or 4096
+    brk = args.break_freq or 1000
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(args.seed)
+    model = build_model(args.model_name, (n_mels, 513, 3), len(labels), dtype).to(dev)
+    if world > 1:
+        with torch.no_grad():
+            for t in list(model.parameters()) + list(model.buffers()):
+                dist.broadcast(t.data, 0)
+    frontend = FrontEnd(n_mels=n_mels, n_fft=n_fft, hop=281, fmin=fmin, fmax=fmax, break_freq=brk,
+                        pcen=args.pcen, dtype=dtype, device=dev).to(dev)
+    trainer = Trainer(model, frontend, lr=args.lr, loss="bce" if args.multi_label else "cce", device=dev)
+    if args.weights:
+        sd = torch.load(args.weights, map_location="cpu", weights_only=True)
+        trainer.holder.load_state_dict(sd)
+    files = tfdataset._files(td / "train")
+    files = files[rank::world] if world > 1 else files
+    train_ds = tfdataset.AudioDataset(files, labels, batch_size=args.batch_size, shuffle=args.shuffle,
+                                      augment=args.augment, device=dev, drop_remainder=world > 1, seed=args.seed)
+    val_dir = td / "validation"
+    val_ds = None
+    if val_dir.exists() and tfdataset._files(val_dir):
+        val_ds = tfdataset.AudioDataset(tfdataset._files(val_dir), labels, batch_size=args.batch_size, shuffle=False,
+                                        device=dev)
+    history = {"loss": [], "val_loss": [], "val_accuracy": [], "clips_per_s": []}
+    out_dir = Path(args.checkpoint_dir) / args.name
+    best = float("inf")
+    for epoch in range(args.epochs):
+        t0, n, lsum, steps = time.perf_counter(), 0, 0.0, 0
+        for item in train_ds:
+            if args.augment:
+                (x1, y1), (x2, y2) = item
+                lam = sample_mixup_lambda(x1.shape[0], 0.5, 0.25, device=dev)
+                loss, _ = trainer.step(x1, mix_labels(y1, y2, lam), x2, lam)
+            else:
+                x1, y1 = item
+                loss, _ = trainer.step(x1, y1)
+            lsum += float(loss) * x1.shape[0]
+            n += x1.shape[0]
+            steps += 1
+            if args.steps_per_epoch and steps >= args.steps_per_epoch:
+                break
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        history["loss"].append(lsum / max(n, 1))
+        history["clips_per_s"].append(n * world / dt)
+        if val_ds is not None and rank == 0:
+            vl, va = evaluate(trainer, val_ds, args.multi_label)
+            history["val_loss"].append(vl)
+            history["val_accuracy"].append(va)
+            if vl < best:  # ModelCheckpoint(save_best_only) on val_loss (audiomodel.py:878-938)
+                best = vl
+                save_checkpoint(out_dir / "val_loss", trainer, {}, None)
+        if rank == 0:
+            logging.info("epoch %d loss %.4f val %s %.1f clips/s", epoch, history["loss"][-1],
+                         history["val_loss"][-1:] or "-", history["clips_per_s"][-1])
+    if rank == 0:
+        meta_out = dict(meta)
+        meta_out.update(name=args.model_name, ebird_labels=labels, labels=labels, n_mels=n_mels, fmin=fmin,
+                        fmax=fmax, n_fft=n_fft, break_freq=brk, hop_length=281, power=2, pcen=args.pcen,
+                        multi_label=args.multi_label, loss_fn="bce" if args.multi_label else "cce",
+                        dtype=args.dtype, training_date=str(time.time()), magv2=True)
+        save_checkpoint(out_dir, trainer, meta_out, history)
+        print(json.dumps({"run": args.name, "epochs": args.epochs, "final_loss": history["loss"][-1],
+                          "val_loss": history["val_loss"][-1:] or None, "clips_per_s": history["clips_per_s"]}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return history
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("name", help="Run name")
+    p.add_argument("-d", "--dataset-dir", required=True)
+    p.add_argument("--epochs", type=int, default=100)
+    p.add_argument("--model-name", default="wr-resnet", choices=sorted(MODEL_NAMES))
+    p.add_argument("--load-raw", default=True, type=str2bool, help="raw audio records (the only supported input)")
+    p.add_argument("--multi-label", type=str2bool, default=False)
+    p.add_argument("--n_mels", type=int, default=None)
+    p.add_argument("--fmin", type=float, default=None)
+    p.add_argument("--fmax", type=float, default=None)
+    p.add_argument("--n_fft", type=int, default=None)
+    p.add_argument("--break-freq", type=float, default=None)
+    p.add_argument("-w", "--weights", help="model.pt to start from")
+    p.add_argument("--lr", type=float, default=0.01)
+    p.add_argument("--batch-size", type=int, default=32)
+    p.add_argument("--shuffle", type=str2bool, default=True)
+    p.add_argument("--augment", type=str2bool, default=True, help="mix_up (tfdataset.py:473-481)")
+    p.add_argument("--pcen", type=str2bool, default=True)
+    p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--steps-per-epoch", type=int, default=0)
+    p.add_argument("--checkpoint-dir", default="checkpoints")
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args(argv)
+
+
+if __name__ == "__main__":
+    logging.basicConfig(level=logging.INFO, format="%(process)d %(thread)s:%(levelname)7s %(message)s")
+    train_model(parse_args())

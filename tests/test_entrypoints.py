@@ -1,0 +1,64 @@
+"""build.py -> audiomodel.py -> predict.py, the reference's three entry points
+(build.py:679, audiomodel.py:1985, predict.py:726) on the acfe path."""
+import json
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PKG
+
+
+def _build(tmp_path, n=24):
+    import build
+
+    assert build.main([str(tmp_path / "ds"), "--synthetic", str(n), "--labels", "bird,noise", "--shards", "2"]) == 0
+    return tmp_path / "ds" / "training-data"
+
+
+def test_build_synthetic_records(tmp_path):
+    import tfrecord as tfr
+
+    td = _build(tmp_path)
+    meta = json.loads((td / "training-meta.json").read_text())
+    assert meta["labels"] == ["bird", "noise"] and meta["type"] == "audio"
+    total = 0
+    seen = {}
+    for split in ("train", "validation", "test"):
+        files = sorted((td / split).glob("*.tfrecord"))
+        n = 0
+        for f in files:
+            for rec in tfr.read_records(f):
+                ex = tfr.parse_audio_example(rec)
+                assert ex["raw"].shape == (144000,) and ex["text"] in ("bird", "noise")
+                seen.setdefault(ex["rec_id"], set()).add(split)
+                n += 1
+        assert n == sum(meta["counts"][split]["sample_counts"].values())
+        total += n
+    assert total == 24
+    assert all(len(v) == 1 for v in seen.values())  # no recording in two splits
+
+
+@pytest.mark.gpu
+def test_train_checkpoint_predict(tmp_path, cuda):
+    import audiomodel
+    import predict
+    from scipy.io import wavfile
+
+    td = _build(tmp_path, 16)
+    args = audiomodel.parse_args(["run1", "-d", str(td), "--epochs", "1", "--batch-size", "4", "--model-name",
+                                  "wr-resnet-bird", "--n_mels", "128", "--checkpoint-dir", str(tmp_path / "ck")])
+    hist = audiomodel.train_model(args)
+    assert np.isfinite(hist["loss"][0])
+    ck = tmp_path / "ck" / "run1"
+    assert (ck / "model.pt").exists() and json.loads((ck / "metadata.txt").read_text())["labels"] == ["bird", "noise"]
+    # 10 s synthetic recording -> 8 windows at 1 s stride
+    import build
+
+    rng = np.random.default_rng(3)
+    rec = np.concatenate([build.synth_clip(rng, False) for _ in range(3)] + [build.synth_clip(rng, True)[:48000]])
+    wavfile.write(tmp_path / "rec.wav", 48000, (rec * 32767).astype(np.int16))
+    p = predict.Predictor(ck)
+    r = p.predict_file(tmp_path / "rec.wav", stride=1.0, batch_size=4)
+    assert r["windows"] == 8
+    assert set(r["mean"]) == {"bird", "noise"} and all(0 <= v <= 1 for v in r["mean"].values())
