@@ -103,12 +103,17 @@ def normalize_stats(x: torch.Tensor, n: int | None = None, clip_stride: int | No
     return st
 
 
-def normalize(x: torch.Tensor) -> torch.Tensor:
-    """tfdataset.normalize (tfdataset.py:1916-1934) on [B, N] fp32."""
-    st = normalize_stats(x)
-    y = torch.empty_like(x)
+def normalize_apply(x: torch.Tensor, st: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """(x - min) / max(x - min) per clip with precomputed stats; [B, N] fp32."""
+    require_cuda(x, st)
+    y = torch.empty_like(x) if out is None else out
     call("acfe_normalize_apply", ptr(x), x.shape[1], x.shape[0], x.shape[1], ptr(st), ptr(y), stream())
     return y
+
+
+def normalize(x: torch.Tensor) -> torch.Tensor:
+    """tfdataset.normalize (tfdataset.py:1916-1934) on [B, N] fp32."""
+    return normalize_apply(x, normalize_stats(x))
 
 
 def mix_up(x1, x2, lam, stats1=None, stats2=None) -> torch.Tensor:

@@ -165,7 +165,7 @@ class _StemFn(torch.autograd.Function):
         # x: [N, H, W] (one folded channel); w: [16, R, S, Crep] fp32
         N, H, W = x.shape
         K, R, S, rep = w.shape
-        weff = _empty((K, R, S), F32, x.device)
+        weff = _empty((R, S, K), F32, x.device)  # folded, RSK
         s = stream()
         call("acfe_stem_fold_weights", ptr(w), K, R, S, rep, ptr(weff), s)
         y = _empty((N, H, W, K), out_dtype, x.device)

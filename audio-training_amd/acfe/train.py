@@ -41,10 +41,13 @@ class FrontEnd(nn.Module):
             st = fe.normalize_stats(src)
         else:
             src, st = x1, st1
+        # Normalise once into a scratch clip (frames overlap ~14.6x, so
+        # normalising on load inside the STFT repeats the divide per frame).
+        src = fe.normalize_apply(src, st, out=src if src is not x1 else None)
         if self.pcen is not None:
-            mel = self.plan.mel(src, st, pad_mode=pad_mode, layout="btm", timer=self.timer)
+            mel = self.plan.mel(src, None, pad_mode=pad_mode, layout="btm", timer=self.timer)
             return self.pcen(mel, scope_minmax)
-        mel = self.plan.mel(src, st, pad_mode=pad_mode, layout="bmt", timer=self.timer)
+        mel = self.plan.mel(src, None, pad_mode=pad_mode, layout="bmt", timer=self.timer)
         return ops.cast(mel, self.dtype)
 
 

@@ -1001,73 +1001,126 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
 
 // ------------------------------------------------------------------ stem (C = 1)
 // y[n,h,w,k] = sum_{r,s} x[n, h - pt + r, w - pl + s] * weff[k][r][s] + b[k]
-// (stride 1, P = H, Q = W).  Tile: 8 rows x 64 cols per block iteration.
-constexpr int STEM_TH = 8, STEM_TW = 64, STEM_K = 16, STEM_MAXR = 7;
+// (stride 1, P = H, Q = W).  Tile: 16 rows x 64 cols; thread = one column x
+// 4 rows (lane = column, so LDS reads of consecutive lanes are consecutive
+// words or 32 B pixels: conflict-free).  The 16 x R x S weights are read
+// with wave-uniform indices (scalar loads), all R x S x 16 taps unrolled.
+constexpr int STEM_TH = 16, STEM_TW = 64, STEM_K = 16, STEM_MAXR = 7, STEM_CAP = 2048;
 
+// 16 channels of one pixel (32 B bf16 / 64 B fp32) from LDS -> fp32
+__device__ __forceinline__ void unpack16(const uint16_t* p, float* f) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(p), b = *reinterpret_cast<const u32x4*>(p + 8);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(a[i] << 16);
+    f[2 * i + 1] = __uint_as_float(a[i] & 0xffff0000u);
+    f[8 + 2 * i] = __uint_as_float(b[i] << 16);
+    f[8 + 2 * i + 1] = __uint_as_float(b[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void unpack16(const float* p, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f4 v = *reinterpret_cast<const f4*>(p + 4 * i);
+    f[4 * i] = v[0]; f[4 * i + 1] = v[1]; f[4 * i + 2] = v[2]; f[4 * i + 3] = v[3];
+  }
+}
+__device__ __forceinline__ void store16(uint16_t* d, const float* f) {
+  u32x4 a, b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+    b[i] = (unsigned)f2bf(f[8 + 2 * i]) | ((unsigned)f2bf(f[8 + 2 * i + 1]) << 16);
+  }
+  *reinterpret_cast<u32x4*>(d) = a;
+  *reinterpret_cast<u32x4*>(d + 8) = b;
+}
+__device__ __forceinline__ void store16(float* d, const float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f4 v = {f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]};
+    *reinterpret_cast<f4*>(d + 4 * i) = v;
+  }
+}
+
+// x halo tile (single channel) -> fp32 LDS, zero outside the image.
+template <typename TI, int XH, int XW>
+__device__ __forceinline__ void stem_load_x(const TI* __restrict__ x, int n, int H, int W, int gh0, int gw0,
+                                            float* xs) {
+  for (int i = threadIdx.x; i < XH * XW; i += 256) {
+    const int yy = i / XW, xx = i - (i / XW) * XW;
+    const int h = gh0 + yy, w = gw0 + xx;
+    float v = 0.f;
+    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = to_f(x[((long long)n * H + h) * W + w]);
+    xs[i] = v;
+  }
+}
+
+// Folded weights are laid out weff[r][s][k] (RSK): the 16 weights of one tap
+// are one 64 B scalar load, used as SGPR operands of v_fmac.
 template <typename TI, typename TO, int R, int S>
 __global__ void __launch_bounds__(256)
 k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int pt, int pl,
            const float* __restrict__ weff, const float* __restrict__ bias, TO* __restrict__ y,
            double* __restrict__ stats, int tiles_h, int tiles_w) {
-  __shared__ float xs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1)];
-  __shared__ float wsm[STEM_K * STEM_MAXR * STEM_MAXR];
+  constexpr int XH = STEM_TH + R - 1, XW = STEM_TW + S - 1, RH = 4 + R - 1;
+  __shared__ float xs[XH * XW];
   __shared__ double red[4][2][STEM_K];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < STEM_K * R * S; i += 256) wsm[i] = weff[i];
-  const int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1;
+  const int tid = threadIdx.x, ox = tid & 63, q = tid >> 6;
   const long long ntiles = (long long)N * tiles_h * tiles_w;
-  double s1[2] = {0, 0}, s2[2] = {0, 0};  // thread owns channels (tid & 7) and (tid & 7) + 8
-  const int kq = tid & 7;
-  float b0 = bias ? bias[kq] : 0.f, b1 = bias ? bias[kq + 8] : 0.f;
+  double s1[STEM_K], s2[STEM_K];
+#pragma unroll
+  for (int k = 0; k < STEM_K; ++k) s1[k] = 0.0, s2[k] = 0.0;
   for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int tw = (int)(t % tiles_w);
     const int th = (int)((t / tiles_w) % tiles_h);
     const int n = (int)(t / ((long long)tiles_w * tiles_h));
     const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
     __syncthreads();
-    for (int i = tid; i < XH * XW; i += 256) {
-      const int yy = i / XW, xx = i - (i / XW) * XW;
-      const int h = h0 - pt + yy, w = w0 - pl + xx;
-      float v = 0.f;
-      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = to_f(x[((long long)n * H + h) * W + w]);
-      xs[i] = v;
-    }
+    stem_load_x<TI, XH, XW>(x, n, H, W, h0 - pt, w0 - pl, xs);
     __syncthreads();
-    // thread -> pixel pix = tid >> 3 + 32*j (j < 16), channels kq, kq+8
-    for (int j = 0; j < STEM_TH * STEM_TW / 32; ++j) {
-      const int pix = (tid >> 3) + 32 * j;
-      const int py = pix / STEM_TW, px = pix - (pix / STEM_TW) * STEM_TW;
-      const int h = h0 + py, w = w0 + px;
-      float a0 = 0.f, a1 = 0.f;
+    float acc[4][STEM_K];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const float xv = xs[(py + r) * XW + px + s];
-          a0 += xv * wsm[(kq * R + r) * S + s];
-          a1 += xv * wsm[((kq + 8) * R + r) * S + s];
-        }
+      for (int k = 0; k < STEM_K; ++k) acc[j][k] = bias ? bias[k] : 0.f;
+    // column s of the thread's halo: RH values; output row j uses halo row j + r
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) {
+      float xc[RH];
+#pragma unroll
+      for (int i = 0; i < RH; ++i) xc[i] = xs[(4 * q + i) * XW + ox + s];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float* wt = weff + (r * S + s) * STEM_K;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int k = 0; k < STEM_K; ++k) acc[j][k] += xc[j + r] * wt[k];
+      }
+    }
+    const int w = w0 + ox;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int h = h0 + 4 * q + j;
       if (h < H && w < W) {
-        const TO o0 = cvt_out(a0 + b0, TO()), o1 = cvt_out(a1 + b1, TO());
-        TO* dst = y + (((long long)n * H + h) * W + w) * STEM_K;
-        dst[kq] = o0;
-        dst[kq + 8] = o1;
-        const float f0 = to_f(o0), f1 = to_f(o1);
-        s1[0] += f0; s2[0] += (double)f0 * f0;
-        s1[1] += f1; s2[1] += (double)f1 * f1;
+        float o[STEM_K];
+#pragma unroll
+        for (int k = 0; k < STEM_K; ++k) o[k] = to_f(cvt_out(acc[j][k], TO()));  // stats of stored values
+        store16(y + (((long long)n * H + h) * W + w) * STEM_K, o);
+        if (stats) {
+#pragma unroll
+          for (int k = 0; k < STEM_K; ++k) s1[k] += o[k], s2[k] += (double)o[k] * o[k];
+        }
       }
     }
   }
   if (stats) {
-    // reduce over the 8 lanes-groups sharing kq within each wave, then waves
-    for (int o = 8; o < 64; o <<= 1) {
-      s1[0] += __shfl_xor(s1[0], o, 64); s1[1] += __shfl_xor(s1[1], o, 64);
-      s2[0] += __shfl_xor(s2[0], o, 64); s2[1] += __shfl_xor(s2[1], o, 64);
-    }
     const int lane = tid & 63, wid = tid >> 6;
-    if (lane < 8) {
-      red[wid][0][lane] = s1[0]; red[wid][0][lane + 8] = s1[1];
-      red[wid][1][lane] = s2[0]; red[wid][1][lane + 8] = s2[1];
+#pragma unroll
+    for (int k = 0; k < STEM_K; ++k) {
+      const double a = wave_sumd(s1[k]), b = wave_sumd(s2[k]);
+      if (lane == 0) red[wid][0][k] = a, red[wid][1][k] = b;
     }
     __syncthreads();
     if (tid < 2 * STEM_K) {
@@ -1078,67 +1131,78 @@ k_stem_fwd(const TI* __restrict__ x, int N, int H, int W, int pt, int pl,
   }
 }
 
-// dx[n,h,w] = sum_{k,r,s} dy[n, h + pt - r, w + pl - s, k] * weff[k][r][s]
-// LDS image channel-major (gs[k][pos]) so the 64 lanes of a wave, which own
-// consecutive pixels, read consecutive words for every (k, r, s).
+// dx[n,h,w] = sum_{k,r,s} dy[n, h + pt - r, w + pl - s, k] * weff[r][s][k]
+// dy halo tile kept pixel-major in LDS (16 channels = 32 B per pixel, copied
+// with 16 B loads/stores); one tile per block.  Per halo column the thread
+// holds its RH x 16 dy values in registers and applies all R taps of that
+// column to its 4 output rows.
 template <typename TG, typename TO, int R, int S>
 __global__ void __launch_bounds__(256)
 k_stem_dgrad(const TG* __restrict__ dy, int N, int H, int W, int pt, int pl,
              const float* __restrict__ weff, TO* __restrict__ dx, int tiles_h, int tiles_w) {
-  constexpr int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1, XP = XH * XW + 1;
-  __shared__ float gs[STEM_K * XP];
-  __shared__ float wsm[STEM_K * R * S];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < STEM_K * R * S; i += 256) wsm[i] = weff[i];
-  const long long ntiles = (long long)N * tiles_h * tiles_w;
-  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int tw = (int)(t % tiles_w);
-    const int th = (int)((t / tiles_w) % tiles_h);
-    const int n = (int)(t / ((long long)tiles_w * tiles_h));
-    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
-    const int gh0 = h0 - (R - 1 - pt), gw0 = w0 - (S - 1 - pl);
-    __syncthreads();
-    for (int i = tid; i < XH * XW * STEM_K; i += 256) {
-      const int k = i % STEM_K, pos = i / STEM_K;
-      const int yy = pos / XW, xx = pos - (pos / XW) * XW;
-      const int h = gh0 + yy, w = gw0 + xx;
-      float v = 0.f;
-      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
-        v = to_f(dy[(((long long)n * H + h) * W + w) * STEM_K + k]);
-      gs[k * XP + pos] = v;
+  constexpr int XH = STEM_TH + R - 1, XW = STEM_TW + S - 1, RH = 4 + R - 1;
+  constexpr int CPP = STEM_K * (int)sizeof(TG) / 16;  // 16 B chunks per pixel
+  __shared__ __attribute__((aligned(16))) TG gs[XH * XW * STEM_K];
+  const int tid = threadIdx.x, ox = tid & 63, q = tid >> 6;
+  const long long t = blockIdx.x;
+  const int tw = (int)(t % tiles_w);
+  const int th = (int)((t / tiles_w) % tiles_h);
+  const int n = (int)(t / ((long long)tiles_w * tiles_h));
+  const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+  const int gh0 = h0 - (R - 1 - pt), gw0 = w0 - (S - 1 - pl);
+  for (int i = tid; i < XH * XW * CPP; i += 256) {
+    const int pos = i / CPP, c = i - (i / CPP) * CPP;
+    const int yy = pos / XW, xx = pos - (pos / XW) * XW;
+    const int h = gh0 + yy, w = gw0 + xx;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+      v = *reinterpret_cast<const u32x4*>(dy + (((long long)n * H + h) * W + w) * STEM_K + c * (16 / (int)sizeof(TG)));
+    *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(gs) + (long long)i * 16) = v;
+  }
+  __syncthreads();
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // halo row 4q + i, col ox + cc holds dy for output row j with r = j + R-1-i, s = S-1-cc
+#pragma unroll 1
+  for (int cc = 0; cc < S; ++cc) {
+    float g[RH][STEM_K];
+#pragma unroll
+    for (int i = 0; i < RH; ++i) unpack16(gs + ((4 * q + i) * XW + ox + cc) * STEM_K, g[i]);
+    const int s = S - 1 - cc;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float* wt = weff + (r * S + s) * STEM_K;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < STEM_K; ++k) acc[j] += g[j + R - 1 - r][k] * wt[k];
     }
-    __syncthreads();
-    for (int pix = tid; pix < STEM_TH * STEM_TW; pix += 256) {
-      const int py = pix / STEM_TW, px = pix - (pix / STEM_TW) * STEM_TW;
-      const int h = h0 + py, w = w0 + px;
-      float a = 0.f;
-      // dy row = h + pt - r  -> gs row = py + (R-1-pt) + pt - r = py + R-1-r
+  }
+  const int w = w0 + ox;
+  if (w < W) {
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int s2 = 0; s2 < S; ++s2) {
-          const int pos = (py + R - 1 - r) * XW + px + S - 1 - s2;
-#pragma unroll
-          for (int k = 0; k < STEM_K; ++k) a += gs[k * XP + pos] * wsm[(k * R + r) * S + s2];
-        }
-      if (h < H && w < W) dx[((long long)n * H + h) * W + w] = cvt_out(a, TO());
+    for (int j = 0; j < 4; ++j) {
+      const int h = h0 + 4 * q + j;
+      if (h < H) dx[((long long)n * H + h) * W + w] = cvt_out(acc[j], TO());
     }
   }
 }
 
-// dweff[k][r][s] partials per block: thread -> (k = tid & 15, pixel group = tid >> 4)
+// dweff[k][r][s] partials per block: thread -> (column ox = lane, channels
+// 4*kq .. 4*kq+3 with kq = wave), R*S*4 fp32 accumulators over the block's
+// tiles, reduced across the wave in double at the end.  The x window of the
+// thread (R rows x S cols) slides down the tile in registers.
 template <typename TI, typename TG, int R, int S>
 __global__ void __launch_bounds__(256)
 k_stem_wgrad(const TI* __restrict__ x, const TG* __restrict__ dy, int N, int H, int W, int pt,
              int pl, double* __restrict__ part, int tiles_h, int tiles_w) {
-  __shared__ float xs[(STEM_TH + STEM_MAXR - 1) * (STEM_TW + STEM_MAXR - 1)];
-  __shared__ float red[16][STEM_K * STEM_MAXR * STEM_MAXR + 1];
-  const int tid = threadIdx.x, k = tid & 15, pg = tid >> 4;
-  const int XW = STEM_TW + S - 1, XH = STEM_TH + R - 1;
-  float acc[R * S];
-  double accd[R * S];
+  constexpr int XH = STEM_TH + R - 1, XW = STEM_TW + S - 1;
+  __shared__ float xs[XH * XW];
+  const int tid = threadIdx.x, ox = tid & 63, kq = tid >> 6;
+  float acc[4][R * S];
 #pragma unroll
-  for (int i = 0; i < R * S; ++i) acc[i] = 0.f, accd[i] = 0.0;
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int i = 0; i < R * S; ++i) acc[kk][i] = 0.f;
   const long long ntiles = (long long)N * tiles_h * tiles_w;
   for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int tw = (int)(t % tiles_w);
@@ -1146,71 +1210,83 @@ k_stem_wgrad(const TI* __restrict__ x, const TG* __restrict__ dy, int N, int H, 
     const int n = (int)(t / ((long long)tiles_w * tiles_h));
     const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
     __syncthreads();
-    for (int i = tid; i < XH * XW; i += 256) {
-      const int yy = i / XW, xx = i - (i / XW) * XW;
-      const int h = h0 - pt + yy, w = w0 - pl + xx;
-      float v = 0.f;
-      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = to_f(x[((long long)n * H + h) * W + w]);
-      xs[i] = v;
-    }
+    stem_load_x<TI, XH, XW>(x, n, H, W, h0 - pt, w0 - pl, xs);
     __syncthreads();
-    for (int pix = pg; pix < STEM_TH * STEM_TW; pix += 16) {
-      const int py = pix / STEM_TW, px = pix - (pix / STEM_TW) * STEM_TW;
-      const int h = h0 + py, w = w0 + px;
-      if (h >= H || w >= W) continue;
-      const float g = to_f(dy[(((long long)n * H + h) * W + w) * STEM_K + k]);
+    const int w = w0 + ox;
+    float win[R][S];
+#pragma unroll
+    for (int r = 0; r < R - 1; ++r)
+#pragma unroll
+      for (int s = 0; s < S; ++s) win[r + 1][s] = xs[r * XW + ox + s];
+#pragma unroll 1
+    for (int oy = 0; oy < STEM_TH; ++oy) {
+#pragma unroll
+      for (int r = 0; r < R - 1; ++r)
+#pragma unroll
+        for (int s = 0; s < S; ++s) win[r][s] = win[r + 1][s];
+#pragma unroll
+      for (int s = 0; s < S; ++s) win[R - 1][s] = xs[(oy + R - 1) * XW + ox + s];
+      const int h = h0 + oy;
+      float g[4] = {0.f, 0.f, 0.f, 0.f};
+      if (h < H && w < W) {
+        const TG* gp = dy + (((long long)n * H + h) * W + w) * STEM_K + 4 * kq;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) g[kk] = to_f(gp[kk]);
+      }
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int s = 0; s < S; ++s) acc[r * S + s] += g * xs[(py + r) * XW + px + s];
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) acc[kk][r * S + s] += g[kk] * win[r][s];
     }
+  }
+  const int lane = tid & 63;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
     for (int i = 0; i < R * S; ++i) {
-      accd[i] += acc[i];
-      acc[i] = 0.f;
+      const double v = wave_sumd((double)acc[kk][i]);
+      if (lane == 0) part[(long long)blockIdx.x * STEM_K * R * S + (4 * kq + kk) * R * S + i] = v;
     }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < R * S; ++i) red[pg][k * R * S + i] = (float)accd[i];
-  __syncthreads();
-  for (int i = tid; i < STEM_K * R * S; i += 256) {
-    double s = 0.0;
-    for (int j = 0; j < 16; ++j) s += red[j][i];
-    part[(long long)blockIdx.x * STEM_K * R * S + i] = s;
-  }
 }
 
+// dweff partials [blocks][k][r][s] -> dw[k][r][s][rep] (+beta*dw); one block per tap.
 __global__ void k_stem_wgrad_reduce(const double* __restrict__ part, int np, int n, int rep, float beta,
                                     float* __restrict__ dw) {
-  // dw layout [K][R][S][rep] (KRSC with C = rep copies of the folded channel)
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    double s = 0.0;
-    for (int j = 0; j < np; ++j) s += part[(long long)j * n + i];
-    for (int c = 0; c < rep; ++c) {
-      float* d = dw + (long long)i * rep + c;
-      *d = beta != 0.f ? *d * beta + (float)s : (float)s;
-    }
+  __shared__ double red[4];
+  const int i = blockIdx.x;
+  double s = 0.0;
+  for (int j = threadIdx.x; j < np; j += 256) s += part[(long long)j * n + i];
+  s = wave_sumd(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x < rep) {
+    const double tot = red[0] + red[1] + red[2] + red[3];
+    float* d = dw + (long long)i * rep + threadIdx.x;
+    *d = beta != 0.f ? *d * beta + (float)tot : (float)tot;
   }
 }
 
-__global__ void k_stem_fold(const float* __restrict__ w, int n, int rep, float* __restrict__ weff) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+// weff[r][s][k] = sum_c w[k][r][s][c]  (folds the identical input channels)
+__global__ void k_stem_fold(const float* __restrict__ w, int K, int RS, int rep, float* __restrict__ weff) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < K * RS; i += gridDim.x * 256) {
+    const int k = i % K, rs = i / K;
     float s = 0.f;
-    for (int c = 0; c < rep; ++c) s += w[(long long)i * rep + c];
+    for (int c = 0; c < rep; ++c) s += w[((long long)k * RS + rs) * rep + c];
     weff[i] = s;
   }
 }
 
 ACFE_API int acfe_stem_blocks(int N, int H, int W) {
   const long long t = (long long)N * ((H + STEM_TH - 1) / STEM_TH) * ((W + STEM_TW - 1) / STEM_TW);
-  return (int)(t < 2048 ? t : 2048);
+  return (int)(t < STEM_CAP ? t : STEM_CAP);
 }
 
-// weff[k][r][s] = sum_c w[k][r][s][c]  (folds the identical input channels)
+// weff[r][s][k] = sum_c w[k][r][s][c]  (folds the identical input channels)
 ACFE_API int acfe_stem_fold_weights(const float* w, int K, int R, int S, int C, float* weff, void* stream) {
   if (!w || !weff || K != STEM_K || R > STEM_MAXR || S > STEM_MAXR || C <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_stem_fold, dim3(cdiv(K * R * S, 256)), dim3(256), 0, strm(stream), w, K * R * S, C, weff);
+  hipLaunchKernelGGL(k_stem_fold, dim3(cdiv(K * R * S, 256)), dim3(256), 0, strm(stream), w, K, R * S, C, weff);
   return launch_rc("acfe_stem_fold_weights");
 }
 
@@ -1238,7 +1314,7 @@ ACFE_API int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, 
   if (!dy || !weff || !dx || N < 0 || R != S || (R != 5 && R != 3)) return ACFE_E_INVAL;
   if (N == 0) return ACFE_OK;
   const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
-  const int grid = acfe_stem_blocks(N, H, W);
+  const long long grid = (long long)N * th * tw;  // one tile per block
 #define SD1(TG, TO, RR)                                                                                      \
   hipLaunchKernelGGL((k_stem_dgrad<TG, TO, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TG*)dy, N, H, \
                      W, pad_top, pad_left, weff, (TO*)dx, th, tw)
@@ -1270,7 +1346,7 @@ ACFE_API int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_
   int rc = launch_rc("acfe_stem_wgrad");
   if (rc) return rc;
   const int n = STEM_K * R * S;
-  hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3(cdiv(n, 256)), dim3(256), 0, strm(stream), workspace, grid, n, rep,
-                     beta, dw);
+  if (rep > 256) return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3(n), dim3(256), 0, strm(stream), workspace, grid, n, rep, beta, dw);
   return launch_rc("acfe_stem_wgrad(reduce)");
 }

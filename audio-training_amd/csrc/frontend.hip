@@ -193,8 +193,8 @@ ACFE_API int acfe_normalize_stats(const float* x, int64_t cs, int batch, int n, 
   return launch_rc("acfe_normalize_stats");
 }
 
-__global__ void k_norm_apply(const float* __restrict__ x, int64_t cs, int n,
-                             const float* __restrict__ stats, float* __restrict__ y) {
+// y may alias x (in place, cs == n): each element is read and written by one thread.
+__global__ void k_norm_apply(const float* x, int64_t cs, int n, const float* __restrict__ stats, float* y) {
   const int b = blockIdx.y;
   const float mn = stats[2 * b], rng = stats[2 * b + 1];
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
@@ -277,6 +277,10 @@ __device__ __forceinline__ void dft<8>(float2* v) {
   v[3] = cadd(e[3], o3);   v[7] = csub(e[3], o3);
 }
 
+// LDS index with one float2 of padding per 8 (breaks the power-of-two strides
+// of the Stockham writes: pass-1 stores go from 8-way conflicted to conflict-free).
+__device__ __forceinline__ int padx(int i) { return i + (i >> 3); }
+
 // One in-place Stockham pass (Govindaraju et al. formulation) over NC points
 // held in LDS `buf`, radix R, span Ns.  256 threads.
 template <int NC, int R>
@@ -292,7 +296,7 @@ __device__ __forceinline__ void stockham_pass(float2* buf, int Ns, const float2*
       const int tstep = jm * (NC / (Ns * R));
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        float2 a = buf[j + r * NB];
+        float2 a = buf[padx(j + r * NB)];
         if (r) a = cmul(a, tw[r * tstep]);
         v[p][r] = a;
       }
@@ -306,7 +310,7 @@ __device__ __forceinline__ void stockham_pass(float2* buf, int Ns, const float2*
       dft<R>(v[p]);
       const int idxD = (j / Ns) * Ns * R + (j & (Ns - 1));
 #pragma unroll
-      for (int r = 0; r < R; ++r) buf[idxD + r * Ns] = v[p][r];
+      for (int r = 0; r < R; ++r) buf[padx(idxD + r * Ns)] = v[p][r];
     }
   }
   __syncthreads();
@@ -337,8 +341,10 @@ __global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int6
   constexpr int L = 2 * NC;
   constexpr int NB0 = NC / 8;  // first pass butterflies
   constexpr int PER0 = (NB0 + 255) / 256;
-  __shared__ float2 buf[NC];
+  __shared__ float2 buf[NC + NC / 8];
   __shared__ float pw[NC + 1];
+  __shared__ float2 stw[NC];      // complex-FFT twiddles, staged once per block
+  for (int i = threadIdx.x; i < NC; i += 256) stw[i] = tw[i];
   const int b = blockIdx.y;
   const float* xb = raw + (int64_t)b * cs;
   const bool do_norm = stats != nullptr;
@@ -370,23 +376,23 @@ __global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int6
         const int j = threadIdx.x + 256 * p;
         if (NB0 % 256 == 0 || j < NB0) {
 #pragma unroll
-          for (int r = 0; r < 8; ++r) buf[j * 8 + r] = v[p][r];
+          for (int r = 0; r < 8; ++r) buf[padx(j * 8 + r)] = v[p][r];
         }
       }
       __syncthreads();
     }
     int Ns = 8;
     while (Ns * 8 <= NC) {
-      stockham_pass<NC, 8>(buf, Ns, tw);
+      stockham_pass<NC, 8>(buf, Ns, stw);
       Ns *= 8;
     }
-    if (NC / Ns == 4) stockham_pass<NC, 4>(buf, Ns, tw);
-    else if (NC / Ns == 2) stockham_pass<NC, 2>(buf, Ns, tw);
+    if (NC / Ns == 4) stockham_pass<NC, 4>(buf, Ns, stw);
+    else if (NC / Ns == 2) stockham_pass<NC, 2>(buf, Ns, stw);
     // ---- real-FFT post-processing + power, only for bins in [kmin, kmax]
     for (int i = threadIdx.x; i < nk; i += 256) {
       const int k = kmin + i;
-      const float2 zk = buf[k & (NC - 1)];
-      const float2 zm = buf[(NC - k) & (NC - 1)];
+      const float2 zk = buf[padx(k & (NC - 1))];
+      const float2 zm = buf[padx((NC - k) & (NC - 1))];
       // E = (zk + conj(zm))/2, O = (zk - conj(zm)) / (2i)
       const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
       const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);

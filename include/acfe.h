@@ -89,7 +89,8 @@ int acfe_plan_num_frames(acfe_plan_t plan, int n_samples, int pad_mode);
  * Clip b is x[b*clip_stride .. b*clip_stride + n). */
 int acfe_normalize_stats(const float* x, int64_t clip_stride, int batch, int n,
                          float* stats, void* stream);
-/* y[b][i] = ((x - min)/range + 1e-6 - 0.5) * 2, in that float32 order. */
+/* y[b][i] = ((x - min)/range + 1e-6 - 0.5) * 2, in that float32 order.
+ * In place (y == x) is allowed when clip_stride == n. */
 int acfe_normalize_apply(const float* x, int64_t clip_stride, int batch, int n,
                          const float* stats, float* y, void* stream);
 /* mix_up on normalised inputs: y = norm(x1)*lam + norm(x2)*(1-lam), per row.
@@ -169,7 +170,8 @@ int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy,
 
 /* Stem convolution with one (folded) input channel and 16 outputs ("same",
  * stride 1, R = S = 5 (wr_resnet_bird) or 3 (wr_resnet)): the three identical
- * channels of tfdataset.py:2053 are folded by weff = sum_c w[...,c]. */
+ * channels of tfdataset.py:2053 are folded by weff[r][s][k] = sum_c w[k][r][s][c]
+ * (weff is tap-major, RSK, so one tap's 16 weights are contiguous). */
 int acfe_stem_blocks(int N, int H, int W);
 int acfe_stem_fold_weights(const float* w_krsc, int K, int R, int S, int C, float* weff, void* stream);
 int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int R, int S, int pad_top, int pad_left,
