@@ -39,6 +39,8 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_pack_weights": [P, I32, I32, I32, I32, I32, I32, P, P],
     "acfe_conv2d_stats_rows": [I64, I32],
     "acfe_conv2d_fwd": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P, P],
+    "acfe_conv2d_fwd_dropout": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P, F32,
+                                C.c_uint64, P],
     "acfe_conv2d_dgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P],
     "acfe_conv2d_wgrad_workspace": [I32, I32, I32, I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_wgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, I32, P, P],
@@ -54,14 +56,18 @@ SIGNATURES: dict[str, list] = {
     "acfe_bn_bwd_reduce": [P, I32, P, I32, I64, I32, P, P, P, P, I32, P, P],
     "acfe_bn_bwd_finalize": [P, I32, I32, F64, P, P, P, P, P, P, P],
     "acfe_bn_bwd_apply": [P, I32, P, I32, I64, I32, P, P, I32, P, P, P, I32, P],
+    "acfe_bn_bwd_apply_dropout": [P, I32, P, I32, I64, I32, P, P, I32, P, F32, C.c_uint64, P, I32, P],
     "acfe_channel_sum": [P, I64, I32, I32, P, P, F32, P],
     "acfe_add": [P, P, I64, I32, P, I32, P],
+    "acfe_add_stats": [P, P, I64, I32, I32, P, I32, P, P],
     "acfe_relu_bwd": [P, P, I64, P, I32, P],
     "acfe_dropout": [P, I64, F32, C.c_uint64, P, I32, P],
     "acfe_cast": [P, I32, I64, P, I32, P],
     "acfe_sigmoid": [P, I64, P, P],
     "acfe_maxpool2d": [P, I32, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_maxpool2d_bwd": [P, P, I32, I32, I32, I32, I32, I32, P, I32, P],
+    "acfe_maxpool2d_fused": [P, I32, I32, I32, I32, I32, I32, P, P, F32, C.c_uint64, P, I32, P],
+    "acfe_maxpool2d_bwd_argmax": [P, P, I32, I32, I32, I32, I32, I32, F32, C.c_uint64, P, I32, P],
     "acfe_avgpool2d": [P, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_avgpool2d_bwd": [P, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_axis_pool": [P, I32, I64, I32, I32, F32, I32, P, P],

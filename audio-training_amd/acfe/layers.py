@@ -71,9 +71,22 @@ class BatchNormalization(nn.Module):
         self.register_buffer("moving_mean", torch.zeros(channels))
         self.register_buffer("moving_variance", torch.ones(channels))
 
-    def forward(self, x, relu=False, stats=None):
+    def forward(self, x, relu=False, stats=None, link=None):
         return ops.batch_norm(x, self.gamma, self.beta, self.moving_mean, self.moving_variance, self.training,
-                              relu, stats, self.eps, self.momentum)
+                              relu, stats, self.eps, self.momentum, link)
+
+
+def conv_dropout_bn(conv: Conv2D, bn: BatchNormalization, x, rate, relu=True):
+    """bn(Dropout(rate)(conv(x))) (+ReLU) as one fused node (ops.conv_dropout_bn)."""
+    return ops.conv_dropout_bn(x, conv.weight, conv.bias, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance,
+                               bn.training, rate, relu=relu, stride=conv.strides, padding=conv.padding,
+                               eps=bn.eps, momentum=bn.momentum)
+
+
+def maxpool_dropout_bn(x, kh, kw, bn: BatchNormalization, rate, relu=True):
+    """bn(Dropout(rate)(MaxPool2D((kh, kw))(x))) (+ReLU) as one fused node."""
+    return ops.maxpool_dropout_bn(x, kh, kw, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance, bn.training,
+                                  rate, relu=relu, eps=bn.eps, momentum=bn.momentum)
 
 
 class Dense(nn.Module):

@@ -8,6 +8,7 @@ fp32 KRSC master copies packed to the compute dtype on every forward.
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 
@@ -15,6 +16,10 @@ from ._lib import call, lib
 from ._torch import dtype_code, ptr, stream
 
 F32, F64 = torch.float32, torch.float64
+
+# ACFE_FUSE=0 runs the fused nodes (conv/pool + dropout + BN, Add + statistics,
+# residual-gradient link) as their separate-op chains, for A/B checks.
+FUSE = os.environ.get("ACFE_FUSE", "1") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -84,22 +89,61 @@ class _Timed:
 
 
 # ------------------------------------------------------------------ conv
+def _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats, drop=None):
+    """acfe_conv2d_fwd[_dropout] -> (y, stats_partial)."""
+    N, H, W, C = x.shape
+    K, R, S, Cw = w.shape
+    assert Cw == C, (Cw, C)
+    dt = dtype_code(x.dtype)
+    wp = pack_weights(w, x.dtype, False)
+    y = _empty((N, P, Q, K), x.dtype, x.device)
+    stats = _no_stats(x.device)
+    if want_stats:
+        rows = lib.acfe_conv2d_stats_rows(N * P * Q, K)
+        stats = _empty((rows, 2, wp.shape[0]), F64, x.device)
+    args = (ptr(x), N, H, W, C, ptr(wp), K, R, S, stride, pt, pl, P, Q, ptr(b), ptr(y), dt,
+            ptr(stats) if want_stats else None)
+    with _Timed(w, "fwd"):
+        if drop is not None and drop[0] > 0.0:
+            call("acfe_conv2d_fwd_dropout", *args, float(drop[0]), int(drop[1]), stream())
+        else:
+            call("acfe_conv2d_fwd", *args, stream())
+    return y, stats
+
+
+def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db):
+    """dgrad / wgrad / bias gradient of _conv_fwd for the conv-output gradient dy."""
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    dt = dtype_code(x.dtype)
+    dy = dy.contiguous()
+    dx = dw = db = None
+    s = stream()
+    if need_dx:
+        wf = pack_weights(w, x.dtype, True)
+        dx = _empty(x.shape, x.dtype, x.device)
+        ws = None
+        if stride > 1:
+            ws = _empty((N * ((P - 1) * stride + 1) * ((Q - 1) * stride + 1) * K,), x.dtype, x.device)
+        with _Timed(w, "dgrad"):
+            call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
+                 ptr(ws), s)
+    if need_dw:
+        dw = _empty(w.shape, F32, w.device)
+        nws = lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, P, Q)
+        ws = _empty((nws,), F32, x.device)
+        with _Timed(w, "wgrad"):
+            call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, stride, pt, pl, P, Q, ptr(dw), 0.0,
+                 dt, ptr(ws), s)
+    if need_db:
+        db = channel_sum(dy, K)
+    return dx, dw, db
+
+
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pt, pl, P, Q, want_stats):
-        N, H, W, C = x.shape
-        K, R, S, Cw = w.shape
-        assert Cw == C, (Cw, C)
-        dt = dtype_code(x.dtype)
-        wp = pack_weights(w, x.dtype, False)
-        y = _empty((N, P, Q, K), x.dtype, x.device)
-        stats = _no_stats(x.device)
-        if want_stats:
-            rows = lib.acfe_conv2d_stats_rows(N * P * Q, K)
-            stats = _empty((rows, 2, wp.shape[0]), F64, x.device)
-        with _Timed(w, "fwd"):
-            call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, stride, pt, pl, P, Q, ptr(b), ptr(y), dt,
-                 ptr(stats) if want_stats else None, stream())
+        y, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pt, pl, P, Q, b is not None)
         ctx.mark_non_differentiable(stats)
@@ -109,30 +153,8 @@ class _Conv2dFn(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         x, w = ctx.saved_tensors
         stride, pt, pl, P, Q, has_b = ctx.conf
-        N, H, W, C = x.shape
-        K, R, S, _ = w.shape
-        dt = dtype_code(x.dtype)
-        dy = dy.contiguous()
-        dx = dw = db = None
-        s = stream()
-        if ctx.needs_input_grad[0]:
-            wf = pack_weights(w, x.dtype, True)
-            dx = _empty(x.shape, x.dtype, x.device)
-            ws = None
-            if stride > 1:
-                ws = _empty((N * ((P - 1) * stride + 1) * ((Q - 1) * stride + 1) * K,), x.dtype, x.device)
-            with _Timed(w, "dgrad"):
-                call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
-                     ptr(ws), s)
-        if ctx.needs_input_grad[1]:
-            dw = _empty(w.shape, F32, w.device)
-            nws = lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, P, Q)
-            ws = _empty((nws,), F32, x.device)
-            with _Timed(w, "wgrad"):
-                call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, stride, pt, pl, P, Q, ptr(dw), 0.0,
-                     dt, ptr(ws), s)
-        if has_b and ctx.needs_input_grad[2]:
-            db = channel_sum(dy, K)
+        dx, dw, db = _conv_bwd(x, w, dy, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               has_b and ctx.needs_input_grad[2])
         return dx, dw, db, None, None, None, None, None, None
 
 
@@ -212,90 +234,195 @@ def stem_conv(x, w, b, out_dtype, want_stats=False):
 
 
 # ------------------------------------------------------------------ batch norm
+class ResidualLink:
+    """Hands the residual-branch gradient of an identity shortcut (ops.add) to
+    the BatchNormalization that reads the same block input, so the two input
+    gradients are summed inside acfe_bn_bwd_apply (its `add` operand) instead
+    of by a separate autograd accumulation pass."""
+
+    def __init__(self):
+        self.grad = None
+
+    @staticmethod
+    def make():
+        return ResidualLink() if FUSE else None
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
+def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype):
+    """Batch statistics (given slab or acfe_bn_stats) -> finalize -> apply. Returns (y, saved)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    dt = dtype_code(x.dtype)
+    dev = x.device
+    s = stream()
+    scale, shift, mean, invstd = (_empty((C,), F32, dev) for _ in range(4))
+    if training:
+        if stats is None or stats.numel() == 0:
+            nrows = lib.acfe_reduce_blocks(rows)
+            part = _empty((nrows * 2 * C,), F64, dev)
+            call("acfe_bn_stats", ptr(x), rows, C, dt, ptr(part), s)
+            ld = C
+        else:
+            part = stats
+            ld = stats.shape[-1]
+            nrows = stats.numel() // (2 * ld)
+        call("acfe_bn_finalize", ptr(part), nrows, ld, C, float(rows), ptr(gamma), ptr(beta), eps, momentum,
+             ptr(mmean), ptr(mvar), 1, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
+    else:
+        call("acfe_bn_finalize", None, 0, C, C, 0.0, ptr(gamma), ptr(beta), eps, momentum, ptr(mmean), ptr(mvar),
+             0, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
+    y = _empty(x.shape, out_dtype, dev)
+    call("acfe_bn_apply", ptr(x), dt, rows, C, ptr(scale), ptr(shift), int(relu), ptr(y), dtype_code(out_dtype), s)
+    return y, (scale, shift, mean, invstd)
+
+
+def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None):
+    """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given."""
+    scale, shift, mean, invstd = saved
+    C = x.shape[-1]
+    rows = x.numel() // C
+    dev = x.device
+    s = stream()
+    dy = dy.contiguous()
+    nrows = lib.acfe_reduce_blocks(rows)
+    part = _empty((nrows * 2 * C,), F64, dev)
+    call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+         ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
+    dgamma, dbeta = _empty((C,), F32, dev), _empty((C,), F32, dev)
+    coef = _empty((3 * C,), F32, dev)
+    # eval mode: statistics are constants -> count -> inf removes the mean terms
+    count = float(rows) if training else 1e300
+    call("acfe_bn_bwd_finalize", ptr(part), nrows, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
+         ptr(dbeta), ptr(coef), s)
+    dx = _empty(x.shape, x.dtype, dev)
+    if drop is not None and drop[0] > 0.0:
+        assert add is None
+        call("acfe_bn_bwd_apply_dropout", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C,
+             ptr(scale), ptr(shift), int(relu), ptr(coef), float(drop[0]), int(drop[1]), ptr(dx),
+             dtype_code(x.dtype), s)
+    else:
+        if add is not None:
+            add = add.contiguous()
+            assert add.dtype == x.dtype and add.shape == x.shape
+        call("acfe_bn_bwd_apply", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+             ptr(shift), int(relu), ptr(coef), ptr(add), ptr(dx), dtype_code(x.dtype), s)
+    return dx, dgamma, dbeta
+
+
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype):
-        C = x.shape[-1]
-        rows = x.numel() // C
-        dt = dtype_code(x.dtype)
-        dev = x.device
-        s = stream()
-        scale, shift, mean, invstd = (_empty((C,), F32, dev) for _ in range(4))
-        if training:
-            if stats is None or stats.numel() == 0:
-                nrows = lib.acfe_reduce_blocks(rows)
-                part = _empty((nrows * 2 * C,), F64, dev)
-                call("acfe_bn_stats", ptr(x), rows, C, dt, ptr(part), s)
-                ld = C
-            else:
-                part = stats
-                ld = stats.shape[-1]
-                nrows = stats.numel() // (2 * ld)
-            call("acfe_bn_finalize", ptr(part), nrows, ld, C, float(rows), ptr(gamma), ptr(beta), eps, momentum,
-                 ptr(mmean), ptr(mvar), 1, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
-        else:
-            call("acfe_bn_finalize", None, 0, C, C, 0.0, ptr(gamma), ptr(beta), eps, momentum, ptr(mmean), ptr(mvar),
-                 0, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
-        y = _empty(x.shape, out_dtype, dev)
-        call("acfe_bn_apply", ptr(x), dt, rows, C, ptr(scale), ptr(shift), int(relu), ptr(y), dtype_code(out_dtype), s)
-        ctx.save_for_backward(x, scale, shift, mean, invstd)
-        ctx.conf = (relu, training)
+    def forward(ctx, x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, link):
+        y, saved = _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype)
+        ctx.save_for_backward(x, *saved)
+        ctx.conf = (relu, training, link)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, scale, shift, mean, invstd = ctx.saved_tensors
-        relu, training = ctx.conf
-        C = x.shape[-1]
-        rows = x.numel() // C
-        dev = x.device
-        s = stream()
-        dy = dy.contiguous()
-        nrows = lib.acfe_reduce_blocks(rows)
-        part = _empty((nrows * 2 * C,), F64, dev)
-        call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
-             ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
-        dgamma, dbeta = _empty((C,), F32, dev), _empty((C,), F32, dev)
-        coef = _empty((3 * C,), F32, dev)
-        # eval mode: statistics are constants -> count -> inf removes the mean terms
-        count = float(rows) if training else 1e300
-        call("acfe_bn_bwd_finalize", ptr(part), nrows, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
-             ptr(dbeta), ptr(coef), s)
-        dx = _empty(x.shape, x.dtype, dev)
-        call("acfe_bn_bwd_apply", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
-             ptr(shift), int(relu), ptr(coef), None, ptr(dx), dtype_code(x.dtype), s)
-        return dx, dgamma, dbeta, None, None, None, None, None, None, None, None
+        x, *saved = ctx.saved_tensors
+        relu, training, link = ctx.conf
+        add = link.take() if link is not None else None
+        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add)
+        return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
-def batch_norm(x, gamma, beta, mmean, mvar, training, relu=False, stats=None, eps=1e-3, momentum=0.99):
+def batch_norm(x, gamma, beta, mmean, mvar, training, relu=False, stats=None, eps=1e-3, momentum=0.99, link=None):
     return _BNFn.apply(x, gamma, beta, stats, mmean, mvar, bool(training), bool(relu), float(eps),
-                       float(momentum), x.dtype)
+                       float(momentum), x.dtype, link)
+
+
+class _ConvDropBNFn(torch.autograd.Function):
+    """BatchNormalization(+ReLU) of Dropout(Conv2D(x)) as one node: the dropout
+    and the BN statistics run in the conv epilogue (acfe_conv2d_fwd_dropout),
+    the dropout backward inside acfe_bn_bwd_apply_dropout."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
+        stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum = conf
+        drop = (rate, seed) if training and rate > 0.0 else None
+        u, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, training, drop)
+        y, saved = _bn_fwd(u, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
+                           u.dtype)
+        ctx.save_for_backward(x, w, u, *saved)
+        ctx.conf = conf
+        ctx.has_b = b is not None
+        ctx.drop = drop
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, u, *saved = ctx.saved_tensors
+        stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum = ctx.conf
+        g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop)
+        dx, dw, db = _conv_bwd(x, w, g, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               ctx.has_b and ctx.needs_input_grad[2])
+        return dx, dw, db, dgamma, dbeta, None, None, None
+
+
+def conv_dropout_bn(x, w, b, gamma, beta, mmean, mvar, training, rate=0.0, seed=None, relu=True, stride=1,
+                    padding="same", eps=1e-3, momentum=0.99):
+    """BN(Dropout(Conv2D(x))) (+ReLU), Keras semantics of each layer."""
+    if not FUSE:
+        u, _ = conv2d(x, w, b, stride, padding)
+        u = dropout(u, rate, training, seed)
+        return batch_norm(u, gamma, beta, mmean, mvar, training, relu=relu, eps=eps, momentum=momentum)
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    if padding == "same":
+        P, pt = same_padding(H, R, stride)
+        Q, pl = same_padding(W, S, stride)
+    else:
+        P, Q, pt, pl = valid_out(H, R, stride), valid_out(W, S, stride), 0, 0
+    if training and rate > 0.0 and seed is None:
+        seed = next_seed()
+    conf = (stride, pt, pl, P, Q, float(rate), int(seed or 0), bool(training), bool(relu), float(eps),
+            float(momentum))
+    return _ConvDropBNFn.apply(x, w, b, gamma, beta, mmean, mvar, conf)
 
 
 # ------------------------------------------------------------------ elementwise / pooling
 class _AddFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b, relu):
+    def forward(ctx, a, b, relu, want_stats, link):
         z = torch.empty_like(a)
-        call("acfe_add", ptr(a), ptr(b), a.numel(), int(relu), ptr(z), dtype_code(a.dtype), stream())
-        ctx.relu = relu
+        stats = _no_stats(a.device)
+        C = a.shape[-1]
+        if want_stats:
+            rows = a.numel() // C
+            stats = _empty((lib.acfe_reduce_blocks(rows), 2, C), F64, a.device)
+            call("acfe_add_stats", ptr(a), ptr(b), rows, C, int(relu), ptr(z), dtype_code(a.dtype), ptr(stats),
+                 stream())
+        else:
+            call("acfe_add", ptr(a), ptr(b), a.numel(), int(relu), ptr(z), dtype_code(a.dtype), stream())
+        ctx.relu, ctx.link = relu, link
         if relu:
             ctx.save_for_backward(z)
-        return z
+        ctx.mark_non_differentiable(stats)
+        return z, stats
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, _gs):
         g = g.contiguous()
         if ctx.relu:
             (z,) = ctx.saved_tensors
             d = torch.empty_like(g)
             call("acfe_relu_bwd", ptr(g), ptr(z), g.numel(), ptr(d), dtype_code(g.dtype), stream())
             g = d
-        return g, g, None
+        if ctx.link is not None:  # the shortcut input's gradient is added by the linked BN backward
+            ctx.link.grad = g
+            return g, None, None, None, None
+        return g, g, None, None, None
 
 
-def add(a, b, relu=False):
-    return _AddFn.apply(a.contiguous(), b.contiguous(), bool(relu))
+def add(a, b, relu=False, want_stats=False, link=None):
+    """z = a + b (+ReLU); with want_stats returns (z, BN statistics slab of z).
+    `link`: ResidualLink whose BN consumer of `b` adds b's gradient itself."""
+    z, st = _AddFn.apply(a.contiguous(), b.contiguous(), bool(relu), bool(want_stats), link)
+    return (z, st) if want_stats else z
 
 
 class _DropoutFn(torch.autograd.Function):
@@ -318,37 +445,124 @@ class _DropoutFn(torch.autograd.Function):
 _seed_counter = itertools.count(1)
 
 
+def next_seed() -> int:
+    return (0x5EED << 32) + next(_seed_counter)
+
+
 def dropout(x, rate, training, seed=None):
     if not training or rate == 0.0:
         return x
     if seed is None:
-        seed = (0x5EED << 32) + next(_seed_counter)
+        seed = next_seed()
     return _DropoutFn.apply(x, float(rate), int(seed))
+
+
+def _pool_fused_ok(x, kh, kw):
+    C = x.shape[-1]
+    return ((kh, kw) in ((1, 2), (2, 2), (3, 3)) and C % 8 == 0 and 256 % (C // 8) == 0 and C <= 2048
+            and x.data_ptr() % 16 == 0)
+
+
+def _maxpool_fwd(x, kh, kw, drop, want_stats):
+    """acfe_maxpool2d_fused -> (y, argmax bytes, stats slab or empty)."""
+    N, H, W, C = x.shape
+    P, Q = H // kh, W // kw
+    y = _empty((N, P, Q, C), x.dtype, x.device)
+    amax = _empty((N, P, Q, C), torch.uint8, x.device)
+    stats = _no_stats(x.device)
+    if want_stats:
+        stats = _empty((lib.acfe_reduce_blocks(N * P * Q), 2, C), F64, x.device)
+    rate, seed = drop if drop is not None else (0.0, 0)
+    call("acfe_maxpool2d_fused", ptr(x), N, H, W, C, kh, kw, ptr(y), ptr(amax), float(rate), int(seed),
+         ptr(stats) if want_stats else None, dtype_code(x.dtype), stream())
+    return y, amax, stats
+
+
+def _maxpool_bwd(amax, g, shape, kh, kw, drop):
+    N, H, W, C = shape
+    g = g.contiguous()
+    dx = _empty(shape, g.dtype, g.device)
+    rate, seed = drop if drop is not None else (0.0, 0)
+    call("acfe_maxpool2d_bwd_argmax", ptr(amax), ptr(g), N, H, W, C, kh, kw, float(rate), int(seed), ptr(dx),
+         dtype_code(g.dtype), stream())
+    return dx
 
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, kh, kw):
-        N, H, W, C = x.shape
-        y = _empty((N, H // kh, W // kw, C), x.dtype, x.device)
-        call("acfe_maxpool2d", ptr(x), N, H, W, C, kh, kw, ptr(y), dtype_code(x.dtype), stream())
-        ctx.save_for_backward(x)
-        ctx.k = (kh, kw)
-        return y
+    def forward(ctx, x, kh, kw, want_stats):
+        ctx.k, ctx.shape = (kh, kw), x.shape
+        if (FUSE or want_stats) and _pool_fused_ok(x, kh, kw):
+            y, amax, stats = _maxpool_fwd(x, kh, kw, None, want_stats)
+            ctx.save_for_backward(amax)
+            ctx.fused = True
+        else:
+            if want_stats:
+                raise ValueError("max_pool statistics need C % 8 == 0 and a (1,2)/(2,2)/(3,3) window")
+            N, H, W, C = x.shape
+            y = _empty((N, H // kh, W // kw, C), x.dtype, x.device)
+            call("acfe_maxpool2d", ptr(x), N, H, W, C, kh, kw, ptr(y), dtype_code(x.dtype), stream())
+            ctx.save_for_backward(x)
+            ctx.fused = False
+            stats = _no_stats(x.device)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
 
     @staticmethod
-    def backward(ctx, g):
-        (x,) = ctx.saved_tensors
+    def backward(ctx, g, _gs):
         kh, kw = ctx.k
+        if ctx.fused:
+            (amax,) = ctx.saved_tensors
+            return _maxpool_bwd(amax, g, ctx.shape, kh, kw, None), None, None, None
+        (x,) = ctx.saved_tensors
         N, H, W, C = x.shape
         g = g.contiguous()
         dx = torch.empty_like(x)
         call("acfe_maxpool2d_bwd", ptr(x), ptr(g), N, H, W, C, kh, kw, ptr(dx), dtype_code(x.dtype), stream())
-        return dx, None, None
+        return dx, None, None, None
 
 
-def max_pool(x, kh, kw):
-    return _MaxPoolFn.apply(x, kh, kw)
+def max_pool(x, kh, kw, want_stats=False):
+    y, st = _MaxPoolFn.apply(x, kh, kw, bool(want_stats))
+    return (y, st) if want_stats else y
+
+
+class _PoolDropBNFn(torch.autograd.Function):
+    """BatchNormalization(+ReLU) of Dropout(MaxPool2D(x)) as one node
+    (acfe_maxpool2d_fused writes the pooled+dropped values, their argmax
+    bytes and BN statistics in one pass; backward from the argmax bytes)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, mmean, mvar, conf):
+        kh, kw, rate, seed, training, relu, eps, momentum = conf
+        drop = (rate, seed) if training and rate > 0.0 else None
+        u, amax, stats = _maxpool_fwd(x, kh, kw, drop, training)
+        y, saved = _bn_fwd(u, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
+                           u.dtype)
+        ctx.save_for_backward(u, amax, *saved)
+        ctx.conf, ctx.drop, ctx.shape = conf, drop, x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        u, amax, *saved = ctx.saved_tensors
+        kh, kw, rate, seed, training, relu, eps, momentum = ctx.conf
+        gu, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training)
+        dx = _maxpool_bwd(amax, gu, ctx.shape, kh, kw, ctx.drop)
+        return dx, dgamma, dbeta, None, None, None
+
+
+def maxpool_dropout_bn(x, kh, kw, gamma, beta, mmean, mvar, training, rate=0.0, seed=None, relu=True, eps=1e-3,
+                       momentum=0.99):
+    """BN(Dropout(MaxPool2D((kh, kw))(x))) (+ReLU)."""
+    if not FUSE or not _pool_fused_ok(x, kh, kw):
+        y = max_pool(x, kh, kw)
+        y = dropout(y, rate, training, seed)
+        return batch_norm(y, gamma, beta, mmean, mvar, training, relu=relu, eps=eps, momentum=momentum)
+    if training and rate > 0.0 and seed is None:
+        seed = next_seed()
+    conf = (kh, kw, float(rate), int(seed or 0), bool(training), bool(relu), float(eps), float(momentum))
+    return _PoolDropBNFn.apply(x, gamma, beta, mmean, mvar, conf)
 
 
 class _AvgPoolFn(torch.autograd.Function):

@@ -65,4 +65,29 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
   return (uint32_t)(z >> 32);
 }
 
+// Rounding to the storage type (the value a separate kernel would have stored).
+__device__ __forceinline__ float rnd(float v, uint16_t) { return bf2f(f2bf(v)); }
+__device__ __forceinline__ float rnd(float v, float) { return v; }
+
+// Dropout keep test + scale of acfe_dropout (flat element index idx).
+struct Drop {
+  uint32_t thr;
+  float scl;
+  unsigned long long seed;
+  bool on;
+};
+inline Drop make_drop(float rate, unsigned long long seed) {
+  Drop d;
+  d.on = rate > 0.f;
+  const float t = rate * 4294967296.0f;  // exact (power-of-two scale); saturate like v_cvt_u32_f32
+  d.thr = t >= 4294967296.0f ? 0xFFFFFFFFu : (uint32_t)t;
+  d.scl = 1.0f / (1.0f - rate);
+  d.seed = seed;
+  return d;
+}
+template <typename T>
+__device__ __forceinline__ float drop_apply(const Drop& d, uint64_t idx, float v) {
+  return hash_u32(d.seed, idx) >= d.thr ? rnd(v * d.scl, T()) : 0.f;
+}
+
 }  // namespace acfe

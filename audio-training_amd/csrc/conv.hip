@@ -40,6 +40,7 @@ struct ConvGeom {
   int Kd, Kdp, Kp;   // R*S*C, padded to BK, K padded to BN
   int ldy;           // output row stride (elements)
   long long M;       // N*P*Q
+  Drop drop;         // optional Dropout of the output (flat index m*K + k), fused in the epilogue
 };
 
 // 64 bytes of zeros in global memory: im2col taps that fall into the padding
@@ -223,7 +224,9 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = wm * TWM + fm * 16 + (lane >> 4) * 4 + j;
-          const T tv = cvt_out(acc[fm][fn][j] + bv, T());
+          T tv = cvt_out(acc[fm][fn][j] + bv, T());
+          if (g.drop.on)
+            tv = cvt_out(drop_apply<T>(g.drop, (uint64_t)(m0 + row) * g.K + gcn, to_f(tv)), T());
           Cs[row * LC + col] = tv;
           if (m0 + row < g.M) {
             const float f = to_f(tv);
@@ -414,7 +417,9 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = wm * TWM + fm * 16 + (lane >> 4) * 4 + j;
-          const T tv = cvt_out(acc[fm][fn][j] + bv, T());
+          T tv = cvt_out(acc[fm][fn][j] + bv, T());
+          if (g.drop.on)
+            tv = cvt_out(drop_apply<T>(g.drop, (uint64_t)(m0 + row) * g.K + gcn, to_f(tv)), T());
           Cs[row * LC + col] = tv;
           if (m0 + row < g.M) {
             const float f = to_f(tv);
@@ -811,6 +816,7 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.Kp = (K + BN - 1) / BN * BN;
   g.ldy = K;
   g.M = (long long)N * P * Q;
+  g.drop = make_drop(0.f, 0);
   return g;
 }
 
@@ -881,10 +887,9 @@ ACFE_API int acfe_conv2d_stats_rows(long long M, int K) {
   return grid_m_for(M, (K + pick_bn(K) - 1) / pick_bn(K));
 }
 
-ACFE_API int acfe_conv2d_fwd(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R,
-                             int S, int stride, int pad_top, int pad_left, int P, int Q,
-                             const float* bias, void* y, int dtype, double* stats_partial,
-                             void* stream) {
+static int conv2d_fwd_impl(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R, int S,
+                           int stride, int pad_top, int pad_left, int P, int Q, const float* bias, void* y,
+                           int dtype, double* stats_partial, const Drop& drop, void* stream) {
   if (!x || !wpacked || !y || N < 0 || H <= 0 || W <= 0 || C <= 0 || K <= 0 || R <= 0 || S <= 0 ||
       stride <= 0 || P <= 0 || Q <= 0 || (dtype != 0 && dtype != 1))
     return ACFE_E_INVAL;
@@ -892,9 +897,29 @@ ACFE_API int acfe_conv2d_fwd(const void* x, int N, int H, int W, int C, const vo
   const int BK = dtype == ACFE_DTYPE_BF16 ? 64 : 32;
   const int bn = pick_bn(K);
   ConvGeom g = make_geom(N, H, W, C, K, R, S, stride, pad_top, pad_left, P, Q, BK, bn);
+  g.drop = drop;
   const int gm = grid_m_for(g.M, g.Kp / bn);
   if (dtype == ACFE_DTYPE_BF16) return launch_fwd<uint16_t>(g, x, wpacked, bias, y, stats_partial, gm, strm(stream));
   return launch_fwd<float>(g, x, wpacked, bias, y, stats_partial, gm, strm(stream));
+}
+
+ACFE_API int acfe_conv2d_fwd(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R,
+                             int S, int stride, int pad_top, int pad_left, int P, int Q,
+                             const float* bias, void* y, int dtype, double* stats_partial,
+                             void* stream) {
+  return conv2d_fwd_impl(x, N, H, W, C, wpacked, K, R, S, stride, pad_top, pad_left, P, Q, bias, y, dtype,
+                         stats_partial, make_drop(0.f, 0), stream);
+}
+
+// y = Dropout(rate, seed)(conv(x)): the epilogue applies acfe_dropout's mask to
+// the rounded outputs; the statistics are those of the dropped-out values.
+ACFE_API int acfe_conv2d_fwd_dropout(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R,
+                                     int S, int stride, int pad_top, int pad_left, int P, int Q,
+                                     const float* bias, void* y, int dtype, double* stats_partial,
+                                     float drop_rate, unsigned long long seed, void* stream) {
+  if (drop_rate < 0.f || drop_rate >= 1.f) return ACFE_E_INVAL;
+  return conv2d_fwd_impl(x, N, H, W, C, wpacked, K, R, S, stride, pad_top, pad_left, P, Q, bias, y, dtype,
+                         stats_partial, make_drop(drop_rate, seed), stream);
 }
 
 // dX = conv^T(dY, W).  wflip = acfe_conv2d_pack_weights(..., flip=1).

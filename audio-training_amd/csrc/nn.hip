@@ -74,6 +74,8 @@ static bool vec_ok(long long n, int C, const void* a, const void* b = nullptr, c
 }
 static int vgrid(long long nvec) { return grid_for(nvec, 256, 16384); }
 
+
+
 // Sum a [nrows][2][ld] double slab over rows for the 32 channels of this block
 // (8 row groups x 32 channels, fixed order): s[j][cl] for j in {0, 1}.
 __device__ __forceinline__ void slab_sum32(const double* __restrict__ part, int nrows, int ld, int C,
@@ -440,7 +442,8 @@ ACFE_API int acfe_bn_bwd_finalize(const double* part, int nrows, int C, double c
 template <typename TG, typename TX, typename TO>
 __global__ void k_bn_bwd_apply(const TG* __restrict__ dy, const TX* __restrict__ x, long long n, int C,
                                const float* __restrict__ scale, const float* __restrict__ shift, int relu,
-                               const float* __restrict__ coef, const TO* __restrict__ add, TO* __restrict__ dx) {
+                               const float* __restrict__ coef, const TO* __restrict__ add, Drop drop,
+                               TO* __restrict__ dx) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const int c = (int)(i % C);
     const float xv = ld(x, i);
@@ -448,6 +451,7 @@ __global__ void k_bn_bwd_apply(const TG* __restrict__ dy, const TX* __restrict__
     if (relu && !(xv * scale[c] + shift[c] > 0.f)) g = 0.f;
     float v = coef[c] * g + coef[C + c] * xv + coef[2 * C + c];
     if (add) v += ld(add, i);
+    if (drop.on) v = drop_apply<TO>(drop, (uint64_t)i, rnd(v, TO()));
     st(dx, i, v);
   }
 }
@@ -456,7 +460,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
                                                        unsigned nvec, int C, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int relu,
                                                        const float* __restrict__ coef, const TO* __restrict__ add,
-                                                       TO* __restrict__ dx) {
+                                                       Drop drop, TO* __restrict__ dx) {
   extern __shared__ float sm[];  // scale, shift, a, b, c
   for (int i = threadIdx.x; i < C; i += 256) {
     sm[i] = scale[i];
@@ -480,13 +484,17 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
       const float r = sm[2 * C + c] * gj + sm[3 * C + c] * xv[j] + sm[4 * C + c];
       o[j] = add ? o[j] + r : r;
     }
+    if (drop.on) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = drop_apply<TO>(drop, (uint64_t)v * 8 + j, rnd(o[j], TO()));
+    }
     st8(dx + (size_t)v * 8, o);
   }
 }
 
-ACFE_API int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
-                               const float* scale, const float* shift, int relu, const float* coef,
-                               const void* add, void* dx, int dx_dtype, void* stream) {
+static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                             const float* scale, const float* shift, int relu, const float* coef, const void* add,
+                             const Drop& d, void* dx, int dx_dtype, void* stream) {
   if (!dy || !x || !scale || !shift || !coef || !dx || rows < 0 || C <= 0) return ACFE_E_INVAL;
   const long long n = rows * C;
   if (n == 0) return ACFE_OK;
@@ -494,13 +502,31 @@ ACFE_API int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int 
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
         hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(vgrid(n / 8)), dim3(256), 5 * C * sizeof(float),
                            strm(stream), (const TG*)dy, (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu,
-                           coef, (const TO*)add, (TO*)dx))));
+                           coef, (const TO*)add, d, (TO*)dx))));
   } else {
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
         hipLaunchKernelGGL((k_bn_bwd_apply<TG, TX, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream),
-                           (const TG*)dy, (const TX*)x, n, C, scale, shift, relu, coef, (const TO*)add, (TO*)dx))));
+                           (const TG*)dy, (const TX*)x, n, C, scale, shift, relu, coef, (const TO*)add, d,
+                           (TO*)dx))));
   }
   return launch_rc("acfe_bn_bwd_apply");
+}
+
+ACFE_API int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                               const float* scale, const float* shift, int relu, const float* coef,
+                               const void* add, void* dx, int dx_dtype, void* stream) {
+  return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, rows, C, scale, shift, relu, coef, add, make_drop(0.f, 0),
+                           dx, dx_dtype, stream);
+}
+
+// As acfe_bn_bwd_apply, then the backward of a Dropout(rate, seed) that produced x.
+ACFE_API int acfe_bn_bwd_apply_dropout(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows,
+                                       int C, const float* scale, const float* shift, int relu, const float* coef,
+                                       float drop_rate, unsigned long long seed, void* dx, int dx_dtype,
+                                       void* stream) {
+  if (drop_rate < 0.f || drop_rate >= 1.f) return ACFE_E_INVAL;
+  return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, rows, C, scale, shift, relu, coef, nullptr,
+                           make_drop(drop_rate, seed), dx, dx_dtype, stream);
 }
 
 // ---------------------------------------------------------------- elementwise
@@ -771,6 +797,216 @@ ACFE_API int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int
   return launch_rc("acfe_maxpool2d_bwd");
 }
 
+// ---------------------------------------------------------------- fused pooling
+// Per-thread 8-channel statistics -> block slab row part[blockIdx][2][C].
+// Requires the grid stride (gridDim.x * 256 vectors) to be a multiple of C/8,
+// so every vector a thread visits has the same channel group.
+__device__ __forceinline__ void stats8_flush(const double* a, const double* b, int cv, int C, bool active,
+                                             double* red, double* __restrict__ part) {
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(&red[cv * 8 + j], a[j]);
+      atomicAdd(&red[C + cv * 8 + j], b[j]);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
+}
+
+// y = [dropout](maxpool(x)); optional argmax byte per output element (first
+// maximum, as the backward of the reference), optional BN statistics of y.
+template <typename T, int KH, int KW>
+__global__ void __launch_bounds__(256) k_maxpool8x(const T* __restrict__ x, int N, int H, int W, int C, int P, int Q,
+                                                   T* __restrict__ y, uint8_t* __restrict__ amax, Drop drop,
+                                                   double* __restrict__ part) {
+  extern __shared__ double red[];  // [2][C] when part
+  if (part) {
+    for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+    __syncthreads();
+  }
+  const int CV = C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  double sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
+  const unsigned v0 = blockIdx.x * 256 + threadIdx.x;
+  for (unsigned v = v0; v < total; v += gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    unsigned t = v / CV;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float m[8];
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY, am[j] = 0;
+#pragma unroll
+    for (int a = 0; a < KH; ++a)
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
+        float f[8];
+        ld8(x + (((size_t)n * H + p * KH + a) * W + q * KW + b) * C + cv * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > m[j]) m[j] = f[j], am[j] = a * KW + b;
+      }
+    if (drop.on) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = drop_apply<T>(drop, (uint64_t)v * 8 + j, m[j]);
+    }
+    st8(y + (size_t)v * 8, m);
+    if (amax) {
+      uint2 pk;
+      pk.x = am[0] | (am[1] << 8) | (am[2] << 16) | (am[3] << 24);
+      pk.y = am[4] | (am[5] << 8) | (am[6] << 16) | (am[7] << 24);
+      *reinterpret_cast<uint2*>(amax + (size_t)v * 8) = pk;
+    }
+    if (part) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float r = rnd(m[j], T());
+        sa[j] += r;
+        sb[j] += (double)r * r;
+      }
+    }
+  }
+  if (part) stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < total, red, part);
+}
+
+// dx from the saved argmax bytes: dy is first passed through the dropout of
+// the forward (when drop.on), exactly as acfe_dropout would have stored it.
+template <typename T, int KH, int KW>
+__global__ void __launch_bounds__(256) k_maxpool_bwd8i(const uint8_t* __restrict__ amax, const T* __restrict__ dy,
+                                                       int N, int H, int W, int C, int P, int Q, Drop drop,
+                                                       T* __restrict__ dx) {
+  const int CV = C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < total; v += gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    unsigned t = v / CV;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float g[8];
+    ld8(dy + (size_t)v * 8, g);
+    if (drop.on) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = drop_apply<T>(drop, (uint64_t)v * 8 + j, g[j]);
+    }
+    const uint2 pk = *reinterpret_cast<const uint2*>(amax + (size_t)v * 8);
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) am[j] = (pk.x >> (8 * j)) & 0xff, am[4 + j] = (pk.y >> (8 * j)) & 0xff;
+#pragma unroll
+    for (int a = 0; a < KH; ++a)
+#pragma unroll
+      for (int b = 0; b < KW; ++b) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = am[j] == a * KW + b ? g[j] : 0.f;
+        st8(dx + (((size_t)n * H + p * KH + a) * W + q * KW + b) * C + cv * 8, o);
+      }
+    const float z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q == Q - 1)
+      for (int a = 0; a < KH; ++a)
+        for (int w = Q * KW; w < W; ++w) st8(dx + (((size_t)n * H + p * KH + a) * W + w) * C + cv * 8, z);
+    if (p == P - 1)
+      for (int h = P * KH; h < H; ++h) {
+        for (int w = q * KW; w < q * KW + KW; ++w) st8(dx + (((size_t)n * H + h) * W + w) * C + cv * 8, z);
+        if (q == Q - 1)
+          for (int w = Q * KW; w < W; ++w) st8(dx + (((size_t)n * H + h) * W + w) * C + cv * 8, z);
+      }
+  }
+}
+
+static bool stats8_ok(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0 && C <= 2048; }
+
+ACFE_API int acfe_maxpool2d_fused(const void* x, int N, int H, int W, int C, int kh, int kw, void* y,
+                                  uint8_t* argmax, float drop_rate, unsigned long long seed, double* stats_part,
+                                  int dtype, void* stream) {
+  if (!x || !y || N <= 0 || kh <= 0 || kw <= 0 || H < kh || W < kw || drop_rate < 0.f || drop_rate >= 1.f)
+    return ACFE_E_INVAL;
+  const int P = H / kh, Q = W / kw;
+  const long long rows = (long long)N * P * Q;
+  if (!vec_ok((long long)N * H * W * C, C, x, y) || ((uintptr_t)argmax & 7) || rows * (C / 8) >= 0xFFFFFFFFll ||
+      (stats_part && !stats8_ok(C)))
+    return ACFE_E_INVAL;
+  const Drop d = make_drop(drop_rate, seed);
+  const int grid = stats_part ? red_blocks(rows) : vgrid(rows * C / 8);
+  const size_t shm = stats_part ? 2 * C * sizeof(double) : 0;
+#define MPF(A, B)                                                                                           \
+  if (kh == A && kw == B) {                                                                                 \
+    DISPATCH1(dtype, T, hipLaunchKernelGGL((k_maxpool8x<T, A, B>), dim3(grid), dim3(256), shm, strm(stream),  \
+                                           (const T*)x, N, H, W, C, P, Q, (T*)y, argmax, d, stats_part));   \
+    return launch_rc("acfe_maxpool2d_fused");                                                               \
+  }
+  MAXPOOL_SHAPES(MPF)
+#undef MPF
+  return ACFE_E_INVAL;
+}
+
+ACFE_API int acfe_maxpool2d_bwd_argmax(const uint8_t* argmax, const void* dy, int N, int H, int W, int C, int kh,
+                                       int kw, float drop_rate, unsigned long long seed, void* dx, int dtype,
+                                       void* stream) {
+  if (!argmax || !dy || !dx || N <= 0 || kh <= 0 || kw <= 0 || H < kh || W < kw || drop_rate < 0.f ||
+      drop_rate >= 1.f)
+    return ACFE_E_INVAL;
+  const int P = H / kh, Q = W / kw;
+  const long long nw = (long long)N * P * Q * (C / 8);
+  if (!vec_ok((long long)N * H * W * C, C, dy, dx) || ((uintptr_t)argmax & 7) || nw >= 0xFFFFFFFFll)
+    return ACFE_E_INVAL;
+  const Drop d = make_drop(drop_rate, seed);
+#define MPBI(A, B)                                                                                          \
+  if (kh == A && kw == B) {                                                                                 \
+    DISPATCH1(dtype, T, hipLaunchKernelGGL((k_maxpool_bwd8i<T, A, B>), dim3(vgrid(nw)), dim3(256), 0,       \
+                                           strm(stream), argmax, (const T*)dy, N, H, W, C, P, Q, d, (T*)dx)); \
+    return launch_rc("acfe_maxpool2d_bwd_argmax");                                                          \
+  }
+  MAXPOOL_SHAPES(MPBI)
+#undef MPBI
+  return ACFE_E_INVAL;
+}
+
+// z = a + b (+ReLU) with the BN statistics of z (slab rows = acfe_reduce_blocks(rows)).
+template <typename T>
+__global__ void __launch_bounds__(256) k_add8s(const T* __restrict__ a, const T* __restrict__ b, unsigned nvec,
+                                               int C, int relu, T* __restrict__ z, double* __restrict__ part) {
+  extern __shared__ double red[];
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+  __syncthreads();
+  const int CV = C >> 3;
+  double sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
+  const unsigned v0 = blockIdx.x * 256 + threadIdx.x;
+  for (unsigned v = v0; v < nvec; v += gridDim.x * 256) {
+    float x[8], y[8];
+    ld8(a + (size_t)v * 8, x);
+    ld8(b + (size_t)v * 8, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[j] = relu ? fmaxf(x[j] + y[j], 0.f) : x[j] + y[j];
+      const float r = rnd(x[j], T());
+      sa[j] += r;
+      sb[j] += (double)r * r;
+    }
+    st8(z + (size_t)v * 8, x);
+  }
+  stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, part);
+}
+
+ACFE_API int acfe_add_stats(const void* a, const void* b, long long rows, int C, int relu, void* z, int dtype,
+                            double* part, void* stream) {
+  if (!a || !b || !z || !part || rows <= 0 || !stats8_ok(C) || !vec_ok(rows * C, C, a, b, z)) return ACFE_E_INVAL;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_add8s<T>, dim3(red_blocks(rows)), dim3(256), 2 * C * sizeof(double),
+                                         strm(stream), (const T*)a, (const T*)b, (unsigned)(rows * C / 8), C, relu,
+                                         (T*)z, part));
+  return launch_rc("acfe_add_stats");
+}
+
 // AveragePooling2D(pool=k, strides=k, padding="same"): P = ceil(H/k); TF pads
 // (total = (P-1)*k + k - H) with pad_top = total/2 and averages over the
 // in-bounds elements only.
@@ -823,12 +1059,76 @@ __global__ void k_avgpool_bwd(const T* __restrict__ dy, int N, int H, int W, int
     st(dx, i, g);
   }
 }
+// 8-channel versions: one thread per (output window, 8 channels); the windows
+// tile the padded input exactly (stride == pool), so the backward writes every
+// input element once.
+template <typename T>
+__global__ void __launch_bounds__(256) k_avgpool8(const T* __restrict__ x, int N, int H, int W, int C, int k, int P,
+                                                  int Q, int pt, int pl, T* __restrict__ y) {
+  const int CV = C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < total; v += gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    unsigned t = v / CV;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int cnt = 0;
+    for (int a = 0; a < k; ++a) {
+      const int h = p * k - pt + a;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int b = 0; b < k; ++b) {
+        const int w = q * k - pl + b;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float f[8];
+        ld8(x + (((size_t)n * H + h) * W + w) * C + cv * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+        ++cnt;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = s[j] / (float)cnt;
+    st8(y + (size_t)v * 8, s);
+  }
+}
+template <typename T>
+__global__ void __launch_bounds__(256) k_avgpool_bwd8(const T* __restrict__ dy, int N, int H, int W, int C, int k,
+                                                      int P, int Q, int pt, int pl, T* __restrict__ dx) {
+  const int CV = C >> 3;
+  const unsigned total = (unsigned)N * P * Q * CV;
+  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < total; v += gridDim.x * 256) {
+    const int cv = (int)(v % CV);
+    unsigned t = v / CV;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    const int h0 = max(p * k - pt, 0), h1 = min(p * k - pt + k, H);
+    const int w0 = max(q * k - pl, 0), w1 = min(q * k - pl + k, W);
+    const float inv = 1.0f / (float)((h1 - h0) * (w1 - w0));
+    float g[8];
+    ld8(dy + (size_t)v * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = g[j] * inv;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) st8(dx + (((size_t)n * H + h) * W + w) * C + cv * 8, g);
+  }
+}
+
 ACFE_API int acfe_avgpool2d(const void* x, int N, int H, int W, int C, int k, void* y, int dtype, void* stream) {
   if (!x || !y || N < 0 || k <= 0) return ACFE_E_INVAL;
   const int P = (H + k - 1) / k, Q = (W + k - 1) / k;
   const int pt = ((P - 1) * k + k - H) / 2, pl = ((Q - 1) * k + k - W) / 2;
   const long long n = (long long)N * P * Q * C;
   if (n == 0) return ACFE_OK;
+  if (vec_ok((long long)N * H * W * C, C, x, y) && n / 8 < 0xFFFFFFFFll) {
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_avgpool8<T>, dim3(vgrid(n / 8)), dim3(256), 0, strm(stream),
+                                           (const T*)x, N, H, W, C, k, P, Q, pt, pl, (T*)y));
+    return launch_rc("acfe_avgpool2d");
+  }
   DISPATCH1(dtype, T, hipLaunchKernelGGL(k_avgpool<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream), (const T*)x,
                                          N, H, W, C, k, P, Q, pt, pl, (T*)y));
   return launch_rc("acfe_avgpool2d");
@@ -840,6 +1140,12 @@ ACFE_API int acfe_avgpool2d_bwd(const void* dy, int N, int H, int W, int C, int 
   const int pt = ((P - 1) * k + k - H) / 2, pl = ((Q - 1) * k + k - W) / 2;
   const long long n = (long long)N * H * W * C;
   if (n == 0) return ACFE_OK;
+  const long long nw = (long long)N * P * Q * (C / 8);
+  if (vec_ok(n, C, dy, dx) && nw < 0xFFFFFFFFll) {
+    DISPATCH1(dtype, T, hipLaunchKernelGGL(k_avgpool_bwd8<T>, dim3(vgrid(nw)), dim3(256), 0, strm(stream),
+                                           (const T*)dy, N, H, W, C, k, P, Q, pt, pl, (T*)dx));
+    return launch_rc("acfe_avgpool2d_bwd");
+  }
   DISPATCH1(dtype, T, hipLaunchKernelGGL(k_avgpool_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
                                          (const T*)dy, N, H, W, C, k, P, Q, pt, pl, (T*)dx));
   return launch_rc("acfe_avgpool2d_bwd");

@@ -11,7 +11,7 @@ import torch
 from torch import nn
 
 from acfe import ops
-from acfe.layers import BatchNormalization, Conv2D, Dense, StemConv2D
+from acfe.layers import BatchNormalization, Conv2D, Dense, StemConv2D, conv_dropout_bn
 
 
 class BasicBlock(nn.Module):
@@ -32,14 +32,17 @@ class BasicBlock(nn.Module):
             self.shortcut = Conv2D(cin, F2, 1, stride, "valid", name=f"conv2d_shortcut_{stage}{block}", seed=seed + 1)
         self.out_channels = F2
 
-    def forward(self, x):
-        y = self.bn2a(x, relu=True)
-        y = self.conv2a(y)
-        y = ops.dropout(y, self.dropout, self.training)
-        y = self.bn2b(y, relu=True)
+    def forward(self, x, x_stats=None):
+        """x -> (block output, its BN statistics slab in training else None);
+        conv2a + Dropout + bn2b run as one fused node (ops.conv_dropout_bn)."""
+        link = ops.ResidualLink.make() if self.shortcut is None else None
+        y = self.bn2a(x, relu=True, stats=x_stats, link=link)
+        y = conv_dropout_bn(self.conv2a, self.bn2b, y, self.dropout)
         y = self.conv2b(y)
         sc = x if self.shortcut is None else self.shortcut(x)
-        return ops.add(y, sc, relu=True)
+        if self.training and ops.FUSE:
+            return ops.add(y, sc, relu=True, want_stats=True, link=link)
+        return ops.add(y, sc, relu=True, link=link), None
 
 
 class WRResNet(nn.Module):
@@ -69,10 +72,12 @@ class WRResNet(nn.Module):
     def forward(self, x):
         if x.dim() == 4:
             x = x[..., 0]
-        y = self.conv1_1(x)
+        y, st = self.conv1_1(x, want_stats=True)
+        if not self.training:
+            st = None
         for blk in self.blocks:
-            y = blk(y)
-        y = self.final_bn(y, relu=True)
+            y, st = blk(y, st)
+        y = self.final_bn(y, relu=True, stats=st)
         y = ops.global_avg_pool(y)
         return self.prediction(y)
 

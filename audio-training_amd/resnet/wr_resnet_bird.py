@@ -19,7 +19,8 @@ import torch
 from torch import nn
 
 from acfe import ops
-from acfe.layers import BatchNormalization, Conv2D, Dense, StemConv2D
+from acfe.layers import (BatchNormalization, Conv2D, Dense, StemConv2D, conv_dropout_bn,
+                         maxpool_dropout_bn)
 
 
 class BasicBlock(nn.Module):
@@ -45,24 +46,31 @@ class BasicBlock(nn.Module):
         self.out_channels = filters
         self.out_height = height // stride if stride > 1 else height
 
-    def forward(self, x):
+    def forward(self, x, x_stats=None):
+        """x -> (block output, its BN statistics slab in training else None).
+        Fused nodes: conv21 + Dropout + bn2b (stride 1) or MaxPool + Dropout +
+        bn2b (stride 2) in one pass each; the Add writes the statistics the
+        next block's first BN consumes; with an identity shortcut the Add's
+        gradient for x is summed inside that BN's backward (ResidualLink)."""
+        training = self.training
+        link = ops.ResidualLink.make() if self.shortcut is None else None
         y = x
         if self.stride > 1:
-            y = self.bn2a0(y, relu=True)
+            y = self.bn2a0(y, relu=True, stats=x_stats, link=link)
             y, st = self.conv2a0(y, want_stats=True)
             y = self.bn2a(y, relu=True, stats=st)
+            y = self.conv21(y)
+            y = maxpool_dropout_bn(y, self.stride, self.stride, self.bn2b, self.dropout)
         else:
-            y = self.bn2a(y, relu=True)
-        y = self.conv21(y)
-        if self.stride > 1:
-            y = ops.max_pool(y, self.stride, self.stride)
-        y = ops.dropout(y, self.dropout, self.training)
-        y = self.bn2b(y, relu=True)
+            y = self.bn2a(y, relu=True, stats=x_stats, link=link)
+            y = conv_dropout_bn(self.conv21, self.bn2b, y, self.dropout)
         y = self.conv2b(y)
         sc = x
         if self.shortcut is not None:
             sc = self.shortcut(ops.avg_pool_same(x, self.stride))
-        return ops.add(y, sc, relu=self.relu_out)
+        if training and ops.FUSE:
+            return ops.add(y, sc, relu=self.relu_out, want_stats=True, link=link)
+        return ops.add(y, sc, relu=self.relu_out, link=link), None
 
 
 class WRResNet(nn.Module):
@@ -107,10 +115,14 @@ class WRResNet(nn.Module):
             x = x[..., 0]
         y, st = self.conv1_1(x, want_stats=True)
         y = self.bn_stem(y, stats=st)
-        y = ops.max_pool(y, 1, 2)
+        st = None
+        if self.training:
+            y, st = ops.max_pool(y, 1, 2, want_stats=True)
+        else:
+            y = ops.max_pool(y, 1, 2)
         for blk in self.blocks:
-            y = blk(y)
-        y = self.final_bn(y, relu=True)
+            y, st = blk(y, st)
+        y = self.final_bn(y, relu=True, stats=st)
         y, st = self.head_conv1(y, want_stats=True)
         y = self.head_bn1(y, stats=st)
         y = ops.dropout(y, self.dropout, self.training)

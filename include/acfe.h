@@ -156,6 +156,13 @@ int acfe_conv2d_stats_rows(long long M, int K);
 int acfe_conv2d_fwd(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R, int S,
                     int stride, int pad_top, int pad_left, int P, int Q, const float* bias, void* y,
                     int dtype, double* stats_partial, void* stream);
+/* As acfe_conv2d_fwd, then Dropout(rate) of the output fused in the epilogue
+ * (mask of acfe_dropout(seed) over the flat NHWC index; wr_resnet_bird.py:141
+ * Dropout after branch 21); stats_partial then holds the dropped-out values. */
+int acfe_conv2d_fwd_dropout(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int R, int S,
+                            int stride, int pad_top, int pad_left, int P, int Q, const float* bias, void* y,
+                            int dtype, double* stats_partial, float drop_rate, unsigned long long seed,
+                            void* stream);
 /* dX of the convolution above (wflip = flip=1 packing).  workspace: for
  * stride > 1, N*((P-1)*stride+1)*((Q-1)*stride+1)*K elements of dtype. */
 int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R, int S,
@@ -203,6 +210,11 @@ int acfe_bn_bwd_finalize(const double* partial, int nrows, int C, double count, 
 int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                       const float* scale, const float* shift, int relu, const float* coef, const void* add,
                       void* dx, int dx_dtype, void* stream);
+/* acfe_bn_bwd_apply followed by the backward of the Dropout(rate, seed) whose
+ * output was this BatchNormalization's input (no add). */
+int acfe_bn_bwd_apply_dropout(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                              const float* scale, const float* shift, int relu, const float* coef,
+                              float drop_rate, unsigned long long seed, void* dx, int dx_dtype, void* stream);
 
 /* out[c] = beta*out[c] + sum_rows x[r][c] (bias gradients); partial as acfe_bn_stats. */
 int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* partial, float* out, float beta,
@@ -210,6 +222,10 @@ int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* pa
 
 /* Elementwise. */
 int acfe_add(const void* a, const void* b, long long n, int relu, void* z, int dtype, void* stream);
+/* z = a + b (+ReLU) over [rows][C] plus the BN statistics slab of z
+ * (double[acfe_reduce_blocks(rows)][2][C]); C % 8 == 0 and 256 % (C/8) == 0. */
+int acfe_add_stats(const void* a, const void* b, long long rows, int C, int relu, void* z, int dtype,
+                   double* partial, void* stream);
 int acfe_relu_bwd(const void* dy, const void* y, long long n, void* dx, int dtype, void* stream);
 int acfe_dropout(const void* x, long long n, float rate, unsigned long long seed, void* y, int dtype,
                  void* stream);
@@ -222,6 +238,14 @@ int acfe_maxpool2d(const void* x, int N, int H, int W, int C, int kh, int kw, vo
                    void* stream);
 int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int W, int C, int kh, int kw, void* dx,
                        int dtype, void* stream);
+/* MaxPool2D (kh,kw) in {(1,2),(2,2),(3,3)} -> optional Dropout(rate, seed) ->
+ * optional BN statistics slab (partial, as acfe_add_stats; may be NULL), and the
+ * argmax byte of every output element (first maximum, may be NULL; 8-B aligned). */
+int acfe_maxpool2d_fused(const void* x, int N, int H, int W, int C, int kh, int kw, void* y, uint8_t* argmax,
+                         float drop_rate, unsigned long long seed, double* partial, int dtype, void* stream);
+/* Backward of acfe_maxpool2d_fused from its argmax bytes (x is not re-read). */
+int acfe_maxpool2d_bwd_argmax(const uint8_t* argmax, const void* dy, int N, int H, int W, int C, int kh, int kw,
+                              float drop_rate, unsigned long long seed, void* dx, int dtype, void* stream);
 int acfe_avgpool2d(const void* x, int N, int H, int W, int C, int k, void* y, int dtype, void* stream);
 int acfe_avgpool2d_bwd(const void* dy, int N, int H, int W, int C, int k, void* dx, int dtype, void* stream);
 /* Reduce the middle axis of [outer][L][inner] to fp32 [outer][inner]:

@@ -1,0 +1,217 @@
+"""GPU parity of the fused nodes against the same kernels run one op at a time.
+
+Kernel level (bit-exact: the fused kernels must store exactly what the
+separate kernels store):
+  acfe_conv2d_fwd_dropout      == acfe_conv2d_fwd -> acfe_dropout
+  acfe_bn_bwd_apply_dropout    == acfe_bn_bwd_apply -> acfe_dropout
+  acfe_maxpool2d_fused         == acfe_maxpool2d -> acfe_dropout (+ argmax bytes)
+  acfe_maxpool2d_bwd_argmax    == acfe_dropout -> acfe_maxpool2d_bwd
+  acfe_add_stats               == acfe_add
+Statistics slabs (different partial grouping) agree to rel 1e-6 with
+acfe_bn_stats of the stored tensor.
+Node level (autograd): conv_dropout_bn / maxpool_dropout_bn / the
+ResidualLink'd block against the unfused op chain, rel-L2 <= 2e-3 on bf16
+outputs and gradients (BN statistics summed in a different order can move a
+bf16 rounding by one ulp).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def env(cuda):
+    from acfe import ops
+    from acfe._lib import call, lib
+    from acfe._torch import ptr, stream
+
+    return ops, call, lib, ptr, stream
+
+
+def _stats_of(env, t):
+    ops, call, lib, ptr, stream = env
+    C = t.shape[-1]
+    rows = t.numel() // C
+    part = torch.empty((lib.acfe_reduce_blocks(rows), 2, C), dtype=torch.float64, device=t.device)
+    call("acfe_bn_stats", ptr(t), rows, C, 1 if t.dtype == torch.bfloat16 else 0, ptr(part), stream())
+    return part.sum(0)
+
+
+def _dropout(env, t, rate, seed):
+    ops, call, lib, ptr, stream = env
+    y = torch.empty_like(t)
+    call("acfe_dropout", ptr(t), t.numel(), rate, seed, ptr(y), 1 if t.dtype == torch.bfloat16 else 0, stream())
+    return y
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32], ids=["bf16", "f32"])
+@pytest.mark.parametrize("K", [128, 64, 32])
+def test_conv_fwd_dropout(env, cuda, dtype, K):
+    ops, call, lib, ptr, stream = env
+    N, H, W, C, R = 2, 12, 40, 64, 3
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randn((N, H, W, C), generator=g).to(dtype).to(cuda)
+    w = (torch.randn((K, R, R, C), generator=g) * 0.05).to(cuda)
+    b = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    dt = 1 if dtype == torch.bfloat16 else 0
+    wp = ops.pack_weights(w, dtype, False)
+    rows = lib.acfe_conv2d_stats_rows(N * H * W, K)
+    y0 = torch.empty((N, H, W, K), dtype=dtype, device=cuda)
+    y1 = torch.empty_like(y0)
+    st = torch.zeros((rows, 2, wp.shape[0]), dtype=torch.float64, device=cuda)
+    call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, R, 1, 1, 1, H, W, ptr(b), ptr(y0), dt, None, stream())
+    call("acfe_conv2d_fwd_dropout", ptr(x), N, H, W, C, ptr(wp), K, R, R, 1, 1, 1, H, W, ptr(b), ptr(y1), dt,
+         ptr(st), 0.1, 12345, stream())
+    ref = _dropout(env, y0, 0.1, 12345)
+    assert torch.equal(y1, ref)
+    assert (ref == 0).float().mean().item() == pytest.approx(0.1, abs=0.02)
+    s_ref = _stats_of(env, ref)
+    # the epilogue sums each wave's 16-row fragment in fp32 before the double atomics
+    torch.testing.assert_close(st.sum(0)[:, :K], s_ref, rtol=1e-6, atol=1e-4)
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_bn_bwd_apply_dropout(env, cuda, relu):
+    ops, call, lib, ptr, stream = env
+    rows, C = 3000, 64
+    g = torch.Generator(device="cpu").manual_seed(2)
+    dy = torch.randn((rows, C), generator=g).to(torch.bfloat16).to(cuda)
+    x = torch.randn((rows, C), generator=g).to(torch.bfloat16).to(cuda)
+    scale, shift, coef = (torch.randn((n,), generator=g).to(cuda) for n in (C, C, 3 * C))
+    d0 = torch.empty_like(x)
+    d1 = torch.empty_like(x)
+    call("acfe_bn_bwd_apply", ptr(dy), 1, ptr(x), 1, rows, C, ptr(scale), ptr(shift), int(relu), ptr(coef), None,
+         ptr(d0), 1, stream())
+    call("acfe_bn_bwd_apply_dropout", ptr(dy), 1, ptr(x), 1, rows, C, ptr(scale), ptr(shift), int(relu), ptr(coef),
+         0.1, 777, ptr(d1), 1, stream())
+    assert torch.equal(d1, _dropout(env, d0, 0.1, 777))
+
+
+@pytest.mark.parametrize("k", [(1, 2), (2, 2), (3, 3)])
+@pytest.mark.parametrize("C", [16, 64, 128])
+def test_maxpool_fused(env, cuda, k, C):
+    ops, call, lib, ptr, stream = env
+    kh, kw = k
+    N, H, W = 2, 13, 35
+    P, Q = H // kh, W // kw
+    g = torch.Generator(device="cpu").manual_seed(3)
+    # coarse values so ties occur (first maximum must win in both paths)
+    x = (torch.randint(-4, 5, (N, H, W, C), generator=g).float() * 0.5).to(torch.bfloat16).to(cuda)
+    y0 = torch.empty((N, P, Q, C), dtype=torch.bfloat16, device=cuda)
+    call("acfe_maxpool2d", ptr(x), N, H, W, C, kh, kw, ptr(y0), 1, stream())
+    ref = _dropout(env, y0, 0.1, 99)
+    y1 = torch.empty_like(y0)
+    am = torch.empty((N, P, Q, C), dtype=torch.uint8, device=cuda)
+    st = torch.empty((lib.acfe_reduce_blocks(N * P * Q), 2, C), dtype=torch.float64, device=cuda)
+    call("acfe_maxpool2d_fused", ptr(x), N, H, W, C, kh, kw, ptr(y1), ptr(am), 0.1, 99, ptr(st), 1, stream())
+    assert torch.equal(y1, ref)
+    torch.testing.assert_close(st.sum(0), _stats_of(env, ref), rtol=1e-6, atol=1e-6)
+    # backward from the argmax bytes == dropout backward then maxpool backward from x
+    gy = torch.randn((N, P, Q, C), generator=g).to(torch.bfloat16).to(cuda)
+    dx0 = torch.empty_like(x)
+    call("acfe_maxpool2d_bwd", ptr(x), ptr(_dropout(env, gy, 0.1, 99)), N, H, W, C, kh, kw, ptr(dx0), 1, stream())
+    dx1 = torch.full_like(x, 7.0)  # leftover rows/cols must be overwritten with zeros
+    call("acfe_maxpool2d_bwd_argmax", ptr(am), ptr(gy), N, H, W, C, kh, kw, 0.1, 99, ptr(dx1), 1, stream())
+    assert torch.equal(dx1, dx0)
+
+
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("C", [16, 64, 256])
+def test_add_stats(env, cuda, relu, C):
+    ops, call, lib, ptr, stream = env
+    rows = 5000
+    g = torch.Generator(device="cpu").manual_seed(4)
+    a = torch.randn((rows, C), generator=g).to(torch.bfloat16).to(cuda)
+    b = torch.randn((rows, C), generator=g).to(torch.bfloat16).to(cuda)
+    z0, z1 = torch.empty_like(a), torch.empty_like(a)
+    call("acfe_add", ptr(a), ptr(b), a.numel(), int(relu), ptr(z0), 1, stream())
+    st = torch.empty((lib.acfe_reduce_blocks(rows), 2, C), dtype=torch.float64, device=cuda)
+    call("acfe_add_stats", ptr(a), ptr(b), rows, C, int(relu), ptr(z1), 1, ptr(st), stream())
+    assert torch.equal(z1, z0)
+    torch.testing.assert_close(st.sum(0), _stats_of(env, z0), rtol=1e-6, atol=1e-6)
+
+
+def _bn_params(C, cuda, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    gamma = (1 + 0.2 * torch.randn((C,), generator=g)).to(cuda).requires_grad_(True)
+    beta = (0.1 * torch.randn((C,), generator=g)).to(cuda).requires_grad_(True)
+    return gamma, beta, torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv_dropout_bn_node(env, cuda, stride):
+    ops = env[0]
+    N, H, W, C, K = 4, 16, 24, 32, 64
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((K, 3, 3, C), generator=g) * 0.1).to(cuda)
+    b0 = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    gy = torch.randn((N, -(-H // stride), -(-W // stride), K), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    for fused in (False, True):
+        x = x0.clone().requires_grad_(True)
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        gamma, beta, mm, mv = _bn_params(K, cuda, 6)
+        if fused:
+            y = ops.conv_dropout_bn(x, w, b, gamma, beta, mm, mv, True, 0.1, seed=4242, relu=True, stride=stride)
+        else:
+            u, _ = ops.conv2d(x, w, b, stride)
+            u = ops.dropout(u, 0.1, True, seed=4242)
+            y = ops.batch_norm(u, gamma, beta, mm, mv, True, relu=True)
+        y.backward(gy)
+        outs.append([y, x.grad, w.grad, b.grad, gamma.grad, beta.grad, mm, mv])
+    for a, b in zip(*outs):
+        assert rel(a, b) < 2e-3, rel(a, b)
+
+
+def test_maxpool_dropout_bn_node(env, cuda):
+    ops = env[0]
+    N, H, W, C = 4, 16, 24, 64
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    gy = torch.randn((N, H // 2, W // 2, C), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    for fused in (False, True):
+        x = x0.clone().requires_grad_(True)
+        gamma, beta, mm, mv = _bn_params(C, cuda, 8)
+        if fused:
+            y = ops.maxpool_dropout_bn(x, 2, 2, gamma, beta, mm, mv, True, 0.1, seed=55)
+        else:
+            u = ops.max_pool(x, 2, 2)
+            u = ops.dropout(u, 0.1, True, seed=55)
+            y = ops.batch_norm(u, gamma, beta, mm, mv, True, relu=True)
+        y.backward(gy)
+        outs.append([y, x.grad, gamma.grad, beta.grad, mm, mv])
+    for a, b in zip(*outs):
+        assert rel(a, b) < 2e-3, rel(a, b)
+
+
+def test_residual_link(env, cuda):
+    """BN(x) ... + x with a ResidualLink == plain autograd accumulation."""
+    ops = env[0]
+    N, H, W, C = 4, 8, 16, 64
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((C, 3, 3, C), generator=g) * 0.05).to(cuda)
+    gz = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    for linked in (False, True):
+        x = x0.clone().requires_grad_(True)
+        gamma, beta, mm, mv = _bn_params(C, cuda, 10)
+        link = ops.ResidualLink() if linked else None
+        y = ops.batch_norm(x, gamma, beta, mm, mv, True, relu=True, link=link)
+        y, _ = ops.conv2d(y, w0, None)
+        z, st = ops.add(y, x, relu=True, want_stats=True, link=link)
+        z.backward(gz)
+        outs.append([z, x.grad, gamma.grad, beta.grad, st.sum(0)])
+    # x.grad: the linked path rounds (bn_dx + residual) once to bf16, autograd
+    # rounds bn_dx first and the sum again -> one-ulp flips on many elements
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert rel(a, b) < (5e-3 if i == 1 else 2e-3), (i, rel(a, b))

@@ -3,12 +3,17 @@ graphs of oracle/models.py (torch-CPU restatement of the Keras models).
 
 Dropout is disabled (rate 0) so both sides are deterministic.
 
-fp32 compute, training-mode BN (the tight check):
-  rel-L2(logits) <= 1e-4 vs the float64 oracle; every parameter gradient within
-  max(4 x e32, 2e-4), where e32 is the error of the SAME oracle run in
-  torch-CPU float32 (tiny-batch BatchNorm makes some gradients ill-conditioned:
-  e32 reaches ~1e-2); gradients that are zero in exact arithmetic (biases of
-  convs feeding a training-mode BN) must be ~0 absolutely.
+fp32 compute, eval-mode BN (the tight check, well conditioned: e32 ~1e-6 for
+  the bird model): rel-L2(logits) <= 1e-4 and every parameter gradient within
+  max(4 x e32, 1e-4), where e32 is the error of the SAME oracle run in
+  torch-CPU float32.
+fp32 compute, training-mode BN: rel-L2(logits) <= 1e-4; every parameter
+  gradient within max(8 x e32, 2e-4) -- tiny-batch training BatchNorm makes
+  gradients ill-conditioned (e32 median 5e-3, max 1e-2 at this size), so any
+  change of summation order (e.g. BN statistics taken in the conv epilogue
+  instead of a separate pass) moves them by a few e32; gradients that are zero
+  in exact arithmetic (biases of convs feeding a training-mode BN) must be ~0
+  absolutely.
 bf16 compute, vs the oracle with the same bf16 storage points (storage="bf16"):
   eval-mode BN: rel-L2(logits) <= 1e-2, rel-L2(gradient arena) <= 5e-2
     (floor measured between fp32- and fp64-accumulating bf16 oracles:
@@ -60,11 +65,11 @@ def _input(n, h, w, seed=1):
     return torch.rand((n, h, w), generator=g, dtype=torch.float64) * 2 - 1
 
 
-CASES = [("f32", True), ("bf16", False), ("bf16", True)]
+CASES = [("f32", True), ("f32", False), ("bf16", False), ("bf16", True)]
 
 
 @pytest.mark.parametrize("kind", ["bird", "wrn"])
-@pytest.mark.parametrize("prec,training", CASES, ids=["f32-train", "bf16-eval", "bf16-train"])
+@pytest.mark.parametrize("prec,training", CASES, ids=["f32-train", "f32-eval", "bf16-eval", "bf16-train"])
 def test_model_step_parity(cuda, kind, prec, training):
     dtype = torch.float32 if prec == "f32" else torch.bfloat16
     H, W, classes, N = 128, 64, 10, 2
@@ -113,7 +118,8 @@ def test_model_step_parity(cuda, kind, prec, training):
                 assert q.grad.double().norm().item() < 1e-5 * gnorm, n
                 continue
             e32 = rel(params32[n].grad, ref)
-            assert rel(q.grad, ref) < max(4 * e32, 2e-4), (n, rel(q.grad, ref), e32)
+            bound = max(8 * e32, 2e-4) if training else max(4 * e32, 1e-4)
+            assert rel(q.grad, ref) < bound, (n, rel(q.grad, ref), e32)
     elif not training:
         assert rel(g_dev, g_ref) < 5e-2, rel(g_dev, g_ref)
     else:

@@ -41,12 +41,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--layers", default="", help="comma-separated layer indices (default all)")
     a = ap.parse_args()
+    sel = {int(i) for i in a.layers.split(",") if i} or set(range(len(LAYERS)))
     from acfe._lib import call, lib
     from acfe._torch import ptr, stream
 
     dev = torch.device("cuda", 0)
-    for name, H, W, C, K, R, S in LAYERS:
+    for li, (name, H, W, C, K, R, S) in enumerate(LAYERS):
+        if li not in sel:
+            continue
         N = a.batch
         x = (torch.randn((N, H, W, C), device=dev) * 0.5).to(torch.bfloat16)
         w = torch.randn((K, R, S, C), device=dev) / (R * S * C) ** 0.5

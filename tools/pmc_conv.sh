@@ -1,0 +1,17 @@
+#!/bin/bash
+# PMC passes over the T1 conv microbench (one counter group per rocprofv3 run,
+# --pmc never combined with trace domains).  Output: gpurun_out/pmc_conv/<pass>/
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+L=${1:-0}
+i=0
+for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+           "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM" \
+           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_conv/p$i -o pmc -- \
+      python tools/conv_bench.py --layers "$L" --iters 2 > gpurun_out/pmc_conv/p$i.log 2>&1 || \
+      { echo "pass $i ($grp) failed"; tail -5 gpurun_out/pmc_conv/p$i.log; }
+  i=$((i+1))
+done
