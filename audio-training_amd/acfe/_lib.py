@@ -57,9 +57,12 @@ SIGNATURES: dict[str, list] = {
     "acfe_bn_bwd_finalize": [P, I32, I32, F64, P, P, P, P, P, P, P],
     "acfe_bn_bwd_apply": [P, I32, P, I32, I64, I32, P, P, I32, P, P, P, I32, P],
     "acfe_bn_bwd_apply_dropout": [P, I32, P, I32, I64, I32, P, P, I32, P, F32, C.c_uint64, P, I32, P],
+    "acfe_bn_bwd_apply_ex": [P, I32, P, I32, I64, I32, P, P, I32, P, P, F32, C.c_uint64, P, I32, P, P],
     "acfe_channel_sum": [P, I64, I32, I32, P, P, F32, P],
     "acfe_add": [P, P, I64, I32, P, I32, P],
     "acfe_add_stats": [P, P, I64, I32, I32, P, I32, P, P],
+    "acfe_relu_bwd_sum": [P, P, I64, I32, P, I32, P, P],
+    "acfe_channel_sum_finalize": [P, I32, I32, F32, P, P],
     "acfe_relu_bwd": [P, P, I64, P, I32, P],
     "acfe_dropout": [P, I64, F32, C.c_uint64, P, I32, P],
     "acfe_cast": [P, I32, I64, P, I32, P],

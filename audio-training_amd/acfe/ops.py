@@ -158,7 +158,26 @@ class _Conv2dFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None, None
 
 
+def _sums_ok(t: torch.Tensor) -> bool:
+    """Fused per-channel sums need C % 8 == 0, 256 % (C/8) == 0 and 16-B alignment."""
+    C = t.shape[-1]
+    return C % 8 == 0 and C <= 2048 and 256 % (C // 8) == 0 and t.data_ptr() % 16 == 0 and t.is_contiguous()
+
+
+def _attach_sum(t: torch.Tensor, part: torch.Tensor, rows: int):
+    """Finalize a fused channel-sum slab and cache it on the gradient tensor it
+    sums, so the convolution receiving `t` as its output gradient takes its
+    bias gradient from there instead of re-reading `t` (channel_sum)."""
+    C = t.shape[-1]
+    db = _empty((C,), F32, t.device)
+    call("acfe_channel_sum_finalize", ptr(part), lib.acfe_reduce_blocks(rows), C, 0.0, ptr(db), stream())
+    t._acfe_chsum = db
+
+
 def channel_sum(x: torch.Tensor, C: int) -> torch.Tensor:
+    cached = getattr(x, "_acfe_chsum", None)
+    if cached is not None and cached.numel() == C:
+        return cached
     rows = x.numel() // C
     out = _empty((C,), F32, x.device)
     part = _empty((lib.acfe_reduce_blocks(rows) * 2 * C,), F64, x.device)
@@ -299,17 +318,19 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None):
     call("acfe_bn_bwd_finalize", ptr(part), nrows, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
          ptr(dbeta), ptr(coef), s)
     dx = _empty(x.shape, x.dtype, dev)
-    if drop is not None and drop[0] > 0.0:
-        assert add is None
-        call("acfe_bn_bwd_apply_dropout", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C,
-             ptr(scale), ptr(shift), int(relu), ptr(coef), float(drop[0]), int(drop[1]), ptr(dx),
-             dtype_code(x.dtype), s)
-    else:
-        if add is not None:
-            add = add.contiguous()
-            assert add.dtype == x.dtype and add.shape == x.shape
-        call("acfe_bn_bwd_apply", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
-             ptr(shift), int(relu), ptr(coef), ptr(add), ptr(dx), dtype_code(x.dtype), s)
+    rate, seed = drop if drop is not None and drop[0] > 0.0 else (0.0, 0)
+    if add is not None:
+        assert rate == 0.0
+        add = add.contiguous()
+        assert add.dtype == x.dtype and add.shape == x.shape
+    # per-channel sums of dx ride along (bias gradient of the conv producing x)
+    want_sum = FUSE and _sums_ok(dx) and _sums_ok(dy) and _sums_ok(x) and (add is None or _sums_ok(add))
+    sums = _empty((nrows, 2, C), F64, dev) if want_sum else None
+    call("acfe_bn_bwd_apply_ex", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+         ptr(shift), int(relu), ptr(coef), ptr(add), float(rate), int(seed), ptr(dx), dtype_code(x.dtype), ptr(sums),
+         s)
+    if want_sum:
+        _attach_sum(dx, sums, rows)
     return dx, dgamma, dbeta
 
 
@@ -410,7 +431,14 @@ class _AddFn(torch.autograd.Function):
         if ctx.relu:
             (z,) = ctx.saved_tensors
             d = torch.empty_like(g)
-            call("acfe_relu_bwd", ptr(g), ptr(z), g.numel(), ptr(d), dtype_code(g.dtype), stream())
+            C = g.shape[-1]
+            if FUSE and g.dim() > 1 and _sums_ok(g) and _sums_ok(z) and _sums_ok(d):
+                rows = g.numel() // C
+                part = _empty((lib.acfe_reduce_blocks(rows), 2, C), F64, g.device)
+                call("acfe_relu_bwd_sum", ptr(g), ptr(z), rows, C, ptr(d), dtype_code(g.dtype), ptr(part), stream())
+                _attach_sum(d, part, rows)
+            else:
+                call("acfe_relu_bwd", ptr(g), ptr(z), g.numel(), ptr(d), dtype_code(g.dtype), stream())
             g = d
         if ctx.link is not None:  # the shortcut input's gradient is added by the linked BN backward
             ctx.link.grad = g

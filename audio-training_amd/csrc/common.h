@@ -58,11 +58,16 @@ __device__ __forceinline__ double wave_sumd(double v) {
 // Counter-based RNG (splitmix-style hash) for dropout masks: deterministic in
 // (seed, index), so the backward regenerates the forward's mask.
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+  // counter-based 32-bit hash (murmur3 finalizer of a Weyl step): three 32-bit
+  // multiplies, cheap enough for the conv epilogue's fused dropout
+  uint32_t h = (uint32_t)idx * 0x9E3779B1u + (uint32_t)seed;
+  h ^= (uint32_t)(idx >> 32) * 0x85EBCA77u ^ (uint32_t)(seed >> 32);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
 
 // Rounding to the storage type (the value a separate kernel would have stored).

