@@ -59,9 +59,11 @@ class FrontEnd(nn.Module):
         view = rec[first * hop:]
         st = fe.normalize_stats(view, n=n, clip_stride=hop, batch=count)
         if self.pcen is not None:
-            mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="btm", n=n, clip_stride=hop, batch=count)
+            mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="btm", n=n, clip_stride=hop, batch=count,
+                                timer=self.timer)
             return self.pcen(mel, scope_minmax)
-        mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="bmt", n=n, clip_stride=hop, batch=count)
+        mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="bmt", n=n, clip_stride=hop, batch=count,
+                            timer=self.timer)
         return ops.cast(mel, self.dtype)
 
 

@@ -151,8 +151,13 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--workload", choices=["train", "infer", "stream"], default="train",
+                    help="train = T1/T8 (the driver's line); infer = config I (B=256 fp32 wr_resnet fwd); "
+                         "stream = config S (60-min recording, 3 s / 1.5 s windows, batch 1024)")
     a = ap.parse_args()
+    if a.workload != "train":
+        return run_inference(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -282,6 +287,103 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_inference(a):
+    """Configs I and S of BASELINE.json (one GPU; shards over ranks with no
+    collective, so only the single-GPU replica is measured here).
+
+    I: fused normalize/STFT/mel/PCEN + wr_resnet forward, batch 256, fp32.
+    S: one 60-min 48 kHz recording resident in HBM, 3 s windows every 1.5 s
+       read in place by the front-end kernel (centred STFT, constant padding as
+       predict_utils.get_spect), PCEN per window batch, model forward, sigmoid;
+       batch 1024 windows.  A step = the whole recording."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from acfe import ops
+    from acfe.train import FrontEnd
+
+    stream = a.workload == "stream"
+    model_name = a.model if (stream or "--model" in sys.argv) else "wrn"
+    dtype = torch.float32 if (a.dtype == "fp32" or ("--dtype" not in sys.argv and not stream)) else torch.bfloat16
+    classes = a.classes if "--classes" in sys.argv else (2 if model_name == "wrn" else 50)
+    if model_name == "bird":
+        from resnet.wr_resnet_bird import WRResNet
+    else:
+        from resnet.wr_resnet import WRResNet
+    torch.manual_seed(1234)
+    model = WRResNet(input_shape=(128, 513, 3), classes=classes, dtype=dtype).to(dev).eval()
+    frontend = FrontEnd(n_mels=128, dtype=dtype, device=dev).to(dev).eval()
+    target = model.blocks[0].conv21 if model_name == "bird" else model.blocks[1].conv2a
+    K, R, S, C = target.weight.shape
+    events, mel_events = [], []
+    if stream:
+        sr, n, hop = 48000, 144000, 72000
+        rec = torch.from_numpy(np.tile(synth_bank(8, seed=4242).reshape(-1), 1500)[: 60 * 60 * sr].copy()).to(dev)
+        n_win = 1 + (rec.numel() - n) // hop
+        bs = 1024 if "--batch" not in sys.argv else a.batch
+
+        @torch.no_grad()
+        def step(i):
+            outs = []
+            for first in range(0, n_win, bs):
+                cnt = min(bs, n_win - first)
+                outs.append(ops.sigmoid(model(frontend.forward_windows(rec, first, cnt, n=n, hop=hop))))
+            return outs
+        units = n_win
+    else:
+        bs = 256 if "--batch" not in sys.argv else a.batch
+        x = make_batches(bs, classes, dev, n_sets=1)[0][0]
+
+        @torch.no_grad()
+        def step(i):
+            return ops.sigmoid(model(frontend(x)))
+        units = bs
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ops.watch_conv(target.weight, events)
+    frontend.timer = mel_events
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ops.watch_conv(target.weight, None)
+    frontend.timer = None
+    d = [e0.elapsed_time(e1) for k, e0, e1 in events if k == "fwd"]
+    fwd_ms = float(np.mean(d)) if d else float("nan")
+    dm = [e0.elapsed_time(e1) for k, e0, e1 in mel_events]
+    mel_ms = float(np.mean(dm)) if dm else float("nan")
+    H_t = 128
+    W_t = 256 if model_name == "bird" else 513
+    # one launch of the target conv covers at most bs clips
+    n_launch = -(-units // bs)
+    avg_clips = units / n_launch
+    flops_launch = 2.0 * avg_clips * H_t * W_t * K * R * S * C
+    peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
+    ach = flops_launch / (fwd_ms * 1e-3) / 1e12
+    value = units * a.steps / elapsed
+    out = {
+        "metric": ("windows/sec streaming inference (60-min 48 kHz recording, 3 s / 1.5 s windows)" if stream
+                   else "clips/sec inference (3s@48kHz, front end + PCEN + wr_resnet fwd)"),
+        "value": round(value, 2), "unit": "windows/s" if stream else "clips/s", "n_gpus": 1,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+        "data": "synthetic (SURVEY 8d chirps+noise, resident in HBM; random-init weights)",
+        "config": {"workload": ("S: streaming predict, 2399 windows/recording, batch %d" % bs) if stream
+                   else ("I: inference batch %d" % bs),
+                   "model": "wr_resnet_bird" if model_name == "bird" else "wr_resnet", "classes": classes,
+                   "units_per_step": units, "batch": bs},
+        "roofline": {"kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t}", "bound": "mfma",
+                     "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                     "traffic": None, "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch},
+        "mel_pipeline": {"avg_launch_ms": round(mel_ms, 4),
+                         "GBps": round(avg_clips * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2)},
+    }
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

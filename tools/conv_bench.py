@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--layers", default="", help="comma-separated layer indices (default all)")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad", help="subset of fwd,dgrad,wgrad")
     a = ap.parse_args()
     sel = {int(i) for i in a.layers.split(",") if i} or set(range(len(LAYERS)))
     from acfe._lib import call, lib
@@ -67,11 +68,13 @@ def main():
         wsz = lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, P, Q)
         ws = torch.empty((wsz,), dtype=torch.float32, device=dev)
         flops = 2.0 * N * H * W * K * R * S * C
-        t_f = timeit(lambda: call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, 1, pt, pl, P, Q, ptr(b),
+        nan = float("nan")
+        run = set(a.passes.split(","))
+        t_f = nan if "fwd" not in run else timeit(lambda: call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, 1, pt, pl, P, Q, ptr(b),
                                   ptr(y), 1, ptr(st), stream()), a.iters)
-        t_d = timeit(lambda: call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, 1, pt, pl, H, W,
+        t_d = nan if "dgrad" not in run else timeit(lambda: call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, 1, pt, pl, H, W,
                                   ptr(dx), 1, None, stream()), a.iters)
-        t_w = timeit(lambda: call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, 1, pt, pl, P, Q,
+        t_w = nan if "wgrad" not in run else timeit(lambda: call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, 1, pt, pl, P, Q,
                                   ptr(dw), 0.0, 1, ptr(ws), stream()), a.iters)
         print(f"{name:28s} fwd {t_f:7.3f} ms {flops / t_f / 1e9:7.1f} TF | dgrad {t_d:7.3f} ms "
               f"{flops / t_d / 1e9:7.1f} TF | wgrad {t_w:7.3f} ms {flops / t_w / 1e9:7.1f} TF", flush=True)
