@@ -18,4 +18,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "GRBM
   fi
   i=$((i+1))
 done
-python tools/pmc_traffic.py $O $TAG
+python tools/pmc_traffic.py $O $TAG   # writes profiles/ on the box: rerun locally on the merged gpurun_out/
