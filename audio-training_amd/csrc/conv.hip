@@ -511,6 +511,284 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
   }
 }
 
+// ------------------------------------------------------------------ forward, 3-stage LDS-DMA pipeline
+// bf16, C % 64 == 0, K % BN == 0 (every 3x3 / 1x1 / (4,10) layer of both
+// networks with >= 64 input channels, and their stride-1 dgrads).
+//  * 512 threads = 8 waves as 4 (M) x 2 (N), each 64 pixels x BN/2 channels on
+//    v_mfma_f32_16x16x32_bf16; tile 256 pixel rows x BN channels, BK = 64.
+//  * Because C % 64 == 0 a K-tile never straddles a filter tap: the tap (r, s)
+//    and channel base are wave-uniform scalars, and each lane keeps one bit per
+//    filter row / column saying whether its pixel's tap is inside the image, so
+//    the im2col address of an LDS-DMA piece is one 64-bit add and one select.
+//  * Three LDS stages, one raw barrier per K-tile, two K-tiles in flight across
+//    it (counted vmcnt); the stream of K-tiles runs on across M tiles, so the
+//    next tile's first two K-tiles are in flight while this tile's epilogue runs.
+//  * The MFMA operands are swapped (weights x pixels) so each lane ends with 4
+//    consecutive channels of a pixel: the epilogue stores 8-byte rows straight
+//    from registers (no LDS staging) and reduces the BatchNormalization sums
+//    with a butterfly (reduce-scatter over 16 lanes, 30 shuffles) before one
+//    LDS double atomic per value.  Out-of-range pixel rows store to a sink so
+//    every wave always issues the same number of stores (vmcnt bookkeeping).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 16-B LDS-DMA with a wave-uniform LDS byte address already in an SGPR.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16_m0(const void* src, unsigned m0v) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0v)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// 16-B buffer_load ... lds: LDS byte address (wave-uniform) in M0, descriptor
+// in SGPRs, per-lane voffset; an out-of-range voffset lands zeros in LDS.
+typedef int i4 __attribute__((ext_vector_type(4)));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void bldsx4(unsigned voff, i4 desc, unsigned m0v) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(desc),
+               "s"(m0v)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ uint2 g_store_sink[64];  // never read: target of masked-off epilogue stores
+
+// One step of a 16-lane butterfly reduce-scatter: lanes whose `BIT` is set keep
+// the upper half of v[0..CNT), the others the lower half, each adding the
+// partner's copy of the half it keeps (partner = DPP pattern CTRL).
+template <int CNT, int BIT, int CTRL, int NV>
+__device__ __forceinline__ void butterfly_step(float (&v)[NV], int lane) {
+  const bool up = (lane & BIT) != 0;
+#pragma unroll
+  for (int k = 0; k < CNT / 2; ++k) {
+    const float send = up ? v[k] : v[k + CNT / 2];
+    const float keep = up ? v[k + CNT / 2] : v[k];
+    const float got = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), CTRL, 0xF, 0xF, false));
+    v[k] = keep + got;
+  }
+}  // never read: target of masked-off epilogue stores
+
+template <int BN>
+__global__ void __launch_bounds__(512, 1)
+k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+             const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_m,
+             int srows) {
+  using T = uint16_t;
+  constexpr int BM = 256, BK = 64, NST = 3;
+  constexpr int AJ = BM / 64, BJ = BN / 64;  // 8-row LDS-DMA pieces per wave per stage
+  constexpr int LPS = AJ + BJ;               // vmcnt entries of one stage, per wave
+  constexpr int TWM = 64, TWN = BN / 2, FM = TWM / 16, FN = TWN / 16, KF = 32;
+  constexpr int NSTORE = FM * FN;            // epilogue stores per lane per tile
+  constexpr int NV = 8 * FN;                 // BN-statistics values per lane (2 x FN x 4)
+  constexpr int STG = (BM + BN) * 128;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NST * STG + 2 * BN * 8];
+  double* sstat = reinterpret_cast<double*>(smem + NST * STG);  // [2][BN]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lrow = lane >> 3, gsw = (lane & 7) ^ (lrow & 7);
+  const int n0 = blockIdx.y * BN;
+  const int nkt = g.Kdp / BK;
+  const int PQ = g.P * g.Q, M = (int)g.M;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
+  for (int i = tid; i < 2 * BN; i += 512) sstat[i] = 0.0;
+  // bias of this lane's output channels, read before any LDS-DMA is in flight
+  float bv[FN][4];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      bv[fn][jj] = bias ? bias[n0 + wn * TWN + fn * 16 + (lane >> 4) * 4 + jj] : 0.f;
+  // ---- issue side: runs up to two K-tiles ahead of the compute, across M tiles.
+  // A and B pieces are buffer_load ... lds with a wave-uniform descriptor whose
+  // base carries the tap / channel offset of the K-tile (SALU only) and a
+  // per-row voffset fixed for the tile; an invalid tap selects an
+  // out-of-range voffset, which the hardware loads as zeros.
+  const TileWalk walk(tiles_m);
+  int itm = walk.tm, ikt = 0, ir = 0, is = 0, ic = 0, ibuf = 0, issued = 0;
+  const long long padshift = ((long long)g.pt * g.W + g.pl) * g.C * 2;
+  long long abase = 0;  // byte address of the tile's first image, shifted back by the padding
+  unsigned voffA[AJ], tmlo[AJ], tmhi[AJ];
+  unsigned voffB[BJ];
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) voffB[j] = ((unsigned)(n0 + (wid * BJ + j) * 8 + lrow) * g.Kdp + gsw * 8) * 2u;
+  const long long bbase = (long long)(uintptr_t)Wp;
+  auto setup = [&](int tm) __attribute__((always_inline)) {
+    const int nfirst = (tm * BM) / PQ;
+    abase = (long long)(uintptr_t)X + (long long)nfirst * g.H * g.W * g.C * 2 - padshift;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int m = tm * BM + (wid * AJ + j) * 8 + lrow;
+      const bool valid = m < M;
+      const int mm = valid ? m : 0;
+      const int n = mm / PQ, rem = mm - n * PQ;
+      const int p = rem / g.Q, q = rem - p * g.Q;
+      const int h0 = p * g.st - g.pt, w0 = q * g.st - g.pl;
+      voffA[j] = (unsigned)(((((n - nfirst) * g.H + h0 + g.pt) * g.W + w0 + g.pl) * g.C + gsw * 8) * 2);
+      // filter rows / columns whose tap lies inside the image
+      const int rlo = h0 < 0 ? -h0 : 0, rhi = g.H - h0 < g.R ? g.H - h0 : g.R;
+      const int slo = w0 < 0 ? -w0 : 0, shi = g.W - w0 < g.S ? g.W - w0 : g.S;
+      const unsigned hm = (valid && rhi > rlo) ? (((1u << rhi) - 1u) & ~((1u << rlo) - 1u)) : 0u;
+      const unsigned long long wmk = shi > slo ? (((1ull << shi) - 1ull) & ~((1ull << slo) - 1ull)) : 0ull;
+      unsigned long long t = 0;
+      for (int r = 0; r < g.R; ++r)
+        if ((hm >> r) & 1u) t |= wmk << (r * g.S);
+      tmlo[j] = (unsigned)t;
+      tmhi[j] = (unsigned)(t >> 32);
+    }
+  };
+  auto issue = [&]() __attribute__((always_inline)) {
+    const unsigned base = lds0 + ibuf * STG + wid * (AJ * 1024);
+    const int tap = ir * g.S + is;
+    const long long a = abase + ((long long)(ir * g.W + is) * g.C + ic) * 2;
+    const i4 da = {(int)(unsigned)a, (int)(unsigned)(a >> 32), (int)0x80000000u, 0x00020000};
+    const bool lo = tap < 32;
+    const unsigned tw = lo ? tap : tap - 32;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const unsigned mk = lo ? tmlo[j] : tmhi[j];
+      const unsigned vo = ((mk >> tw) & 1u) ? voffA[j] : 0x80000000u;
+      bldsx4(vo, da, base + j * 1024);
+    }
+    const long long bb = bbase + (long long)ikt * BK * 2;
+    const i4 db = {(int)(unsigned)bb, (int)(unsigned)(bb >> 32), (int)0x80000000u, 0x00020000};
+    const unsigned bbase_l = lds0 + ibuf * STG + BM * 128 + wid * (BJ * 1024);
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) bldsx4(voffB[j], db, bbase_l + j * 1024);
+    ++issued;
+    ibuf = ibuf == NST - 1 ? 0 : ibuf + 1;
+    ic += BK;
+    if (ic == g.C) {
+      ic = 0;
+      if (++is == g.S) { is = 0; ++ir; }
+    }
+    if (++ikt == nkt) {
+      ikt = ir = is = ic = 0;
+      itm += walk.step;
+      if (itm < walk.end) setup(itm);
+    }
+  };
+
+  if (itm < walk.end) {
+    setup(itm);
+    issue();
+    if (itm < walk.end) issue();
+  }
+  int ctm = walk.tm, ckt = 0, cbuf = 0, done = 0;
+  bool pend = false;  // the previous iteration ended a tile: its stores are in the vmcnt queue
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  while (ctm < walk.end) {
+    // stage `done` landed: leave the younger stage (if issued) and stores in flight
+    const bool two = issued - done >= 2;
+    if (pend) {
+      if (two) wait_vmcnt<LPS + NSTORE>();
+      else wait_vmcnt<NSTORE>();
+    } else {
+      if (two) wait_vmcnt<LPS>();
+      else wait_vmcnt<0>();
+    }
+    lds_barrier();
+    pend = false;
+    if (itm < walk.end) issue();
+    {
+      const unsigned char* Ab = smem + cbuf * STG;
+      const unsigned char* Bb = Ab + BM * 128;
+#pragma unroll
+      for (int kk = 0; kk < BK / KF; ++kk) {
+        const int gi = kk * 4 + (lane >> 4);
+        uint4 af[FM], bfr[FN];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int row = wn * TWN + fn * 16 + (lane & 15);
+          bfr[fn] = *reinterpret_cast<const uint4*>(Bb + row * 128 + ((gi ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int row = wm * TWM + fm * 16 + (lane & 15);
+          af[fm] = *reinterpret_cast<const uint4*>(Ab + row * 128 + ((gi ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], bfr[fn], af[fm], T());
+      }
+    }
+    cbuf = cbuf == NST - 1 ? 0 : cbuf + 1;
+    ++done;
+    if (++ckt < nkt) continue;
+    // ---- epilogue of tile ctm (acc[fm][fn][jj] = channel (lane>>4)*4+jj of pixel lane&15)
+    ckt = 0;
+    float sv[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) sv[i] = 0.f;
+    const int pbase = ctm * BM + wm * TWM + (lane & 15);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int pix = pbase + fm * 16;
+      const bool inb = pix < M;
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
+        uint16_t h[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          h[jj] = f2bf(acc[fm][fn][jj] + bv[fn][jj]);
+          if (g.drop.on) h[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(h[jj])));
+          const float f = inb ? bf2f(h[jj]) : 0.f;
+          sv[fn * 4 + jj] += f;
+          sv[FN * 4 + fn * 4 + jj] += f * f;
+        }
+        uint2 v;
+        v.x = (unsigned)h[0] | ((unsigned)h[1] << 16);
+        v.y = (unsigned)h[2] | ((unsigned)h[3] << 16);
+        uint2* dst = inb ? reinterpret_cast<uint2*>(Y + (long long)pix * g.ldy + c) : &g_store_sink[lane];
+        *dst = v;
+        acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    pend = true;
+    if (stats) {
+      // butterfly reduce-scatter over the 16 lanes of equal lane>>4, partners
+      // by DPP (no LDS traffic): row_ror:8 pairs bit 3, row_half_mirror pairs
+      // bit 2 (keeping bit 3), quad_perm xor-2 / xor-1 pair bits 1 / 0
+      butterfly_step<NV, 8, 0x128>(sv, lane);
+      butterfly_step<NV / 2, 4, 0x141>(sv, lane);
+      butterfly_step<NV / 4, 2, 0x4E>(sv, lane);
+      butterfly_step<NV / 8, 1, 0xB1>(sv, lane);
+      const int l4 = lane & 15;
+      const int b0 = ((l4 >> 3) & 1) * (NV / 2) + ((l4 >> 2) & 1) * (NV / 4) + ((l4 >> 1) & 1) * (NV / 8) +
+                     (l4 & 1) * (NV / 16);
+#pragma unroll
+      for (int k = 0; k < NV / 16; ++k) {
+        const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
+        const int col = wn * TWN + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+        atomicAdd(&sstat[st * BN + col], (double)sv[k]);
+      }
+    }
+    ctm += walk.step;
+  }
+  wait_vmcnt<0>();
+  lds_barrier();
+  if (stats) {
+    for (int c = tid; c < BN; c += 512) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + n0 + c] = sstat[c];
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + n0 + c] = sstat[BN + c];
+    }
+    // the persistent grid is smaller than acfe_conv2d_stats_rows(): zero the rest
+    for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
+      for (int c = tid; c < 2 * BN; c += 512) stats[((long long)rr * 2 + (c / BN)) * g.Kp + n0 + (c % BN)] = 0.0;
+  }
+}
+
 // ------------------------------------------------------------------ weight packing
 // forward:  out[k][(r*S+s)*C + c] = w[k][r][s][c]      (KRSC, zero-padded to [Kp][Kdp])
 // flipped:  out[c][(r*S+s)*K + k] = w[k][R-1-r][S-1-s][c]   (dgrad operand)
@@ -870,6 +1148,13 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   return g;
 }
 
+// Debug / A-B switch read once per process (e.g. ACFE_CONV_NO_PIPE=1 selects the
+// 2-stage k_conv_fwd_g path instead of k_conv_fwd_p).
+static bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] && v[0] != '0';
+}
+
 static int pick_bn(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
 template <typename T, int BN, int WM, int WN>
@@ -877,6 +1162,24 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
                         double* stats, int grid_m, hipStream_t s) {
   const int tiles_m = (int)((g.M + 127) / 128);
   dim3 grid(grid_m, g.Kp / BN);
+  if constexpr (sizeof(T) == 2 && BN >= 64) {
+    static const bool no_pipe = getenv_flag("ACFE_CONV_NO_PIPE");
+    // k_conv_fwd_p preconditions: whole K-tiles per tap, whole N tiles, a
+    // 64-bit tap mask, 32-bit pixel index and < 2 GiB of input per M tile
+    const long long img = (long long)g.H * g.W * g.C * 2;
+    const long long span = ((256 + (long long)g.P * g.Q - 1) / ((long long)g.P * g.Q) + 1) * img;
+    if (g.C % 64 == 0 && g.K % BN == 0 && g.R * g.S <= 64 && g.R < 32 && g.M < (1ll << 31) &&
+        span < (1ll << 31) && !no_pipe) {
+      // persistent: one 512-thread workgroup per CU (256 CUs), a multiple of 8
+      const int ny = g.Kp / BN, tiles = (int)((g.M + 255) / 256);
+      int gp = 256 / ny;
+      if (gp > tiles) gp = tiles;
+      if (gp >= 64) gp &= ~7;
+      hipLaunchKernelGGL((k_conv_fwd_p<BN>), dim3(gp, ny), dim3(512), 0, s, g, (const uint16_t*)x,
+                         (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles, grid_m);
+      return launch_rc("acfe_conv2d_fwd");
+    }
+  }
   if (g.C % TT<T>::GR == 0)
     hipLaunchKernelGGL((k_conv_fwd_g<T, 128, BN, WM, WN>), grid, dim3(256), 0, s, g, (const T*)x,
                        (const T*)wp, bias, (T*)y, stats, tiles_m);

@@ -95,6 +95,44 @@ def test_conv_fwd_dgrad_wgrad(ops, cuda, case, dtype):
     assert rel(bd.grad, br.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
+# bf16 shapes large enough that the persistent 3-stage kernel (k_conv_fwd_p:
+# 256-row tiles, one workgroup per CU) walks several M tiles per workgroup,
+# with a ragged last tile, nkt = 1 / 2 / 9 / 18 K-tiles, and two N tiles.
+BIG_CASES = [
+    (2, 128, 512, 64, 64, 3, 3),
+    (1, 128, 515, 128, 128, 3, 3),
+    (2, 128, 300, 16, 128, 1, 1),
+    (1, 128, 600, 128, 64, 1, 1),
+    (1, 64, 520, 128, 256, 3, 3),
+]
+
+
+@pytest.mark.parametrize("case", BIG_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_conv_pipelined_multi_tile(ops, cuda, case):
+    N, H, W, C, K, R, S = case
+    x = rnd((N, H, W, C), 11).to(torch.bfloat16).double()
+    w = rnd((K, R, S, C), 12, 1.0 / math.sqrt(R * S * C))
+    wq = w.to(torch.bfloat16).double()
+    b = rnd((K,), 13, 0.1)
+    gy = rnd((N, H, W, K), 14).to(torch.bfloat16).double()
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    wr = wq.clone().requires_grad_(True)
+    yr = ref_conv(xr, wr, b, 1, "same")
+    (yr * gy.permute(0, 3, 1, 2)).sum().backward()
+    xd = x.to(torch.bfloat16).to(cuda).requires_grad_(True)
+    wd = w.float().to(cuda).requires_grad_(True)
+    yd, st = ops.conv2d(xd, wd, b.float().to(cuda), 1, "same", want_stats=True)
+    yd.backward(gy.to(torch.bfloat16).to(cuda))
+    assert rel(yd.float(), yr.permute(0, 2, 3, 1)) < 6e-3
+    assert rel(xd.grad.float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    assert rel(wd.grad, wr.grad) < 1e-2
+    # BN partial statistics of the rounded outputs (every stats row written)
+    yf = yd.detach().float().cpu().double()
+    s = st.cpu().sum(0)
+    np.testing.assert_allclose(s[0, :K].numpy(), yf.sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(s[1, :K].numpy(), (yf ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
+
+
 def test_conv_fused_bn_stats(ops, cuda):
     x = rnd((2, 10, 12, 64), 5).to(torch.bfloat16)
     w = rnd((64, 3, 3, 64), 6, 1 / 24)

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--layers", default="", help="comma-separated layer indices (default all)")
+    ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--no-bias", action="store_true")
     ap.add_argument("--passes", default="fwd,dgrad,wgrad", help="subset of fwd,dgrad,wgrad")
     a = ap.parse_args()
     sel = {int(i) for i in a.layers.split(",") if i} or set(range(len(LAYERS)))
@@ -70,8 +72,8 @@ def main():
         flops = 2.0 * N * H * W * K * R * S * C
         nan = float("nan")
         run = set(a.passes.split(","))
-        t_f = nan if "fwd" not in run else timeit(lambda: call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, 1, pt, pl, P, Q, ptr(b),
-                                  ptr(y), 1, ptr(st), stream()), a.iters)
+        t_f = nan if "fwd" not in run else timeit(lambda: call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, R, S, 1, pt, pl, P, Q, None if a.no_bias else ptr(b),
+                                  ptr(y), 1, None if a.no_stats else ptr(st), stream()), a.iters)
         t_d = nan if "dgrad" not in run else timeit(lambda: call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, 1, pt, pl, H, W,
                                   ptr(dx), 1, None, stream()), a.iters)
         t_w = nan if "wgrad" not in run else timeit(lambda: call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, 1, pt, pl, P, Q,

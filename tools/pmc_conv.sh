@@ -11,9 +11,9 @@ for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
            "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM" \
            "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
-           "FETCH_SIZE" "WRITE_SIZE"; do
+           "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_conv/p$i -o pmc -- \
-      python tools/conv_bench.py --layers "$L" --iters 2 > gpurun_out/pmc_conv/p$i.log 2>&1
+      python tools/conv_bench.py --layers "$L" --passes "${PASSES:-fwd,dgrad,wgrad}" --iters 2 > gpurun_out/pmc_conv/p$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then
     echo "pass $i ($grp) rc=$rc -- stopping"
