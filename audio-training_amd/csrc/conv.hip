@@ -41,6 +41,7 @@ struct ConvGeom {
   int ldy;           // output row stride (elements)
   long long M;       // N*P*Q
   Drop drop;         // optional Dropout of the output (flat index m*K + k), fused in the epilogue
+  int dbg;           // diagnostics (ACFE_CONV_DBG=8: loop-segment cycle stamps), 0 in production
 };
 
 // 64 bytes of zeros in global memory: im2col taps that fall into the padding
@@ -556,6 +557,34 @@ __device__ __forceinline__ void bldsx4(unsigned voff, i4 desc, unsigned m0v) {
 }
 #pragma clang diagnostic pop
 
+// ACFE_CONV_DBG=8 diagnostic: per-wave cycle totals of the conv main-loop
+// segments (top / wait / barrier / issue / compute / epilogue), read back by
+// acfe_debug_conv_stamps().  Written only when g.dbg == 8.
+__device__ unsigned long long g_conv_stamps[4096 * 8];
+ACFE_API int acfe_debug_conv_stamps(unsigned long long* host, int n) {
+  if (n > 4096 * 8) n = 4096 * 8;
+  return hip_rc(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), sizeof(unsigned long long) * n), "stamps");
+}
+struct Stamps {
+  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0}, last = 0;
+  bool on;
+  __device__ explicit Stamps(bool o) : on(o) { if (on) last = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void mark(int i) {
+    if (on) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[i] += t - last;
+      last = t;
+    }
+  }
+  __device__ void flush(int wid) {
+    if (on && (threadIdx.x & 63) == 0) {
+      const int slot = (blockIdx.x * gridDim.y + blockIdx.y) * 8 + wid;
+      if (slot < 4096)
+        for (int i = 0; i < 6; ++i) g_conv_stamps[slot * 8 + i] = acc[i];
+    }
+  }
+};
+
 __device__ uint2 g_store_sink[64];  // never read: target of masked-off epilogue stores
 
 // One step of a 16-lane butterfly reduce-scatter: lanes whose `BIT` is set keep
@@ -686,7 +715,9 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  Stamps stp(g.dbg == 8);
   while (ctm < walk.end) {
+    stp.mark(0);
     // stage `done` landed: leave the younger stage (if issued) and stores in flight
     const bool two = issued - done >= 2;
     if (pend) {
@@ -696,9 +727,12 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       if (two) wait_vmcnt<LPS>();
       else wait_vmcnt<0>();
     }
+    stp.mark(1);
     lds_barrier();
+    stp.mark(2);
     pend = false;
     if (itm < walk.end) issue();
+    stp.mark(3);
     {
       const unsigned char* Ab = smem + cbuf * STG;
       const unsigned char* Bb = Ab + BM * 128;
@@ -722,6 +756,7 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
           for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], bfr[fn], af[fm], T());
       }
     }
+    stp.mark(4);
     cbuf = cbuf == NST - 1 ? 0 : cbuf + 1;
     ++done;
     if (++ckt < nkt) continue;
@@ -775,7 +810,9 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       }
     }
     ctm += walk.step;
+    stp.mark(5);
   }
+  stp.flush(wid);
   wait_vmcnt<0>();
   lds_barrier();
   if (stats) {
@@ -1145,6 +1182,8 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.ldy = K;
   g.M = (long long)N * P * Q;
   g.drop = make_drop(0.f, 0);
+  static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
+  g.dbg = dbg;
   return g;
 }
 
