@@ -51,7 +51,8 @@ class MelPlan:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        # at interpreter shutdown the module globals may already be gone
+        if h is not None and h.value and lib is not None:
             lib.acfe_plan_destroy(h)
             self._h = None
 

@@ -262,7 +262,7 @@ def main():
             "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
         },
         "roofline": {
-            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv_fwd<bf16,128,128>)",
+            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv_fwd_p<128>, persistent 3-stage LDS-DMA)",
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
