@@ -1161,12 +1161,33 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 
 // sum of split slabs -> dW (optionally accumulated, optionally replicated over
 // `rep` input channels for the folded stem)
-__global__ void k_wgrad_reduce(const float* __restrict__ ws, int nsplit, long long n, float beta,
-                               float* __restrict__ dw) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    float s = 0.f;
-    for (int z = 0; z < nsplit; ++z) s += ws[(long long)z * n + i];
-    dw[i] = beta != 0.f ? dw[i] * beta + s : s;
+// Deterministic split-K combine: dw = beta*dw + sum_z ws[z].  Each thread owns
+// four consecutive outputs (16-B loads) and keeps eight slab loads in flight
+// (independent partial sums, fixed combine order), so the pass runs at HBM
+// rate instead of one dependent load per split.
+__global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ ws, int nsplit, long long n,
+                                                      float beta, float* __restrict__ dw) {
+  // vector path only when every slab (z * n floats) stays 16-B aligned
+  const long long nv = ((n & 3) == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)dw & 15) == 0) ? n >> 2 : 0;
+  for (long long v = (long long)blockIdx.x * 256 + threadIdx.x; v < nv; v += (long long)gridDim.x * 256) {
+    f4 s[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] = f4{0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= nsplit; z += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += *reinterpret_cast<const f4*>(ws + (long long)(z + u) * n + v * 4);
+    }
+    for (; z < nsplit; ++z) s[0] += *reinterpret_cast<const f4*>(ws + (long long)z * n + v * 4);
+    const f4 t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    f4* d = reinterpret_cast<f4*>(dw + v * 4);
+    *d = beta != 0.f ? *d * beta + t : t;
+  }
+  // scalar tail (n % 4)
+  for (long long i = (nv << 2) + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float t = 0.f;
+    for (int z = 0; z < nsplit; ++z) t += ws[(long long)z * n + i];
+    dw[i] = beta != 0.f ? dw[i] * beta + t : t;
   }
 }
 
@@ -1416,8 +1437,8 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   }
   if (rc) return rc;
   const long long n = (long long)K * kd;
-  int grid = cdiv(n, 256);
-  if (grid > 4096) grid = 4096;
+  int grid = cdiv((n + 3) / 4, 256);
+  if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, strm(stream), workspace, (int)splits, n, beta, dw);
   return launch_rc("acfe_conv2d_wgrad(reduce)");
 }
