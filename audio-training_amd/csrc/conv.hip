@@ -32,6 +32,7 @@ typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 // Native 16-byte vector for register staging (HIP's uint4 struct-with-union
 // defeats SROA: arrays of it were demoted to scratch).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t T16;
 
 struct ConvGeom {
   int N, H, W, C;    // input
@@ -1161,6 +1162,150 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 
 // sum of split slabs -> dW (optionally accumulated, optionally replicated over
 // `rep` input channels for the folded stem)
+// ------------------------------------------------------------------ wgrad, 3x3 stride 1, halo-staged
+// dW[k][r][s][c] for the 3x3 stride-1 layers with C % 64 == 0, K in {64, 128}
+// and Q % 64 == 0 (wr_resnet_bird stages 1-2: ~70 % of the step's wgrad time).
+// A workgroup owns one 64-channel chunk and ALL nine taps (output tile
+// K x 576) and reduces over a contiguous range of 64-pixel output-row segments
+// (split-K over pixels, slabs combined by k_wgrad_reduce).  Per segment it
+// stages dY[64 px][K] and the input halo X[3 rows][66 px][64 ch] in LDS ONCE;
+// the nine taps are shifted views of the halo (the im2col kernel re-reads every
+// input pixel nine times).  Per 64-pixel step each wave runs 72 MFMAs (vs 32),
+// so the per-step synchronisation is amortised over 4.5x the matrix work.
+// LDS images are pixel-major with rows padded to 160 / 288 B so the
+// ds_read_b64_tr_b16 fragment reads (8 pixel rows x 32 B per half-wave) hit 64
+// distinct banks; register-staged double buffer, one barrier per step.
+template <int KB>
+__global__ void __launch_bounds__(512, 1)
+k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
+                float* __restrict__ ws, int nchunk, int nseg, int segs_per_split) {
+  constexpr int SEGW = 64, HW = SEGW + 2;
+  constexpr int LDD = KB + 16, LDX = 64 + 16;
+  constexpr int DS = SEGW * LDD, XS = 3 * HW * LDX;
+  constexpr int FM = KB / 32, FN = 9;
+  constexpr int DGR = KB / 8, DG = SEGW * DGR, XG = 3 * HW * 8;
+  constexpr int DPT = (DG + 511) / 512, XPT = (XG + 511) / 512;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (DS + XS)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wid >> 2, wc = wid & 3;
+  const int xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
+  const int cc = bi % nchunk, split = (bi / nchunk) * 8 + xcd;
+  const int sbeg = split * segs_per_split;
+  const int send = sbeg + segs_per_split < nseg ? sbeg + segs_per_split : nseg;
+  const int QS = g.Q / SEGW;
+  const T16* zp = reinterpret_cast<const T16*>(g_zero_page);
+
+  u32x4 rd[DPT], rx[XPT];
+  auto gload = [&](int sg) __attribute__((always_inline)) {
+    const int n = sg / (g.P * QS), rem = sg - n * (g.P * QS);
+    const int h = rem / QS, w0 = (rem - h * QS) * SEGW;
+    const T16* dyrow = dY + (((long long)n * g.P + h) * g.Q + w0) * g.K;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int px = idx / DGR, cg = idx - px * DGR;
+      rd[i] = *reinterpret_cast<const u32x4*>(idx < DG ? dyrow + px * g.K + cg * 8 : zp);
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int hr = idx / (HW * 8), r2 = idx - hr * (HW * 8), hp = r2 >> 3, cg = r2 & 7;
+      const int hin = h - g.pt + hr, win = w0 - g.pl + hp;
+      const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
+      rx[i] = *reinterpret_cast<const u32x4*>(
+          ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + cg * 8 : zp);
+    }
+  };
+  auto sstore = [&](int buf) __attribute__((always_inline)) {
+    uint16_t* Ds = smem + buf * (DS + XS);
+    uint16_t* Xh = Ds + DS;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int px = idx / DGR, cg = idx - px * DGR;
+      if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx >> 3, cg = idx & 7;  // row = hr * HW + hp
+      if (idx < XG) *reinterpret_cast<u32x4*>(Xh + row * LDX + cg * 8) = rx[i];
+    }
+  };
+
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // this wave's nine 16-column blocks: block b = wc * 9 + fn -> tap b / 4, channels (b % 4) * 16
+  int boff[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int b = wc * 9 + fn, t = b >> 2;
+    boff[fn] = ((t / 3) * HW + (t % 3)) * LDX + (b & 3) * 16;
+  }
+  const int grp = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  typedef __attribute__((address_space(3))) bf4* lp;
+
+  if (sbeg < send) {
+    gload(sbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int sg = sbeg; sg < send; ++sg) {
+    const bool more = sg + 1 < send;
+    if (more) gload(sg + 1);
+    const uint16_t* Ds = smem + buf * (DS + XS);
+    const uint16_t* Xh = Ds + DS;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const int rb = kc * 32;
+      bf8 af[FM];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int col = wk * (KB / 2) + fm * 16 + 4 * pp;
+        const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(Ds + (rb + 4 * grp + q) * LDD + col)));
+        const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(Ds + (rb + 16 + 4 * grp + q) * LDD + col)));
+        af[fm] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const uint16_t* xb = Xh + boff[fn] + 4 * pp;
+        const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(xb + (rb + 4 * grp + q) * LDX)));
+        const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lp)(reinterpret_cast<const __bf16*>(xb + (rb + 16 + 4 * grp + q) * LDX)));
+        const bf8 bv = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bv, acc[fm][fn], 0, 0, 0);
+      }
+    }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // slab write: D[k][c] -> ws[split][k][tap * C + cc * 64 + c]
+  const long long kd = 9ll * g.C;
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int b = wc * 9 + fn, t = b >> 2;
+      const int col = t * g.C + cc * 64 + (b & 3) * 16 + (lane & 15);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int k = wk * (KB / 2) + fm * 16 + (lane >> 4) * 4 + jj;
+        ws[((long long)split * g.K + k) * kd + col] = acc[fm][fn][jj];
+      }
+    }
+}
+
 // Deterministic split-K combine: dw = beta*dw + sum_z ws[z].  Each thread owns
 // four consecutive outputs (16-B loads) and keeps eight slab loads in flight
 // (independent partial sums, fixed combine order), so the pass runs at HBM
@@ -1426,16 +1571,38 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   ConvGeom g = make_geom(N, H, W, C, K, R, S, stride, pad_top, pad_left, P, Q, 64, 128);
   g.ldy = K;
   int rc;
-  if (dtype == ACFE_DTYPE_BF16) {
+  static const bool no_halo_w = getenv_flag("ACFE_WGRAD_NO_HALO");
+  if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 && C % 64 == 0 && (K == 64 || K == 128) &&
+      Q % 64 == 0 && (long long)N * P * (Q / 64) < (1ll << 31) && !no_halo_w) {
+    // halo-staged kernel; its split count stays within the planned workspace
+    const int nchunk = C / 64, nseg = (int)((long long)N * P * (Q / 64));
+    int sp = 256 / nchunk;
+    if (sp > splits) sp = (int)splits;
+    sp &= ~7;
+    if (sp < 8) sp = 8;
+    if (sp > splits) sp = (int)splits;  // splits is a multiple of 8 (wgrad_plan)
+    const int per = (nseg + sp - 1) / sp;
+    const dim3 gr(nchunk * sp);
+    if (K == 128)
+      hipLaunchKernelGGL((k_wgrad3x3_halo<128>), gr, dim3(512), 0, strm(stream), g, (const uint16_t*)x,
+                         (const uint16_t*)dy, workspace, nchunk, nseg, per);
+    else
+      hipLaunchKernelGGL((k_wgrad3x3_halo<64>), gr, dim3(512), 0, strm(stream), g, (const uint16_t*)x,
+                         (const uint16_t*)dy, workspace, nchunk, nseg, per);
+    rc = launch_rc("acfe_conv2d_wgrad(halo)");
+    if (rc) return rc;
+    splits = sp;
+  } else if (dtype == ACFE_DTYPE_BF16) {
     if (bmw == 32) rc = launch_wgrad_t<uint16_t, 32>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
     else if (bmw == 64) rc = launch_wgrad_t<uint16_t, 64>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
     else rc = launch_wgrad_t<uint16_t, 128>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+    if (rc) return rc;
   } else {
     if (bmw == 32) rc = launch_wgrad_t<float, 32>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
     else if (bmw == 64) rc = launch_wgrad_t<float, 64>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
     else rc = launch_wgrad_t<float, 128>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
+    if (rc) return rc;
   }
-  if (rc) return rc;
   const long long n = (long long)K * kd;
   int grid = cdiv((n + 3) / 4, 256);
   if (grid > 2048) grid = 2048;

@@ -51,6 +51,10 @@ CONV_CASES = [
     (2, 22, 31, 128, 256, 3, 3, 3, "same"),
     (2, 22, 31, 128, 256, 1, 1, 3, "valid"),
     (1, 300, 5, 16, 64, 3, 3, 1, "same"),
+    # halo-staged 3x3 wgrad (Q % 64 == 0, C % 64 == 0, K in {64, 128}): 1-3 channel chunks
+    (2, 10, 64, 128, 128, 3, 3, 1, "same"),
+    (2, 9, 128, 64, 64, 3, 3, 1, "same"),
+    (1, 6, 64, 192, 128, 3, 3, 1, "same"),
 ]
 
 
