@@ -827,6 +827,200 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   }
 }
 
+// ------------------------------------------------------------------ 3x3 stride-1 conv, row-halo steps
+// Forward (and stride-1 dgrad) of the 3x3 layers with C % 64 == 0,
+// K in {64, 128}, Q % 64 == 0.  Built like k_wgrad3x3_halo, whose measured
+// lesson is that each pipeline step carries a fixed ~1 us of non-MFMA time,
+// so the matrix work per step has to be large: a workgroup owns 3 output rows
+// x 64 pixels x K channels, and one step = one 64-channel chunk x one filter
+// row r (three taps): the 3 input rows (h0 + i + r - pt) x 66 pixels and the
+// weights W[k][r][0..2][chunk] are staged in LDS once (register-staged double
+// buffer, one barrier per step) and feed 72 MFMAs per wave (vs 32 per K-tile
+// in k_conv_fwd_p).  Input rows are 144-B padded (16 consecutive pixels of a
+// fragment read hit distinct banks at any tap shift); weight rows are 128 B
+// with the k & 7 XOR swizzle.  Operands swapped (weights x pixels) so the
+// epilogue is k_conv_fwd_p's: 8-byte channel quads straight from registers,
+// bias from LDS, fused Dropout, DPP-butterfly BatchNormalization sums.
+template <int KB>
+__global__ void __launch_bounds__(512, 1)
+k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+               const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
+               int tiles_w, int ntiles, int srows) {
+  using T = uint16_t;
+  constexpr int TR = 3, SEGW = 64, HWX = SEGW + 2, XRB = 144;   // rows per tile, pixels per row, halo row bytes
+  constexpr int FN = KB / 32, FM = 3;                            // per wave: KB/2 channels x 48 pixels
+  constexpr int NV = 8 * FN;
+  constexpr int XBYTES = TR * HWX * XRB, WBYTES = 3 * KB * 128, BUFB = XBYTES + WBYTES;
+  constexpr int XG = TR * HWX * 8, WG = 3 * KB * 8;             // 16-B granules per step
+  constexpr int XPT = (XG + 511) / 512, WPT = WG / 512;
+  static_assert(WG % 512 == 0, "weight granules per thread");
+  constexpr int OFF_STAT = 2 * BUFB, OFF_BIAS = OFF_STAT + 2 * KB * 8;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_BIAS + KB * 4];
+  double* sstat = reinterpret_cast<double*>(smem + OFF_STAT);
+  float* sbias = reinterpret_cast<float*>(smem + OFF_BIAS);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wid >> 2, wp = wid & 3;
+  const int nch = g.C / 64, nsteps_t = nch * 3;
+  const int tpi = tiles_h * tiles_w;
+  const T* zp = reinterpret_cast<const T*>(g_zero_page);
+  for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
+  for (int i = tid; i < KB; i += 512) sbias[i] = bias ? bias[i] : 0.f;
+  const TileWalk walk(ntiles);
+  const int ntl = walk.tm < walk.end ? (walk.end - walk.tm + walk.step - 1) / walk.step : 0;
+  const int L = ntl * nsteps_t;
+
+  // ---- global -> register staging of step t (tile, chunk, filter row)
+  u32x4 rx[XPT], rw[WPT];
+  auto gload = [&](int t) __attribute__((always_inline)) {
+    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
+    const int tm = walk.tm + tl * walk.step;
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    const int h0 = hb * TR, w0 = wb * SEGW;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx / (HWX * 8), r2 = idx - row * (HWX * 8), hp = r2 >> 3, gr = r2 & 7;
+      const int hin = h0 + row + r - g.pt, win = w0 + hp - g.pl;
+      const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
+      rx[i] = *reinterpret_cast<const u32x4*>(
+          ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + gr * 8 : zp);
+    }
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int s = idx / (KB * 8), r2 = idx - s * (KB * 8), k = r2 >> 3, gr = r2 & 7;
+      rw[i] = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + (r * 3 + s) * g.C + cc * 64 + gr * 8);
+    }
+  };
+  auto sstore = [&](int buf) __attribute__((always_inline)) {
+    unsigned char* Xl = smem + buf * BUFB;
+    unsigned char* Wl = Xl + XBYTES;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx >> 3, gr = idx & 7;  // row = halo row * HWX + pixel
+      if (idx < XG) *reinterpret_cast<u32x4*>(Xl + row * XRB + gr * 16) = rx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx >> 3, gr = idx & 7;  // row = s * KB + k
+      *reinterpret_cast<u32x4*>(Wl + row * 128 + ((gr ^ (row & 7)) << 4)) = rw[i];
+    }
+  };
+
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // this wave's three 16-pixel fragments: tile pixel wp*48 + fm*16 + l16 = (row, col)
+  int xoff[FM];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int p = wp * 48 + fm * 16;
+    xoff[fm] = ((p / SEGW) * HWX + (p % SEGW) + l16) * XRB + (lane >> 4) * 16;
+  }
+  int woff[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) woff[fn] = wk * (KB / 2) + fn * 16 + l16;
+
+  auto epilogue = [&](int tm) __attribute__((always_inline)) {
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    float sv[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) sv[i] = 0.f;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int p = wp * 48 + fm * 16;
+      const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+      const bool inb = h < g.P && w < g.Q;
+      const long long pix = ((long long)n * g.P + h) * g.Q + w;
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
+        uint16_t hv[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          hv[jj] = f2bf(acc[fm][fn][jj] + sbias[c + jj]);
+          if (g.drop.on) hv[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(hv[jj])));
+          const float f = inb ? bf2f(hv[jj]) : 0.f;
+          sv[fn * 4 + jj] += f;
+          sv[FN * 4 + fn * 4 + jj] += f * f;
+        }
+        uint2 v;
+        v.x = (unsigned)hv[0] | ((unsigned)hv[1] << 16);
+        v.y = (unsigned)hv[2] | ((unsigned)hv[3] << 16);
+        uint2* dst = inb ? reinterpret_cast<uint2*>(Y + pix * g.ldy + c) : &g_store_sink[lane];
+        *dst = v;
+        acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if (stats) {
+      butterfly_step<NV, 8, 0x128>(sv, lane);
+      butterfly_step<NV / 2, 4, 0x141>(sv, lane);
+      butterfly_step<NV / 4, 2, 0x4E>(sv, lane);
+      butterfly_step<NV / 8, 1, 0xB1>(sv, lane);
+      const int b0 = ((l16 >> 3) & 1) * (NV / 2) + ((l16 >> 2) & 1) * (NV / 4) + ((l16 >> 1) & 1) * (NV / 8) +
+                     (l16 & 1) * (NV / 16);
+#pragma unroll
+      for (int k = 0; k < NV / 16; ++k) {
+        const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
+        const int col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+        atomicAdd(&sstat[st * KB + col], (double)sv[k]);
+      }
+    }
+  };
+
+  if (L > 0) {
+    gload(0);
+    sstore(0);
+  }
+  __syncthreads();
+  int buf = 0, cst = 0, ctm = walk.tm;
+  for (int t = 0; t < L; ++t) {
+    const bool more = t + 1 < L;
+    if (more) gload(t + 1);
+    const unsigned char* Xl = smem + buf * BUFB;
+    const unsigned char* Wl = Xl + XBYTES;
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        uint4 wf[FN], xf[FM];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int k = woff[fn];
+          wf[fn] = *reinterpret_cast<const uint4*>(Wl + (s * KB + k) * 128 + (((kk * 4 + (lane >> 4)) ^ (k & 7)) << 4));
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          xf[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + s * XRB + kk * 64);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], wf[fn], xf[fm], T());
+      }
+    if (more) sstore(buf ^ 1);
+    if (++cst == nsteps_t) {
+      cst = 0;
+      epilogue(ctm);
+      ctm += walk.step;
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (stats) {
+    for (int c = tid; c < KB; c += 512) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = sstat[c];
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = sstat[KB + c];
+    }
+    for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
+      for (int c = tid; c < 2 * KB; c += 512) stats[((long long)rr * 2 + (c / KB)) * g.Kp + (c % KB)] = 0.0;
+  }
+}
+
 // ------------------------------------------------------------------ weight packing
 // forward:  out[k][(r*S+s)*C + c] = w[k][r][s][c]      (KRSC, zero-padded to [Kp][Kdp])
 // flipped:  out[c][(r*S+s)*K + k] = w[k][R-1-r][S-1-s][c]   (dgrad operand)
@@ -1369,6 +1563,19 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
   dim3 grid(grid_m, g.Kp / BN);
   if constexpr (sizeof(T) == 2 && BN >= 64) {
     static const bool no_pipe = getenv_flag("ACFE_CONV_NO_PIPE");
+    static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS");
+    if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && g.Q % 64 == 0 && !no_rows) {
+      const int tiles_h = (g.P + 2) / 3, tiles_w = g.Q / 64;
+      const long long nt = (long long)g.N * tiles_h * tiles_w;
+      if (nt < (1ll << 31)) {
+        int gp = 256;
+        if (gp > nt) gp = (int)nt;
+        if (gp >= 64) gp &= ~7;
+        hipLaunchKernelGGL((k_conv3x3_rows<BN>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                           (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
+        return launch_rc("acfe_conv2d_fwd");
+      }
+    }
     // k_conv_fwd_p preconditions: whole K-tiles per tap, whole N tiles, a
     // 64-bit tap mask, 32-bit pixel index and < 2 GiB of input per M tile
     const long long img = (long long)g.H * g.W * g.C * 2;
