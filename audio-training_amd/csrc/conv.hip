@@ -841,20 +841,21 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 // with the k & 7 XOR swizzle.  Operands swapped (weights x pixels) so the
 // epilogue is k_conv_fwd_p's: 8-byte channel quads straight from registers,
 // bias from LDS, fused Dropout, DPP-butterfly BatchNormalization sums.
-template <int KB>
+template <int KB, int TR>
 __global__ void __launch_bounds__(512, 1)
 k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
                const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
                int tiles_w, int ntiles, int srows) {
   using T = uint16_t;
-  constexpr int TR = 3, SEGW = 64, HWX = SEGW + 2, XRB = 144;   // rows per tile, pixels per row, halo row bytes
-  constexpr int FN = KB / 32, FM = 3;                            // per wave: KB/2 channels x 48 pixels
+  constexpr int SEGW = 64, HWX = SEGW + 2, XRB = 144;           // pixels per row, halo row bytes
+  constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
+  constexpr int NBUF = TR <= 3 ? 2 : 1;                          // LDS buffers (single: store after a barrier)
   constexpr int NV = 8 * FN;
   constexpr int XBYTES = TR * HWX * XRB, WBYTES = 3 * KB * 128, BUFB = XBYTES + WBYTES;
   constexpr int XG = TR * HWX * 8, WG = 3 * KB * 8;             // 16-B granules per step
   constexpr int XPT = (XG + 511) / 512, WPT = WG / 512;
   static_assert(WG % 512 == 0, "weight granules per thread");
-  constexpr int OFF_STAT = 2 * BUFB, OFF_BIAS = OFF_STAT + 2 * KB * 8;
+  constexpr int OFF_STAT = NBUF * BUFB, OFF_BIAS = OFF_STAT + 2 * KB * 8;
   __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_BIAS + KB * 4];
   double* sstat = reinterpret_cast<double*>(smem + OFF_STAT);
   float* sbias = reinterpret_cast<float*>(smem + OFF_BIAS);
@@ -919,7 +920,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   int xoff[FM];
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm) {
-    const int p = wp * 48 + fm * 16;
+    const int p = wp * (TR * 16) + fm * 16;
     xoff[fm] = ((p / SEGW) * HWX + (p % SEGW) + l16) * XRB + (lane >> 4) * 16;
   }
   int woff[FN];
@@ -933,7 +934,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     for (int i = 0; i < NV; ++i) sv[i] = 0.f;
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
-      const int p = wp * 48 + fm * 16;
+      const int p = wp * (TR * 16) + fm * 16;
       const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
       const bool inb = h < g.P && w < g.Q;
       const long long pix = ((long long)n * g.P + h) * g.Q + w;
@@ -1002,14 +1003,19 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
           for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], wf[fn], xf[fm], T());
       }
-    if (more) sstore(buf ^ 1);
+    if (NBUF == 2 && more) sstore(buf ^ 1);
     if (++cst == nsteps_t) {
       cst = 0;
       epilogue(ctm);
       ctm += walk.step;
     }
     __syncthreads();
-    buf ^= 1;
+    if (NBUF == 2) {
+      buf ^= 1;
+    } else if (more) {
+      sstore(0);  // single buffer: every wave has finished reading it
+      __syncthreads();
+    }
   }
   if (stats) {
     for (int c = tid; c < KB; c += 512) {
@@ -1565,14 +1571,22 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
     static const bool no_pipe = getenv_flag("ACFE_CONV_NO_PIPE");
     static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS");
     if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && g.Q % 64 == 0 && !no_rows) {
-      const int tiles_h = (g.P + 2) / 3, tiles_w = g.Q / 64;
+      // 6 output rows per tile halves the weight traffic per pixel, but at K = 128
+      // its register staging spills (measured 1.4x slower): 3 rows there
+      static const int rows_tr = getenv("ACFE_CONV_ROWS_TR") ? atoi(getenv("ACFE_CONV_ROWS_TR")) : 0;
+      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr : (BN == 64 ? 6 : 3);
+      const int tiles_h = (g.P + tr - 1) / tr, tiles_w = g.Q / 64;
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
         int gp = 256;
         if (gp > nt) gp = (int)nt;
         if (gp >= 64) gp &= ~7;
-        hipLaunchKernelGGL((k_conv3x3_rows<BN>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
-                           (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
+        if (tr == 3)
+          hipLaunchKernelGGL((k_conv3x3_rows<BN, 3>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
+        else
+          hipLaunchKernelGGL((k_conv3x3_rows<BN, 6>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
         return launch_rc("acfe_conv2d_fwd");
       }
     }
