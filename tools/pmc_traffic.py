@@ -15,7 +15,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNEL = "k_conv_fwd_g"
+KERNEL = "k_conv3x3_rows"
 
 
 def per_dispatch(d):
@@ -44,7 +44,7 @@ def main():
     B, H, W, C, K = 512, 128, 256, 128, 128
     algo = (B * H * W * C + B * H * W * K) * 2 + K * 9 * C * 2
     res = {
-        "kernel": "k_conv_fwd_g<bf16,128,128,2,2> (s1b0 conv21 3x3 128->128 @128x256, batch 512)",
+        "kernel": "k_conv3x3_rows<128,3> (s1b0 conv21 3x3 128->128 @128x256, batch 512)",
         "source": "rocprofv3 --pmc, separate passes (tools/pmc_traffic.sh), conv_bench --layers 0 --passes fwd",
         "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,

@@ -5,7 +5,7 @@
 # script.  Then tools/pmc_traffic.py writes profiles/pmc_dominant_<tag>.json.
 # usage: tools/pmc_traffic.sh [tag]
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-TAG=${1:-r01}
+TAG=${1:-r01g}
 O=gpurun_out/pmc_traffic
 mkdir -p $O
 i=0
