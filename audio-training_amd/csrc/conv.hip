@@ -1027,6 +1027,151 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   }
 }
 
+// ------------------------------------------------------------------ 1x1 conv, register-resident weights
+// 1x1 stride-1 convolutions with few input or few output channels (C or K <= 32:
+// the 16->128 stage-1 entry conv, the 16->64 shortcut, and their dgrads
+// 128->16 / 64->16).  These are HBM-streaming problems (a few FLOP per byte),
+// so the whole packed weight matrix lives in VGPRs as MFMA A-fragments and each
+// wave streams 16-pixel blocks: one 16-B load per lane per 32-channel step,
+// v_mfma_f32_16x16x32_bf16 (weights x pixels), then k_conv_fwd_p's epilogue
+// (8-byte channel quads, bias, Dropout, BatchNormalization sums kept in
+// registers across the whole grid-stride loop and reduced once per wave by the
+// DPP butterfly).  C padded to 32 reads zeros from the packed weights and from
+// a lane-constant select on the pixel side.
+template <int NCS, int NKB>
+__global__ void __launch_bounds__(256)
+k_conv1x1_reg(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats) {
+  using T = uint16_t;
+  constexpr int KB = NKB * 16, NV = 8 * NKB, UNR = 2;
+  // wide outputs (K >= 64) go through a wave-private LDS tile so that every
+  // global store is 16 B per lane over whole pixel rows (4 rows per wave store)
+  constexpr bool WIDE = NKB >= 4;
+  constexpr int TROW = KB * 2 + 16;  // padded tile row (bytes): conflict-free 8-B quad writes
+  __shared__ double sstat[2 * KB];
+  __shared__ float sbias[KB];
+  __shared__ __attribute__((aligned(16))) unsigned char stile[WIDE ? 4 * 16 * TROW : 16];
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4;
+  const int wid = tid >> 6;
+  for (int i = tid; i < 2 * KB; i += 256) sstat[i] = 0.0;
+  for (int i = tid; i < KB; i += 256) sbias[i] = (bias && i < g.K) ? bias[i] : 0.f;
+  uint4 wa[NKB][NCS];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int cs = 0; cs < NCS; ++cs)
+      wa[kb][cs] = *reinterpret_cast<const uint4*>(Wp + (long long)(kb * 16 + l16) * g.Kdp + cs * 32 + q * 8);
+  __syncthreads();
+  bool cok[NCS];
+#pragma unroll
+  for (int cs = 0; cs < NCS; ++cs) cok[cs] = cs * 32 + q * 8 < g.C;
+  constexpr int NSV = WIDE ? 4 : NV;  // WIDE: lane owns channels 2*lane, 2*lane+1 (sum, sum of squares)
+  float sv[NSV];
+#pragma unroll
+  for (int i = 0; i < NSV; ++i) sv[i] = 0.f;
+  const T* zp = reinterpret_cast<const T*>(g_zero_page);
+  const long long nblk = (g.M + 15) / 16;
+  const long long wstride = (long long)gridDim.x * 4 * UNR;
+  for (long long b0 = ((long long)blockIdx.x * 4 + wid) * UNR; b0 < nblk; b0 += wstride) {
+    uint4 xb[UNR][NCS];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const long long px = (b0 + u) * 16 + l16;
+      const bool pv = px < g.M;
+#pragma unroll
+      for (int cs = 0; cs < NCS; ++cs)
+        xb[u][cs] = *reinterpret_cast<const uint4*>((pv && cok[cs]) ? X + px * g.C + cs * 32 + q * 8 : zp);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const long long px = (b0 + u) * 16 + l16;
+      const bool inb = px < g.M;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cs = 0; cs < NCS; ++cs) mma(acc, wa[kb][cs], xb[u][cs], T());
+        const int c = kb * 16 + q * 4;
+        uint16_t hv[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          hv[jj] = f2bf(acc[jj] + sbias[c + jj]);
+          if (g.drop.on) hv[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)px * g.K + c + jj, bf2f(hv[jj])));
+          if constexpr (!WIDE) {
+            const float f = (inb && c + jj < g.K) ? bf2f(hv[jj]) : 0.f;
+            sv[kb * 4 + jj] += f;
+            sv[NKB * 4 + kb * 4 + jj] += f * f;
+          }
+        }
+        uint2 v;
+        v.x = (unsigned)hv[0] | ((unsigned)hv[1] << 16);
+        v.y = (unsigned)hv[2] | ((unsigned)hv[3] << 16);
+        if constexpr (WIDE) {
+          *reinterpret_cast<uint2*>(stile + wid * 16 * TROW + l16 * TROW + c * 2) = v;
+        } else if (inb && c < g.K) {
+          *reinterpret_cast<uint2*>(Y + px * g.ldy + c) = v;
+        }
+      }
+      if constexpr (WIDE) {
+        // the wave's 16 pixel rows (K channels each) back out as 16-B row segments
+        constexpr int LPR = KB / 8;          // lanes per pixel row
+        constexpr int RPI = 64 / LPR;        // rows per store instruction
+        const long long pxb = (b0 + u) * 16;
+        if (stats && 2 * lane < KB) {
+#pragma unroll 4
+          for (int row = 0; row < 16; ++row) {
+            const unsigned pr = *reinterpret_cast<const unsigned*>(stile + wid * 16 * TROW + row * TROW + lane * 4);
+            const float f0 = pxb + row < g.M ? __uint_as_float(pr << 16) : 0.f;
+            const float f1 = pxb + row < g.M ? __uint_as_float(pr & 0xffff0000u) : 0.f;
+            sv[0] += f0;
+            sv[1] += f0 * f0;
+            sv[2] += f1;
+            sv[3] += f1 * f1;
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < 16 / RPI; ++it) {
+          const int row = it * RPI + lane / LPR, seg = lane % LPR;
+          const uint4 v = *reinterpret_cast<const uint4*>(stile + wid * 16 * TROW + row * TROW + seg * 16);
+          if (pxb + row < g.M) *reinterpret_cast<uint4*>(Y + (pxb + row) * g.ldy + seg * 8) = v;
+        }
+      }
+    }
+  }
+  if (stats && WIDE) {
+    if (2 * lane < KB) {
+      atomicAdd(&sstat[2 * lane], (double)sv[0]);
+      atomicAdd(&sstat[KB + 2 * lane], (double)sv[1]);
+      atomicAdd(&sstat[2 * lane + 1], (double)sv[2]);
+      atomicAdd(&sstat[KB + 2 * lane + 1], (double)sv[3]);
+    }
+    __syncthreads();
+    for (int c = tid; c < g.Kp; c += 256) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = c < KB ? sstat[c] : 0.0;
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = c < KB ? sstat[KB + c] : 0.0;
+    }
+  } else if (stats) {
+    butterfly_step<NV, 8, 0x128>(sv, lane);
+    butterfly_step<NV / 2, 4, 0x141>(sv, lane);
+    butterfly_step<NV / 4, 2, 0x4E>(sv, lane);
+    butterfly_step<NV / 8, 1, 0xB1>(sv, lane);
+    const int b0i = ((l16 >> 3) & 1) * (NV / 2) + ((l16 >> 2) & 1) * (NV / 4) + ((l16 >> 1) & 1) * (NV / 8) +
+                    (l16 & 1) * (NV / 16);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV / 16; ++k) {
+      const int idx = b0i + k, st = idx / (NKB * 4), rm = idx - st * (NKB * 4);
+      const int col = (rm >> 2) * 16 + q * 4 + (rm & 3);
+      atomicAdd(&sstat[st * KB + col], (double)sv[k]);
+    }
+    __syncthreads();
+    for (int c = tid; c < g.Kp; c += 256) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = c < KB ? sstat[c] : 0.0;
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = c < KB ? sstat[KB + c] : 0.0;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ weight packing
 // forward:  out[k][(r*S+s)*C + c] = w[k][r][s][c]      (KRSC, zero-padded to [Kp][Kdp])
 // flipped:  out[c][(r*S+s)*K + k] = w[k][R-1-r][S-1-s][c]   (dgrad operand)
@@ -1615,9 +1760,29 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
   return launch_rc("acfe_conv2d_fwd");
 }
 
+template <int NCS, int NKB>
+static int launch_1x1(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+                      int grid_m, hipStream_t s) {
+  hipLaunchKernelGGL((k_conv1x1_reg<NCS, NKB>), dim3(grid_m), dim3(256), 0, s, g, (const uint16_t*)x,
+                     (const uint16_t*)wp, bias, (uint16_t*)y, stats);
+  return launch_rc("acfe_conv2d_fwd(1x1)");
+}
+
 template <typename T>
 static int launch_fwd(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                       double* stats, int grid_m, hipStream_t s) {
+  static const bool no_1x1 = getenv_flag("ACFE_CONV_NO_1X1");
+  if (sizeof(T) == 2 && g.R == 1 && g.S == 1 && g.st == 1 && g.pt == 0 && g.pl == 0 && g.C % 8 == 0 &&
+      g.K % 4 == 0 && g.ldy == g.K && !no_1x1 && ((g.C <= 32 && g.K <= 128) || (g.K <= 32 && g.C <= 128))) {
+    const int ncs = (g.C + 31) / 32, nkb = (g.K + 15) / 16;
+    if (nkb >= 4 && g.K != nkb * 16) goto general;  // WIDE tile stores whole 16-channel blocks
+    // dispatch on (reduction steps, 16-channel output blocks)
+#define L1(A, B) if (ncs == A && nkb == B) return launch_1x1<A, B>(g, x, wp, bias, y, stats, grid_m, s)
+    L1(1, 1); L1(1, 2); L1(1, 4); L1(1, 8);
+    L1(2, 1); L1(2, 2); L1(4, 1); L1(4, 2);
+#undef L1
+  }
+general:
   const int bn = pick_bn(g.K);
   if (bn == 32) return launch_fwd_t<T, 32, 4, 1>(g, x, wp, bias, y, stats, grid_m, s);
   if (bn == 64) return launch_fwd_t<T, 64, 2, 2>(g, x, wp, bias, y, stats, grid_m, s);

@@ -55,6 +55,10 @@ CONV_CASES = [
     (2, 10, 64, 128, 128, 3, 3, 1, "same"),
     (2, 9, 128, 64, 64, 3, 3, 1, "same"),
     (1, 6, 64, 192, 128, 3, 3, 1, "same"),
+    # register-weight 1x1 kernel (C or K <= 32)
+    (2, 18, 30, 16, 64, 1, 1, 1, "valid"),
+    (2, 11, 37, 32, 96, 1, 1, 1, "same"),
+    (2, 11, 37, 128, 32, 1, 1, 1, "same"),
 ]
 
 
