@@ -850,12 +850,16 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   constexpr int SEGW = 64, HWX = SEGW + 2, XRB = 144;           // pixels per row, halo row bytes
   constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
   constexpr int NBUF = TR <= 3 ? 2 : 1;                          // LDS buffers (single: store after a barrier)
+  // 6-row tiles: weights by LDS-DMA into a double buffer (no staging VGPRs,
+  // which spilled at K = 128), input rows register-staged into one buffer
+  constexpr bool WDMA = TR > 3;
   constexpr int NV = 8 * FN;
   constexpr int XBYTES = TR * HWX * XRB, WBYTES = 3 * KB * 128, BUFB = XBYTES + WBYTES;
   constexpr int XG = TR * HWX * 8, WG = 3 * KB * 8;             // 16-B granules per step
   constexpr int XPT = (XG + 511) / 512, WPT = WG / 512;
   static_assert(WG % 512 == 0, "weight granules per thread");
-  constexpr int OFF_STAT = NBUF * BUFB, OFF_BIAS = OFF_STAT + 2 * KB * 8;
+  constexpr int OFF_W2 = WDMA ? XBYTES + 2 * WBYTES : 0;           // WDMA layout: [X][W0][W1]
+  constexpr int OFF_STAT = WDMA ? OFF_W2 : NBUF * BUFB, OFF_BIAS = OFF_STAT + 2 * KB * 8;
   __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_BIAS + KB * 4];
   double* sstat = reinterpret_cast<double*>(smem + OFF_STAT);
   float* sbias = reinterpret_cast<float*>(smem + OFF_BIAS);
@@ -872,7 +876,28 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   const int L = ntl * nsteps_t;
 
   // ---- global -> register staging of step t (tile, chunk, filter row)
-  u32x4 rx[XPT], rw[WPT];
+  u32x4 rx[XPT], rw[WDMA ? 1 : WPT];
+  // WDMA: piece j of this wave = 8 weight rows (s*KB + k) of 128 B, granule
+  // slot (lane & 7) holds global granule slot ^ (row & 7) (source-side swizzle)
+  constexpr int WPW = WG / 64 / 8;  // pieces per wave per step
+  unsigned voffW[WDMA ? WPW : 1];
+  if constexpr (WDMA) {
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int row = (wid * WPW + j) * 8 + (lane >> 3);
+      const int s_ = row / KB, k = row - s_ * KB, gr = (lane & 7) ^ (row & 7);
+      voffW[j] = (unsigned)(((long long)k * g.Kdp + s_ * g.C + gr * 8) * 2);
+    }
+  }
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
+  auto wdma = [&](int t, int wb) __attribute__((always_inline)) {
+    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
+    const long long base = (long long)(uintptr_t)Wp + ((long long)r * 3 * g.C + cc * 64) * 2;
+    const i4 dw = {(int)(unsigned)base, (int)(unsigned)(base >> 32), (int)0x80000000u, 0x00020000};
+    const unsigned lb = lds0 + XBYTES + wb * WBYTES + wid * WPW * 1024;
+#pragma unroll
+    for (int j = 0; j < (WDMA ? WPW : 0); ++j) bldsx4(voffW[j], dw, lb + j * 1024);
+  };
   auto gload = [&](int t) __attribute__((always_inline)) {
     const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
     const int tm = walk.tm + tl * walk.step;
@@ -887,11 +912,13 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       rx[i] = *reinterpret_cast<const u32x4*>(
           ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + gr * 8 : zp);
     }
+    if constexpr (!WDMA) {
 #pragma unroll
-    for (int i = 0; i < WPT; ++i) {
-      const int idx = tid + 512 * i;
-      const int s = idx / (KB * 8), r2 = idx - s * (KB * 8), k = r2 >> 3, gr = r2 & 7;
-      rw[i] = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + (r * 3 + s) * g.C + cc * 64 + gr * 8);
+      for (int i = 0; i < WPT; ++i) {
+        const int idx = tid + 512 * i;
+        const int s = idx / (KB * 8), r2 = idx - s * (KB * 8), k = r2 >> 3, gr = r2 & 7;
+        rw[i] = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + (r * 3 + s) * g.C + cc * 64 + gr * 8);
+      }
     }
   };
   auto sstore = [&](int buf) __attribute__((always_inline)) {
@@ -903,11 +930,13 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       const int row = idx >> 3, gr = idx & 7;  // row = halo row * HWX + pixel
       if (idx < XG) *reinterpret_cast<u32x4*>(Xl + row * XRB + gr * 16) = rx[i];
     }
+    if constexpr (!WDMA) {
 #pragma unroll
-    for (int i = 0; i < WPT; ++i) {
-      const int idx = tid + 512 * i;
-      const int row = idx >> 3, gr = idx & 7;  // row = s * KB + k
-      *reinterpret_cast<u32x4*>(Wl + row * 128 + ((gr ^ (row & 7)) << 4)) = rw[i];
+      for (int i = 0; i < WPT; ++i) {
+        const int idx = tid + 512 * i;
+        const int row = idx >> 3, gr = idx & 7;  // row = s * KB + k
+        *reinterpret_cast<u32x4*>(Wl + row * 128 + ((gr ^ (row & 7)) << 4)) = rw[i];
+      }
     }
   };
 
@@ -976,15 +1005,20 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 
   if (L > 0) {
     gload(0);
+    if constexpr (WDMA) wdma(0, 0);
     sstore(0);
   }
+  if constexpr (WDMA) wait_vmcnt<0>();
   __syncthreads();
   int buf = 0, cst = 0, ctm = walk.tm;
   for (int t = 0; t < L; ++t) {
     const bool more = t + 1 < L;
-    if (more) gload(t + 1);
+    if (more) {
+      gload(t + 1);
+      if constexpr (WDMA) wdma(t + 1, (t + 1) & 1);
+    }
     const unsigned char* Xl = smem + buf * BUFB;
-    const unsigned char* Wl = Xl + XBYTES;
+    const unsigned char* Wl = WDMA ? smem + XBYTES + (t & 1) * WBYTES : Xl + XBYTES;
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
@@ -1014,6 +1048,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       buf ^= 1;
     } else if (more) {
       sstore(0);  // single buffer: every wave has finished reading it
+      if constexpr (WDMA) wait_vmcnt<0>();  // next step's weight pieces landed
       __syncthreads();
     }
   }
@@ -1719,7 +1754,7 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
       // 6 output rows per tile halves the weight traffic per pixel, but at K = 128
       // its register staging spills (measured 1.4x slower): 3 rows there
       static const int rows_tr = getenv("ACFE_CONV_ROWS_TR") ? atoi(getenv("ACFE_CONV_ROWS_TR")) : 0;
-      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr : (BN == 64 ? 6 : 3);
+      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr : 6;
       const int tiles_h = (g.P + tr - 1) / tr, tiles_w = g.Q / 64;
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
