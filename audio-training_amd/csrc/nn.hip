@@ -78,24 +78,39 @@ static int vgrid(long long nvec) { return grid_for(nvec, 256, 16384); }
 
 // Sum a [nrows][2][ld] double slab over rows for the 32 channels of this block
 // (8 row groups x 32 channels, fixed order): s[j][cl] for j in {0, 1}.
+// Fixed-order (deterministic) column sums of a partial-statistics slab
+// part[nrows][2][ld] for the 32 channels of this block: 1024 threads = 32 row
+// groups x 32 channels, each thread keeps four independent (sum, sum) pairs so
+// eight loads are in flight, then a fixed-order tree over the row groups.
+// (The finalizers were latency-bound at 40-60 us with 8 row groups.)
+constexpr int SLAB_THREADS = 1024;
 __device__ __forceinline__ void slab_sum32(const double* __restrict__ part, int nrows, int ld, int C,
                                            double (*s)[32]) {
-  __shared__ double tmp[8][2][32];
+  __shared__ double tmp[32][2][32];
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
-  double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int r = rg; r < nrows; r += 8) {
-      a += part[((long long)r * 2 + 0) * ld + c];
-      b += part[((long long)r * 2 + 1) * ld + c];
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C) {
+    int r = rg;
+    for (; r + 96 < nrows; r += 128) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] += part[((long long)(r + 32 * u) * 2 + 0) * ld + c];
+        b[u] += part[((long long)(r + 32 * u) * 2 + 1) * ld + c];
+      }
     }
-  tmp[rg][0][cl] = a;
-  tmp[rg][1][cl] = b;
+    for (int u = 0; r < nrows; r += 32, ++u) {
+      a[u & 3] += part[((long long)r * 2 + 0) * ld + c];
+      b[u & 3] += part[((long long)r * 2 + 1) * ld + c];
+    }
+  }
+  tmp[rg][0][cl] = (a[0] + a[1]) + (a[2] + a[3]);
+  tmp[rg][1][cl] = (b[0] + b[1]) + (b[2] + b[3]);
   __syncthreads();
   if (rg == 0) {
     double x = 0.0, y = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 32; ++i) {
       x += tmp[i][0][cl];
       y += tmp[i][1][cl];
     }
@@ -220,7 +235,7 @@ ACFE_API int acfe_bn_stats(const void* x, long long rows, int C, int dtype, doub
 // out (each fp32[C], any may be NULL except scale/shift):
 //   scale = gamma * invstd, shift = beta - mean * scale, mean, invstd
 // training: batch statistics + moving-average update (momentum); else moving stats.
-__global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ part, int nrows, int ld, int C,
+__global__ void __launch_bounds__(SLAB_THREADS) k_bn_finalize(const double* __restrict__ part, int nrows, int ld, int C,
                                                      double count, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps, float momentum,
                                                      float* __restrict__ mmean, float* __restrict__ mvar,
@@ -258,7 +273,7 @@ ACFE_API int acfe_bn_finalize(const double* part, int nrows, int ld, int C, doub
   if (!scale || !shift || C <= 0 || (training && (!part || nrows <= 0 || count <= 0)) ||
       (!training && (!moving_mean || !moving_var)))
     return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, nrows, ld, C, count,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, ld, C, count,
                      gamma, beta, eps, momentum, moving_mean, moving_var, training, scale, shift, mean, invstd);
   return launch_rc("acfe_bn_finalize");
 }
@@ -427,7 +442,7 @@ ACFE_API int acfe_bn_bwd_reduce(const void* dy, int dy_dtype, const void* x, int
 }
 
 // coef[3][C] = {a, b, c} with dx = a*g + b*x + c; dgamma = sum g xhat, dbeta = sum g
-__global__ void __launch_bounds__(256) k_bn_bwd_finalize(const double* __restrict__ part, int nrows, int C,
+__global__ void __launch_bounds__(SLAB_THREADS) k_bn_bwd_finalize(const double* __restrict__ part, int nrows, int C,
                                                          double count, const float* __restrict__ scale,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ invstd,
@@ -451,7 +466,7 @@ ACFE_API int acfe_bn_bwd_finalize(const double* part, int nrows, int C, double c
                                   const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                   float* coef, void* stream) {
   if (!part || !scale || !mean || !invstd || !coef || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, nrows, C, count, scale,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, count, scale,
                      mean, invstd, dgamma, dbeta, coef);
   return launch_rc("acfe_bn_bwd_finalize");
 }
@@ -1499,7 +1514,7 @@ ACFE_API int acfe_cast(const void* x, int x_dtype, long long n, void* y, int y_d
 }
 
 // out[c] = beta*out[c] + sum_rows x[r][c]  (bias gradients); part: bn_stats slab
-__global__ void __launch_bounds__(256) k_chan_sum_fin(const double* __restrict__ part, int nrows, int C, float beta,
+__global__ void __launch_bounds__(SLAB_THREADS) k_chan_sum_fin(const double* __restrict__ part, int nrows, int C, float beta,
                                                       float* __restrict__ out) {
   __shared__ double s[2][32];
   slab_sum32(part, nrows, C, C, s);
@@ -1510,7 +1525,7 @@ __global__ void __launch_bounds__(256) k_chan_sum_fin(const double* __restrict__
 // out[c] = beta*out[c] + sum of a slab's first row set (part [nrows][2][C]).
 ACFE_API int acfe_channel_sum_finalize(const double* part, int nrows, int C, float beta, float* out, void* stream) {
   if (!part || !out || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, nrows, C, beta, out);
+  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, beta, out);
   return launch_rc("acfe_channel_sum_finalize");
 }
 ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* part, float* out,
@@ -1519,7 +1534,7 @@ ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, d
   if (rows == 0) return hip_rc(hipMemsetAsync(out, 0, sizeof(float) * C, strm(stream)), "acfe_channel_sum");
   int rc = acfe_bn_stats(x, rows, C, dtype, part, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(256), 0, strm(stream), part, red_blocks(rows), C, beta,
+  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, red_blocks(rows), C, beta,
                      out);
   return launch_rc("acfe_channel_sum");
 }
