@@ -58,6 +58,11 @@ SIGNATURES: dict[str, list] = {
     "acfe_bn_bwd_apply": [P, I32, P, I32, I64, I32, P, P, I32, P, P, P, I32, P],
     "acfe_bn_bwd_apply_dropout": [P, I32, P, I32, I64, I32, P, P, I32, P, F32, C.c_uint64, P, I32, P],
     "acfe_bn_bwd_apply_ex": [P, I32, P, I32, I64, I32, P, P, I32, P, P, F32, C.c_uint64, P, I32, P, P],
+    "acfe_c1bn_supported": [I32, I32],
+    "acfe_c1bn_workspace": [I64, I32, I32],
+    "acfe_c1bn_stats": [P, I64, I32, P, I32, P, P, P, P, P],
+    "acfe_c1bn_apply": [P, I64, I32, P, I32, P, P, P, I32, P, P],
+    "acfe_c1bn_bwd": [P, P, I64, I32, P, I32, P, P, P, P, P, I32, F64, P, P, P, P, P, P, P, P],
     "acfe_channel_sum": [P, I64, I32, I32, P, P, F32, P],
     "acfe_add": [P, P, I64, I32, P, I32, P],
     "acfe_add_stats": [P, P, I64, I32, I32, P, I32, P, P],
@@ -80,7 +85,8 @@ SIGNATURES: dict[str, list] = {
     "acfe_loss": [P, P, I32, I32, I32, F32, P, P, P, P],
     "acfe_adam_step": [P, P, P, P, I64, F32, F32, F32, F32, F32, P],
 }
-_RESTYPES = {"acfe_last_error": C.c_char_p, "acfe_conv2d_wgrad_workspace": I64, "acfe_crc32c": C.c_uint32}
+_RESTYPES = {"acfe_last_error": C.c_char_p, "acfe_conv2d_wgrad_workspace": I64, "acfe_crc32c": C.c_uint32,
+             "acfe_c1bn_workspace": I64}
 
 PAD_END, PAD_CENTER_CONSTANT, PAD_CENTER_REFLECT = 0, 1, 2
 LAYOUT_BTM, LAYOUT_BMT = 0, 1

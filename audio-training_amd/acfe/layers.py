@@ -83,6 +83,13 @@ def conv_dropout_bn(conv: Conv2D, bn: BatchNormalization, x, rate, relu=True):
                                eps=bn.eps, momentum=bn.momentum)
 
 
+def conv_bn(conv: Conv2D, bn: BatchNormalization, x, relu=True):
+    """bn(conv(x)) (+ReLU) as one node (ops.conv_bn: the recomputing 1x1 node
+    when the conv has 16 input channels)."""
+    return ops.conv_bn(x, conv.weight, conv.bias, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance, bn.training,
+                       relu=relu, stride=conv.strides, padding=conv.padding, eps=bn.eps, momentum=bn.momentum)
+
+
 def maxpool_dropout_bn(x, kh, kw, bn: BatchNormalization, rate, relu=True):
     """bn(Dropout(rate)(MaxPool2D((kh, kw))(x))) (+ReLU) as one fused node."""
     return ops.maxpool_dropout_bn(x, kh, kw, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance, bn.training,

@@ -405,6 +405,76 @@ def conv_dropout_bn(x, w, b, gamma, beta, mmean, mvar, training, rate=0.0, seed=
     return _ConvDropBNFn.apply(x, w, b, gamma, beta, mmean, mvar, conf)
 
 
+# ------------------------------------------------------------------ 1x1 conv + BN, conv output recomputed
+def _c1bn_ok(x, w, stride) -> bool:
+    K, R, S, C = w.shape
+    return (FUSE and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous() and x.data_ptr() % 16 == 0
+            and R == 1 and S == 1 and stride == 1 and w.is_contiguous() and bool(lib.acfe_c1bn_supported(C, K)))
+
+
+class _C1BNFn(torch.autograd.Function):
+    """BatchNormalization(+ReLU) of a 1x1 Conv2D with 16 input channels as one
+    node (csrc/c1bn.hip): the conv output is never stored; its statistics come
+    from the 16x16 Gram matrix of x, the backward's sums from g^T x."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
+        training, relu, eps, momentum = conf
+        N, H, W, C = x.shape
+        K = w.shape[0]
+        M = N * H * W
+        dev, s = x.device, stream()
+        scale, shift, mean, invstd = (_empty((K,), F32, dev) for _ in range(4))
+        ws = _empty((lib.acfe_c1bn_workspace(M, C, K),), F32, dev)
+        gram = _empty((272,), F32, dev)
+        part = _empty((1, 2, K), F64, dev)
+        call("acfe_c1bn_stats", ptr(x), M, C, ptr(w), K, ptr(b), ptr(part), ptr(gram), ptr(ws), s)
+        if training:
+            call("acfe_bn_finalize", ptr(part), 1, K, K, float(M), ptr(gamma), ptr(beta), eps, momentum,
+                 ptr(mmean), ptr(mvar), 1, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
+        else:
+            call("acfe_bn_finalize", None, 0, K, K, 0.0, ptr(gamma), ptr(beta), eps, momentum, ptr(mmean),
+                 ptr(mvar), 0, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
+        y = _empty((N, H, W, K), x.dtype, dev)
+        call("acfe_c1bn_apply", ptr(x), M, C, ptr(w), K, ptr(b), ptr(scale), ptr(shift), int(relu), ptr(y), s)
+        ctx.save_for_backward(x, w, b, scale, shift, mean, invstd, gram)
+        ctx.conf = conf
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, scale, shift, mean, invstd, gram = ctx.saved_tensors
+        training, relu, eps, momentum = ctx.conf
+        N, H, W, C = x.shape
+        K = w.shape[0]
+        M = N * H * W
+        dev = x.device
+        dy = dy.contiguous()
+        dx = _empty(x.shape, x.dtype, dev)
+        dw = _empty(w.shape, F32, dev)
+        db = _empty((K,), F32, dev) if b is not None else None
+        dgamma, dbeta = _empty((K,), F32, dev), _empty((K,), F32, dev)
+        ws = _empty((lib.acfe_c1bn_workspace(M, C, K),), F32, dev)
+        # eval mode: statistics are constants -> count -> inf removes the mean terms
+        call("acfe_c1bn_bwd", ptr(dy), ptr(x), M, C, ptr(w), K, ptr(b), ptr(scale), ptr(shift), ptr(mean),
+             ptr(invstd), int(relu), float(M) if training else 1e300, ptr(gram), ptr(dx), ptr(dw), ptr(db),
+             ptr(dgamma), ptr(dbeta), ptr(ws), stream())
+        return dx, dw, db, dgamma, dbeta, None, None, None
+
+
+def conv_bn(x, w, b, gamma, beta, mmean, mvar, training, relu=True, stride=1, padding="same", eps=1e-3,
+            momentum=0.99):
+    """BatchNormalization(Conv2D(x)) (+ReLU), Keras semantics of each layer.  A
+    bf16 1x1 conv with 16 input channels runs as the recomputing node _C1BNFn;
+    anything else as the two layers (conv epilogue statistics -> BN)."""
+    if _c1bn_ok(x, w, stride):
+        return _C1BNFn.apply(x, w, b, gamma, beta, mmean, mvar,
+                             (bool(training), bool(relu), float(eps), float(momentum)))
+    u, st = conv2d(x, w, b, stride, padding, want_stats=bool(training))
+    return batch_norm(u, gamma, beta, mmean, mvar, training, relu=relu, stats=st if training else None, eps=eps,
+                      momentum=momentum)
+
+
 # ------------------------------------------------------------------ elementwise / pooling
 class _AddFn(torch.autograd.Function):
     @staticmethod

@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from acfe import ops
-from acfe.layers import (BatchNormalization, Conv2D, Dense, StemConv2D, conv_dropout_bn,
+from acfe.layers import (BatchNormalization, Conv2D, Dense, StemConv2D, conv_bn, conv_dropout_bn,
                          maxpool_dropout_bn)
 
 
@@ -57,8 +57,7 @@ class BasicBlock(nn.Module):
         y = x
         if self.stride > 1:
             y = self.bn2a0(y, relu=True, stats=x_stats, link=link)
-            y, st = self.conv2a0(y, want_stats=True)
-            y = self.bn2a(y, relu=True, stats=st)
+            y = conv_bn(self.conv2a0, self.bn2a, y, relu=True)
             y = self.conv21(y)
             y = maxpool_dropout_bn(y, self.stride, self.stride, self.bn2b, self.dropout)
         else:

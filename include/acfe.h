@@ -224,6 +224,28 @@ int acfe_bn_bwd_apply_ex(const void* dy, int dy_dtype, const void* x, int x_dtyp
                          float drop_rate, unsigned long long seed, void* dx, int dx_dtype, double* sum_partial,
                          void* stream);
 
+/* Conv2D(1x1, 16 -> K in {64, 128}, bias) -> BatchNormalization -> (ReLU) as one
+ * node whose conv output A = W x + b is never stored (csrc/c1bn.hip;
+ * res{s}b0_branch2a0 + bn{s}b0_branch2a of resnet/wr_resnet_bird.py:121-131).
+ * bf16 x [M][16] (16-B aligned), fp32 w [K][16] (KRSC, R = S = 1), bf16 y / dy
+ * [M][K]; workspace float[acfe_c1bn_workspace(M, 16, K)].
+ * Forward: acfe_c1bn_stats (training) writes partial = double[1][2][K] {sum A,
+ * sum A^2} for acfe_bn_finalize(partial, 1, K, K, count = M, ...) and
+ * gram = float[272] (sum x x^T, sum x; keep it for the backward; in eval mode
+ * fill it with acfe_c1bn_stats too), then acfe_c1bn_apply writes y.
+ * Backward: acfe_c1bn_bwd -> dx [M][16], dw [K][16], db [K], dgamma, dbeta
+ * (nullable); count = M in training, 1e300 in eval. */
+int acfe_c1bn_supported(int C, int K);
+long long acfe_c1bn_workspace(long long M, int C, int K);
+int acfe_c1bn_stats(const void* x, long long M, int C, const float* w, int K, const float* bias, double* partial,
+                    float* gram, float* workspace, void* stream);
+int acfe_c1bn_apply(const void* x, long long M, int C, const float* w, int K, const float* bias, const float* scale,
+                    const float* shift, int relu, void* y, void* stream);
+int acfe_c1bn_bwd(const void* dy, const void* x, long long M, int C, const float* w, int K, const float* bias,
+                  const float* scale, const float* shift, const float* mean, const float* invstd, int relu,
+                  double count, const float* gram, void* dx, float* dw, float* db, float* dgamma, float* dbeta,
+                  float* workspace, void* stream);
+
 /* out[c] = beta*out[c] + sum_rows x[r][c] (bias gradients); partial as acfe_bn_stats. */
 int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* partial, float* out, float beta,
                      void* stream);

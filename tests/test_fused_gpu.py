@@ -247,3 +247,72 @@ def test_fused_channel_sums(env, cuda, C):
     s = torch.empty((C,), device=cuda)
     call("acfe_channel_sum_finalize", ptr(part), nb, C, 0.0, ptr(s), stream())
     torch.testing.assert_close(s, ops.channel_sum(d0, C), rtol=1e-5, atol=1e-4)
+
+
+def _c1bn_reference(x0, w0, b0, gamma, beta, mm, mv, gy, training, eps=1e-3, momentum=0.99):
+    """float64 torch-CPU restatement of Conv2D(1x1) -> BatchNormalization (Keras:
+    biased batch variance, moving averages with momentum) -> ReLU, on the
+    bf16-rounded weights the kernels multiply with."""
+    x = x0.double().cpu().requires_grad_(True)
+    w = w0.to(torch.bfloat16).double().cpu().reshape(w0.shape[0], -1).requires_grad_(True)
+    b = b0.double().cpu().requires_grad_(True)
+    g = gamma.detach().double().cpu().requires_grad_(True)
+    be = beta.detach().double().cpu().requires_grad_(True)
+    a = x @ w.T + b
+    if training:
+        mean, var = a.mean((0, 1, 2)), a.var((0, 1, 2), unbiased=False)
+    else:
+        mean, var = mm.double().cpu(), mv.double().cpu()
+    y = torch.relu(g * (a - mean) / torch.sqrt(var + eps) + be)
+    y.backward(gy.double().cpu())
+    mm1, mv1 = mm.double().cpu(), mv.double().cpu()
+    if training:
+        mm1 = mm1 * momentum + mean.detach() * (1 - momentum)
+        mv1 = mv1 * momentum + var.detach() * (1 - momentum)
+    return [y, x.grad, w.grad.reshape(w0.shape), g.grad, be.grad, mm1, mv1, b.grad]
+
+
+@pytest.mark.parametrize("shape", [(3, 10, 37), (5, 128, 469)], ids=["ragged", "multi-pass"])
+@pytest.mark.parametrize("K", [128, 64])
+@pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
+def test_conv1x1_bn_node(env, cuda, shape, K, training):
+    """The 1x1-conv + BN node (csrc/c1bn.hip: conv output never stored, its
+    statistics from the Gram matrix of x, the backward sums from g^T x) and the
+    unfused conv2d -> batch_norm chain, both against a float64 restatement: the
+    fused node must be as accurate as the unfused chain (rel-L2 error at most
+    1.25x the unfused error + 1e-3 on y, every gradient and the moving
+    statistics).  In training mode the conv-bias gradient is zero in exact
+    arithmetic: bounded absolutely.  'ragged': 1110 pixels (a partial last
+    32-pixel chunk); 'multi-pass': 300160 pixels, several grid-stride passes
+    per wave in every kernel."""
+    ops = env[0]
+    N, H, W = shape
+    C = 16
+    g = torch.Generator(device="cpu").manual_seed(12)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((K, 1, 1, C), generator=g) * 0.2).to(cuda)
+    b0 = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    gy = torch.randn((N, H, W, K), generator=g).to(torch.bfloat16).to(cuda)
+    gamma, beta, mm, mv = _bn_params(K, cuda, 13)
+    ref = _c1bn_reference(x0, w0, b0, gamma, beta, mm, mv, gy, training)
+    outs = []
+    for fused in (False, True):
+        x = x0.clone().requires_grad_(True)
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        gamma, beta, mm, mv = _bn_params(K, cuda, 13)
+        if fused:
+            assert ops._c1bn_ok(x, w, 1)
+            y = ops.conv_bn(x, w, b, gamma, beta, mm, mv, training, relu=True)
+        else:
+            u, st = ops.conv2d(x, w, b, 1, want_stats=training)
+            y = ops.batch_norm(u, gamma, beta, mm, mv, training, relu=True, stats=st if training else None)
+        y.backward(gy)
+        outs.append([y, x.grad, w.grad, gamma.grad, beta.grad, mm, mv, b.grad])
+    names = ["y", "dx", "dw", "dgamma", "dbeta", "moving_mean", "moving_var", "db"]
+    for i in range(7):
+        ef, eu = rel(outs[1][i], ref[i]), rel(outs[0][i], ref[i])
+        assert ef <= 1.25 * eu + 1e-3, (names[i], ef, eu)
+    if training:
+        assert (outs[1][-1].double().cpu() - ref[-1]).norm().item() < 1e-3 * ref[2].norm().item()
+    else:
+        assert rel(outs[1][-1], ref[-1]) <= 1.25 * rel(outs[0][-1], ref[-1]) + 1e-3

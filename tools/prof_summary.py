@@ -19,18 +19,18 @@ def main():
     print("| kernel | calls | total ms | avg us | % |")
     print("|---|---:|---:|---:|---:|")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
-        name = r["Name"].split("(")[0]
+        name = r["Name"].replace("(anonymous namespace)::", "").split("(")[0]
         print(f"| `{name[:90]}` | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.2f} | "
               f"{float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.1f} |")
     print(f"\nTotal kernel time {tot/1e6:.1f} ms" + (f" over {steps} steps = {tot/1e6/steps:.2f} ms/step" if steps else ""))
     by = defaultdict(list)
     for r in csv.DictReader(open(trace)):
-        key = (r["Kernel_Name"].split("(")[0], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
+        key = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
         by[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     print("\nLongest dispatch groups (kernel, grid):")
     print("| kernel | grid | dispatches | avg us | min us | max us |")
     print("|---|---|---:|---:|---:|---:|")
-    for (k, gx, gy, gz), d in sorted(by.items(), key=lambda kv: -sum(kv[1]))[:15]:
+    for (k, gx, gy, gz), d in sorted(by.items(), key=lambda kv: -sum(kv[1]))[:30]:
         print(f"| `{k[:80]}` | {gx}x{gy}x{gz} | {len(d)} | {sum(d)/len(d):.1f} | {min(d):.1f} | {max(d):.1f} |")
 
 
