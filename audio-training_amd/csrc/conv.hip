@@ -2310,6 +2310,242 @@ __global__ void k_stem_fold(const float* __restrict__ w, int K, int RS, int rep,
   }
 }
 
+// ---- MFMA stem (bf16 activations; R*S <= 32 taps) -------------------------
+// Same tiles (16 rows x 64 columns, grid-stride) and slab contracts as the
+// VALU kernels above; the 5x5 taps become the 32-deep reduction of
+// v_mfma_f32_16x16x32_bf16 (zero-padded from 25), so the VALU work per pixel
+// is an LDS gather instead of 400 FMAs:
+//   fwd:   D[k][px] = sum_t weff[t][k] * x[px + off_t]      (A = weights, B = im2col gather)
+//   dgrad: D[.][px] = sum_{t,k} dy[px - off_t][k] weff[t][k] (B = 16-B dy reads, 2 taps x 16
+//          channels per k-step; the A rows are replicated, one row is the result)
+//   wgrad: D[k][t]  = sum_px dy[px][k] * x[px + off_t]      (A = dy chunk read transposed,
+//          B = im2col gather; k-dimension = 32 pixels of one row)
+// Weights are bf16 (the VALU kernels keep fp32 weights: the fp32 path).
+typedef __attribute__((address_space(3))) bf4* stem_lp;
+
+__device__ __forceinline__ unsigned stem_pack2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+
+template <int R, int S>
+__global__ void __launch_bounds__(256)
+k_stem_fwd_mfma(const uint16_t* __restrict__ x, int N, int H, int W, int pt, int pl, const float* __restrict__ weff,
+                const float* __restrict__ bias, uint16_t* __restrict__ y, double* __restrict__ stats, int tiles_h,
+                int tiles_w) {
+  constexpr int XH = STEM_TH + R - 1, XW = STEM_TW + S - 1, NT = R * S;
+  static_assert(NT <= 32, "taps");
+  __shared__ uint16_t xs[XH * XW];
+  __shared__ double red[2][STEM_K];
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
+  for (int i = tid; i < 2 * STEM_K; i += 256) (&red[0][0])[i] = 0.0;
+  uint4 wa;
+  int toff[8];
+  {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = q * 8 + j;
+      v[j] = t < NT ? weff[t * STEM_K + l16] : 0.f;
+      toff[j] = t < NT ? (t / S) * XW + (t % S) : 0;
+    }
+    wa = uint4{stem_pack2(v[0], v[1]), stem_pack2(v[2], v[3]), stem_pack2(v[4], v[5]), stem_pack2(v[6], v[7])};
+  }
+  float bk[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bk[r] = bias ? bias[q * 4 + r] : 0.f;
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  const long long ntiles = (long long)N * tiles_h * tiles_w;
+  for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    const int tw = (int)(tt % tiles_w), th = (int)((tt / tiles_w) % tiles_h);
+    const int n = (int)(tt / ((long long)tiles_w * tiles_h));
+    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+    __syncthreads();
+    for (int i = tid; i < XH * XW; i += 256) {
+      const int yy = i / XW, xx = i - yy * XW;
+      const int h = h0 - pt + yy, w = w0 - pl + xx;
+      xs[i] = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? x[((long long)n * H + h) * W + w] : 0;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int blk = 0; blk < 16; ++blk) {
+      const int ry = wid * 4 + (blk >> 2), cx = (blk & 3) * 16 + l16;
+      const uint16_t* src = xs + ry * XW + cx;
+      unsigned tv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tv[j] = (q * 8 + j < NT) ? src[toff[j]] : 0u;
+      const uint4 b = uint4{tv[0] | (tv[1] << 16), tv[2] | (tv[3] << 16), tv[4] | (tv[5] << 16), tv[6] | (tv[7] << 16)};
+      const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, wa), __builtin_bit_cast(bf8, b),
+                                                             f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int h = h0 + ry, w = w0 + cx;
+      if (h < H && w < W) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = bf2f(f2bf(acc[r] + bk[r]));
+        *reinterpret_cast<uint2*>(y + (((long long)n * H + h) * W + w) * STEM_K + q * 4) =
+            uint2{stem_pack2(o[0], o[1]), stem_pack2(o[2], o[3])};
+        if (stats) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s1[r] += o[r], s2[r] += (double)o[r] * o[r];
+        }
+      }
+    }
+  }
+  if (stats) {
+    // lanes with the same q hold the same 4 channels: reduce over l16
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        s1[r] += __shfl_xor(s1[r], o, 64);
+        s2[r] += __shfl_xor(s2[r], o, 64);
+      }
+    }
+    __syncthreads();
+    if (l16 == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        atomicAdd(&red[0][q * 4 + r], s1[r]);
+        atomicAdd(&red[1][q * 4 + r], s2[r]);
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * STEM_K) stats[(long long)blockIdx.x * 2 * STEM_K + tid] = (&red[0][0])[tid];
+  }
+}
+
+template <int R, int S>
+__global__ void __launch_bounds__(256)
+k_stem_dgrad_mfma(const uint16_t* __restrict__ dy, int N, int H, int W, int pt, int pl,
+                  const float* __restrict__ weff, uint16_t* __restrict__ dx, int tiles_h, int tiles_w) {
+  constexpr int XH = STEM_TH + R - 1, XW = STEM_TW + S - 1, NT = R * S, NKT = (NT + 1) / 2;
+  __shared__ __attribute__((aligned(16))) uint16_t gs[XH * XW * STEM_K];
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
+  // k-step kt: k-slot q*8 + j <-> (tap 2kt + (q >> 1), channel (q & 1)*8 + j); A rows replicated
+  uint4 wa[NKT];
+  int goff[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int t = 2 * kt + (q >> 1), r = t / S, s = t % S;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t < NT ? weff[t * STEM_K + (q & 1) * 8 + j] : 0.f;
+    wa[kt] = uint4{stem_pack2(v[0], v[1]), stem_pack2(v[2], v[3]), stem_pack2(v[4], v[5]), stem_pack2(v[6], v[7])};
+    goff[kt] = t < NT ? ((R - 1 - r) * XW + (S - 1 - s)) * STEM_K + (q & 1) * 8 : -1;
+  }
+  const uint4 z4 = {0u, 0u, 0u, 0u};
+  const long long ntiles = (long long)N * tiles_h * tiles_w;
+  for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    const int tw = (int)(tt % tiles_w), th = (int)((tt / tiles_w) % tiles_h);
+    const int n = (int)(tt / ((long long)tiles_w * tiles_h));
+    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+    const int gh0 = h0 - (R - 1 - pt), gw0 = w0 - (S - 1 - pl);
+    __syncthreads();
+    for (int i = tid; i < XH * XW * 2; i += 256) {
+      const int pos = i >> 1, c = i & 1;
+      const int yy = pos / XW, xx = pos - yy * XW;
+      const int h = gh0 + yy, w = gw0 + xx;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+        v = *reinterpret_cast<const u32x4*>(dy + (((long long)n * H + h) * W + w) * STEM_K + c * 8);
+      *reinterpret_cast<u32x4*>(gs + (long long)i * 8) = v;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int blk = 0; blk < 16; ++blk) {
+      const int ry = wid * 4 + (blk >> 2), cx = (blk & 3) * 16 + l16;
+      const uint16_t* base = gs + (ry * XW + cx) * STEM_K;
+      f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const uint4 b = goff[kt] >= 0 ? *reinterpret_cast<const uint4*>(base + goff[kt]) : z4;
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, wa[kt]), __builtin_bit_cast(bf8, b), acc,
+                                                      0, 0, 0);
+      }
+      const int h = h0 + ry, w = w0 + cx;
+      if (q == 0 && h < H && w < W) dx[((long long)n * H + h) * W + w] = f2bf(acc[0]);
+    }
+  }
+}
+
+template <int R, int S>
+__global__ void __launch_bounds__(256)
+k_stem_wgrad_mfma(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int N, int H, int W, int pt,
+                  int pl, double* __restrict__ part, int tiles_h, int tiles_w) {
+  constexpr int XH = STEM_TH + R - 1, XW = STEM_TW + S - 1, NT = R * S, LDG = 24;
+  __shared__ uint16_t xs[XH * XW];
+  __shared__ __attribute__((aligned(16))) uint16_t gch[4][32 * LDG];  // per wave: 32 px x 16 ch of dy
+  __shared__ float red[4][STEM_K][32];
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
+  const int grp = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  // B k-slot (q, j) <-> chunk pixel j<4: 4q+j, else 16+4q+(j-4) (the transposed-read order)
+  int tof0, tof1;
+  {
+    const int t0 = l16, t1 = 16 + l16;
+    tof0 = t0 < NT ? (t0 / S) * XW + (t0 % S) : -1;
+    tof1 = t1 < NT ? (t1 / S) * XW + (t1 % S) : -1;
+  }
+  f4 d0 = f4{0.f, 0.f, 0.f, 0.f}, d1 = d0;
+  uint16_t* gw = gch[wid];
+  const long long ntiles = (long long)N * tiles_h * tiles_w;
+  for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    const int tw = (int)(tt % tiles_w), th = (int)((tt / tiles_w) % tiles_h);
+    const int n = (int)(tt / ((long long)tiles_w * tiles_h));
+    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+    __syncthreads();
+    for (int i = tid; i < XH * XW; i += 256) {
+      const int yy = i / XW, xx = i - yy * XW;
+      const int h = h0 - pt + yy, w = w0 - pl + xx;
+      xs[i] = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? x[((long long)n * H + h) * W + w] : 0;
+    }
+    __syncthreads();
+    for (int c = 0; c < 8; ++c) {  // the wave's 4 rows x 64 columns in 32-pixel chunks
+      const int ry = wid * 4 + (c >> 1), cx0 = (c & 1) * 32;
+      const int h = h0 + ry;
+      {
+        const int px = lane >> 1, half = lane & 1, w = w0 + cx0 + px;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (h < H && w < W)
+          v = *reinterpret_cast<const u32x4*>(dy + (((long long)n * H + h) * W + w) * STEM_K + half * 8);
+        *reinterpret_cast<u32x4*>(gw + px * LDG + half * 8) = v;
+      }
+      const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (stem_lp)(reinterpret_cast<const __bf16*>(gw + (4 * grp + qq) * LDG + 4 * pp)));
+      const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (stem_lp)(reinterpret_cast<const __bf16*>(gw + (16 + 4 * grp + qq) * LDG + 4 * pp)));
+      const bf8 a = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const uint16_t* src = xs + ry * XW + cx0;
+      unsigned b0[8], b1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int px = j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4);
+        b0[j] = tof0 >= 0 ? src[px + tof0] : 0u;
+        b1[j] = tof1 >= 0 ? src[px + tof1] : 0u;
+      }
+      const uint4 B0 = uint4{b0[0] | (b0[1] << 16), b0[2] | (b0[3] << 16), b0[4] | (b0[5] << 16), b0[6] | (b0[7] << 16)};
+      const uint4 B1 = uint4{b1[0] | (b1[1] << 16), b1[2] | (b1[3] << 16), b1[4] | (b1[5] << 16), b1[6] | (b1[7] << 16)};
+      d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf8, B0), d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf8, B1), d1, 0, 0, 0);
+    }
+  }
+  // D lane: row k = q*4 + r, column t = l16 (+16)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[wid][q * 4 + r][l16] = d0[r];
+    red[wid][q * 4 + r][16 + l16] = d1[r];
+  }
+  __syncthreads();
+  for (int i = tid; i < STEM_K * NT; i += 256) {
+    const int k = i / NT, t = i - k * NT;
+    part[(long long)blockIdx.x * STEM_K * NT + i] =
+        ((double)red[0][k][t] + (double)red[1][k][t]) + ((double)red[2][k][t] + (double)red[3][k][t]);
+  }
+}
+
+static bool stem_mfma_on() {
+  static const bool off = getenv("ACFE_STEM_VALU") && getenv("ACFE_STEM_VALU")[0] == '1';
+  return !off;
+}
+
 ACFE_API int acfe_stem_blocks(int N, int H, int W) {
   const long long t = (long long)N * ((H + STEM_TH - 1) / STEM_TH) * ((W + STEM_TW - 1) / STEM_TW);
   return (int)(t < STEM_CAP ? t : STEM_CAP);
@@ -2333,7 +2569,14 @@ ACFE_API int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int 
   hipLaunchKernelGGL((k_stem_fwd<TI, TO, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x, N, H, W, \
                      pad_top, pad_left, weff, bias, (TO*)y, stats_partial, th, tw)
 #define SF(TI, TO) if (R == 5) SF1(TI, TO, 5); else SF1(TI, TO, 3)
-  if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16) SF(uint16_t, uint16_t);
+  if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16 && stem_mfma_on()) {
+    if (R == 5)
+      hipLaunchKernelGGL((k_stem_fwd_mfma<5, 5>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, N, H, W,
+                         pad_top, pad_left, weff, bias, (uint16_t*)y, stats_partial, th, tw);
+    else
+      hipLaunchKernelGGL((k_stem_fwd_mfma<3, 3>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, N, H, W,
+                         pad_top, pad_left, weff, bias, (uint16_t*)y, stats_partial, th, tw);
+  } else if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16) SF(uint16_t, uint16_t);
   else if (x_dtype == ACFE_DTYPE_BF16) SF(uint16_t, float);
   else if (y_dtype == ACFE_DTYPE_BF16) SF(float, uint16_t);
   else SF(float, float);
@@ -2351,7 +2594,15 @@ ACFE_API int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, 
   hipLaunchKernelGGL((k_stem_dgrad<TG, TO, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TG*)dy, N, H, \
                      W, pad_top, pad_left, weff, (TO*)dx, th, tw)
 #define SD(TG, TO) if (R == 5) SD1(TG, TO, 5); else SD1(TG, TO, 3)
-  if (dy_dtype == ACFE_DTYPE_BF16 && dx_dtype == ACFE_DTYPE_BF16) SD(uint16_t, uint16_t);
+  if (dy_dtype == ACFE_DTYPE_BF16 && dx_dtype == ACFE_DTYPE_BF16 && stem_mfma_on()) {
+    const int g2 = acfe_stem_blocks(N, H, W);
+    if (R == 5)
+      hipLaunchKernelGGL((k_stem_dgrad_mfma<5, 5>), dim3(g2), dim3(256), 0, strm(stream), (const uint16_t*)dy, N, H,
+                         W, pad_top, pad_left, weff, (uint16_t*)dx, th, tw);
+    else
+      hipLaunchKernelGGL((k_stem_dgrad_mfma<3, 3>), dim3(g2), dim3(256), 0, strm(stream), (const uint16_t*)dy, N, H,
+                         W, pad_top, pad_left, weff, (uint16_t*)dx, th, tw);
+  } else if (dy_dtype == ACFE_DTYPE_BF16 && dx_dtype == ACFE_DTYPE_BF16) SD(uint16_t, uint16_t);
   else if (dy_dtype == ACFE_DTYPE_BF16) SD(uint16_t, float);
   else if (dx_dtype == ACFE_DTYPE_BF16) SD(float, uint16_t);
   else SD(float, float);
@@ -2370,7 +2621,14 @@ ACFE_API int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_
   hipLaunchKernelGGL((k_stem_wgrad<TI, TG, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x,        \
                      (const TG*)dy, N, H, W, pad_top, pad_left, workspace, th, tw)
 #define SW(TI, TG) if (R == 5) SW1(TI, TG, 5); else SW1(TI, TG, 3)
-  if (x_dtype == ACFE_DTYPE_BF16 && dy_dtype == ACFE_DTYPE_BF16) SW(uint16_t, uint16_t);
+  if (x_dtype == ACFE_DTYPE_BF16 && dy_dtype == ACFE_DTYPE_BF16 && stem_mfma_on()) {
+    if (R == 5)
+      hipLaunchKernelGGL((k_stem_wgrad_mfma<5, 5>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x,
+                         (const uint16_t*)dy, N, H, W, pad_top, pad_left, workspace, th, tw);
+    else
+      hipLaunchKernelGGL((k_stem_wgrad_mfma<3, 3>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x,
+                         (const uint16_t*)dy, N, H, W, pad_top, pad_left, workspace, th, tw);
+  } else if (x_dtype == ACFE_DTYPE_BF16 && dy_dtype == ACFE_DTYPE_BF16) SW(uint16_t, uint16_t);
   else if (x_dtype == ACFE_DTYPE_BF16) SW(uint16_t, float);
   else if (dy_dtype == ACFE_DTYPE_BF16) SW(float, uint16_t);
   else SW(float, float);
