@@ -96,6 +96,14 @@ def maxpool_dropout_bn(x, kh, kw, bn: BatchNormalization, rate, relu=True):
                                   rate, relu=relu, eps=bn.eps, momentum=bn.momentum)
 
 
+def conv_maxpool_dropout_bn(conv: Conv2D, x, k, bn: BatchNormalization, rate, relu=True):
+    """bn(Dropout(rate)(MaxPool2D((k, k))(conv(x)))) (+ReLU) as one fused node
+    (the pooling runs in the conv epilogue when the kernel covers the shape)."""
+    return ops.conv_maxpool_dropout_bn(x, conv.weight, conv.bias, conv.strides, conv.padding, k, k, bn.gamma, bn.beta,
+                                       bn.moving_mean, bn.moving_variance, bn.training, rate, relu=relu, eps=bn.eps,
+                                       momentum=bn.momentum)
+
+
 class Dense(nn.Module):
     """tf.keras.layers.Dense(units) logits; the sigmoid of the reference's
     Dense(activation="sigmoid") is applied by predict()/the loss."""

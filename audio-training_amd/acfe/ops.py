@@ -20,6 +20,10 @@ F32, F64 = torch.float32, torch.float64
 # ACFE_FUSE=0 runs the fused nodes (conv/pool + dropout + BN, Add + statistics,
 # residual-gradient link) as their separate-op chains, for A/B checks.
 FUSE = os.environ.get("ACFE_FUSE", "1") != "0"
+# ACFE_UNPOOL=0: the pooled-conv node's backward materialises the 2x2 max-pool
+# backward and runs the plain dgrad / wgrad instead of expanding it in their
+# input staging (A/B switch).
+UNPOOL = os.environ.get("ACFE_UNPOOL", "1") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -661,6 +665,90 @@ def maxpool_dropout_bn(x, kh, kw, gamma, beta, mmean, mvar, training, rate=0.0, 
         seed = next_seed()
     conf = (kh, kw, float(rate), int(seed or 0), bool(training), bool(relu), float(eps), float(momentum))
     return _PoolDropBNFn.apply(x, gamma, beta, mmean, mvar, conf)
+
+
+def _conv_pool_ok(x, w, stride, padding, kh, kw) -> bool:
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    return (FUSE and x.dtype == torch.bfloat16 and stride == 1 and padding == "same" and (kh, kw) == (2, 2)
+            and x.is_contiguous() and x.data_ptr() % 16 == 0
+            and bool(lib.acfe_conv2d_pool_supported(N, H, W, C, K, R, S, dtype_code(x.dtype)))
+            and bool(lib.acfe_conv2d_pool_supported(N, H, W, K, C, R, S, dtype_code(x.dtype))))
+
+
+class _ConvPoolBNFn(torch.autograd.Function):
+    """BatchNormalization(+ReLU) of Dropout(MaxPool2D(2, 2)(Conv2D 3x3(x))) as one
+    node: pooling, dropout and the BN statistics run in the conv epilogue
+    (acfe_conv2d_fwd_pool stores only the pooled tensor and its argmax bytes);
+    the backward expands the pooled gradient inside the dgrad / wgrad input
+    staging (acfe_conv2d_{dgrad,wgrad}_unpool)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
+        pt, pl, rate, seed, training, relu, eps, momentum = conf
+        N, H, W, C = x.shape
+        K = w.shape[0]
+        dev = x.device
+        drop = (rate, seed) if training and rate > 0.0 else None
+        wp = pack_weights(w, x.dtype, False)
+        u = _empty((N, H // 2, W // 2, K), x.dtype, dev)
+        amax = _empty((N, H // 2, W // 2, K), torch.uint8, dev)
+        stats = _empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), F64, dev) if training else None
+        r_, s_ = drop if drop is not None else (0.0, 0)
+        with _Timed(w, "fwd"):
+            call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(u), ptr(amax),
+                 float(r_), int(s_), ptr(stats), dtype_code(x.dtype), stream())
+        y, saved = _bn_fwd(u, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, u.dtype)
+        ctx.save_for_backward(x, w, u, amax, *saved)
+        ctx.conf, ctx.drop, ctx.has_b = conf, drop, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, u, amax, *saved = ctx.saved_tensors
+        pt, pl, rate, seed, training, relu, eps, momentum = ctx.conf
+        N, H, W, C = x.shape
+        K = w.shape[0]
+        dev, s = x.device, stream()
+        g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop)
+        if not UNPOOL:  # materialise the pool backward, then the plain dgrad / wgrad
+            dfull = _maxpool_bwd(amax, g, (N, H, W, K), 2, 2, None)
+            dx, dw, db = _conv_bwd(x, w, dfull, 1, pt, pl, H, W, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                   ctx.has_b and ctx.needs_input_grad[2])
+            return dx, dw, db, dgamma, dbeta, None, None, None
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wf = pack_weights(w, x.dtype, True)
+            dx = _empty(x.shape, x.dtype, dev)
+            with _Timed(w, "dgrad"):
+                call("acfe_conv2d_dgrad_unpool", ptr(g), ptr(amax), N, H, W, K, ptr(wf), C, pt, pl, ptr(dx),
+                     dtype_code(x.dtype), s)
+        if ctx.needs_input_grad[1]:
+            dw = _empty(w.shape, F32, dev)
+            ws = _empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), F32, dev)
+            with _Timed(w, "wgrad"):
+                call("acfe_conv2d_wgrad_unpool", ptr(x), N, H, W, C, ptr(g), ptr(amax), K, pt, pl, ptr(dw), 0.0,
+                     dtype_code(x.dtype), ptr(ws), s)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = channel_sum(g, K)  # the pool backward scatters: sum of the pooled gradient
+        return dx, dw, db, dgamma, dbeta, None, None, None
+
+
+def conv_maxpool_dropout_bn(x, w, b, stride, padding, kh, kw, gamma, beta, mmean, mvar, training, rate=0.0,
+                            seed=None, relu=True, eps=1e-3, momentum=0.99):
+    """BN(Dropout(MaxPool2D((kh, kw))(Conv2D(x)))) (+ReLU): one node with the
+    pooling in the conv epilogue when the kernel covers the shape, else the
+    conv followed by maxpool_dropout_bn."""
+    if not _conv_pool_ok(x, w, stride, padding, kh, kw):
+        y, _ = conv2d(x, w, b, stride, padding)
+        return maxpool_dropout_bn(y, kh, kw, gamma, beta, mmean, mvar, training, rate, seed, relu, eps, momentum)
+    if training and rate > 0.0 and seed is None:
+        seed = next_seed()
+    K, R, S, _ = w.shape
+    _, pt = same_padding(x.shape[1], R, 1)
+    _, pl = same_padding(x.shape[2], S, 1)
+    conf = (pt, pl, float(rate), int(seed or 0), bool(training), bool(relu), float(eps), float(momentum))
+    return _ConvPoolBNFn.apply(x, w, b, gamma, beta, mmean, mvar, conf)
 
 
 class _AvgPoolFn(torch.autograd.Function):

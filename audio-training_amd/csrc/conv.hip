@@ -87,6 +87,18 @@ __device__ __forceinline__ void mma(f4& acc, const uint4& a, const uint4& b, flo
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
 }
+// 2x2 max-pool backward on the fly: 8 bf16 of the pooled gradient and their 8
+// argmax bytes -> the values that land on tap `pos` ((row & 1) * 2 + (col & 1)) of
+// the window, zeros elsewhere (acfe_maxpool2d_bwd_argmax's scatter, gathered).
+__device__ __forceinline__ u32x4 unpool_mask(uint2 a, unsigned pos) {
+  u32x4 m;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const unsigned w = d < 2 ? a.x : a.y, sh = (d & 1) * 16;
+    m[d] = (((w >> sh) & 0xffu) == pos ? 0xFFFFu : 0u) | (((w >> (sh + 8)) & 0xffu) == pos ? 0xFFFF0000u : 0u);
+  }
+  return m;
+}
 __device__ __forceinline__ uint16_t cvt_out(float v, uint16_t) { return f2bf(v); }
 __device__ __forceinline__ float cvt_out(float v, float) { return v; }
 __device__ __forceinline__ float to_f(uint16_t v) { return bf2f(v); }
@@ -841,11 +853,18 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 // with the k & 7 XOR swizzle.  Operands swapped (weights x pixels) so the
 // epilogue is k_conv_fwd_p's: 8-byte channel quads straight from registers,
 // bias from LDS, fused Dropout, DPP-butterfly BatchNormalization sums.
-template <int KB, int TR>
+// PM (pooling mode): 0 plain; 1 = the output feeds MaxPool2D(2, 2) -> Dropout:
+// the epilogue pools row pairs x column pairs (waves own 16-column strips of
+// all TR rows), stores only the pooled values, their first-maximum argmax byte
+// (amax) and their BN statistics; 2 = dgrad whose dY is the 2x2 max-pool
+// backward of X = the pooled gradient with argmax bytes amax (expanded while
+// staging, the full-resolution dY is never stored).
+template <int KB, int TR, int PM>
 __global__ void __launch_bounds__(512, 1)
 k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
                const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
-               int tiles_w, int ntiles, int srows) {
+               int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
+  static_assert(PM != 1 || TR % 2 == 0, "2x2 pooling needs row pairs");
   using T = uint16_t;
   constexpr int SEGW = 64, HWX = SEGW + 2, XRB = 144;           // pixels per row, halo row bytes
   constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
@@ -877,6 +896,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 
   // ---- global -> register staging of step t (tile, chunk, filter row)
   u32x4 rx[XPT], rw[WDMA ? 1 : WPT];
+  // PM 2: argmax bytes and window taps of the staged granules, applied at the
+  // LDS store (after the MFMAs) so the loads stay in flight during the step
+  uint2 ra[PM == 2 ? XPT : 1];
+  unsigned rpos = 0;
   // WDMA: piece j of this wave = 8 weight rows (s*KB + k) of 128 B, granule
   // slot (lane & 7) holds global granule slot ^ (row & 7) (source-side swizzle)
   constexpr int WPW = WG / 64 / 8;  // pieces per wave per step
@@ -909,8 +932,17 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       const int row = idx / (HWX * 8), r2 = idx - row * (HWX * 8), hp = r2 >> 3, gr = r2 & 7;
       const int hin = h0 + row + r - g.pt, win = w0 + hp - g.pl;
       const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
-      rx[i] = *reinterpret_cast<const u32x4*>(
-          ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + gr * 8 : zp);
+      if constexpr (PM == 2) {
+        const long long e =
+            (((long long)n * (g.H >> 1) + (hin >> 1)) * (g.W >> 1) + (win >> 1)) * g.C + cc * 64 + gr * 8;
+        rx[i] = *reinterpret_cast<const u32x4*>(ok ? X + e : zp);
+        ra[i] = *reinterpret_cast<const uint2*>(ok ? amax + e : reinterpret_cast<const uint8_t*>(zp));
+        if (i == 0) rpos = 0;
+        rpos |= (unsigned)(((hin & 1) << 1) | (win & 1)) << (2 * i);
+      } else {
+        rx[i] = *reinterpret_cast<const u32x4*>(
+            ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + gr * 8 : zp);
+      }
     }
     if constexpr (!WDMA) {
 #pragma unroll
@@ -928,7 +960,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + 512 * i;
       const int row = idx >> 3, gr = idx & 7;  // row = halo row * HWX + pixel
-      if (idx < XG) *reinterpret_cast<u32x4*>(Xl + row * XRB + gr * 16) = rx[i];
+      if constexpr (PM == 2) {
+        if (idx < XG)
+          *reinterpret_cast<u32x4*>(Xl + row * XRB + gr * 16) = rx[i] & unpool_mask(ra[i], (rpos >> (2 * i)) & 3u);
+      } else {
+        if (idx < XG) *reinterpret_cast<u32x4*>(Xl + row * XRB + gr * 16) = rx[i];
+      }
     }
     if constexpr (!WDMA) {
 #pragma unroll
@@ -949,7 +986,9 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   int xoff[FM];
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm) {
-    const int p = wp * (TR * 16) + fm * 16;
+    // PM 1: wave wp owns columns wp*16.. of every row (fragment fm = row fm) so
+    // each lane holds both rows of its 2x2 windows
+    const int p = PM == 1 ? fm * SEGW + wp * 16 : wp * (TR * 16) + fm * 16;
     xoff[fm] = ((p / SEGW) * HWX + (p % SEGW) + l16) * XRB + (lane >> 4) * 16;
   }
   int woff[FN];
@@ -961,8 +1000,54 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     float sv[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) sv[i] = 0.f;
+    if constexpr (PM == 1) {
+      // 2x2 windows: rows (2i, 2i+1) in this lane's fragments, columns (l16, l16^1)
+      // in the neighbouring lane; window order (0,0),(0,1),(1,0),(1,1), first max wins
+      const int P2 = g.P >> 1, Q2 = g.Q >> 1;
+      const int wq = (wb * SEGW + wp * 16 + l16) >> 1;
+      const bool evn = (l16 & 1) == 0;
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
+      for (int i = 0; i < TR / 2; ++i) {
+        const int hp2 = ((hb * TR) >> 1) + i;
+        const bool inb = evn && hp2 < P2 && wq < Q2;
+        const long long pp = ((long long)n * P2 + hp2) * Q2 + wq;
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
+          uint16_t hv[4];
+          unsigned amb = 0;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const float a0 = bf2f(f2bf(acc[2 * i][fn][jj] + sbias[c + jj]));
+            const float a2 = bf2f(f2bf(acc[2 * i + 1][fn][jj] + sbias[c + jj]));
+            const float a1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a0), 0xB1, 0xF, 0xF, false));
+            const float a3 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a2), 0xB1, 0xF, 0xF, false));
+            float m = -INFINITY;
+            unsigned am = 0;
+            if (a0 > m) m = a0, am = 0;
+            if (a1 > m) m = a1, am = 1;
+            if (a2 > m) m = a2, am = 2;
+            if (a3 > m) m = a3, am = 3;
+            if (g.drop.on) m = drop_apply<T>(g.drop, (uint64_t)pp * g.K + c + jj, m);
+            hv[jj] = f2bf(m);
+            const float f = inb ? bf2f(hv[jj]) : 0.f;
+            sv[fn * 4 + jj] += f;
+            sv[FN * 4 + fn * 4 + jj] += f * f;
+            amb |= am << (8 * jj);
+          }
+          if (inb) {
+            uint2 v;
+            v.x = (unsigned)hv[0] | ((unsigned)hv[1] << 16);
+            v.y = (unsigned)hv[2] | ((unsigned)hv[3] << 16);
+            *reinterpret_cast<uint2*>(Y + pp * g.ldy + c) = v;
+            *reinterpret_cast<unsigned*>(amax + pp * g.K + c) = amb;
+          }
+          acc[2 * i][fn] = acc[2 * i + 1][fn] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+#pragma unroll
+    for (int fm = 0; fm < (PM == 1 ? 0 : FM); ++fm) {
       const int p = wp * (TR * 16) + fm * 16;
       const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
       const bool inb = h < g.P && w < g.Q;
@@ -1555,10 +1640,12 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 // LDS images are pixel-major with rows padded to 160 / 288 B so the
 // ds_read_b64_tr_b16 fragment reads (8 pixel rows x 32 B per half-wave) hit 64
 // distinct banks; register-staged double buffer, one barrier per step.
-template <int KB>
+// UNP: dY is the 2x2 max-pool backward of the pooled gradient dY (argmax bytes
+// amax), expanded while staging.
+template <int KB, bool UNP>
 __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
-                float* __restrict__ ws, int nchunk, int nseg, int segs_per_split) {
+                float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
   constexpr int SEGW = 64, HW = SEGW + 2;
   constexpr int LDD = KB + 16, LDX = 64 + 16;
   constexpr int DS = SEGW * LDD, XS = 3 * HW * LDX;
@@ -1577,6 +1664,8 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   const T16* zp = reinterpret_cast<const T16*>(g_zero_page);
 
   u32x4 rd[DPT], rx[XPT];
+  uint2 rda[UNP ? DPT : 1];  // UNP: argmax bytes + window taps, applied at the LDS store
+  unsigned dpos = 0;
   auto gload = [&](int sg) __attribute__((always_inline)) {
     const int n = sg / (g.P * QS), rem = sg - n * (g.P * QS);
     const int h = rem / QS, w0 = (rem - h * QS) * SEGW;
@@ -1585,7 +1674,16 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     for (int i = 0; i < DPT; ++i) {
       const int idx = tid + 512 * i;
       const int px = idx / DGR, cg = idx - px * DGR;
-      rd[i] = *reinterpret_cast<const u32x4*>(idx < DG ? dyrow + px * g.K + cg * 8 : zp);
+      if constexpr (UNP) {
+        const int w = w0 + px;
+        const long long e = (((long long)n * (g.P >> 1) + (h >> 1)) * (g.Q >> 1) + (w >> 1)) * g.K + cg * 8;
+        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG ? dY + e : zp);
+        rda[i] = *reinterpret_cast<const uint2*>(idx < DG ? amax + e : reinterpret_cast<const uint8_t*>(zp));
+        if (i == 0) dpos = 0;
+        dpos |= (unsigned)(((h & 1) << 1) | (w & 1)) << (2 * i);
+      } else {
+        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG ? dyrow + px * g.K + cg * 8 : zp);
+      }
     }
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
@@ -1604,7 +1702,12 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     for (int i = 0; i < DPT; ++i) {
       const int idx = tid + 512 * i;
       const int px = idx / DGR, cg = idx - px * DGR;
-      if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i];
+      if constexpr (UNP) {
+        if (idx < DG)
+          *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i] & unpool_mask(rda[i], (dpos >> (2 * i)) & 3u);
+      } else {
+        if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
@@ -1762,11 +1865,13 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
         if (gp > nt) gp = (int)nt;
         if (gp >= 64) gp &= ~7;
         if (tr == 3)
-          hipLaunchKernelGGL((k_conv3x3_rows<BN, 3>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
-                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
+          hipLaunchKernelGGL((k_conv3x3_rows<BN, 3, 0>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m,
+                             nullptr);
         else
-          hipLaunchKernelGGL((k_conv3x3_rows<BN, 6>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
-                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
+          hipLaunchKernelGGL((k_conv3x3_rows<BN, 6, 0>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m,
+                             nullptr);
         return launch_rc("acfe_conv2d_fwd");
       }
     }
@@ -1977,6 +2082,31 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
   return launch_rc("acfe_conv2d_wgrad");
 }
 
+// k_wgrad3x3_halo launch (3x3 stride 1, C % 64 == 0, K in {64, 128}, Q % 64 ==
+// 0): split count within the planned workspace (`splits`), returned in *used.
+static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
+                             long long splits, hipStream_t s, int* used) {
+  const int nchunk = g.C / 64, nseg = (int)((long long)g.N * g.P * (g.Q / 64));
+  int sp = 256 / nchunk;
+  if (sp > splits) sp = (int)splits;
+  sp &= ~7;
+  if (sp < 8) sp = 8;
+  if (sp > splits) sp = (int)splits;  // splits is a multiple of 8 (wgrad_plan)
+  const int per = (nseg + sp - 1) / sp;
+  const dim3 gr(nchunk * sp);
+#define WH(KB_, U_)                                                                                              \
+  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, U_>), gr, dim3(512), 0, s, g, (const uint16_t*)x, (const uint16_t*)dy, \
+                     ws, nchunk, nseg, per, amax)
+  if (g.K == 128) {
+    if (amax) WH(128, true); else WH(128, false);
+  } else {
+    if (amax) WH(64, true); else WH(64, false);
+  }
+#undef WH
+  *used = sp;
+  return launch_rc(amax ? "acfe_conv2d_wgrad_unpool" : "acfe_conv2d_wgrad(halo)");
+}
+
 // dW[k][r][s][c] (fp32, KRSC) = sum over pixels.  beta: dW = beta*dW + grad.
 ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy, int K, int R, int S,
                                int stride, int pad_top, int pad_left, int P, int Q, float* dw, float beta,
@@ -1996,23 +2126,10 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 && C % 64 == 0 && (K == 64 || K == 128) &&
       Q % 64 == 0 && (long long)N * P * (Q / 64) < (1ll << 31) && !no_halo_w) {
     // halo-staged kernel; its split count stays within the planned workspace
-    const int nchunk = C / 64, nseg = (int)((long long)N * P * (Q / 64));
-    int sp = 256 / nchunk;
-    if (sp > splits) sp = (int)splits;
-    sp &= ~7;
-    if (sp < 8) sp = 8;
-    if (sp > splits) sp = (int)splits;  // splits is a multiple of 8 (wgrad_plan)
-    const int per = (nseg + sp - 1) / sp;
-    const dim3 gr(nchunk * sp);
-    if (K == 128)
-      hipLaunchKernelGGL((k_wgrad3x3_halo<128>), gr, dim3(512), 0, strm(stream), g, (const uint16_t*)x,
-                         (const uint16_t*)dy, workspace, nchunk, nseg, per);
-    else
-      hipLaunchKernelGGL((k_wgrad3x3_halo<64>), gr, dim3(512), 0, strm(stream), g, (const uint16_t*)x,
-                         (const uint16_t*)dy, workspace, nchunk, nseg, per);
-    rc = launch_rc("acfe_conv2d_wgrad(halo)");
+    int used = 0;
+    rc = wgrad_halo_launch(g, x, dy, nullptr, workspace, splits, strm(stream), &used);
     if (rc) return rc;
-    splits = sp;
+    splits = used;
   } else if (dtype == ACFE_DTYPE_BF16) {
     if (bmw == 32) rc = launch_wgrad_t<uint16_t, 32>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
     else if (bmw == 64) rc = launch_wgrad_t<uint16_t, 64>(g, x, dy, workspace, chunk, (int)splits, strm(stream));
@@ -2029,6 +2146,86 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, strm(stream), workspace, (int)splits, n, beta, dw);
   return launch_rc("acfe_conv2d_wgrad(reduce)");
+}
+
+// ------------------------------------------------------------------ conv + 2x2 max-pool
+// Conv2D 3x3 "same" stride 1 followed by MaxPool2D(2, 2) -> Dropout
+// (resnet/wr_resnet_bird.py:139-148: res{s}b0_branch21 -> pooling -> dropout):
+// k_conv3x3_rows<K, 6, 1> pools in its epilogue, so the full-resolution conv
+// output is never written; the backward reads the pooled gradient + argmax
+// bytes and expands them in its input staging (dgrad: k_conv3x3_rows<C, 6, 2>,
+// wgrad: k_wgrad3x3_halo<K, true>).
+template <int KB, int PM>
+static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+                       int srows, uint8_t* amax, hipStream_t s, const char* what) {
+  constexpr int TR = 6;
+  const int tiles_h = (g.P + TR - 1) / TR, tiles_w = g.Q / 64;
+  const long long nt = (long long)g.N * tiles_h * tiles_w;
+  int gp = 256;
+  if (gp > nt) gp = (int)nt;
+  if (gp >= 64) gp &= ~7;
+  hipLaunchKernelGGL((k_conv3x3_rows<KB, TR, PM>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                     (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
+  return launch_rc(what);
+}
+
+ACFE_API int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {
+  static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS") || getenv_flag("ACFE_CONV_NO_POOL");
+  return !no_rows && dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
+         (K == 64 || K == 128) && W > 0 && W % 64 == 0 && H >= 2 && H % 2 == 0 &&
+         (long long)N * ((H + 5) / 6) * (W / 64) < (1ll << 31) && (long long)N * H * (W / 64) < (1ll << 31);
+}
+
+ACFE_API int acfe_conv2d_fwd_pool(const void* x, int N, int H, int W, int C, const void* wpacked, int K,
+                                  int pad_top, int pad_left, const float* bias, void* y, uint8_t* argmax,
+                                  float drop_rate, unsigned long long seed, double* stats_partial, int dtype,
+                                  void* stream) {
+  if (!x || !wpacked || !y || !argmax || drop_rate < 0.f || drop_rate >= 1.f ||
+      !acfe_conv2d_pool_supported(N, H, W, C, K, 3, 3, dtype) || ((uintptr_t)y & 7) || ((uintptr_t)argmax & 3))
+    return ACFE_E_INVAL;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
+  g.drop = make_drop(drop_rate, seed);
+  const int srows = grid_m_for(g.M, 1);  // == acfe_conv2d_stats_rows(N*H*W, K)
+  if (K == 128)
+    return launch_rows<128, 1>(g, x, wpacked, bias, y, stats_partial, srows, argmax, strm(stream),
+                               "acfe_conv2d_fwd_pool");
+  return launch_rows<64, 1>(g, x, wpacked, bias, y, stats_partial, srows, argmax, strm(stream),
+                            "acfe_conv2d_fwd_pool");
+}
+
+ACFE_API int acfe_conv2d_dgrad_unpool(const void* dyp, const uint8_t* argmax, int N, int P, int Q, int K,
+                                      const void* wflip, int C, int pad_top, int pad_left, void* dx, int dtype,
+                                      void* stream) {
+  if (!dyp || !argmax || !wflip || !dx || !acfe_conv2d_pool_supported(N, P, Q, K, C, 3, 3, dtype) ||
+      ((uintptr_t)dyp & 15) || ((uintptr_t)argmax & 7))
+    return ACFE_E_INVAL;
+  // stride-1 conv of the (virtual) unpooled dY with the flipped weights: K -> C channels
+  ConvGeom g = make_geom(N, P, Q, K, C, 3, 3, 1, 2 - pad_top, 2 - pad_left, P, Q, 64, C);
+  if (C == 128)
+    return launch_rows<128, 2>(g, dyp, wflip, nullptr, dx, nullptr, 0, const_cast<uint8_t*>(argmax),
+                               strm(stream), "acfe_conv2d_dgrad_unpool");
+  return launch_rows<64, 2>(g, dyp, wflip, nullptr, dx, nullptr, 0, const_cast<uint8_t*>(argmax), strm(stream),
+                            "acfe_conv2d_dgrad_unpool");
+}
+
+ACFE_API int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C, const void* dyp,
+                                      const uint8_t* argmax, int K, int pad_top, int pad_left, float* dw,
+                                      float beta, int dtype, float* workspace, void* stream) {
+  if (!x || !dyp || !argmax || !dw || !workspace || !acfe_conv2d_pool_supported(N, H, W, C, K, 3, 3, dtype) ||
+      ((uintptr_t)dyp & 15) || ((uintptr_t)argmax & 7))
+    return ACFE_E_INVAL;
+  long long splits, chunk;
+  wgrad_plan((long long)N * H * W, 9 * C, K, &splits, &chunk);
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, 128);
+  g.ldy = K;
+  int used = 0;
+  int rc = wgrad_halo_launch(g, x, dyp, argmax, workspace, splits, strm(stream), &used);
+  if (rc) return rc;
+  const long long n = (long long)K * 9 * C;
+  int grid = cdiv((n + 3) / 4, 256);
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, strm(stream), workspace, used, n, beta, dw);
+  return launch_rc("acfe_conv2d_wgrad_unpool(reduce)");
 }
 
 // ------------------------------------------------------------------ stem (C = 1)

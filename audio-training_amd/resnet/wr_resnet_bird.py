@@ -20,7 +20,7 @@ from torch import nn
 
 from acfe import ops
 from acfe.layers import (BatchNormalization, Conv2D, Dense, StemConv2D, conv_bn, conv_dropout_bn,
-                         maxpool_dropout_bn)
+                         conv_maxpool_dropout_bn)
 
 
 class BasicBlock(nn.Module):
@@ -58,8 +58,7 @@ class BasicBlock(nn.Module):
         if self.stride > 1:
             y = self.bn2a0(y, relu=True, stats=x_stats, link=link)
             y = conv_bn(self.conv2a0, self.bn2a, y, relu=True)
-            y = self.conv21(y)
-            y = maxpool_dropout_bn(y, self.stride, self.stride, self.bn2b, self.dropout)
+            y = conv_maxpool_dropout_bn(self.conv21, y, self.stride, self.bn2b, self.dropout)
         else:
             y = self.bn2a(y, relu=True, stats=x_stats, link=link)
             y = conv_dropout_bn(self.conv21, self.bn2b, y, self.dropout)

@@ -224,6 +224,27 @@ int acfe_bn_bwd_apply_ex(const void* dy, int dy_dtype, const void* x, int x_dtyp
                          float drop_rate, unsigned long long seed, void* dx, int dx_dtype, double* sum_partial,
                          void* stream);
 
+/* Conv2D 3x3 "same" stride 1 -> MaxPool2D(2, 2) -> Dropout(rate, seed) with the
+ * full-resolution conv output never stored (res{s}b0_branch21 -> pooling ->
+ * dropout of resnet/wr_resnet_bird.py:139-148).  Supported shapes:
+ * acfe_conv2d_pool_supported (bf16, C % 64 == 0, K in {64, 128}, W % 64 == 0,
+ * H even).  acfe_conv2d_fwd_pool writes y [N][H/2][W/2][K], argmax bytes of the
+ * same shape (first maximum, acfe_maxpool2d_fused's convention) and the BN
+ * statistics slab of y (rows = acfe_conv2d_stats_rows(N*H*W, K), nullable).
+ * The backward takes the gradient of the pooled, dropped-out values with the
+ * dropout backward already applied (e.g. acfe_bn_bwd_apply_dropout):
+ * acfe_conv2d_dgrad_unpool (wflip = acfe_conv2d_pack_weights(flip=1)) and
+ * acfe_conv2d_wgrad_unpool (workspace as acfe_conv2d_wgrad, R = S = 3). */
+int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R, int S, int dtype);
+int acfe_conv2d_fwd_pool(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                         int pad_left, const float* bias, void* y, uint8_t* argmax, float drop_rate,
+                         unsigned long long seed, double* stats_partial, int dtype, void* stream);
+int acfe_conv2d_dgrad_unpool(const void* dy_pooled, const uint8_t* argmax, int N, int P, int Q, int K,
+                             const void* wflip, int C, int pad_top, int pad_left, void* dx, int dtype, void* stream);
+int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C, const void* dy_pooled, const uint8_t* argmax,
+                             int K, int pad_top, int pad_left, float* dw, float beta, int dtype, float* workspace,
+                             void* stream);
+
 /* Conv2D(1x1, 16 -> K in {64, 128}, bias) -> BatchNormalization -> (ReLU) as one
  * node whose conv output A = W x + b is never stored (csrc/c1bn.hip;
  * res{s}b0_branch2a0 + bn{s}b0_branch2a of resnet/wr_resnet_bird.py:121-131).

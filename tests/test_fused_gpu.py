@@ -316,3 +316,79 @@ def test_conv1x1_bn_node(env, cuda, shape, K, training):
         assert (outs[1][-1].double().cpu() - ref[-1]).norm().item() < 1e-3 * ref[2].norm().item()
     else:
         assert rel(outs[1][-1], ref[-1]) <= 1.25 * rel(outs[0][-1], ref[-1]) + 1e-3
+
+
+@pytest.mark.parametrize("K,C", [(128, 128), (64, 64), (64, 128)])
+def test_conv_pool_kernels(env, cuda, K, C):
+    """Pooled-epilogue conv and its unpooling backward against the separate
+    kernels, bit-exact: acfe_conv2d_fwd_pool == acfe_conv2d_fwd ->
+    acfe_maxpool2d_fused (values, argmax bytes; statistics to 1e-6),
+    acfe_conv2d_{dgrad,wgrad}_unpool == acfe_maxpool2d_bwd_argmax ->
+    acfe_conv2d_{dgrad,wgrad}.  H = 14: the last 6-row tile is partly outside."""
+    ops, call, lib, ptr, stream = env
+    N, H, W = 2, 14, 128
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(21)
+    x = torch.randn((N, H, W, C), generator=g).to(bf).to(cuda)
+    w = (torch.randn((K, 3, 3, C), generator=g) * 0.05).to(cuda)
+    b = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    assert lib.acfe_conv2d_pool_supported(N, H, W, C, K, 3, 3, 1) and lib.acfe_conv2d_pool_supported(N, H, W, K, C, 3,
+                                                                                                        3, 1)
+    wp = ops.pack_weights(w, bf, False)
+    y0 = torch.empty((N, H, W, K), dtype=bf, device=cuda)
+    call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b), ptr(y0), 1, None, stream())
+    P, Q = H // 2, W // 2
+    yp0 = torch.empty((N, P, Q, K), dtype=bf, device=cuda)
+    am0 = torch.empty((N, P, Q, K), dtype=torch.uint8, device=cuda)
+    st0 = torch.empty((lib.acfe_reduce_blocks(N * P * Q), 2, K), dtype=torch.float64, device=cuda)
+    call("acfe_maxpool2d_fused", ptr(y0), N, H, W, K, 2, 2, ptr(yp0), ptr(am0), 0.1, 77, ptr(st0), 1, stream())
+    yp1, am1 = torch.empty_like(yp0), torch.empty_like(am0)
+    st1 = torch.empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), dtype=torch.float64, device=cuda)
+    call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(yp1), ptr(am1), 0.1, 77, ptr(st1),
+         1, stream())
+    assert torch.equal(yp1, yp0)
+    assert torch.equal(am1, am0)
+    torch.testing.assert_close(st1.sum(0)[:, :K], st0.sum(0), rtol=1e-6, atol=1e-4)
+    # backward from a pooled gradient
+    gp = torch.randn((N, P, Q, K), generator=g).to(bf).to(cuda)
+    dfull = torch.empty((N, H, W, K), dtype=bf, device=cuda)
+    call("acfe_maxpool2d_bwd_argmax", ptr(am0), ptr(gp), N, H, W, K, 2, 2, 0.0, 0, ptr(dfull), 1, stream())
+    wf = ops.pack_weights(w, bf, True)
+    dx0, dx1 = (torch.empty((N, H, W, C), dtype=bf, device=cuda) for _ in range(2))
+    call("acfe_conv2d_dgrad", ptr(dfull), N, H, W, K, ptr(wf), C, 3, 3, 1, 1, 1, H, W, ptr(dx0), 1, None, stream())
+    call("acfe_conv2d_dgrad_unpool", ptr(gp), ptr(am0), N, H, W, K, ptr(wf), C, 1, 1, ptr(dx1), 1, stream())
+    assert torch.equal(dx1, dx0)
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+    dw0, dw1 = (torch.empty((K, 3, 3, C), device=cuda) for _ in range(2))
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dfull), K, 3, 3, 1, 1, 1, H, W, ptr(dw0), 0.0, 1, ptr(ws),
+         stream())
+    call("acfe_conv2d_wgrad_unpool", ptr(x), N, H, W, C, ptr(gp), ptr(am0), K, 1, 1, ptr(dw1), 0.0, 1, ptr(ws),
+         stream())
+    assert torch.equal(dw1, dw0)
+
+
+def test_conv_maxpool_dropout_bn_node(env, cuda):
+    """The pooled-epilogue node against conv2d -> maxpool_dropout_bn (same
+    dropout seed): outputs and every gradient within rel-L2 2e-3."""
+    ops = env[0]
+    N, H, W, C, K = 3, 16, 64, 64, 64
+    g = torch.Generator(device="cpu").manual_seed(22)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((K, 3, 3, C), generator=g) * 0.05).to(cuda)
+    b0 = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    gy = torch.randn((N, H // 2, W // 2, K), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    for fused in (False, True):
+        x = x0.clone().requires_grad_(True)
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        gamma, beta, mm, mv = _bn_params(K, cuda, 23)
+        if fused:
+            assert ops._conv_pool_ok(x, w, 1, "same", 2, 2)
+            y = ops.conv_maxpool_dropout_bn(x, w, b, 1, "same", 2, 2, gamma, beta, mm, mv, True, 0.1, seed=99)
+        else:
+            u, _ = ops.conv2d(x, w, b, 1)
+            y = ops.maxpool_dropout_bn(u, 2, 2, gamma, beta, mm, mv, True, 0.1, seed=99)
+        y.backward(gy)
+        outs.append([y, x.grad, w.grad, b.grad, gamma.grad, beta.grad, mm, mv])
+    for i, (a, r) in enumerate(zip(outs[1], outs[0])):
+        assert rel(a, r) < 2e-3, (i, rel(a, r))
