@@ -303,8 +303,10 @@ def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, o
     return y, (scale, shift, mean, invstd)
 
 
-def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None):
-    """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given."""
+def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False):
+    """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given;
+    mask_in: x is a ReLU output (ops.add), its backward [x > 0] is applied to dx here
+    and dx is marked so that ops.add's backward skips its own pass."""
     scale, shift, mean, invstd = saved
     C = x.shape[-1]
     rows = x.numel() // C
@@ -330,11 +332,14 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None):
     # per-channel sums of dx ride along (bias gradient of the conv producing x)
     want_sum = FUSE and _sums_ok(dx) and _sums_ok(dy) and _sums_ok(x) and (add is None or _sums_ok(add))
     sums = _empty((nrows, 2, C), F64, dev) if want_sum else None
+    flags = int(relu) | (2 if mask_in else 0)
     call("acfe_bn_bwd_apply_ex", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
-         ptr(shift), int(relu), ptr(coef), ptr(add), float(rate), int(seed), ptr(dx), dtype_code(x.dtype), ptr(sums),
+         ptr(shift), flags, ptr(coef), ptr(add), float(rate), int(seed), ptr(dx), dtype_code(x.dtype), ptr(sums),
          s)
     if want_sum:
         _attach_sum(dx, sums, rows)
+    if mask_in:
+        dx._acfe_relu_masked = True
     return dx, dgamma, dbeta
 
 
@@ -344,6 +349,7 @@ class _BNFn(torch.autograd.Function):
         y, saved = _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype)
         ctx.save_for_backward(x, *saved)
         ctx.conf = (relu, training, link)
+        ctx.mask_in = FUSE and getattr(x, "_acfe_relu_out", False)
         return y
 
     @staticmethod
@@ -351,7 +357,7 @@ class _BNFn(torch.autograd.Function):
         x, *saved = ctx.saved_tensors
         relu, training, link = ctx.conf
         add = link.take() if link is not None else None
-        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add)
+        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
@@ -496,13 +502,14 @@ class _AddFn(torch.autograd.Function):
         ctx.relu, ctx.link = relu, link
         if relu:
             ctx.save_for_backward(z)
+            z._acfe_relu_out = True  # a BatchNormalization reading z folds in the ReLU backward
         ctx.mark_non_differentiable(stats)
         return z, stats
 
     @staticmethod
     def backward(ctx, g, _gs):
         g = g.contiguous()
-        if ctx.relu:
+        if ctx.relu and not getattr(g, "_acfe_relu_masked", False):
             (z,) = ctx.saved_tensors
             d = torch.empty_like(g)
             C = g.shape[-1]

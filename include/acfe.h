@@ -215,6 +215,9 @@ int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, 
 int acfe_bn_bwd_apply_dropout(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                               const float* scale, const float* shift, int relu, const float* coef,
                               float drop_rate, unsigned long long seed, void* dx, int dx_dtype, void* stream);
+/* relu flags of acfe_bn_bwd_apply*: bit 0 = the BN's own ReLU (mask x*scale+shift > 0),
+ * bit 1 = x itself is a ReLU output: dx (after the `add`) is multiplied by [x > 0],
+ * the upstream ReLU's backward folded in. */
 /* General form: residual `add` (nullable), Dropout backward (drop_rate > 0,
  * then add must be NULL), and per-channel sums of the stored dx into
  * sum_partial (nullable; slab as acfe_add_stats) -- the bias gradient of the
