@@ -265,6 +265,7 @@ class ResidualLink:
 
     def __init__(self):
         self.grad = None
+        self.pool = None  # (pooled gradient, k) from an avg_pool_same(x, k, link=...) shortcut
 
     @staticmethod
     def make():
@@ -273,6 +274,10 @@ class ResidualLink:
     def take(self):
         g, self.grad = self.grad, None
         return g
+
+    def take_pool(self):
+        p, self.pool = self.pool, None
+        return p
 
 
 def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype):
@@ -303,7 +308,7 @@ def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, o
     return y, (scale, shift, mean, invstd)
 
 
-def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False):
+def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None):
     """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given;
     mask_in: x is a ReLU output (ops.add), its backward [x > 0] is applied to dx here
     and dx is marked so that ops.add's backward skips its own pass."""
@@ -333,6 +338,18 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False):
     want_sum = FUSE and _sums_ok(dx) and _sums_ok(dy) and _sums_ok(x) and (add is None or _sums_ok(add))
     sums = _empty((nrows, 2, C), F64, dev) if want_sum else None
     flags = int(relu) | (2 if mask_in else 0)
+    if pool is not None:  # shortcut AveragePooling2D(x) backward folded in
+        gp, k = pool
+        gp = gp.contiguous()
+        assert rate == 0.0 and add is None and gp.dtype == x.dtype
+        N, H, W, _ = x.shape
+        call("acfe_bn_bwd_apply_pool", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), N, H, W, C,
+             ptr(scale), ptr(shift), flags, ptr(coef), ptr(gp), int(k), ptr(dx), dtype_code(x.dtype), ptr(sums), s)
+        if want_sum:
+            _attach_sum(dx, sums, rows)
+        if mask_in:
+            dx._acfe_relu_masked = True
+        return dx, dgamma, dbeta
     call("acfe_bn_bwd_apply_ex", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
          ptr(shift), flags, ptr(coef), ptr(add), float(rate), int(seed), ptr(dx), dtype_code(x.dtype), ptr(sums),
          s)
@@ -356,8 +373,12 @@ class _BNFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, *saved = ctx.saved_tensors
         relu, training, link = ctx.conf
-        add = link.take() if link is not None else None
-        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in)
+        add = pool = None
+        if link is not None:
+            add, pool = link.take(), link.take_pool()
+            if add is None and pool is None:
+                raise RuntimeError("ResidualLink: the shortcut gradient was not delivered before this BN's backward")
+        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
@@ -760,24 +781,30 @@ def conv_maxpool_dropout_bn(x, w, b, stride, padding, kh, kw, gamma, beta, mmean
 
 class _AvgPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k):
+    def forward(ctx, x, k, link):
         N, H, W, C = x.shape
         y = _empty((N, -(-H // k), -(-W // k), C), x.dtype, x.device)
         call("acfe_avgpool2d", ptr(x), N, H, W, C, k, ptr(y), dtype_code(x.dtype), stream())
-        ctx.shape, ctx.k = x.shape, k
+        ctx.shape, ctx.k, ctx.link = x.shape, k, link
         return y
 
     @staticmethod
     def backward(ctx, g):
         N, H, W, C = ctx.shape
         g = g.contiguous()
+        if ctx.link is not None:  # the linked BN reading x adds the spread-out gradient itself
+            ctx.link.pool = (g, ctx.k)
+            return None, None, None
         dx = _empty(ctx.shape, g.dtype, g.device)
         call("acfe_avgpool2d_bwd", ptr(g), N, H, W, C, ctx.k, ptr(dx), dtype_code(g.dtype), stream())
-        return dx, None
+        return dx, None, None
 
 
-def avg_pool_same(x, k):
-    return _AvgPoolFn.apply(x, k)
+def avg_pool_same(x, k, link=None):
+    """AveragePooling2D(k, strides=k, "same"); with a ResidualLink the backward
+    hands the pooled gradient to the BN that reads x (acfe_bn_bwd_apply_pool)."""
+    ok = link is not None and x.dim() == 4 and x.shape[-1] % 8 == 0 and x.data_ptr() % 16 == 0
+    return _AvgPoolFn.apply(x, k, link if ok else None)
 
 
 class _AxisPoolFn(torch.autograd.Function):

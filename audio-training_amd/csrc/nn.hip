@@ -489,12 +489,21 @@ __global__ void k_bn_bwd_apply(const TG* __restrict__ dy, const TX* __restrict__
     st(dx, i, v);
   }
 }
+// Gradient of an AveragePooling2D(k, strides=k, "same") whose input is this
+// BN's input x, added on the fly (the pooled gradient g [N][P][Q][C] spread
+// over the window's in-bounds elements, as acfe_avgpool2d_bwd stores it).
+struct PoolAdd {
+  const void* g;
+  int H, W, k, P, Q, pt, pl;
+};
+
 template <typename TG, typename TX, typename TO>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy, const TX* __restrict__ x,
                                                        unsigned nvec, int C, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int relu,
                                                        const float* __restrict__ coef, const TO* __restrict__ add,
-                                                       Drop drop, TO* __restrict__ dx, double* __restrict__ sum_part) {
+                                                       Drop drop, TO* __restrict__ dx, double* __restrict__ sum_part,
+                                                       PoolAdd pa) {
   // dynamic LDS: [2][C] doubles (channel sums, when sum_part) then scale, shift, a, b, c
   extern __shared__ double smd[];
   double* red = smd;
@@ -519,12 +528,24 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
     ld8(dy + (size_t)v * 8, g);
     ld8(x + (size_t)v * 8, xv);
     if (add) ld8(add + (size_t)v * 8, o);
+    if (pa.g) {
+      const unsigned row = v / CV, t = row / (unsigned)pa.W;
+      const int w = (int)(row - t * (unsigned)pa.W), h = (int)(t % (unsigned)pa.H), nn = (int)(t / (unsigned)pa.H);
+      const int p = (h + pa.pt) / pa.k, q = (w + pa.pl) / pa.k;
+      const int h0 = max(p * pa.k - pa.pt, 0), h1 = min(p * pa.k - pa.pt + pa.k, pa.H);
+      const int w0 = max(q * pa.k - pa.pl, 0), w1 = min(q * pa.k - pa.pl + pa.k, pa.W);
+      const float inv = 1.0f / (float)((h1 - h0) * (w1 - w0));
+      ld8(reinterpret_cast<const TO*>(pa.g) + (((size_t)nn * pa.P + p) * pa.Q + q) * C + c0, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] *= inv;
+    }
+    const bool has_add = add || pa.g;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + j;
       const float gj = ((relu & 1) && !(xv[j] * sm[c] + sm[C + c] > 0.f)) ? 0.f : g[j];
       const float r = sm[2 * C + c] * gj + sm[3 * C + c] * xv[j] + sm[4 * C + c];
-      o[j] = add ? o[j] + r : r;
+      o[j] = has_add ? o[j] + r : r;
       if ((relu & 2) && !(xv[j] > 0.f)) o[j] = 0.f;  // x = ReLU output upstream: its backward
     }
     if (drop.on) {
@@ -546,10 +567,12 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
 
 static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                              const float* scale, const float* shift, int relu, const float* coef, const void* add,
-                             const Drop& d, void* dx, int dx_dtype, double* sum_part, void* stream) {
+                             const Drop& d, void* dx, int dx_dtype, double* sum_part, void* stream,
+                             PoolAdd pa = PoolAdd{nullptr, 0, 0, 0, 0, 0, 0, 0}) {
   if (!dy || !x || !scale || !shift || !coef || !dx || rows < 0 || C <= 0) return ACFE_E_INVAL;
   const long long n = rows * C;
   if (n == 0) return ACFE_OK;
+  if (pa.g && (!vec_ok(n, C, dy, x, pa.g, dx) || C > 2048 || add)) return ACFE_E_INVAL;
   if (vec_ok(n, C, dy, x, add, dx) && C <= 2048) {
     if (sum_part && !stats8_ok(C)) return ACFE_E_INVAL;
     const int grid = sum_part ? red_blocks(rows) : vgrid(n / 8);
@@ -557,7 +580,7 @@ static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
         hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(grid), dim3(256), shm, strm(stream), (const TG*)dy,
                            (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu, coef, (const TO*)add, d, (TO*)dx,
-                           sum_part))));
+                           sum_part, pa))));
   } else {
     if (sum_part) return ACFE_E_INVAL;
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
@@ -595,6 +618,26 @@ ACFE_API int acfe_bn_bwd_apply_ex(const void* dy, int dy_dtype, const void* x, i
   if (drop_rate < 0.f || drop_rate >= 1.f || (add && drop_rate > 0.f)) return ACFE_E_INVAL;
   return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, rows, C, scale, shift, relu, coef, add,
                            make_drop(drop_rate, seed), dx, dx_dtype, sum_partial, stream);
+}
+
+// acfe_bn_bwd_apply_ex with, instead of `add`, the backward of
+// AveragePooling2D(k, strides=k, "same")(x): gpool [N][ceil(H/k)][ceil(W/k)][C].
+ACFE_API int acfe_bn_bwd_apply_pool(const void* dy, int dy_dtype, const void* x, int x_dtype, int N, int H, int W,
+                                    int C, const float* scale, const float* shift, int relu, const float* coef,
+                                    const void* gpool, int k, void* dx, int dx_dtype, double* sum_partial,
+                                    void* stream) {
+  if (!gpool || N <= 0 || H <= 0 || W <= 0 || k <= 0) return ACFE_E_INVAL;
+  PoolAdd pa;
+  pa.g = gpool;
+  pa.H = H;
+  pa.W = W;
+  pa.k = k;
+  pa.P = (H + k - 1) / k;
+  pa.Q = (W + k - 1) / k;
+  pa.pt = ((pa.P - 1) * k + k - H) / 2;
+  pa.pl = ((pa.Q - 1) * k + k - W) / 2;
+  return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, (long long)N * H * W, C, scale, shift, relu, coef, nullptr,
+                           make_drop(0.f, 0), dx, dx_dtype, sum_partial, stream, pa);
 }
 
 // ---------------------------------------------------------------- elementwise

@@ -53,7 +53,9 @@ class BasicBlock(nn.Module):
         next block's first BN consumes; with an identity shortcut the Add's
         gradient for x is summed inside that BN's backward (ResidualLink)."""
         training = self.training
-        link = ops.ResidualLink.make() if self.shortcut is None else None
+        # identity shortcut: the Add's gradient for x, conv shortcut: the pooled
+        # gradient of its AveragePooling2D, both summed inside the BN reading x
+        link = ops.ResidualLink.make()
         y = x
         if self.stride > 1:
             y = self.bn2a0(y, relu=True, stats=x_stats, link=link)
@@ -65,10 +67,11 @@ class BasicBlock(nn.Module):
         y = self.conv2b(y)
         sc = x
         if self.shortcut is not None:
-            sc = self.shortcut(ops.avg_pool_same(x, self.stride))
+            sc = self.shortcut(ops.avg_pool_same(x, self.stride, link=link))
+        add_link = link if self.shortcut is None else None
         if training and ops.FUSE:
-            return ops.add(y, sc, relu=self.relu_out, want_stats=True, link=link)
-        return ops.add(y, sc, relu=self.relu_out, link=link), None
+            return ops.add(y, sc, relu=self.relu_out, want_stats=True, link=add_link)
+        return ops.add(y, sc, relu=self.relu_out, link=add_link), None
 
 
 class WRResNet(nn.Module):

@@ -270,6 +270,14 @@ int acfe_c1bn_bwd(const void* dy, const void* x, long long M, int C, const float
                   double count, const float* gram, void* dx, float* dw, float* db, float* dgamma, float* dbeta,
                   float* workspace, void* stream);
 
+/* acfe_bn_bwd_apply_ex whose residual term is the backward of
+ * AveragePooling2D(k, strides=k, "same") applied to x (the conv shortcut of the
+ * stride-2 blocks): gpool = gradient of the pooled tensor [N][ceil(H/k)][ceil(W/k)][C]
+ * (same dtype as dx), spread over each window's in-bounds elements. */
+int acfe_bn_bwd_apply_pool(const void* dy, int dy_dtype, const void* x, int x_dtype, int N, int H, int W, int C,
+                           const float* scale, const float* shift, int relu, const float* coef, const void* gpool,
+                           int k, void* dx, int dx_dtype, double* sum_partial, void* stream);
+
 /* out[c] = beta*out[c] + sum_rows x[r][c] (bias gradients); partial as acfe_bn_stats. */
 int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* partial, float* out, float beta,
                      void* stream);

@@ -392,3 +392,31 @@ def test_conv_maxpool_dropout_bn_node(env, cuda):
         outs.append([y, x.grad, w.grad, b.grad, gamma.grad, beta.grad, mm, mv])
     for i, (a, r) in enumerate(zip(outs[1], outs[0])):
         assert rel(a, r) < 2e-3, (i, rel(a, r))
+
+
+def test_pool_link(env, cuda):
+    """BN(x) ... + Conv(AvgPool(x)) with the pooled shortcut gradient folded into
+    the BN backward (acfe_bn_bwd_apply_pool via ResidualLink) == plain autograd
+    accumulation of the AveragePooling2D backward; the input being a ReLU output
+    also folds that ReLU's backward in (relu flag bit 1)."""
+    ops = env[0]
+    N, H, W, C = 4, 10, 18, 16  # odd pooled extents are not needed: H, W even as in the model
+    g = torch.Generator(device="cpu").manual_seed(31)
+    a0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    b0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((32, 1, 1, C), generator=g) * 0.2).to(cuda)
+    gz = torch.randn((N, H // 2, W // 2, 32), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    for linked in (False, True):
+        a, b = a0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        gamma, beta, mm, mv = _bn_params(C, cuda, 32)
+        x = ops.add(a, b, relu=True)  # ReLU output: its backward folds into the BN
+        link = ops.ResidualLink() if linked else None
+        u = ops.batch_norm(x, gamma, beta, mm, mv, True, relu=True, link=link)
+        u, _ = ops.conv2d(ops.avg_pool_same(u, 2), w0, None)
+        s, _ = ops.conv2d(ops.avg_pool_same(x, 2, link=link), w0, None)
+        z = ops.add(u, s)
+        z.backward(gz)
+        outs.append([z, a.grad, b.grad, gamma.grad, beta.grad])
+    for i, (p, r) in enumerate(zip(outs[1], outs[0])):
+        assert rel(p, r) < (5e-3 if i in (1, 2) else 2e-3), (i, rel(p, r))
