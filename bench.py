@@ -233,7 +233,7 @@ def main():
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
     traffic = None
-    pmc = ROOT / "profiles" / "pmc_dominant_r01g.json"
+    pmc = ROOT / "profiles" / "pmc_dominant_r01l.json"
     if pmc.exists():
         try:
             traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
@@ -262,7 +262,7 @@ def main():
             "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
         },
         "roofline": {
-            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_rows<128,3>: 3 rows x 64 px x 128 ch per workgroup, register-staged row halo)",
+            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_rows<128,6,1>: 6 rows x 64 px x 128 ch per workgroup, 2x2 max-pool + dropout + BN sums in the epilogue)",
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
