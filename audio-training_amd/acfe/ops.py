@@ -555,6 +555,77 @@ def add(a, b, relu=False, want_stats=False, link=None):
     return (z, st) if want_stats else z
 
 
+def _conv_add_ok(x, w, sc, stride, padding) -> bool:
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    return (FUSE and x.dtype == torch.bfloat16 and stride == 1 and padding == "same" and x.is_contiguous()
+            and x.data_ptr() % 16 == 0 and sc.dtype == x.dtype and tuple(sc.shape) == (N, H, W, K)
+            and bool(lib.acfe_conv2d_rows_supported(N, H, W, C, K, R, S, dtype_code(x.dtype))))
+
+
+class _ConvAddFn(torch.autograd.Function):
+    """(ReLU)(Conv2D 3x3(x) + shortcut) as one node: the residual Add, its ReLU
+    and the next BN's statistics run in the conv epilogue (acfe_conv2d_fwd_add);
+    the conv output itself is never stored."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, sc, relu, want_stats, link):
+        N, H, W, C = x.shape
+        K, R, S, _ = w.shape
+        _, pt = same_padding(H, R, 1)
+        _, pl = same_padding(W, S, 1)
+        wp = pack_weights(w, x.dtype, False)
+        sc = sc.contiguous()
+        z = _empty((N, H, W, K), x.dtype, x.device)
+        stats = _no_stats(x.device)
+        if want_stats:
+            stats = _empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), F64, x.device)
+        with _Timed(w, "fwd"):
+            call("acfe_conv2d_fwd_add", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(sc), int(relu), ptr(z),
+                 ptr(stats) if want_stats else None, dtype_code(x.dtype), stream())
+        ctx.save_for_backward(x, w, z if relu else None)
+        ctx.conf = (pt, pl, relu, b is not None, link)
+        if relu:
+            z._acfe_relu_out = True  # a BatchNormalization reading z folds in the ReLU backward
+        ctx.mark_non_differentiable(stats)
+        return z, stats
+
+    @staticmethod
+    def backward(ctx, g, _gs):
+        x, w, z = ctx.saved_tensors
+        pt, pl, relu, has_b, link = ctx.conf
+        N, H, W, C = x.shape
+        K = w.shape[0]
+        g = g.contiguous()
+        if relu and not getattr(g, "_acfe_relu_masked", False):
+            d = torch.empty_like(g)
+            if _sums_ok(g) and _sums_ok(z) and _sums_ok(d):
+                rows = g.numel() // K
+                part = _empty((lib.acfe_reduce_blocks(rows), 2, K), F64, g.device)
+                call("acfe_relu_bwd_sum", ptr(g), ptr(z), rows, K, ptr(d), dtype_code(g.dtype), ptr(part), stream())
+                _attach_sum(d, part, rows)
+            else:
+                call("acfe_relu_bwd", ptr(g), ptr(z), g.numel(), ptr(d), dtype_code(g.dtype), stream())
+            g = d
+        dx, dw, db = _conv_bwd(x, w, g, 1, pt, pl, H, W, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                               has_b and ctx.needs_input_grad[2])
+        if link is not None:  # the shortcut input's gradient is added by the linked BN backward
+            link.grad = g
+            return dx, dw, db, None, None, None, None
+        return dx, dw, db, g, None, None, None
+
+
+def conv_add(x, w, b, sc, relu=False, want_stats=False, link=None, stride=1, padding="same"):
+    """(ReLU)(Conv2D(x) + sc) -> (z, BN statistics slab of z or empty): one node
+    when the conv epilogue covers the shape, else conv2d then add."""
+    if _conv_add_ok(x, w, sc, stride, padding):
+        return _ConvAddFn.apply(x, w, b, sc, bool(relu), bool(want_stats), link)
+    y, _ = conv2d(x, w, b, stride, padding)
+    if want_stats:
+        return add(y, sc, relu=relu, want_stats=True, link=link)
+    return add(y, sc, relu=relu, link=link), _no_stats(x.device)
+
+
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, rate, seed):

@@ -43,6 +43,8 @@ struct ConvGeom {
   long long M;       // N*P*Q
   Drop drop;         // optional Dropout of the output (flat index m*K + k), fused in the epilogue
   int dbg;           // diagnostics (ACFE_CONV_DBG=8: loop-segment cycle stamps), 0 in production
+  const uint16_t* res;  // k_conv3x3_rows PM 3: residual added in the epilogue (same layout as Y)
+  int res_relu;         // PM 3: ReLU after the residual add
 };
 
 // 64 bytes of zeros in global memory: im2col taps that fall into the padding
@@ -853,7 +855,8 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 // with the k & 7 XOR swizzle.  Operands swapped (weights x pixels) so the
 // epilogue is k_conv_fwd_p's: 8-byte channel quads straight from registers,
 // bias from LDS, fused Dropout, DPP-butterfly BatchNormalization sums.
-// PM (pooling mode): 0 plain; 1 = the output feeds MaxPool2D(2, 2) -> Dropout:
+// PM (epilogue mode): 0 plain; 3 = z = (ReLU)(conv + residual g.res) as
+// ops.add stores it, BN sums of z; 1 = the output feeds MaxPool2D(2, 2) -> Dropout:
 // the epilogue pools row pairs x column pairs (waves own 16-column strips of
 // all TR rows), stores only the pooled values, their first-maximum argmax byte
 // (amax) and their BN statistics; 2 = dgrad whose dY is the 2x2 max-pool
@@ -1056,10 +1059,18 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       for (int fn = 0; fn < FN; ++fn) {
         const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
         uint16_t hv[4];
+        uint2 rv = {0u, 0u};
+        if constexpr (PM == 3) rv = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           hv[jj] = f2bf(acc[fm][fn][jj] + sbias[c + jj]);
           if (g.drop.on) hv[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(hv[jj])));
+          if constexpr (PM == 3) {
+            const unsigned rw = jj < 2 ? rv.x : rv.y;
+            float z = bf2f(hv[jj]) + __uint_as_float((jj & 1) ? (rw & 0xffff0000u) : (rw << 16));
+            if (g.res_relu) z = fmaxf(z, 0.f);
+            hv[jj] = f2bf(z);
+          }
           const float f = inb ? bf2f(hv[jj]) : 0.f;
           sv[fn * 4 + jj] += f;
           sv[FN * 4 + fn * 4 + jj] += f * f;
@@ -1831,6 +1842,8 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.ldy = K;
   g.M = (long long)N * P * Q;
   g.drop = make_drop(0.f, 0);
+  g.res = nullptr;
+  g.res_relu = 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
   return g;
@@ -2226,6 +2239,35 @@ ACFE_API int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C,
   if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, strm(stream), workspace, used, n, beta, dw);
   return launch_rc("acfe_conv2d_wgrad_unpool(reduce)");
+}
+
+// Conv2D 3x3 "same" stride 1 whose output is summed with the block shortcut
+// (resnet/wr_resnet_bird.py:173-178: res{s}{b}_branch2b + Add (+ReLU)):
+// y = (ReLU)(conv(x) + res) stored by the conv epilogue with its BN statistics
+// (slab rows = acfe_conv2d_stats_rows(N*H*W, K), nullable); the conv output
+// itself is never stored.  Shapes: acfe_conv2d_rows_supported.
+ACFE_API int acfe_conv2d_rows_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {
+  static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS") || getenv_flag("ACFE_CONV_NO_ADD");
+  return !no_rows && dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
+         (K == 64 || K == 128) && W > 0 && W % 64 == 0 && H > 0 &&
+         (long long)N * ((H + 5) / 6) * (W / 64) < (1ll << 31);
+}
+
+ACFE_API int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                                 int pad_left, const float* bias, const void* res, int relu, void* y,
+                                 double* stats_partial, int dtype, void* stream) {
+  if (!x || !wpacked || !y || !res || !acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, dtype) ||
+      ((uintptr_t)y & 7) || ((uintptr_t)res & 7))
+    return ACFE_E_INVAL;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
+  g.res = (const uint16_t*)res;
+  g.res_relu = relu ? 1 : 0;
+  const int srows = grid_m_for(g.M, 1);
+  if (K == 128)
+    return launch_rows<128, 3>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
+                               "acfe_conv2d_fwd_add");
+  return launch_rows<64, 3>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
+                            "acfe_conv2d_fwd_add");
 }
 
 // ------------------------------------------------------------------ stem (C = 1)

@@ -64,14 +64,16 @@ class BasicBlock(nn.Module):
         else:
             y = self.bn2a(y, relu=True, stats=x_stats, link=link)
             y = conv_dropout_bn(self.conv21, self.bn2b, y, self.dropout)
-        y = self.conv2b(y)
+        # the shortcut is built after the residual branch (its backward then runs
+        # first, delivering the linked gradient before the BN reading x needs it)
         sc = x
         if self.shortcut is not None:
             sc = self.shortcut(ops.avg_pool_same(x, self.stride, link=link))
         add_link = link if self.shortcut is None else None
-        if training and ops.FUSE:
-            return ops.add(y, sc, relu=self.relu_out, want_stats=True, link=add_link)
-        return ops.add(y, sc, relu=self.relu_out, link=add_link), None
+        want = training and ops.FUSE
+        z, st = ops.conv_add(y, self.conv2b.weight, self.conv2b.bias, sc, relu=self.relu_out, want_stats=want,
+                             link=add_link, stride=self.conv2b.strides, padding=self.conv2b.padding)
+        return z, (st if want else None)
 
 
 class WRResNet(nn.Module):

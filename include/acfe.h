@@ -248,6 +248,15 @@ int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C, const vo
                              int K, int pad_top, int pad_left, float* dw, float beta, int dtype, float* workspace,
                              void* stream);
 
+/* Conv2D 3x3 "same" stride 1 followed by the residual Add (+ReLU) of the block
+ * (res{s}{b}_branch2b + Add, resnet/wr_resnet_bird.py:173-178): y = (ReLU)(conv(x)
+ * + res), res/y [N][H][W][K] bf16, BN statistics of y into stats_partial (rows =
+ * acfe_conv2d_stats_rows(N*H*W, K), nullable).  Shapes: acfe_conv2d_rows_supported. */
+int acfe_conv2d_rows_supported(int N, int H, int W, int C, int K, int R, int S, int dtype);
+int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                        int pad_left, const float* bias, const void* res, int relu, void* y, double* stats_partial,
+                        int dtype, void* stream);
+
 /* Conv2D(1x1, 16 -> K in {64, 128}, bias) -> BatchNormalization -> (ReLU) as one
  * node whose conv output A = W x + b is never stored (csrc/c1bn.hip;
  * res{s}b0_branch2a0 + bn{s}b0_branch2a of resnet/wr_resnet_bird.py:121-131).

@@ -420,3 +420,35 @@ def test_pool_link(env, cuda):
         outs.append([z, a.grad, b.grad, gamma.grad, beta.grad])
     for i, (p, r) in enumerate(zip(outs[1], outs[0])):
         assert rel(p, r) < (5e-3 if i in (1, 2) else 2e-3), (i, rel(p, r))
+
+
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128)])
+def test_conv_add_node(env, cuda, relu, C, K):
+    """(ReLU)(conv 3x3 + shortcut) with the Add in the conv epilogue
+    (acfe_conv2d_fwd_add) == conv2d -> add: z bit-exact, statistics to 1e-6,
+    gradients of x, w, b and the shortcut identical up to summation order."""
+    ops = env[0]
+    N, H, W = 2, 14, 128
+    g = torch.Generator(device="cpu").manual_seed(41)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    s0 = torch.randn((N, H, W, K), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((K, 3, 3, C), generator=g) * 0.05).to(cuda)
+    b0 = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    gz = torch.randn((N, H, W, K), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    for fused in (False, True):
+        x, s = x0.clone().requires_grad_(True), s0.clone().requires_grad_(True)
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        if fused:
+            assert ops._conv_add_ok(x, w, s, 1, "same")
+            z, st = ops.conv_add(x, w, b, s, relu=relu, want_stats=True)
+        else:
+            y, _ = ops.conv2d(x, w, b)
+            z, st = ops.add(y, s, relu=relu, want_stats=True)
+        z.backward(gz)
+        outs.append([z, st.sum(0)[:, :K], x.grad, w.grad, b.grad, s.grad])
+    assert torch.equal(outs[1][0], outs[0][0])
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-6, atol=1e-4)
+    for i in range(2, 6):
+        assert rel(outs[1][i], outs[0][i]) < 1e-3, (i, rel(outs[1][i], outs[0][i]))
