@@ -998,6 +998,27 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) woff[fn] = wk * (KB / 2) + fn * 16 + l16;
 
+  // PM 3 with K = 64: the tile's residual quads are loaded at the start of its
+  // last step (in flight during that step's MFMAs) instead of in the epilogue
+  constexpr bool RPRE = PM == 3 && KB == 64;
+  uint2 rres[RPRE ? FM : 1][RPRE ? FN : 1];
+  auto rload = [&](int tm) __attribute__((always_inline)) {
+    if constexpr (RPRE) {
+      const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int p = wp * (TR * 16) + fm * 16;
+        const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+        const bool inb = h < g.P && w < g.Q;
+        const long long pix = ((long long)n * g.P + h) * g.Q + w;
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
+          rres[fm][fn] = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
+        }
+      }
+    }
+  };
   auto epilogue = [&](int tm) __attribute__((always_inline)) {
     const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
     float sv[NV];
@@ -1060,7 +1081,8 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
         const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
         uint16_t hv[4];
         uint2 rv = {0u, 0u};
-        if constexpr (PM == 3) rv = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
+        if constexpr (RPRE) rv = rres[fm][fn];
+        else if constexpr (PM == 3) rv = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           hv[jj] = f2bf(acc[fm][fn][jj] + sbias[c + jj]);
@@ -1112,6 +1134,9 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     if (more) {
       gload(t + 1);
       if constexpr (WDMA) wdma(t + 1, (t + 1) & 1);
+    }
+    if constexpr (RPRE) {
+      if (cst + 1 == nsteps_t) rload(ctm);
     }
     const unsigned char* Xl = smem + buf * BUFB;
     const unsigned char* Wl = WDMA ? smem + XBYTES + (t & 1) * WBYTES : Xl + XBYTES;
