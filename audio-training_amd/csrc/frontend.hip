@@ -357,6 +357,11 @@ __device__ __forceinline__ float fetch(const float* __restrict__ xb, int n, int 
   return do_norm ? norm1(v, mn, rng) : v;
 }
 
+// Whether fetch() reads a signal sample at idx (else it returns the zero pad).
+__device__ __forceinline__ bool in_sig(int idx, int n, int pad_mode) {
+  return pad_mode == ACFE_PAD_CENTER_REFLECT || (idx >= 0 && idx < n);
+}
+
 template <int NC>
 __global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int64_t cs, int n,
                                              const float* __restrict__ stats, int pad_mode,
@@ -444,6 +449,246 @@ __global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int6
   }
 }
 
+// ---- wave-per-frame variant for n_fft = 4096 (NC = 2048 = 16 x 16 x 8).
+// One 64-lane workgroup owns its frames end to end: the three Stockham passes
+// (radix 16, 16, 8) keep every butterfly in VGPRs and exchange through the
+// wave's own LDS slice, so no workgroup of 4 waves waits at a barrier for its
+// slowest global load; 6-7 independent waves per CU hide each other's latency.
+template <>
+__device__ __forceinline__ void dft<16>(float2* v) {
+  // X[k1 + 4 k2] = DFT4_{n2}( W16^{n2 k1} * DFT4_{n1}(x[4 n1 + n2])[k1] )
+  float2 a[4][4];
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[4 * n1 + n2];
+    dft<4>(a[n2]);
+  }
+  const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f, h = 0.70710678118654752440f;
+  a[1][1] = cmul(a[1][1], make_float2(c1, -s1));  // W16^1
+  a[1][2] = cmul(a[1][2], make_float2(h, -h));    // W16^2
+  a[1][3] = cmul(a[1][3], make_float2(s1, -c1));  // W16^3
+  a[2][1] = cmul(a[2][1], make_float2(h, -h));    // W16^2
+  a[2][2] = mul_mi(a[2][2]);                      // W16^4
+  a[2][3] = cmul(a[2][3], make_float2(-h, -h));   // W16^6
+  a[3][1] = cmul(a[3][1], make_float2(s1, -c1));  // W16^3
+  a[3][2] = cmul(a[3][2], make_float2(-h, -h));   // W16^6
+  a[3][3] = cmul(a[3][3], make_float2(-c1, s1));  // W16^9
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    float2 b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
+    dft<4>(b);
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
+  }
+}
+
+// In-place Stockham pass over the wave's NC points, span NS, radix R: all of a
+// lane's butterfly inputs are read before any output is written.  NB and NS
+// are multiples of 8, so every padded LDS address is the lane's base plus a
+// compile-time offset; the twiddles W^{r t} come from W^t, W^{2t}, W^{4t},
+// W^{8t} (at most two extra complex products each).
+template <int R>
+__device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
+  // bw = {W^t, W^2t, W^4t, W^8t}
+  w[0] = make_float2(1.f, 0.f);
+  w[1] = bw[0];
+  w[2] = bw[1];
+  w[3] = cmul(w[1], w[2]);
+  w[4] = bw[2];
+#pragma unroll
+  for (int r = 5; r < 8 && r < R; ++r) w[r] = cmul(w[4], w[r - 4]);
+  if constexpr (R == 16) {
+    w[8] = bw[3];
+#pragma unroll
+    for (int r = 9; r < 16; ++r) w[r] = cmul(w[8], w[r - 8]);
+  }
+}
+
+template <int NC, int R, int NS>
+__device__ __forceinline__ void stockham_pass_w(float2* buf, const float2 (*bw)[4], int lane) {
+  constexpr int NB = NC / R, PER = NB / 64;
+  static_assert(NB % 64 == 0 && NB % 8 == 0 && NS % 8 == 0, "pass shape");
+  float2 v[PER][R];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int j = lane + 64 * p, jm = j & (NS - 1);
+    const float2* src = buf + padx(j);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[p][r] = src[r * (NB + NB / 8)];
+    float2 w[R];
+    twiddle_pows<R>(bw[p], w);
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[p][r] = cmul(v[p][r], w[r]);
+  }
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int j = lane + 64 * p, jm = j & (NS - 1);
+    dft<R>(v[p]);
+    float2* dst = buf + padx((j / NS) * NS * R + jm);
+#pragma unroll
+    for (int r = 0; r < R; ++r) dst[r * (NS + NS / 8)] = v[p][r];
+  }
+  __syncthreads();  // one-wave workgroup: orders the lanes' LDS exchange
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_mel_w(const float* __restrict__ raw, int64_t cs, int n,
+                                              const float* __restrict__ stats, int pad_mode, int power,
+                                              int n_frames, int fpw, int hop, const float2* __restrict__ tw,
+                                              const float2* __restrict__ rtw, const float* __restrict__ win,
+                                              const int* __restrict__ band, const float* __restrict__ vals,
+                                              int n_mels, int kmin, int kmax, float* __restrict__ out,
+                                              int layout) {
+  constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16;
+  extern __shared__ float2 wbuf[];  // [NC + NC/8] padded points, then [nk] power bins
+  float* pw = reinterpret_cast<float*>(wbuf + NC + NC / 8);
+  const int lane = threadIdx.x;
+  const int b = blockIdx.y;
+  const float* xb = raw + (int64_t)b * cs;
+  const bool do_norm = stats != nullptr;
+  const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
+  const int nk = kmax - kmin + 1;
+  const int f0 = blockIdx.x * fpw;
+  // the lane's base twiddles of passes 2 and 3 (W^{t}, W^{2t}, W^{4t}, W^{8t}
+  // with t = jm * NC / (NS R)) stay in 32 VGPRs for all of its frames
+  float2 bw2[2][4], bw3[4][4];
+  {
+    const int t = (lane & 15) * 8;  // pass 2: jm = j & 15 is the same for both butterflies
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bw2[0][q] = bw2[1][q] = tw[(t << q) & (NC - 1)];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) bw3[p][q] = tw[((lane + 64 * p) << q) & (NC - 1)];
+      bw3[p][3] = make_float2(1.f, 0.f);
+    }
+  }
+  for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
+    // the per-lane window loads are frame-invariant: an opaque zero offset
+    // keeps the compiler from hoisting their 64 VGPRs out of the frame loop
+    int zo;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
+    const float* winf = win + zo;
+    // and the powers of the base twiddles are recomputed per frame rather than
+    // hoisted (116 VGPRs): the empty asm makes the bases opaque each iteration
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      asm volatile("" : "+v"(bw2[0][q].x), "+v"(bw2[0][q].y));
+      bw2[1][q] = bw2[0][q];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(bw3[p][q].x), "+v"(bw3[p][q].y));
+    }
+    const int start = (pad_mode == ACFE_PAD_END) ? f * hop : f * hop - L / 2;
+    const bool inb = start >= 0 && start + L <= n;
+    // pass 1 (NS = 1, radix 16) from memory: z[j + r*NB0] = x[2(j + r NB0)] + i x[2(j + r NB0) + 1]
+    __syncthreads();  // the previous frame's readers of wbuf / pw are done
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int j = lane + 64 * p;
+      // uniform branch outside the unrolled loads: all 32 sample loads of an
+      // interior frame are issued back to back
+      float xa[16], xc[16], wa[16], wc[16];
+      const float* ws = winf + 2 * j;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wa[r] = ws[2 * r * NB0], wc[r] = ws[2 * r * NB0 + 1];
+      if (inb) {
+        const float* xs = xb + start + 2 * j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xa[r] = xs[2 * r * NB0], xc[r] = xs[2 * r * NB0 + 1];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int nn = 2 * (j + r * NB0);
+          xa[r] = fetch(xb, n, start + nn, pad_mode, false, 0.f, 1.f);
+          xc[r] = fetch(xb, n, start + nn + 1, pad_mode, false, 0.f, 1.f);
+        }
+      }
+      float2 v[16];
+      if (do_norm) {
+        // zero padding is applied after normalisation (fetch returns 0 outside)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int nn = 2 * (j + r * NB0);
+          const bool ia = inb || in_sig(start + nn, n, pad_mode), ic = inb || in_sig(start + nn + 1, n, pad_mode);
+          v[r] = make_float2(ia ? norm1(xa[r], mn, rng) * wa[r] : 0.f, ic ? norm1(xc[r], mn, rng) * wc[r] : 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = make_float2(xa[r] * wa[r], xc[r] * wc[r]);
+      }
+      dft<16>(v);
+      float2* dst = wbuf + j * 18;  // padx(16 j + r) = 18 j + r + r / 8
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[r + (r >> 3)] = v[r];
+    }
+    __syncthreads();
+    stockham_pass_w<NC, 16, 16>(wbuf, bw2, lane);
+    stockham_pass_w<NC, 8, 256>(wbuf, bw3, lane);
+    // real-FFT post-processing + power for bins [kmin, kmax], up to 16 bins
+    // per lane per round with their rtw loads issued together
+    for (int i0 = lane; i0 < nk; i0 += 1024) {
+      float2 rt[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) rt[u] = i0 + 64 * u < nk ? rtw[kmin + i0 + 64 * u] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = i0 + 64 * u;
+        if (i < nk) {
+          const int k = kmin + i;
+          const float2 zk = wbuf[padx(k & (NC - 1))];
+          const float2 zm = wbuf[padx((NC - k) & (NC - 1))];
+          const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+          const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
+          const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
+          const float2 X = cadd(E, cmul(rt[u], O));
+          const float p2 = X.x * X.x + X.y * X.y;
+          pw[i] = power == 2 ? p2 : sqrtf(p2);
+        }
+      }
+    }
+    __syncthreads();
+    // banded mel: the lane's two bands (m, m + 64) advance together, eight taps
+    // each per round, so 16 filter loads are in flight instead of one
+    for (int m0 = lane; m0 < n_mels; m0 += 128) {
+      const int m1 = m0 + 64;
+      const bool h1 = m1 < n_mels;
+      const int s0 = band[3 * m0], len0 = band[3 * m0 + 1], off0 = band[3 * m0 + 2];
+      const int s1 = h1 ? band[3 * m1] : kmin, len1 = h1 ? band[3 * m1 + 1] : 0, off1 = h1 ? band[3 * m1 + 2] : 0;
+      const int lmax = len0 > len1 ? len0 : len1;
+      float acc0 = 0.f, acc1 = 0.f;
+      for (int i0 = 0; i0 < lmax; i0 += 8) {
+        float w0[8], w1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          w0[u] = i0 + u < len0 ? vals[off0 + i0 + u] : 0.f;
+          w1[u] = i0 + u < len1 ? vals[off1 + i0 + u] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (i0 + u < len0) acc0 += w0[u] * pw[s0 - kmin + i0 + u];
+          if (i0 + u < len1) acc1 += w1[u] * pw[s1 - kmin + i0 + u];
+        }
+      }
+      const size_t o0 = layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m0
+                                                  : ((size_t)b * n_mels + m0) * n_frames + f;
+      out[o0] = acc0;
+      if (h1) {
+        const size_t o1 = layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m1
+                                                    : ((size_t)b * n_mels + m1) * n_frames + f;
+        out[o1] = acc1;
+      }
+    }
+  }
+}
+
+static bool mel_wave_path() {
+  static const int v = [] {
+    const char* e = getenv("ACFE_MEL_BLOCK");
+    return (e && atoi(e)) ? 0 : 1;
+  }();
+  return v != 0;
+}
+
 ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch, int n,
                           const float* stats, int pad_mode, int power, float* out, int layout,
                           void* stream) {
@@ -454,6 +699,15 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   if (pad_mode == ACFE_PAD_CENTER_REFLECT && n <= p->n_fft / 2) return ACFE_E_INVAL;
   if (batch == 0) return ACFE_OK;
   const int T = acfe_plan_num_frames(p, n, pad_mode);
+  if (p->n_fft == 4096 && mel_wave_path()) {
+    const int fpw = 4;
+    const int nk = p->kmax - p->kmin + 1;
+    const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + sizeof(float) * nk;
+    hipLaunchKernelGGL(k_mel_w, dim3(cdiv(T, fpw), batch), dim3(64), shm, strm(stream), raw, cs, n, stats,
+                       pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
+                       p->n_mels, p->kmin, p->kmax, out, layout);
+    return launch_rc("acfe_mel_fwd");
+  }
   const int fpb = 4;
   dim3 grid(cdiv(T, fpb), batch);
 #define LAUNCH_MEL(NC)                                                                          \
