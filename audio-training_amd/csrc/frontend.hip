@@ -98,6 +98,7 @@ ACFE_API int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmi
     band[3 * m + 1] = e - s + 1;
     band[3 * m + 2] = (int)vals.size();
     for (int k = s; k <= e; ++k) vals.push_back(w_host[(size_t)m * nb + k]);
+    while (vals.size() & 7) vals.push_back(0.f);  // k_mel_w reads whole 8-tap groups
     kmin = s < kmin ? s : kmin;
     kmax = e > kmax ? e : kmax;
   }
@@ -548,6 +549,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const bool do_norm = stats != nullptr;
   const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
   const int nk = kmax - kmin + 1;
+  if (lane < 8) pw[nk + lane] = 0.f;
   const int f0 = blockIdx.x * fpw;
   // the lane's base twiddles of passes 2 and 3 (W^{t}, W^{2t}, W^{4t}, W^{8t}
   // with t = jm * NC / (NS R)) stay in 32 VGPRs for all of its frames
@@ -641,42 +643,43 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
           const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
           const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
           const float2 X = cadd(E, cmul(rt[u], O));
-          const float p2 = X.x * X.x + X.y * X.y;
-          pw[i] = power == 2 ? p2 : sqrtf(p2);
+          pw[i] = X.x * X.x + X.y * X.y;
         }
       }
     }
+    if (power != 2) {
+      for (int k = lane; k < nk; k += 64) pw[k] = sqrtf(pw[k]);
+    }
     __syncthreads();
-    // banded mel: the lane's two bands (m, m + 64) advance together, eight taps
-    // each per round, so 16 filter loads are in flight instead of one
-    for (int m0 = lane; m0 < n_mels; m0 += 128) {
-      const int m1 = m0 + 64;
-      const bool h1 = m1 < n_mels;
-      const int s0 = band[3 * m0], len0 = band[3 * m0 + 1], off0 = band[3 * m0 + 2];
-      const int s1 = h1 ? band[3 * m1] : kmin, len1 = h1 ? band[3 * m1 + 1] : 0, off1 = h1 ? band[3 * m1 + 2] : 0;
-      const int lmax = len0 > len1 ? len0 : len1;
+    // banded mel over balanced band pairs (m, n_mels-1-m): a short low band and
+    // a long high band per lane, their taps in whole 8-tap groups (the plan pads
+    // each band's taps with zeros, pw has 8 zero floats past nk)
+    for (int q = lane; q < (n_mels + 1) / 2; q += 64) {
+      const int m0 = q, m1 = n_mels - 1 - q;
+      const bool h1 = m1 != m0;
+      const int s0 = band[3 * m0], pl0 = (band[3 * m0 + 1] + 7) & ~7, off0 = band[3 * m0 + 2];
+      const int s1 = band[3 * m1], pl1 = h1 ? (band[3 * m1 + 1] + 7) & ~7 : 0, off1 = band[3 * m1 + 2];
+      const float4* v0 = reinterpret_cast<const float4*>(vals + off0);
+      const float4* v1 = reinterpret_cast<const float4*>(vals + off1);
+      const float* p0 = pw + (s0 - kmin);
+      const float* p1 = pw + (s1 - kmin);
       float acc0 = 0.f, acc1 = 0.f;
+      const int lmax = pl0 > pl1 ? pl0 : pl1;
       for (int i0 = 0; i0 < lmax; i0 += 8) {
-        float w0[8], w1[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          w0[u] = i0 + u < len0 ? vals[off0 + i0 + u] : 0.f;
-          w1[u] = i0 + u < len1 ? vals[off1 + i0 + u] : 0.f;
+        if (i0 < pl0) {
+          const float4 a = v0[i0 / 4], c = v0[i0 / 4 + 1];
+          acc0 += a.x * p0[i0] + a.y * p0[i0 + 1] + a.z * p0[i0 + 2] + a.w * p0[i0 + 3] + c.x * p0[i0 + 4] +
+                  c.y * p0[i0 + 5] + c.z * p0[i0 + 6] + c.w * p0[i0 + 7];
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (i0 + u < len0) acc0 += w0[u] * pw[s0 - kmin + i0 + u];
-          if (i0 + u < len1) acc1 += w1[u] * pw[s1 - kmin + i0 + u];
+        if (i0 < pl1) {
+          const float4 a = v1[i0 / 4], c = v1[i0 / 4 + 1];
+          acc1 += a.x * p1[i0] + a.y * p1[i0 + 1] + a.z * p1[i0 + 2] + a.w * p1[i0 + 3] + c.x * p1[i0 + 4] +
+                  c.y * p1[i0 + 5] + c.z * p1[i0 + 6] + c.w * p1[i0 + 7];
         }
       }
-      const size_t o0 = layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m0
-                                                  : ((size_t)b * n_mels + m0) * n_frames + f;
-      out[o0] = acc0;
-      if (h1) {
-        const size_t o1 = layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m1
-                                                    : ((size_t)b * n_mels + m1) * n_frames + f;
-        out[o1] = acc1;
-      }
+      const size_t rowo = layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels : 0;
+      out[layout == ACFE_LAYOUT_BTM ? rowo + m0 : ((size_t)b * n_mels + m0) * n_frames + f] = acc0;
+      if (h1) out[layout == ACFE_LAYOUT_BTM ? rowo + m1 : ((size_t)b * n_mels + m1) * n_frames + f] = acc1;
     }
   }
 }
@@ -702,7 +705,7 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   if (p->n_fft == 4096 && mel_wave_path()) {
     const int fpw = 4;
     const int nk = p->kmax - p->kmin + 1;
-    const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + sizeof(float) * nk;
+    const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + sizeof(float) * (nk + 8);
     hipLaunchKernelGGL(k_mel_w, dim3(cdiv(T, fpw), batch), dim3(64), shm, strm(stream), raw, cs, n, stats,
                        pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
                        p->n_mels, p->kmin, p->kmax, out, layout);
