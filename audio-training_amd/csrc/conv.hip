@@ -1829,6 +1829,40 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 // four consecutive outputs (16-B loads) and keeps eight slab loads in flight
 // (independent partial sums, fixed combine order), so the pass runs at HBM
 // rate instead of one dependent load per split.
+// Split-K combine with the splits spread over the workgroup: 16 columns of
+// float4 x 16 split groups per 256 threads (each thread sums every 16th slab of
+// its column, eight loads in flight), then a fixed-order LDS sum of the 16
+// group partials -- deterministic, and enough workgroups for the narrow 3x3
+// layers whose column-only version ran 36-144 workgroups of long serial sums.
+__global__ void __launch_bounds__(256) k_wgrad_reduce_g(const float* __restrict__ ws, int nsplit, long long nv,
+                                                        long long n, float beta, float* __restrict__ dw) {
+  __shared__ f4 part[16][17];
+  const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const long long v = (long long)blockIdx.x * 16 + col;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  if (v < nv) {
+    const float* src = ws + v * 4;
+    int z = grp;
+    for (; z + 7 * 16 < nsplit; z += 8 * 16) {
+      f4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const f4*>(src + (long long)(z + 16 * u) * n);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; z < nsplit; z += 16) acc += *reinterpret_cast<const f4*>(src + (long long)z * n);
+  }
+  part[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0 && v < nv) {
+    f4 t = part[0][col];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) t += part[g][col];
+    f4* d = reinterpret_cast<f4*>(dw + v * 4);
+    *d = beta != 0.f ? *d * beta + t : t;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ ws, int nsplit, long long n,
                                                       float beta, float* __restrict__ dw) {
   // vector path only when every slab (z * n floats) stays 16-B aligned
@@ -2083,6 +2117,18 @@ ACFE_API int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const
 
 // Split-K plan of the wgrad: `splits` pixel chunks of `chunk` rows, splits a
 // multiple of 8 so the XCD mapping of k_conv_wgrad is a bijection.
+static void wgrad_combine(const float* ws, int nsplit, long long n, float beta, float* dw, int grid,
+                          hipStream_t st) {
+  const bool vec = (n & 3) == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)dw & 15) == 0;
+  if (vec && nsplit >= 16) {
+    const long long nv = n >> 2;
+    hipLaunchKernelGGL(k_wgrad_reduce_g, dim3((unsigned)((nv + 15) / 16)), dim3(256), 0, st, ws, nsplit, nv, n, beta,
+                       dw);
+  } else {
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, st, ws, nsplit, n, beta, dw);
+  }
+}
+
 static void wgrad_plan(long long M, int kd, int K, long long* splits_o, long long* chunk_o) {
   const int bmw = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
@@ -2182,7 +2228,7 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   const long long n = (long long)K * kd;
   int grid = cdiv((n + 3) / 4, 256);
   if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, strm(stream), workspace, (int)splits, n, beta, dw);
+  wgrad_combine(workspace, (int)splits, n, beta, dw, grid, strm(stream));
   return launch_rc("acfe_conv2d_wgrad(reduce)");
 }
 
@@ -2262,7 +2308,7 @@ ACFE_API int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C,
   const long long n = (long long)K * 9 * C;
   int grid = cdiv((n + 3) / 4, 256);
   if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(grid), dim3(256), 0, strm(stream), workspace, used, n, beta, dw);
+  wgrad_combine(workspace, used, n, beta, dw, grid, strm(stream));
   return launch_rc("acfe_conv2d_wgrad_unpool(reduce)");
 }
 
