@@ -136,6 +136,7 @@ class ParamArena:
                 self.flat[o:o + n].copy_(p.detach().reshape(-1).to(device))
                 p.data = self.flat[o:o + n].view(p.shape)
                 p.grad = self.grad[o:o + n].view(p.shape)
+                p._acfe_arena = True  # ops.direct_grad: kernels may accumulate into p.grad
                 self.offsets.append((o, n))
                 o += n
 

@@ -115,6 +115,18 @@ def _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats, drop=None):
     return y, stats
 
 
+def direct_grad(p):
+    """The flat-arena .grad view of parameter p when its gradient may be
+    accumulated in place by the producing kernel (layers.ParamArena marks its
+    parameters and zeroes the arena before each backward), else None."""
+    if not getattr(p, "_acfe_arena", False):
+        return None
+    g = p.grad
+    if g is None or g.dtype != F32 or not g.is_contiguous() or g.shape != p.shape:
+        return None
+    return g
+
+
 def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db):
     """dgrad / wgrad / bias gradient of _conv_fwd for the conv-output gradient dy."""
     N, H, W, C = x.shape
@@ -133,12 +145,18 @@ def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db):
             call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
                  ptr(ws), s)
     if need_dw:
-        dw = _empty(w.shape, F32, w.device)
+        # arena parameters: the split-K combine accumulates straight into the
+        # flat gradient buffer (beta 1) and autograd gets None -- no separate
+        # add kernel per weight
+        tgt = direct_grad(w)
+        dw = tgt if tgt is not None else _empty(w.shape, F32, w.device)
         nws = lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, P, Q)
         ws = _empty((nws,), F32, x.device)
         with _Timed(w, "wgrad"):
-            call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, stride, pt, pl, P, Q, ptr(dw), 0.0,
-                 dt, ptr(ws), s)
+            call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, stride, pt, pl, P, Q, ptr(dw),
+                 1.0 if tgt is not None else 0.0, dt, ptr(ws), s)
+        if tgt is not None:
+            dw = None
     if need_db:
         db = channel_sum(dy, K)
     return dx, dw, db
@@ -823,11 +841,14 @@ class _ConvPoolBNFn(torch.autograd.Function):
                 call("acfe_conv2d_dgrad_unpool", ptr(g), ptr(amax), N, H, W, K, ptr(wf), C, pt, pl, ptr(dx),
                      dtype_code(x.dtype), s)
         if ctx.needs_input_grad[1]:
-            dw = _empty(w.shape, F32, dev)
+            tgt = direct_grad(w)
+            dw = tgt if tgt is not None else _empty(w.shape, F32, dev)
             ws = _empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), F32, dev)
             with _Timed(w, "wgrad"):
-                call("acfe_conv2d_wgrad_unpool", ptr(x), N, H, W, C, ptr(g), ptr(amax), K, pt, pl, ptr(dw), 0.0,
-                     dtype_code(x.dtype), ptr(ws), s)
+                call("acfe_conv2d_wgrad_unpool", ptr(x), N, H, W, C, ptr(g), ptr(amax), K, pt, pl, ptr(dw),
+                     1.0 if tgt is not None else 0.0, dtype_code(x.dtype), ptr(ws), s)
+            if tgt is not None:
+                dw = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = channel_sum(g, K)  # the pool backward scatters: sum of the pooled gradient
         return dx, dw, db, dgamma, dbeta, None, None, None

@@ -703,7 +703,12 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   if (batch == 0) return ACFE_OK;
   const int T = acfe_plan_num_frames(p, n, pad_mode);
   if (p->n_fft == 4096 && mel_wave_path()) {
-    const int fpw = 4;
+    static const int fpw_env = [] {
+      const char* e = getenv("ACFE_MEL_FPW");
+      const int v = e ? atoi(e) : 0;
+      return v > 0 && v <= 64 ? v : 4;
+    }();
+    const int fpw = fpw_env;
     const int nk = p->kmax - p->kmin + 1;
     const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + sizeof(float) * (nk + 8);
     hipLaunchKernelGGL(k_mel_w, dim3(cdiv(T, fpw), batch), dim3(64), shm, strm(stream), raw, cs, n, stats,
