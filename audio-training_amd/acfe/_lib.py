@@ -55,6 +55,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_bn_apply": [P, I32, I64, I32, P, P, I32, P, I32, P],
     "acfe_bn_bwd_reduce": [P, I32, P, I32, I64, I32, P, P, P, P, I32, P, P],
     "acfe_bn_bwd_finalize": [P, I32, I32, F64, P, P, P, P, P, P, P],
+    "acfe_bn_bwd_finalize_ex": [P, I32, I32, F64, P, P, P, P, P, P, I32, P],
     "acfe_bn_bwd_apply": [P, I32, P, I32, I64, I32, P, P, I32, P, P, P, I32, P],
     "acfe_bn_bwd_apply_dropout": [P, I32, P, I32, I64, I32, P, P, I32, P, F32, C.c_uint64, P, I32, P],
     "acfe_bn_bwd_apply_ex": [P, I32, P, I32, I64, I32, P, P, I32, P, P, F32, C.c_uint64, P, I32, P, P],

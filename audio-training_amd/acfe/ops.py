@@ -127,7 +127,7 @@ def direct_grad(p):
     return g
 
 
-def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db):
+def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=None):
     """dgrad / wgrad / bias gradient of _conv_fwd for the conv-output gradient dy."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
@@ -158,13 +158,17 @@ def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db):
         if tgt is not None:
             dw = None
     if need_db:
-        db = channel_sum(dy, K)
+        tb = direct_grad(bias) if bias is not None else None
+        db = channel_sum(dy, K, into=tb)
+        if tb is not None:
+            db = None
     return dx, dw, db
 
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pt, pl, P, Q, want_stats):
+        ctx.bias = b
         y, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pt, pl, P, Q, b is not None)
@@ -176,7 +180,7 @@ class _Conv2dFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         stride, pt, pl, P, Q, has_b = ctx.conf
         dx, dw, db = _conv_bwd(x, w, dy, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               has_b and ctx.needs_input_grad[2])
+                               has_b and ctx.needs_input_grad[2], bias=ctx.bias)
         return dx, dw, db, None, None, None, None, None, None
 
 
@@ -190,20 +194,22 @@ def _attach_sum(t: torch.Tensor, part: torch.Tensor, rows: int):
     """Finalize a fused channel-sum slab and cache it on the gradient tensor it
     sums, so the convolution receiving `t` as its output gradient takes its
     bias gradient from there instead of re-reading `t` (channel_sum)."""
-    C = t.shape[-1]
-    db = _empty((C,), F32, t.device)
-    call("acfe_channel_sum_finalize", ptr(part), lib.acfe_reduce_blocks(rows), C, 0.0, ptr(db), stream())
-    t._acfe_chsum = db
+    t._acfe_chpart = (part, rows)  # finalized by channel_sum, possibly into an arena gradient
 
 
-def channel_sum(x: torch.Tensor, C: int) -> torch.Tensor:
-    cached = getattr(x, "_acfe_chsum", None)
-    if cached is not None and cached.numel() == C:
-        return cached
+def channel_sum(x: torch.Tensor, C: int, into: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-channel sum of x [..., C] in fp32; with `into` (an arena gradient
+    view) it is accumulated there instead (beta 1)."""
+    out = into if into is not None else _empty((C,), F32, x.device)
+    beta = 1.0 if into is not None else 0.0
+    lazy = getattr(x, "_acfe_chpart", None)
+    if lazy is not None and lazy[0].shape[-1] == C:
+        part, prow = lazy
+        call("acfe_channel_sum_finalize", ptr(part), lib.acfe_reduce_blocks(prow), C, beta, ptr(out), stream())
+        return out
     rows = x.numel() // C
-    out = _empty((C,), F32, x.device)
     part = _empty((lib.acfe_reduce_blocks(rows) * 2 * C,), F64, x.device)
-    call("acfe_channel_sum", ptr(x), rows, C, dtype_code(x.dtype), ptr(part), ptr(out), 0.0, stream())
+    call("acfe_channel_sum", ptr(x), rows, C, dtype_code(x.dtype), ptr(part), ptr(out), beta, stream())
     return out
 
 
@@ -326,7 +332,7 @@ def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, o
     return y, (scale, shift, mean, invstd)
 
 
-def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None):
+def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None, params=None):
     """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given;
     mask_in: x is a ReLU output (ops.add), its backward [x > 0] is applied to dx here
     and dx is marked so that ops.add's backward skips its own pass."""
@@ -340,12 +346,22 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
     part = _empty((nrows * 2 * C,), F64, dev)
     call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
          ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
-    dgamma, dbeta = _empty((C,), F32, dev), _empty((C,), F32, dev)
+    # arena parameters (gamma, beta): the finalizer accumulates into their
+    # gradient views and autograd gets None
+    tg = tb = None
+    if params is not None:
+        tg, tb = direct_grad(params[0]), direct_grad(params[1])
+        if tg is None or tb is None:
+            tg = tb = None
+    dgamma = tg if tg is not None else _empty((C,), F32, dev)
+    dbeta = tb if tb is not None else _empty((C,), F32, dev)
     coef = _empty((3 * C,), F32, dev)
     # eval mode: statistics are constants -> count -> inf removes the mean terms
     count = float(rows) if training else 1e300
-    call("acfe_bn_bwd_finalize", ptr(part), nrows, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
-         ptr(dbeta), ptr(coef), s)
+    call("acfe_bn_bwd_finalize_ex", ptr(part), nrows, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
+         ptr(dbeta), ptr(coef), int(tg is not None), s)
+    if tg is not None:
+        dgamma = dbeta = None
     dx = _empty(x.shape, x.dtype, dev)
     rate, seed = drop if drop is not None and drop[0] > 0.0 else (0.0, 0)
     if add is not None:
@@ -381,6 +397,7 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
 class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, link):
+        ctx.gb = (gamma, beta)
         y, saved = _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype)
         ctx.save_for_backward(x, *saved)
         ctx.conf = (relu, training, link)
@@ -396,7 +413,8 @@ class _BNFn(torch.autograd.Function):
             add, pool = link.take(), link.take_pool()
             if add is None and pool is None:
                 raise RuntimeError("ResidualLink: the shortcut gradient was not delivered before this BN's backward")
-        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool)
+        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool,
+                                    params=ctx.gb)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
@@ -412,6 +430,8 @@ class _ConvDropBNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
+        ctx.bias = b
+        ctx.gb = (gamma, beta)
         stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum = conf
         drop = (rate, seed) if training and rate > 0.0 else None
         u, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, training, drop)
@@ -427,9 +447,9 @@ class _ConvDropBNFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, u, *saved = ctx.saved_tensors
         stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum = ctx.conf
-        g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop)
+        g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop, params=ctx.gb)
         dx, dw, db = _conv_bwd(x, w, g, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               ctx.has_b and ctx.needs_input_grad[2])
+                               ctx.has_b and ctx.needs_input_grad[2], bias=ctx.bias)
         return dx, dw, db, dgamma, dbeta, None, None, None
 
 
@@ -468,6 +488,8 @@ class _C1BNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
+        ctx.bias = b
+        ctx.gb = (gamma, beta)
         training, relu, eps, momentum = conf
         N, H, W, C = x.shape
         K = w.shape[0]
@@ -588,6 +610,7 @@ class _ConvAddFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, sc, relu, want_stats, link):
+        ctx.bias = b
         N, H, W, C = x.shape
         K, R, S, _ = w.shape
         _, pt = same_padding(H, R, 1)
@@ -626,7 +649,7 @@ class _ConvAddFn(torch.autograd.Function):
                 call("acfe_relu_bwd", ptr(g), ptr(z), g.numel(), ptr(d), dtype_code(g.dtype), stream())
             g = d
         dx, dw, db = _conv_bwd(x, w, g, 1, pt, pl, H, W, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               has_b and ctx.needs_input_grad[2])
+                               has_b and ctx.needs_input_grad[2], bias=ctx.bias)
         if link is not None:  # the shortcut input's gradient is added by the linked BN backward
             link.grad = g
             return dx, dw, db, None, None, None, None
@@ -753,6 +776,7 @@ class _PoolDropBNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, mmean, mvar, conf):
+        ctx.gb = (gamma, beta)
         kh, kw, rate, seed, training, relu, eps, momentum = conf
         drop = (rate, seed) if training and rate > 0.0 else None
         u, amax, stats = _maxpool_fwd(x, kh, kw, drop, training)
@@ -766,7 +790,7 @@ class _PoolDropBNFn(torch.autograd.Function):
     def backward(ctx, dy):
         u, amax, *saved = ctx.saved_tensors
         kh, kw, rate, seed, training, relu, eps, momentum = ctx.conf
-        gu, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training)
+        gu, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, params=ctx.gb)
         dx = _maxpool_bwd(amax, gu, ctx.shape, kh, kw, ctx.drop)
         return dx, dgamma, dbeta, None, None, None
 
@@ -802,6 +826,8 @@ class _ConvPoolBNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
+        ctx.bias = b
+        ctx.gb = (gamma, beta)
         pt, pl, rate, seed, training, relu, eps, momentum = conf
         N, H, W, C = x.shape
         K = w.shape[0]
@@ -827,11 +853,11 @@ class _ConvPoolBNFn(torch.autograd.Function):
         N, H, W, C = x.shape
         K = w.shape[0]
         dev, s = x.device, stream()
-        g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop)
+        g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop, params=ctx.gb)
         if not UNPOOL:  # materialise the pool backward, then the plain dgrad / wgrad
             dfull = _maxpool_bwd(amax, g, (N, H, W, K), 2, 2, None)
             dx, dw, db = _conv_bwd(x, w, dfull, 1, pt, pl, H, W, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                                   ctx.has_b and ctx.needs_input_grad[2])
+                                   ctx.has_b and ctx.needs_input_grad[2], bias=ctx.bias)
             return dx, dw, db, dgamma, dbeta, None, None, None
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -850,7 +876,10 @@ class _ConvPoolBNFn(torch.autograd.Function):
             if tgt is not None:
                 dw = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = channel_sum(g, K)  # the pool backward scatters: sum of the pooled gradient
+            tb = direct_grad(ctx.bias)  # the pool backward scatters: sum of the pooled gradient
+            db = channel_sum(g, K, into=tb)
+            if tb is not None:
+                db = None
         return dx, dw, db, dgamma, dbeta, None, None, None
 
 

@@ -447,14 +447,14 @@ __global__ void __launch_bounds__(SLAB_THREADS) k_bn_bwd_finalize(const double* 
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ invstd,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                         float* __restrict__ coef) {
+                                                         float* __restrict__ coef, int acc) {
   __shared__ double s[2][32];
   slab_sum32(part, nrows, C, C, s);
   const int c = blockIdx.x * 32 + threadIdx.x;
   if (threadIdx.x >= 32 || c >= C) return;
   const double sg = s[0][threadIdx.x], sgx = s[1][threadIdx.x];
-  if (dgamma) dgamma[c] = (float)sgx;
-  if (dbeta) dbeta[c] = (float)sg;
+  if (dgamma) dgamma[c] = acc ? dgamma[c] + (float)sgx : (float)sgx;
+  if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)sg : (float)sg;
   const double sc = scale[c], is = invstd[c], mu = mean[c];
   const double mg = sg / count, mgx = sgx / count;
   coef[c] = (float)sc;
@@ -462,13 +462,19 @@ __global__ void __launch_bounds__(SLAB_THREADS) k_bn_bwd_finalize(const double* 
   coef[2 * C + c] = (float)(-sc * mg + sc * mgx * is * mu);
 }
 
+ACFE_API int acfe_bn_bwd_finalize_ex(const double* part, int nrows, int C, double count, const float* scale,
+                                     const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                     float* coef, int accumulate, void* stream) {
+  if (!part || !scale || !mean || !invstd || !coef || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, count, scale,
+                     mean, invstd, dgamma, dbeta, coef, accumulate ? 1 : 0);
+  return launch_rc("acfe_bn_bwd_finalize");
+}
+
 ACFE_API int acfe_bn_bwd_finalize(const double* part, int nrows, int C, double count, const float* scale,
                                   const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                   float* coef, void* stream) {
-  if (!part || !scale || !mean || !invstd || !coef || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, count, scale,
-                     mean, invstd, dgamma, dbeta, coef);
-  return launch_rc("acfe_bn_bwd_finalize");
+  return acfe_bn_bwd_finalize_ex(part, nrows, C, count, scale, mean, invstd, dgamma, dbeta, coef, 0, stream);
 }
 
 // dx = a*g + b*x + c  (+ add[i] if add != NULL); g relu-masked as in the reduce

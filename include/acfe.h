@@ -207,6 +207,11 @@ int acfe_bn_bwd_reduce(const void* dy, int dy_dtype, const void* x, int x_dtype,
 int acfe_bn_bwd_finalize(const double* partial, int nrows, int C, double count, const float* scale,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
                          void* stream);
+/* As acfe_bn_bwd_finalize; accumulate != 0 adds dgamma / dbeta into the given
+ * buffers (a framework's gradient arena) instead of overwriting them. */
+int acfe_bn_bwd_finalize_ex(const double* partial, int nrows, int C, double count, const float* scale,
+                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
+                            int accumulate, void* stream);
 int acfe_bn_bwd_apply(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                       const float* scale, const float* shift, int relu, const float* coef, const void* add,
                       void* dx, int dx_dtype, void* stream);
