@@ -154,3 +154,42 @@ def test_bird_shapes_reference_config(cuda):
     n = sum(p.numel() for p in m.parameters())
     assert 2.2e6 < n < 2.4e6, n
     assert abs(flops_per_clip(m) / 1e9 - 16.91) < 0.05
+
+
+@pytest.mark.parametrize("kind", ["bird", "wrn"])
+@pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
+def test_arena_gradients_match_autograd(cuda, kind, training):
+    """Parameters in a ParamArena get their conv-weight, conv-bias and BN
+    gamma/beta gradients accumulated in place by the producing kernels (beta 1
+    into the zeroed arena, autograd sees None): bit-identical to the gradients
+    autograd assigns without the arena, and a second backward without
+    zero_grad accumulates (2x)."""
+    from acfe import ops
+    from acfe.layers import ParamArena
+
+    H, W, classes, N = 128, 64, 10, 2
+    tgt = torch.zeros(N, classes, device=cuda)
+    tgt[0, 3] = tgt[1, 7] = 1
+    x = _input(N, H, W).to(torch.bfloat16).to(cuda)
+    grads = []
+    for use_arena in (False, True):
+        m = _build(kind, (H, W, 3), classes, torch.bfloat16, cuda)
+        m.train(training)
+        arena = ParamArena(m, cuda) if use_arena else None
+        if arena is not None:
+            arena.zero_grad()
+        z = m(x)
+        _, dz = ops.loss_and_grad(z, tgt, "cce")
+        z.backward(dz)
+        grads.append([p.grad.detach().clone() for p in m.parameters()])
+        if arena is not None:
+            z = m(x)
+            _, dz = ops.loss_and_grad(z, tgt, "cce")
+            z.backward(dz)
+            again = [p.grad.detach().clone() for p in m.parameters()]
+    names = [n for n, _ in m.named_parameters()]
+    for n, a, b in zip(names, grads[0], grads[1]):
+        assert torch.equal(a, b), (n, rel(b, a))
+    for n, a, b in zip(names, grads[1], again):
+        if not training:  # training-mode BN statistics move between the two forwards
+            torch.testing.assert_close(b, 2 * a, rtol=1e-5, atol=1e-6, msg=n)
