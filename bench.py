@@ -271,11 +271,14 @@ def main():
             "wgrad_tflops": round(flops_launch / (wgrad_ms * 1e-3) / 1e12, 2),
         },
         "mel_pipeline": {
-            "kernel": "k_mel<2048> (frame+Hann+4096 rFFT+|X|^2+banded mel)",
+            "kernel": "k_mel_w (wave per frame: frame+Hann+4096 rFFT+|X|^2+banded mel)",
             "avg_launch_ms": round(mel_ms, 4),
             "GBps": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2),
             "hbm_frac": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9 / MI355X_PEAK_HBM_GBS, 4),
             "bytes_per_clip": FRONTEND_BYTES_PER_CLIP,
+            # 68.87 MFLOP per clip (FFT + power + banded mel), fp32 VALU peak 157.3 TFLOP/s
+            "valu_tflops": round(a.batch * 68.87e6 / (mel_ms * 1e-3) / 1e12, 2),
+            "valu_frac": round(a.batch * 68.87e6 / (mel_ms * 1e-3) / 1e12 / 157.3, 4),
         },
         "model_tflops_fwd_bwd": round(3 * (flops_per_clip(model) if flops_per_clip else 64.956e9) * value / 1e12, 2),
         "final_loss": round(loss_v, 5),
