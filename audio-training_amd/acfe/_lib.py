@@ -83,6 +83,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_maxpool2d": [P, I32, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_maxpool2d_bwd": [P, P, I32, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_maxpool2d_fused": [P, I32, I32, I32, I32, I32, I32, P, P, F32, C.c_uint64, P, I32, P],
+    "acfe_bn_maxpool2d_fused": [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, P, I32, P],
     "acfe_maxpool2d_bwd_argmax": [P, P, I32, I32, I32, I32, I32, I32, F32, C.c_uint64, P, I32, P],
     "acfe_avgpool2d": [P, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_avgpool2d_bwd": [P, I32, I32, I32, I32, I32, P, I32, P],

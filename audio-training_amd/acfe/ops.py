@@ -327,6 +327,8 @@ def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, o
     else:
         call("acfe_bn_finalize", None, 0, C, C, 0.0, ptr(gamma), ptr(beta), eps, momentum, ptr(mmean), ptr(mvar),
              0, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
+    if out_dtype is None:  # affine only: the caller applies it (bn_max_pool)
+        return None, (scale, shift, mean, invstd)
     y = _empty(x.shape, out_dtype, dev)
     call("acfe_bn_apply", ptr(x), dt, rows, C, ptr(scale), ptr(shift), int(relu), ptr(y), dtype_code(out_dtype), s)
     return y, (scale, shift, mean, invstd)
@@ -762,6 +764,55 @@ class _MaxPoolFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         call("acfe_maxpool2d_bwd", ptr(x), ptr(g), N, H, W, C, kh, kw, ptr(dx), dtype_code(x.dtype), stream())
         return dx, None, None, None
+
+
+class _BNPoolFn(torch.autograd.Function):
+    """MaxPool2D((kh, kw))(BatchNormalization(x)) (+ReLU) as one node: the
+    normalised tensor is formed at load time inside the pooling kernel
+    (acfe_bn_maxpool2d_fused) and never stored; the backward expands the pooled
+    gradient from the argmax bytes and runs the BN backward on x."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, mmean, mvar, stats, conf):
+        ctx.gb = (gamma, beta)
+        kh, kw, training, relu, eps, momentum, want_stats = conf
+        _, saved = _bn_fwd(x, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
+                           None)
+        N, H, W, C = x.shape
+        P, Q = H // kh, W // kw
+        y = _empty((N, P, Q, C), x.dtype, x.device)
+        amax = _empty((N, P, Q, C), torch.uint8, x.device)
+        pst = _no_stats(x.device)
+        if want_stats:
+            pst = _empty((lib.acfe_reduce_blocks(N * P * Q), 2, C), F64, x.device)
+        call("acfe_bn_maxpool2d_fused", ptr(x), N, H, W, C, ptr(saved[0]), ptr(saved[1]), int(relu), kh, kw, ptr(y),
+             ptr(amax), ptr(pst) if want_stats else None, dtype_code(x.dtype), stream())
+        ctx.save_for_backward(x, amax, *saved)
+        ctx.conf = conf
+        ctx.mark_non_differentiable(pst)
+        return y, pst
+
+    @staticmethod
+    def backward(ctx, g, _gs):
+        x, amax, *saved = ctx.saved_tensors
+        kh, kw, training, relu, eps, momentum, want_stats = ctx.conf
+        gu = _maxpool_bwd(amax, g, x.shape, kh, kw, None)
+        dx, dgamma, dbeta = _bn_bwd(x, gu, saved, relu, training, params=ctx.gb)
+        return dx, dgamma, dbeta, None, None, None, None
+
+
+def bn_max_pool(x, gamma, beta, mmean, mvar, training, kh, kw, relu=False, stats=None, eps=1e-3, momentum=0.99,
+                want_stats=False):
+    """MaxPool2D((kh, kw))(BatchNormalization(x)) (+ReLU) -> (y, stats slab of y
+    or None).  wr_resnet_bird.py:29-30 (stem BN -> MaxPool2D((1, 2)))."""
+    if not FUSE or not _pool_fused_ok(x, kh, kw):
+        y = batch_norm(x, gamma, beta, mmean, mvar, training, relu=relu, stats=stats, eps=eps, momentum=momentum)
+        if want_stats:
+            return max_pool(y, kh, kw, want_stats=True)
+        return max_pool(y, kh, kw), None
+    conf = (kh, kw, bool(training), bool(relu), float(eps), float(momentum), bool(want_stats))
+    y, st = _BNPoolFn.apply(x, gamma, beta, mmean, mvar, stats, conf)
+    return y, (st if want_stats else None)
 
 
 def max_pool(x, kh, kw, want_stats=False):

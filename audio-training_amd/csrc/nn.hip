@@ -957,7 +957,8 @@ ACFE_API int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int
 template <typename T, int KH, int KW>
 __global__ void __launch_bounds__(256) k_maxpool8x(const T* __restrict__ x, int N, int H, int W, int C, int P, int Q,
                                                    T* __restrict__ y, uint8_t* __restrict__ amax, Drop drop,
-                                                   double* __restrict__ part) {
+                                                   double* __restrict__ part, const float* __restrict__ bsc,
+                                                   const float* __restrict__ bsh, int brelu) {
   extern __shared__ double red[];  // [2][C] when part
   if (part) {
     for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
@@ -976,16 +977,29 @@ __global__ void __launch_bounds__(256) k_maxpool8x(const T* __restrict__ x, int 
     t /= Q;
     const int p = (int)(t % P);
     const int n = (int)(t / P);
-    float m[8];
+    float m[8], s8[8], h8[8];
     int am[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = -INFINITY, am[j] = 0;
+    if (bsc) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s8[j] = bsc[cv * 8 + j], h8[j] = bsh[cv * 8 + j];
+    }
 #pragma unroll
     for (int a = 0; a < KH; ++a)
 #pragma unroll
       for (int b = 0; b < KW; ++b) {
         float f[8];
         ld8(x + (((size_t)n * H + p * KH + a) * W + q * KW + b) * C + cv * 8, f);
+        if (bsc) {
+          // the BatchNormalization (+ReLU) output acfe_bn_apply would have stored
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float v = f[j] * s8[j] + h8[j];
+            if (brelu) v = fmaxf(v, 0.f);
+            f[j] = rnd(v, T());
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (f[j] > m[j]) m[j] = f[j], am[j] = a * KW + b;
@@ -1061,15 +1075,15 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd8i(const uint8_t* __restrict
 }
 
 
-ACFE_API int acfe_maxpool2d_fused(const void* x, int N, int H, int W, int C, int kh, int kw, void* y,
-                                  uint8_t* argmax, float drop_rate, unsigned long long seed, double* stats_part,
-                                  int dtype, void* stream) {
+static int maxpool_fused_impl(const void* x, int N, int H, int W, int C, int kh, int kw, void* y, uint8_t* argmax,
+                              float drop_rate, unsigned long long seed, double* stats_part, int dtype,
+                              const float* bsc, const float* bsh, int brelu, void* stream) {
   if (!x || !y || N <= 0 || kh <= 0 || kw <= 0 || H < kh || W < kw || drop_rate < 0.f || drop_rate >= 1.f)
     return ACFE_E_INVAL;
   const int P = H / kh, Q = W / kw;
   const long long rows = (long long)N * P * Q;
   if (!vec_ok((long long)N * H * W * C, C, x, y) || ((uintptr_t)argmax & 7) || rows * (C / 8) >= 0xFFFFFFFFll ||
-      (stats_part && !stats8_ok(C)))
+      (stats_part && !stats8_ok(C)) || (!bsc != !bsh))
     return ACFE_E_INVAL;
   const Drop d = make_drop(drop_rate, seed);
   const int grid = stats_part ? red_blocks(rows) : vgrid(rows * C / 8);
@@ -1077,12 +1091,30 @@ ACFE_API int acfe_maxpool2d_fused(const void* x, int N, int H, int W, int C, int
 #define MPF(A, B)                                                                                           \
   if (kh == A && kw == B) {                                                                                 \
     DISPATCH1(dtype, T, hipLaunchKernelGGL((k_maxpool8x<T, A, B>), dim3(grid), dim3(256), shm, strm(stream),  \
-                                           (const T*)x, N, H, W, C, P, Q, (T*)y, argmax, d, stats_part));   \
+                                           (const T*)x, N, H, W, C, P, Q, (T*)y, argmax, d, stats_part, bsc,  \
+                                           bsh, brelu));                                                     \
     return launch_rc("acfe_maxpool2d_fused");                                                               \
   }
   MAXPOOL_SHAPES(MPF)
 #undef MPF
   return ACFE_E_INVAL;
+}
+
+ACFE_API int acfe_maxpool2d_fused(const void* x, int N, int H, int W, int C, int kh, int kw, void* y,
+                                  uint8_t* argmax, float drop_rate, unsigned long long seed, double* stats_part,
+                                  int dtype, void* stream) {
+  return maxpool_fused_impl(x, N, H, W, C, kh, kw, y, argmax, drop_rate, seed, stats_part, dtype, nullptr, nullptr, 0,
+                            stream);
+}
+
+// MaxPool2D of BatchNormalization(x) (+ReLU): the normalised tensor is formed in
+// registers at load time and never stored (scale / shift from acfe_bn_finalize).
+ACFE_API int acfe_bn_maxpool2d_fused(const void* x, int N, int H, int W, int C, const float* scale,
+                                     const float* shift, int relu, int kh, int kw, void* y, uint8_t* argmax,
+                                     double* stats_part, int dtype, void* stream) {
+  if (!scale || !shift) return ACFE_E_INVAL;
+  return maxpool_fused_impl(x, N, H, W, C, kh, kw, y, argmax, 0.f, 0, stats_part, dtype, scale, shift, relu ? 1 : 0,
+                            stream);
 }
 
 ACFE_API int acfe_maxpool2d_bwd_argmax(const uint8_t* argmax, const void* dy, int N, int H, int W, int C, int kh,

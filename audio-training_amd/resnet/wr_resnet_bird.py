@@ -117,12 +117,9 @@ class WRResNet(nn.Module):
         if x.dim() == 4:
             x = x[..., 0]
         y, st = self.conv1_1(x, want_stats=True)
-        y = self.bn_stem(y, stats=st)
-        st = None
-        if self.training:
-            y, st = ops.max_pool(y, 1, 2, want_stats=True)
-        else:
-            y = ops.max_pool(y, 1, 2)
+        bn = self.bn_stem  # BN -> MaxPool2D((1, 2)) as one node: the normalised stem output is never stored
+        y, st = ops.bn_max_pool(y, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance, self.training, 1, 2,
+                                stats=st, eps=bn.eps, momentum=bn.momentum, want_stats=self.training)
         for blk in self.blocks:
             y, st = blk(y, st)
         y = self.final_bn(y, relu=True, stats=st)

@@ -324,6 +324,14 @@ int acfe_maxpool2d_bwd(const void* x, const void* dy, int N, int H, int W, int C
  * argmax byte of every output element (first maximum, may be NULL; 8-B aligned). */
 int acfe_maxpool2d_fused(const void* x, int N, int H, int W, int C, int kh, int kw, void* y, uint8_t* argmax,
                          float drop_rate, unsigned long long seed, double* partial, int dtype, void* stream);
+/* MaxPool2D((kh, kw)) of BatchNormalization(x) (+ReLU) with y = x * scale[c] +
+ * shift[c] formed at load time and rounded to the storage type, exactly the
+ * values acfe_bn_apply would store; argmax bytes and BN statistics of the
+ * pooled output as acfe_maxpool2d_fused (no dropout).  Replaces the
+ * BatchNormalization -> MaxPool2D((1, 2)) pair of wr_resnet_bird.py:29-30. */
+int acfe_bn_maxpool2d_fused(const void* x, int N, int H, int W, int C, const float* scale, const float* shift,
+                            int relu, int kh, int kw, void* y, uint8_t* argmax, double* stats_part, int dtype,
+                            void* stream);
 /* Backward of acfe_maxpool2d_fused from its argmax bytes (x is not re-read). */
 int acfe_maxpool2d_bwd_argmax(const uint8_t* argmax, const void* dy, int N, int H, int W, int C, int kh, int kw,
                               float drop_rate, unsigned long long seed, void* dx, int dtype, void* stream);

@@ -452,3 +452,36 @@ def test_conv_add_node(env, cuda, relu, C, K):
     torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-6, atol=1e-4)
     for i in range(2, 6):
         assert rel(outs[1][i], outs[0][i]) < 1e-3, (i, rel(outs[1][i], outs[0][i]))
+
+
+@pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32], ids=["bf16", "f32"])
+def test_bn_maxpool_node(env, cuda, training, dtype, monkeypatch):
+    """MaxPool2D((1, 2))(BatchNormalization(x)) with the BN formed at load time
+    inside the pooling kernel (acfe_bn_maxpool2d_fused) == batch_norm -> max_pool:
+    pooled output bit-exact, statistics of it to 1e-6, gradients of x, gamma
+    and beta identical up to summation order."""
+    ops = env[0]
+    N, H, W, C = 2, 16, 66, 16
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x0 = (torch.randn((N, H, W, C), generator=g) * 2 + 0.3).to(dtype).to(cuda)
+    gamma0 = (1 + 0.2 * torch.randn(C, generator=g)).to(cuda)
+    beta0 = (0.1 * torch.randn(C, generator=g)).to(cuda)
+    mm0 = (0.1 * torch.randn(C, generator=g)).to(cuda)
+    mv0 = (1 + torch.rand(C, generator=g)).to(cuda)
+    gy = torch.randn((N, H, W // 2, C), generator=g).to(dtype).to(cuda)
+    outs = []
+    for fuse in (False, True):
+        monkeypatch.setattr(ops, "FUSE", fuse)
+        x = x0.clone().requires_grad_(True)
+        gamma, beta = gamma0.clone().requires_grad_(True), beta0.clone().requires_grad_(True)
+        mm, mv = mm0.clone(), mv0.clone()
+        y, st = ops.bn_max_pool(x, gamma, beta, mm, mv, training, 1, 2, want_stats=training)
+        y.backward(gy)
+        outs.append([y, st, x.grad, gamma.grad, beta.grad, mm, mv])
+    assert torch.equal(outs[1][0], outs[0][0])
+    if training:
+        torch.testing.assert_close(outs[1][1].sum(0), outs[0][1].sum(0), rtol=1e-6, atol=1e-4)
+        assert torch.equal(outs[1][5], outs[0][5]) and torch.equal(outs[1][6], outs[0][6])
+    for i in (2, 3, 4):
+        assert rel(outs[1][i], outs[0][i]) < 1e-5, (i, rel(outs[1][i], outs[0][i]))
