@@ -740,7 +740,12 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
 // Outputs go through an LDS tile so the [B][M][T] writes are row-contiguous.
 constexpr int PCEN_TCH = 32;
 
-ACFE_API int acfe_pcen_partials(int batch, int n_mels) { return cdiv((int64_t)batch * n_mels, 256); }
+// 64 (b, m) rows per 256-thread workgroup: one wave runs the sequential EMA of
+// a 32-step chunk (a few dependent VALU ops per step, from LDS), then all four
+// waves evaluate the compression terms (the powf / logf bulk) of 8 steps each,
+// so 4 waves per SIMD instead of one hide the transcendental latency.
+constexpr int PCEN_RB = 64;
+ACFE_API int acfe_pcen_partials(int batch, int n_mels) { return cdiv((int64_t)batch * n_mels, PCEN_RB); }
 
 struct PcenP {
   float g, b, r, w, inv_r, bpow;
@@ -765,32 +770,52 @@ __device__ __forceinline__ float ema_step(float w, float x, float a) {
 __global__ void __launch_bounds__(256) k_pcen_fwd(const float* __restrict__ mel, int B, int T, int M,
                                                   const float* __restrict__ prm, float eps,
                                                   float* __restrict__ y, float* __restrict__ part) {
-  __shared__ float tile[256][PCEN_TCH + 1];
+  __shared__ float xs[PCEN_TCH][PCEN_RB + 1];    // x chunk [t][row]
+  __shared__ float as[PCEN_TCH][PCEN_RB + 1];    // EMA a_t
+  __shared__ float tile[PCEN_RB][PCEN_TCH + 1];  // output chunk [row][t]
   const PcenP P = pcen_params(prm);
   const int64_t rows = (int64_t)B * M;
-  const int64_t row0 = (int64_t)blockIdx.x * 256;
-  const int64_t gr = row0 + threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * PCEN_RB;
+  const int r = threadIdx.x & (PCEN_RB - 1), sub = threadIdx.x / PCEN_RB;
+  const int64_t gr = row0 + r;
   const bool valid = gr < rows;
   const int bb = valid ? (int)(gr / M) : 0, m = valid ? (int)(gr % M) : 0;
   const float* xr = mel + (int64_t)bb * T * M + m;
-  float a = valid ? xr[0] : 0.f;
+  float a = (valid && sub == 0) ? xr[0] : 0.f;
   float lmin = INFINITY, lmax = -INFINITY;
-  const int nrow = (int)((rows - row0) < 256 ? (rows - row0) : 256);
+  const int nrow = (int)((rows - row0) < PCEN_RB ? (rows - row0) : PCEN_RB);
+  constexpr int PER = PCEN_TCH / 4;
   for (int t0 = 0; t0 < T; t0 += PCEN_TCH) {
     const int tn = (T - t0) < PCEN_TCH ? (T - t0) : PCEN_TCH;
     if (valid) {
-      // the chunk's inputs are independent of the recurrence: issue all loads first
-      float xs[PCEN_TCH];
 #pragma unroll
-      for (int tt = 0; tt < PCEN_TCH; ++tt) xs[tt] = tt < tn ? xr[(int64_t)(t0 + tt) * M] : 0.f;
+      for (int k = 0; k < PER; ++k) {
+        const int tt = sub * PER + k;
+        if (tt < tn) xs[tt][r] = xr[(int64_t)(t0 + tt) * M];
+      }
+    }
+    __syncthreads();
+    if (valid && sub == 0) {
+      float xv[PCEN_TCH];
 #pragma unroll
-      for (int tt = 0; tt < PCEN_TCH; ++tt) {
+      for (int tt = 0; tt < PCEN_TCH; ++tt) xv[tt] = xs[tt][r];
+#pragma unroll
+      for (int tt = 0; tt < PCEN_TCH; ++tt)
         if (tt < tn) {
-          const float x = xs[tt];
-          a = ema_step(P.w, x, a);
+          a = ema_step(P.w, xv[tt], a);
+          as[tt][r] = a;
+        }
+    }
+    __syncthreads();
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int tt = sub * PER + k;
+        if (tt < tn) {
+          const float x = xs[tt][r], at = as[tt][r];
           const float v =
-              __fsub_rn(powf(__fadd_rn(__fdiv_rn(x, powf(__fadd_rn(eps, a), P.g)), P.b), P.inv_r), P.bpow);
-          tile[threadIdx.x][tt] = v;
+              __fsub_rn(powf(__fadd_rn(__fdiv_rn(x, powf(__fadd_rn(eps, at), P.g)), P.b), P.inv_r), P.bpow);
+          tile[r][tt] = v;
           lmin = fminf(lmin, v);
           lmax = fmaxf(lmax, v);
         }
@@ -798,10 +823,10 @@ __global__ void __launch_bounds__(256) k_pcen_fwd(const float* __restrict__ mel,
     }
     __syncthreads();
     for (int i = threadIdx.x; i < nrow * PCEN_TCH; i += 256) {
-      const int r = i / PCEN_TCH, tt = i % PCEN_TCH;
-      if (tt < tn) y[(row0 + r) * T + t0 + tt] = tile[r][tt];
+      const int r2 = i / PCEN_TCH, tt = i % PCEN_TCH;
+      if (tt < tn) y[(row0 + r2) * T + t0 + tt] = tile[r2][tt];
     }
-    __syncthreads();
+    // the next chunk writes xs, then (after a barrier) as, then tile: no barrier needed here
   }
   __shared__ float smn[4], smx[4];
   lmin = wave_min(lmin);
@@ -900,45 +925,67 @@ __global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel,
                                                   const float* __restrict__ st,
                                                   const void* __restrict__ dout, int ddt,
                                                   double* __restrict__ part) {
-  __shared__ float tile[256][PCEN_TCH + 1];
+  __shared__ float xs[PCEN_TCH][PCEN_RB + 1];
+  __shared__ float as[PCEN_TCH][PCEN_RB + 1];    // a_t
+  __shared__ float das[PCEN_TCH][PCEN_RB + 1];   // d a_t / d w
+  __shared__ float tile[PCEN_RB][PCEN_TCH + 1];  // dL/dout chunk [row][t]
   __shared__ double red[4][PCEN_NACC];
   const PcenP P = pcen_params(prm);
   const float mn = st[0], mx = st[1];
   const int64_t rows = (int64_t)B * M;
-  const int64_t row0 = (int64_t)blockIdx.x * 256;
-  const int64_t gr = row0 + threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * PCEN_RB;
+  const int r = threadIdx.x & (PCEN_RB - 1), sub = threadIdx.x / PCEN_RB;
+  const int64_t gr = row0 + r;
   const bool valid = gr < rows;
   const int bb = valid ? (int)(gr / M) : 0, m = valid ? (int)(gr % M) : 0;
   const float* xr = mel + (int64_t)bb * T * M + m;
-  const int nrow = (int)((rows - row0) < 256 ? (rows - row0) : 256);
+  const int nrow = (int)((rows - row0) < PCEN_RB ? (rows - row0) : PCEN_RB);
+  constexpr int PER = PCEN_TCH / 4;
   float acc[PCEN_NACC];
 #pragma unroll
   for (int i = 0; i < PCEN_NACC; ++i) acc[i] = 0.f;
-  float a = valid ? xr[0] : 0.f, da = 0.f;
+  float a = (valid && sub == 0) ? xr[0] : 0.f, da = 0.f;
   const float lnb = logf(P.b);
   for (int t0 = 0; t0 < T; t0 += PCEN_TCH) {
     const int tn = (T - t0) < PCEN_TCH ? (T - t0) : PCEN_TCH;
     for (int i = threadIdx.x; i < nrow * PCEN_TCH; i += 256) {
-      const int r = i / PCEN_TCH, tt = i % PCEN_TCH;
+      const int r2 = i / PCEN_TCH, tt = i % PCEN_TCH;
       if (tt < tn) {
-        const int64_t o = (row0 + r) * T + t0 + tt;
-        tile[r][tt] = ddt == ACFE_DTYPE_BF16 ? bf2f(reinterpret_cast<const uint16_t*>(dout)[o])
-                                             : reinterpret_cast<const float*>(dout)[o];
+        const int64_t o = (row0 + r2) * T + t0 + tt;
+        tile[r2][tt] = ddt == ACFE_DTYPE_BF16 ? bf2f(reinterpret_cast<const uint16_t*>(dout)[o])
+                                              : reinterpret_cast<const float*>(dout)[o];
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int tt = sub * PER + k;
+        if (tt < tn) xs[tt][r] = xr[(int64_t)(t0 + tt) * M];
       }
     }
     __syncthreads();
+    if (valid && sub == 0) {
+      float xv[PCEN_TCH];
+#pragma unroll
+      for (int tt = 0; tt < PCEN_TCH; ++tt) xv[tt] = xs[tt][r];
+#pragma unroll
+      for (int tt = 0; tt < PCEN_TCH; ++tt)
+        if (tt < tn) {
+          const float a_prev = a;
+          a = ema_step(P.w, xv[tt], a);                // bit-identical to the forward
+          da = (xv[tt] - a_prev) + (1.0f - P.w) * da;  // d a_t / d w
+          as[tt][r] = a;
+          das[tt][r] = da;
+        }
+    }
+    __syncthreads();
     if (valid) {
-      float xs[PCEN_TCH];
 #pragma unroll
-      for (int tt = 0; tt < PCEN_TCH; ++tt) xs[tt] = tt < tn ? xr[(int64_t)(t0 + tt) * M] : 0.f;
-#pragma unroll
-      for (int tt = 0; tt < PCEN_TCH; ++tt) {
+      for (int k = 0; k < PER; ++k) {
+        const int tt = sub * PER + k;
         if (tt >= tn) continue;
-        const float x = xs[tt];
-        const float a_prev = a;
-        a = ema_step(P.w, x, a);                     // bit-identical to the forward
-        da = (x - a_prev) + (1.0f - P.w) * da;       // d a_t / d w
-        const float s = __fadd_rn(eps, a);
+        const float x = xs[tt][r], at = as[tt][r], dat = das[tt][r];
+        const float s = __fadd_rn(eps, at);
         const float sg = powf(s, P.g);
         const float q = __fdiv_rn(x, sg);
         const float u = __fadd_rn(q, P.b);
@@ -948,8 +995,8 @@ __global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel,
         const float d_g = dydu * (-q * logf(s));
         const float d_b = dydu - P.inv_r * P.bpow / P.b;
         const float d_r = -(P.inv_r * P.inv_r) * (ur * logf(u) - P.bpow * lnb);
-        const float d_w = dydu * (-P.g * q / s) * da;
-        const float d = tile[threadIdx.x][tt];
+        const float d_w = dydu * (-P.g * q / s) * dat;
+        const float d = tile[r][tt];
         acc[0] += d * d_g; acc[1] += d * d_b; acc[2] += d * d_r; acc[3] += d * d_w;
         if (y == mx) { acc[4] += d_g; acc[5] += d_b; acc[6] += d_r; acc[7] += d_w; }
         if (y == mn) { acc[8] += d_g; acc[9] += d_b; acc[10] += d_r; acc[11] += d_w; }
@@ -957,7 +1004,7 @@ __global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel,
         acc[13] += d * y;
       }
     }
-    __syncthreads();
+    __syncthreads();  // tile / xs / as are rewritten by the next chunk
   }
 #pragma unroll
   for (int i = 0; i < PCEN_NACC; ++i) {
@@ -970,14 +1017,23 @@ __global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel,
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-__global__ void __launch_bounds__(64) k_pcen_bwd_fin(const double* __restrict__ part, int np,
-                                                     const float* __restrict__ prm,
-                                                     const float* __restrict__ st,
-                                                     float* __restrict__ dparams) {
+__global__ void __launch_bounds__(256) k_pcen_bwd_fin(const double* __restrict__ part, int np,
+                                                      const float* __restrict__ prm,
+                                                      const float* __restrict__ st,
+                                                      float* __restrict__ dparams) {
+  // 16 lanes per accumulator, each summing every 16th partial; fixed-order combine
+  __shared__ double ps[PCEN_NACC][17];
   __shared__ double tot[PCEN_NACC];
+  const int acc_i = threadIdx.x >> 4, l = threadIdx.x & 15;
+  if (acc_i < PCEN_NACC) {
+    double s = 0.0;
+    for (int i = l; i < np; i += 16) s += part[(int64_t)i * 16 + acc_i];
+    ps[acc_i][l] = s;
+  }
+  __syncthreads();
   if (threadIdx.x < PCEN_NACC) {
     double s = 0.0;
-    for (int i = 0; i < np; ++i) s += part[(int64_t)i * 16 + threadIdx.x];
+    for (int j = 0; j < 16; ++j) s += ps[threadIdx.x][j];
     tot[threadIdx.x] = s;
   }
   __syncthreads();
@@ -1013,7 +1069,7 @@ ACFE_API int acfe_pcen_bwd(const float* mel, int batch, int t, int m, const floa
                      stats, dout, ddt, part);
   int rc = launch_rc("acfe_pcen_bwd");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_pcen_bwd_fin, dim3(1), dim3(64), 0, strm(stream), part, np, params, stats,
+  hipLaunchKernelGGL(k_pcen_bwd_fin, dim3(1), dim3(256), 0, strm(stream), part, np, params, stats,
                      dparams);
   return launch_rc("acfe_pcen_bwd_fin");
 }

@@ -33,7 +33,7 @@ def test_host_only_calls():
     from acfe import _lib
 
     assert _lib.lib.acfe_version() >= 100
-    assert _lib.lib.acfe_pcen_partials(512, 128) == 256
+    assert _lib.lib.acfe_pcen_partials(512, 128) == 1024  # 64 (b, m) rows per PCEN workgroup
     # invalid arguments are reported, not crashed on
     assert _lib.lib.acfe_mel_filterbank(0, 128, 100.0, 11000.0, 4096, 1000.0, None) == _lib.E_INVAL
 
