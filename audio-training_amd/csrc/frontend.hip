@@ -541,15 +541,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
                                               int n_mels, int kmin, int kmax, float* __restrict__ out,
                                               int layout) {
   constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16;
-  extern __shared__ float2 wbuf[];  // [NC + NC/8] padded points, then [nk] power bins
-  float* pw = reinterpret_cast<float*>(wbuf + NC + NC / 8);
+  // [NC + NC/8] padded points; the nk (+8 zero) power bins reuse the front of
+  // that buffer once the FFT has been read (nk <= 1024: 18 KB per wave, so 8
+  // waves fit a CU's LDS), else they follow it
+  extern __shared__ float2 wbuf[];
+  const int nk = kmax - kmin + 1;
+  const bool alias = nk <= 1024;
+  float* pw = alias ? reinterpret_cast<float*>(wbuf) : reinterpret_cast<float*>(wbuf + NC + NC / 8);
   const int lane = threadIdx.x;
   const int b = blockIdx.y;
   const float* xb = raw + (int64_t)b * cs;
   const bool do_norm = stats != nullptr;
   const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
-  const int nk = kmax - kmin + 1;
-  if (lane < 8) pw[nk + lane] = 0.f;
   const int f0 = blockIdx.x * fpw;
   // the lane's base twiddles of passes 2 and 3 (W^{t}, W^{2t}, W^{4t}, W^{8t}
   // with t = jm * NC / (NS R)) stay in 32 VGPRs for all of its frames
@@ -630,11 +633,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // per lane per round with their rtw loads issued together
     for (int i0 = lane; i0 < nk; i0 += 1024) {
       float2 rt[16];
+      float pv[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) rt[u] = i0 + 64 * u < nk ? rtw[kmin + i0 + 64 * u] : make_float2(0.f, 0.f);
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int i = i0 + 64 * u;
+        pv[u] = 0.f;
         if (i < nk) {
           const int k = kmin + i;
           const float2 zk = wbuf[padx(k & (NC - 1))];
@@ -643,10 +648,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
           const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
           const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
           const float2 X = cadd(E, cmul(rt[u], O));
-          pw[i] = X.x * X.x + X.y * X.y;
+          pv[u] = X.x * X.x + X.y * X.y;
         }
       }
+      if (alias) __syncthreads();  // every lane's FFT reads precede the aliased writes (one round)
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (i0 + 64 * u < nk) pw[i0 + 64 * u] = pv[u];
     }
+    if (lane < 8) pw[nk + lane] = 0.f;  // the mel loop's padded 8-tap groups read up to nk + 7
     if (power != 2) {
       for (int k = lane; k < nk; k += 64) pw[k] = sqrtf(pw[k]);
     }
@@ -710,7 +720,7 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
     }();
     const int fpw = fpw_env;
     const int nk = p->kmax - p->kmin + 1;
-    const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + sizeof(float) * (nk + 8);
+    const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + (nk <= 1024 ? 0 : sizeof(float) * (nk + 8));
     hipLaunchKernelGGL(k_mel_w, dim3(cdiv(T, fpw), batch), dim3(64), shm, strm(stream), raw, cs, n, stats,
                        pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
                        p->n_mels, p->kmin, p->kmax, out, layout);
