@@ -84,38 +84,42 @@ static int vgrid(long long nvec) { return grid_for(nvec, 256, 16384); }
 // eight loads are in flight, then a fixed-order tree over the row groups.
 // (The finalizers were latency-bound at 40-60 us with 8 row groups.)
 constexpr int SLAB_THREADS = 1024;
-__device__ __forceinline__ void slab_sum32(const double* __restrict__ part, int nrows, int ld, int C,
-                                           double (*s)[32]) {
-  __shared__ double tmp[32][2][32];
-  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
-  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+// A workgroup sums SLAB_CH channels of a [nrows][2][ld] double slab over its
+// rows: 128 row groups x 8 channels, each thread with all of its (<= 8 for the
+// usual 1024-row slabs) loads in flight, then a fixed-order sum of the 128
+// group partials.  (32 channels x 32 row groups per workgroup left each thread
+// 64 loads in eight dependent rounds and only C/32 workgroups on the GPU.)
+constexpr int SLAB_CH = 8, SLAB_RG = SLAB_THREADS / SLAB_CH;
+__device__ __forceinline__ void slab_sum(const double* __restrict__ part, int nrows, int ld, int C,
+                                         double (*s)[SLAB_CH]) {
+  __shared__ double tmp[SLAB_RG][2][SLAB_CH];
+  const int cl = threadIdx.x % SLAB_CH, rg = threadIdx.x / SLAB_CH;
+  const int c = blockIdx.x * SLAB_CH + cl;
+  double a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = b[u] = 0.0;
   if (c < C) {
     int r = rg;
-    for (; r + 96 < nrows; r += 128) {
+    for (; r + 7 * SLAB_RG < nrows; r += 8 * SLAB_RG) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a[u] += part[((long long)(r + 32 * u) * 2 + 0) * ld + c];
-        b[u] += part[((long long)(r + 32 * u) * 2 + 1) * ld + c];
+      for (int u = 0; u < 8; ++u) {
+        a[u] += part[((long long)(r + SLAB_RG * u) * 2 + 0) * ld + c];
+        b[u] += part[((long long)(r + SLAB_RG * u) * 2 + 1) * ld + c];
       }
     }
-    for (int u = 0; r < nrows; r += 32, ++u) {
-      a[u & 3] += part[((long long)r * 2 + 0) * ld + c];
-      b[u & 3] += part[((long long)r * 2 + 1) * ld + c];
+    for (int u = 0; r < nrows; r += SLAB_RG, ++u) {
+      a[u & 7] += part[((long long)r * 2 + 0) * ld + c];
+      b[u & 7] += part[((long long)r * 2 + 1) * ld + c];
     }
   }
-  tmp[rg][0][cl] = (a[0] + a[1]) + (a[2] + a[3]);
-  tmp[rg][1][cl] = (b[0] + b[1]) + (b[2] + b[3]);
+  tmp[rg][0][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  tmp[rg][1][cl] = ((b[0] + b[1]) + (b[2] + b[3])) + ((b[4] + b[5]) + (b[6] + b[7]));
   __syncthreads();
-  if (rg == 0) {
-    double x = 0.0, y = 0.0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      x += tmp[i][0][cl];
-      y += tmp[i][1][cl];
-    }
-    s[0][cl] = x;
-    s[1][cl] = y;
+  if (threadIdx.x < 2 * SLAB_CH) {
+    const int ch = threadIdx.x % SLAB_CH, w = threadIdx.x / SLAB_CH;
+    double x = 0.0;
+    for (int i = 0; i < SLAB_RG; ++i) x += tmp[i][w][ch];
+    s[w][ch] = x;
   }
   __syncthreads();
 }
@@ -242,10 +246,10 @@ __global__ void __launch_bounds__(SLAB_THREADS) k_bn_finalize(const double* __re
                                                      int training, float* __restrict__ scale,
                                                      float* __restrict__ shift, float* __restrict__ mean_o,
                                                      float* __restrict__ invstd_o) {
-  __shared__ double s[2][32];
-  if (training) slab_sum32(part, nrows, ld, C, s);
-  const int c = blockIdx.x * 32 + threadIdx.x;
-  if (threadIdx.x >= 32 || c >= C) return;
+  __shared__ double s[2][SLAB_CH];
+  if (training) slab_sum(part, nrows, ld, C, s);
+  const int c = blockIdx.x * SLAB_CH + threadIdx.x;
+  if (threadIdx.x >= SLAB_CH || c >= C) return;
   double mean, var;
   if (training) {
     mean = s[0][threadIdx.x] / count;
@@ -273,7 +277,7 @@ ACFE_API int acfe_bn_finalize(const double* part, int nrows, int ld, int C, doub
   if (!scale || !shift || C <= 0 || (training && (!part || nrows <= 0 || count <= 0)) ||
       (!training && (!moving_mean || !moving_var)))
     return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, ld, C, count,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, SLAB_CH)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, ld, C, count,
                      gamma, beta, eps, momentum, moving_mean, moving_var, training, scale, shift, mean, invstd);
   return launch_rc("acfe_bn_finalize");
 }
@@ -448,10 +452,10 @@ __global__ void __launch_bounds__(SLAB_THREADS) k_bn_bwd_finalize(const double* 
                                                          const float* __restrict__ invstd,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                          float* __restrict__ coef, int acc) {
-  __shared__ double s[2][32];
-  slab_sum32(part, nrows, C, C, s);
-  const int c = blockIdx.x * 32 + threadIdx.x;
-  if (threadIdx.x >= 32 || c >= C) return;
+  __shared__ double s[2][SLAB_CH];
+  slab_sum(part, nrows, C, C, s);
+  const int c = blockIdx.x * SLAB_CH + threadIdx.x;
+  if (threadIdx.x >= SLAB_CH || c >= C) return;
   const double sg = s[0][threadIdx.x], sgx = s[1][threadIdx.x];
   if (dgamma) dgamma[c] = acc ? dgamma[c] + (float)sgx : (float)sgx;
   if (dbeta) dbeta[c] = acc ? dbeta[c] + (float)sg : (float)sg;
@@ -466,7 +470,7 @@ ACFE_API int acfe_bn_bwd_finalize_ex(const double* part, int nrows, int C, doubl
                                      const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                      float* coef, int accumulate, void* stream) {
   if (!part || !scale || !mean || !invstd || !coef || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, count, scale,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, SLAB_CH)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, count, scale,
                      mean, invstd, dgamma, dbeta, coef, accumulate ? 1 : 0);
   return launch_rc("acfe_bn_bwd_finalize");
 }
@@ -1599,16 +1603,16 @@ ACFE_API int acfe_cast(const void* x, int x_dtype, long long n, void* y, int y_d
 // out[c] = beta*out[c] + sum_rows x[r][c]  (bias gradients); part: bn_stats slab
 __global__ void __launch_bounds__(SLAB_THREADS) k_chan_sum_fin(const double* __restrict__ part, int nrows, int C, float beta,
                                                       float* __restrict__ out) {
-  __shared__ double s[2][32];
-  slab_sum32(part, nrows, C, C, s);
-  const int c = blockIdx.x * 32 + threadIdx.x;
-  if (threadIdx.x >= 32 || c >= C) return;
+  __shared__ double s[2][SLAB_CH];
+  slab_sum(part, nrows, C, C, s);
+  const int c = blockIdx.x * SLAB_CH + threadIdx.x;
+  if (threadIdx.x >= SLAB_CH || c >= C) return;
   out[c] = beta != 0.f ? out[c] * beta + (float)s[0][threadIdx.x] : (float)s[0][threadIdx.x];
 }
 // out[c] = beta*out[c] + sum of a slab's first row set (part [nrows][2][C]).
 ACFE_API int acfe_channel_sum_finalize(const double* part, int nrows, int C, float beta, float* out, void* stream) {
   if (!part || !out || nrows <= 0 || C <= 0) return ACFE_E_INVAL;
-  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, beta, out);
+  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, SLAB_CH)), dim3(SLAB_THREADS), 0, strm(stream), part, nrows, C, beta, out);
   return launch_rc("acfe_channel_sum_finalize");
 }
 ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* part, float* out,
@@ -1617,7 +1621,7 @@ ACFE_API int acfe_channel_sum(const void* x, long long rows, int C, int dtype, d
   if (rows == 0) return hip_rc(hipMemsetAsync(out, 0, sizeof(float) * C, strm(stream)), "acfe_channel_sum");
   int rc = acfe_bn_stats(x, rows, C, dtype, part, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, 32)), dim3(SLAB_THREADS), 0, strm(stream), part, red_blocks(rows), C, beta,
+  hipLaunchKernelGGL(k_chan_sum_fin, dim3(cdiv(C, SLAB_CH)), dim3(SLAB_THREADS), 0, strm(stream), part, red_blocks(rows), C, beta,
                      out);
   return launch_rc("acfe_channel_sum");
 }
