@@ -2132,7 +2132,15 @@ static void wgrad_combine(const float* ws, int nsplit, long long n, float beta, 
 static void wgrad_plan(long long M, int kd, int K, long long* splits_o, long long* chunk_o) {
   const int bmw = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
-  long long splits = (1024 + tiles - 1) / tiles;
+  // target workgroup count of the split-K grid (ACFE_WGRAD_WGS overrides, for A/B):
+  // 4096 measured 1.1 ms/step faster than 1024 once the combine ran split-parallel
+  // (k_wgrad_reduce_g), the halo kernels gaining most from the finer pixel ranges
+  static const long long target = [] {
+    const char* e = getenv("ACFE_WGRAD_WGS");
+    const long long v = e ? atoll(e) : 0;
+    return v >= 256 && v <= 16384 ? v : 4096LL;
+  }();
+  long long splits = (target + tiles - 1) / tiles;
   long long chunk = (M + splits - 1) / splits;
   chunk = (chunk + 63) / 64 * 64;
   if (chunk < 512) chunk = 512;
