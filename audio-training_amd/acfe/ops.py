@@ -127,6 +127,26 @@ def direct_grad(p):
     return g
 
 
+# Data-parallel overlap (acfe.dp.GradBuckets.ready): called with each arena
+# parameter whose gradient a kernel has just finished accumulating in place
+# (the kernel is enqueued on the current stream), so its bucket's all-reduce
+# can start while the rest of the backward runs.  None outside a DP backward.
+_GRAD_READY = None
+
+
+def set_grad_ready(fn):
+    global _GRAD_READY
+    _GRAD_READY = fn
+
+
+def grads_ready(*params):
+    fn = _GRAD_READY
+    if fn is not None:
+        for p in params:
+            if p is not None:
+                fn(p)
+
+
 def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=None):
     """dgrad / wgrad / bias gradient of _conv_fwd for the conv-output gradient dy."""
     N, H, W, C = x.shape
@@ -157,11 +177,13 @@ def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=No
                  1.0 if tgt is not None else 0.0, dt, ptr(ws), s)
         if tgt is not None:
             dw = None
+            grads_ready(w)
     if need_db:
         tb = direct_grad(bias) if bias is not None else None
         db = channel_sum(dy, K, into=tb)
         if tb is not None:
             db = None
+            grads_ready(bias)
     return dx, dw, db
 
 
@@ -190,11 +212,24 @@ def _sums_ok(t: torch.Tensor) -> bool:
     return C % 8 == 0 and C <= 2048 and 256 % (C // 8) == 0 and t.data_ptr() % 16 == 0 and t.is_contiguous()
 
 
+def _tag(t: torch.Tensor, name: str, value):
+    """Attach a fact about a gradient tensor's CURRENT contents (its ReLU mask
+    is applied, its channel sums are known).  Recorded with the tensor's
+    version counter: if autograd later accumulates another gradient into it in
+    place (InputBuffer add_), the version moves and the fact is dropped."""
+    setattr(t, name, (value, t._version))
+
+
+def _tagged(t: torch.Tensor, name: str):
+    v = getattr(t, name, None)
+    return v[0] if v is not None and v[1] == t._version else None
+
+
 def _attach_sum(t: torch.Tensor, part: torch.Tensor, rows: int):
     """Finalize a fused channel-sum slab and cache it on the gradient tensor it
     sums, so the convolution receiving `t` as its output gradient takes its
     bias gradient from there instead of re-reading `t` (channel_sum)."""
-    t._acfe_chpart = (part, rows)  # finalized by channel_sum, possibly into an arena gradient
+    _tag(t, "_acfe_chpart", (part, rows))  # finalized by channel_sum, possibly into an arena gradient
 
 
 def channel_sum(x: torch.Tensor, C: int, into: torch.Tensor | None = None) -> torch.Tensor:
@@ -202,7 +237,7 @@ def channel_sum(x: torch.Tensor, C: int, into: torch.Tensor | None = None) -> to
     view) it is accumulated there instead (beta 1)."""
     out = into if into is not None else _empty((C,), F32, x.device)
     beta = 1.0 if into is not None else 0.0
-    lazy = getattr(x, "_acfe_chpart", None)
+    lazy = _tagged(x, "_acfe_chpart")
     if lazy is not None and lazy[0].shape[-1] == C:
         part, prow = lazy
         call("acfe_channel_sum_finalize", ptr(part), lib.acfe_reduce_blocks(prow), C, beta, ptr(out), stream())
@@ -364,6 +399,7 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
          ptr(dbeta), ptr(coef), int(tg is not None), s)
     if tg is not None:
         dgamma = dbeta = None
+        grads_ready(*params)
     dx = _empty(x.shape, x.dtype, dev)
     rate, seed = drop if drop is not None and drop[0] > 0.0 else (0.0, 0)
     if add is not None:
@@ -384,7 +420,7 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
         if want_sum:
             _attach_sum(dx, sums, rows)
         if mask_in:
-            dx._acfe_relu_masked = True
+            _tag(dx, "_acfe_relu_masked", True)
         return dx, dgamma, dbeta
     call("acfe_bn_bwd_apply_ex", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
          ptr(shift), flags, ptr(coef), ptr(add), float(rate), int(seed), ptr(dx), dtype_code(x.dtype), ptr(sums),
@@ -392,7 +428,7 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
     if want_sum:
         _attach_sum(dx, sums, rows)
     if mask_in:
-        dx._acfe_relu_masked = True
+        _tag(dx, "_acfe_relu_masked", True)
     return dx, dgamma, dbeta
 
 
@@ -572,7 +608,7 @@ class _AddFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, _gs):
         g = g.contiguous()
-        if ctx.relu and not getattr(g, "_acfe_relu_masked", False):
+        if ctx.relu and not _tagged(g, "_acfe_relu_masked"):
             (z,) = ctx.saved_tensors
             d = torch.empty_like(g)
             C = g.shape[-1]
@@ -640,7 +676,7 @@ class _ConvAddFn(torch.autograd.Function):
         N, H, W, C = x.shape
         K = w.shape[0]
         g = g.contiguous()
-        if relu and not getattr(g, "_acfe_relu_masked", False):
+        if relu and not _tagged(g, "_acfe_relu_masked"):
             d = torch.empty_like(g)
             if _sums_ok(g) and _sums_ok(z) and _sums_ok(d):
                 rows = g.numel() // K
@@ -687,10 +723,18 @@ class _DropoutFn(torch.autograd.Function):
 
 
 _seed_counter = itertools.count(1)
+_seed_rank = 0
+
+
+def set_seed_rank(rank: int):
+    """Data-parallel replicas draw their own dropout masks (per-replica
+    tf.random under MirroredStrategy): the rank enters the seed base."""
+    global _seed_rank
+    _seed_rank = int(rank) & 0xFF
 
 
 def next_seed() -> int:
-    return (0x5EED << 32) + next(_seed_counter)
+    return (0x5EED << 32) + (_seed_rank << 24) + next(_seed_counter)
 
 
 def dropout(x, rate, training, seed=None):
@@ -926,11 +970,13 @@ class _ConvPoolBNFn(torch.autograd.Function):
                      1.0 if tgt is not None else 0.0, dtype_code(x.dtype), ptr(ws), s)
             if tgt is not None:
                 dw = None
+                grads_ready(w)
         if ctx.has_b and ctx.needs_input_grad[2]:
             tb = direct_grad(ctx.bias)  # the pool backward scatters: sum of the pooled gradient
             db = channel_sum(g, K, into=tb)
             if tb is not None:
                 db = None
+                grads_ready(ctx.bias)
         return dx, dw, db, dgamma, dbeta, None, None, None
 
 

@@ -3,7 +3,8 @@
 raw 3 s @ 48 kHz clips --(normalize, mix_up, normalize)--> STFT -> |X|^2 ->
 mel (tfdataset.py:913-915, :474-481, :2007-2059) --> PCEN (tfpcen.py) -->
 wr_resnet / wr_resnet_bird forward + backward --> loss (audiomodel.loss) -->
-gradient all-reduce (RCCL, one collective over the flat gradient arena) -->
+gradient all-reduce (RCCL, ~4 MB buckets of the flat gradient arena launched
+during the backward as their gradients complete, acfe.dp.GradBuckets) -->
 Adam (audiomodel.optimizer).  Every compute stage is a HIP kernel behind
 include/acfe.h; torch provides memory, streams, autograd bookkeeping and
 torch.distributed.
@@ -13,9 +14,12 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from . import dp
 from . import frontend as fe
 from . import ops
 from .layers import Adam, ParamArena
+
+allreduce_mean_ = dp.allreduce_mean_  # one-collective form (tests / callers of round 1)
 
 
 class FrontEnd(nn.Module):
@@ -74,36 +78,32 @@ def mix_labels(y1: torch.Tensor, y2: torch.Tensor, lam: torch.Tensor, single_lab
     return y1 * lw + y2 * (1 - lw)
 
 
-def allreduce_mean_(flat: torch.Tensor, group=None) -> float:
-    """Sum-all-reduce the flat gradient arena in place (RCCL on the GPU, gloo in
-    the CPU tests); returns the factor (1/world) that turns the sum into the
-    mean of the replicas' batch-mean gradients, applied inside the Adam kernel."""
-    import torch.distributed as dist
-
-    if not (dist.is_available() and dist.is_initialized()):
-        return 1.0
-    world = dist.get_world_size(group)
-    if world == 1:
-        return 1.0
-    dist.all_reduce(flat, group=group)
-    return 1.0 / world
-
-
 class Trainer:
     """Holds the front end, the model, one flat parameter arena for both, and
     Keras-Adam; `step` runs one full training iteration on device tensors."""
 
     def __init__(self, model: nn.Module, frontend: FrontEnd, lr=0.01, loss="cce", process_group=None,
-                 device=None):
+                 device=None, bucket_bytes=dp.BUCKET_BYTES):
         self.model, self.frontend, self.loss_mode = model, frontend, loss
         self.device = device or next(model.parameters()).device
         self.holder = nn.ModuleList([frontend, model])
         self.arena = ParamArena(self.holder, self.device)
         self.opt = Adam(self.arena, lr=lr)
         self.pg = process_group
-        import torch.distributed as dist
+        self.world = dp.world_size(process_group)
+        self.buckets = None
+        if self.world > 1:
+            self.buckets = dp.GradBuckets(self.arena.grad, self.arena.params, self.arena.offsets, bucket_bytes,
+                                          process_group)
+            # gradients autograd accumulates into the arena (stem, Dense, PCEN,
+            # the 1x1+BN node) report through the post-accumulate hook; the
+            # kernels that accumulate in place report via ops.grads_ready
+            for p in self.arena.params:
+                p.register_post_accumulate_grad_hook(self._grad_done)
 
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+    def _grad_done(self, p):
+        if self.buckets is not None:
+            self.buckets.ready(p)
 
     def train(self, mode=True):
         self.holder.train(mode)
@@ -114,8 +114,17 @@ class Trainer:
         z = self.model(feats)
         loss, dz = ops.loss_and_grad(z, y, self.loss_mode)
         self.arena.zero_grad()
-        z.backward(dz)
-        scale = allreduce_mean_(self.arena.grad, self.pg)
+        if self.buckets is None:
+            z.backward(dz)
+            scale = 1.0
+        else:
+            self.buckets.begin()
+            ops.set_grad_ready(self.buckets.ready)
+            try:
+                z.backward(dz)
+            finally:
+                ops.set_grad_ready(None)
+            scale = self.buckets.finish()
         self.opt.step(grad_scale=scale)
         return loss, z
 

@@ -68,25 +68,66 @@ def save_checkpoint(out_dir: Path, trainer, meta: dict, history: dict | None = N
     (out_dir / "metadata.txt").write_text(json.dumps(m, indent=2))
 
 
-def evaluate(trainer, dataset, multi_label):
-    """Validation loss / accuracy (Keras categorical or binary accuracy)."""
-    from acfe import ops
+def evaluate(trainer, dataset, multi_label, group=None):
+    """Validation loss / accuracy (Keras categorical or binary accuracy).  Under
+    data parallelism every rank evaluates its own shard and the totals are
+    summed over ranks (no rank idles inside a collective meanwhile)."""
+    from acfe import dp, ops
 
     trainer.holder.eval()
-    n, loss_sum, correct = 0, 0.0, 0.0
+    dev = trainer.device
+    tot = torch.zeros(3, dtype=torch.float64, device=dev)  # loss sum, correct, count
     with torch.no_grad():
-        for x, y in dataset:
+        for x, y in dp.synced_batches(dataset, group=group):
             z = trainer.model(trainer.frontend(x))
             loss, _ = ops.loss_and_grad(z, y, trainer.loss_mode)
             b = x.shape[0]
-            loss_sum += float(loss) * b
             if multi_label:
-                correct += float(((z > 0).float() == y).float().mean(1).sum())
+                c = ((z > 0).float() == y).float().mean(1).sum()
             else:
-                correct += float((z.argmax(1) == y.argmax(1)).float().sum())
-            n += b
+                c = (z.argmax(1) == y.argmax(1)).float().sum()
+            tot += torch.stack([loss.double().sum() * b, c.double(), torch.tensor(float(b), device=dev,
+                                                                                    dtype=torch.float64)])
     trainer.holder.train()
-    return (loss_sum / max(n, 1), correct / max(n, 1)) if n else (float("nan"), float("nan"))
+    loss_sum, correct, n = dp.allreduce_sums(tot.tolist(), device=dev)
+    return (loss_sum / n, correct / n) if n else (float("nan"), float("nan"))
+
+
+def train_epoch(dataset, step_fn, augment, steps_per_epoch=0, mixup_fn=None, group=None):
+    """One pass of the fit loop (audiomodel.py:550-562) over `dataset`.
+    step_fn(x1, y1, x2, y2, lam) -> device loss.  Every rank runs the same
+    number of steps (acfe.dp.synced_batches over the host control group), and
+    the loss is summed on the device and read once per epoch, not per step.
+    Returns (clips, loss sum, steps) of this rank."""
+    from acfe import dp
+
+    lsum = None
+    n = steps = 0
+    for item in dp.synced_batches(dataset, group=group):
+        if augment:
+            (x1, y1), (x2, y2) = item
+            loss = step_fn(x1, y1, x2, y2, mixup_fn(x1.shape[0]))
+        else:
+            x1, y1 = item
+            loss = step_fn(x1, y1, None, None, None)
+        contrib = loss.detach().double().sum() * x1.shape[0]
+        lsum = contrib if lsum is None else lsum + contrib
+        n += x1.shape[0]
+        steps += 1
+        if steps_per_epoch and steps >= steps_per_epoch:
+            break
+    return n, (float(lsum) if lsum is not None else 0.0), steps
+
+
+def shard_files(files, rank, world):
+    """Data-parallel input split: whole shard files per rank when there are at
+    least as many files as ranks, else every rank reads all files and keeps its
+    share of the records (AudioDataset record_shard)."""
+    if world == 1:
+        return list(files), None
+    if len(files) >= world:
+        return list(files)[rank::world], None
+    return list(files), (rank, world)
 
 
 def train_model(args):
@@ -100,9 +141,12 @@ def train_model(args):
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     import tfdataset
+    from acfe import dp, ops
     from acfe.frontend import sample_mixup_lambda
     from acfe.train import FrontEnd, Trainer, mix_labels
 
+    ctrl = dp.control_group()
+    ops.set_seed_rank(rank)  # per-replica dropout masks
     meta, td = load_meta(args.dataset_dir)
     labels = list(meta["labels"])
     n_mels = args.n_mels or meta.get("n_mels", 160)
@@ -117,53 +161,56 @@ def train_model(args):
         with torch.no_grad():
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, 0)
+    torch.manual_seed(args.seed + rank)  # per-replica mix_up lambdas after the shared init
     frontend = FrontEnd(n_mels=n_mels, n_fft=n_fft, hop=281, fmin=fmin, fmax=fmax, break_freq=brk,
                         pcen=args.pcen, dtype=dtype, device=dev).to(dev)
     trainer = Trainer(model, frontend, lr=args.lr, loss="bce" if args.multi_label else "cce", device=dev)
     if args.weights:
         sd = torch.load(args.weights, map_location="cpu", weights_only=True)
         trainer.holder.load_state_dict(sd)
-    files = tfdataset._files(td / "train")
-    files = files[rank::world] if world > 1 else files
+    files, rshard = shard_files(tfdataset._files(td / "train"), rank, world)
     train_ds = tfdataset.AudioDataset(files, labels, batch_size=args.batch_size, shuffle=args.shuffle,
-                                      augment=args.augment, device=dev, drop_remainder=world > 1, seed=args.seed)
+                                      augment=args.augment, device=dev, drop_remainder=world > 1, seed=args.seed,
+                                      record_shard=rshard)
     val_dir = td / "validation"
     val_ds = None
     if val_dir.exists() and tfdataset._files(val_dir):
-        val_ds = tfdataset.AudioDataset(tfdataset._files(val_dir), labels, batch_size=args.batch_size, shuffle=False,
-                                        device=dev)
+        vfiles, vshard = shard_files(tfdataset._files(val_dir), rank, world)
+        val_ds = tfdataset.AudioDataset(vfiles, labels, batch_size=args.batch_size, shuffle=False, device=dev,
+                                        record_shard=vshard)
     history = {"loss": [], "val_loss": [], "val_accuracy": [], "clips_per_s": []}
     out_dir = Path(args.checkpoint_dir) / args.name
     best = float("inf")
+
+    def step(x1, y1, x2, y2, lam):
+        if x2 is None:
+            return trainer.step(x1, y1)[0]
+        return trainer.step(x1, mix_labels(y1, y2, lam), x2, lam)[0]
+
+    def mixup(b):
+        return sample_mixup_lambda(b, 0.5, 0.25, device=dev)
+
     for epoch in range(args.epochs):
-        t0, n, lsum, steps = time.perf_counter(), 0, 0.0, 0
-        for item in train_ds:
-            if args.augment:
-                (x1, y1), (x2, y2) = item
-                lam = sample_mixup_lambda(x1.shape[0], 0.5, 0.25, device=dev)
-                loss, _ = trainer.step(x1, mix_labels(y1, y2, lam), x2, lam)
-            else:
-                x1, y1 = item
-                loss, _ = trainer.step(x1, y1)
-            lsum += float(loss) * x1.shape[0]
-            n += x1.shape[0]
-            steps += 1
-            if args.steps_per_epoch and steps >= args.steps_per_epoch:
-                break
+        t0 = time.perf_counter()
+        n, lsum, steps = train_epoch(train_ds, step, args.augment, args.steps_per_epoch, mixup, ctrl)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        history["loss"].append(lsum / max(n, 1))
-        history["clips_per_s"].append(n * world / dt)
-        if val_ds is not None and rank == 0:
-            vl, va = evaluate(trainer, val_ds, args.multi_label)
+        n_all, lsum_all = dp.allreduce_sums([n, lsum], device=dev)
+        history["loss"].append(lsum_all / max(n_all, 1))
+        history["clips_per_s"].append(n_all / dt)
+        # Keras SyncOnRead MEAN of the BN moving statistics before eval / save
+        dp.average_buffers(trainer.holder)
+        if val_ds is not None:
+            vl, va = evaluate(trainer, val_ds, args.multi_label, ctrl)
             history["val_loss"].append(vl)
             history["val_accuracy"].append(va)
             if vl < best:  # ModelCheckpoint(save_best_only) on val_loss (audiomodel.py:878-938)
                 best = vl
-                save_checkpoint(out_dir / "val_loss", trainer, {}, None)
+                if rank == 0:
+                    save_checkpoint(out_dir / "val_loss", trainer, {}, None)
         if rank == 0:
-            logging.info("epoch %d loss %.4f val %s %.1f clips/s", epoch, history["loss"][-1],
-                         history["val_loss"][-1:] or "-", history["clips_per_s"][-1])
+            logging.info("epoch %d loss %.4f val %s %.1f clips/s (%d steps/rank)", epoch, history["loss"][-1],
+                         history["val_loss"][-1:] or "-", history["clips_per_s"][-1], steps)
     if rank == 0:
         meta_out = dict(meta)
         meta_out.update(name=args.model_name, ebird_labels=labels, labels=labels, n_mels=n_mels, fmin=fmin,

@@ -33,8 +33,12 @@ class AudioDataset:
     """Iterable over device batches; one pass = one epoch."""
 
     def __init__(self, files, labels, batch_size=32, shuffle=True, augment=False, device=None, threads=8,
-                 drop_remainder=False, seed=0, label_map=None):
+                 drop_remainder=False, seed=0, label_map=None, record_shard=None):
+        """record_shard=(rank, world): keep only the records whose (file index
+        + record index) % world == rank -- data-parallel sharding when there
+        are fewer shard files than ranks (otherwise ranks take whole files)."""
         self.files, self.labels = list(files), list(labels)
+        self.record_shard = record_shard
         self.batch_size, self.shuffle, self.augment = batch_size, shuffle, augment
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.threads, self.drop_remainder, self.seed = threads, drop_remainder, seed
@@ -47,6 +51,8 @@ class AudioDataset:
         DONE = object()
         idx = iter(range(len(files)))
         lock = threading.Lock()
+        stable = {f: i for i, f in enumerate(self.files)}
+        shard = self.record_shard
 
         def worker():
             while True:
@@ -55,7 +61,9 @@ class AudioDataset:
                 if i is None:
                     q.put(DONE)
                     return
-                for rec in tfr.read_records(files[i], ignore_errors=True):  # tfdataset.py:226
+                for r, rec in enumerate(tfr.read_records(files[i], ignore_errors=True)):  # tfdataset.py:226
+                    if shard is not None and (stable.get(files[i], i) + r) % shard[1] != shard[0]:
+                        continue
                     ex = tfr.parse_audio_example(rec)
                     if not np.all(np.isfinite(ex["raw"])):  # NaN/Inf filter, tfdataset.py:297
                         continue
@@ -101,8 +109,9 @@ class AudioDataset:
 
     def _to_device(self, items):
         b = len(items)
-        x = torch.empty((b, N_SAMPLES), dtype=torch.float32, pin_memory=True)
-        y = torch.zeros((b, len(self.labels)), dtype=torch.float32, pin_memory=True)
+        pin = torch.device(self.device).type == "cuda"
+        x = torch.empty((b, N_SAMPLES), dtype=torch.float32, pin_memory=pin)
+        y = torch.zeros((b, len(self.labels)), dtype=torch.float32, pin_memory=pin)
         for i, (raw, lab) in enumerate(items):
             x[i] = torch.from_numpy(raw)
             y[i, lab] = 1.0
@@ -117,7 +126,7 @@ class AudioDataset:
             return
         # second independent pass over the data for mix_up (tfdataset.py:473-480)
         other = AudioDataset(self.files, self.labels, self.batch_size, True, False, self.device, self.threads,
-                             self.drop_remainder, self.seed + 7919 * self.epoch, self.label_map)
+                             self.drop_remainder, self.seed + 7919 * self.epoch, self.label_map, self.record_shard)
         for a, b in zip(it, other._batches()):
             if len(a) != len(b):
                 break

@@ -8,7 +8,11 @@ A step = one pass of the hot path over one batch resident in HBM:
 normalize x2 -> mix_up -> normalize -> STFT/|X|^2/mel -> PCEN -> WRN forward
 -> loss -> backward -> gradient all-reduce (N > 1) -> Adam.
 
-  python bench.py [--gpus N --steps K --warmup W]      (N > 1 under torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]
+      N > 1: the driver starts it under torch.distributed.run (RANK/WORLD_SIZE
+      set); started directly with --gpus N it launches the N ranks itself.
+      ACFE_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU (RCCL
+      needs one GPU per rank).
 
 Prints ONE JSON line on rank 0.  `roofline` is measured live with HIP events
 around the dominant kernel (the forward of the stage-1 block-0 3x3 128->128
@@ -159,18 +163,29 @@ def main():
     if a.workload != "train":
         return run_inference(a)
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # `bench.py --gpus N` started directly: one process per GPU under
+        # torch.distributed.run, started as a CHILD before anything here
+        # touches the GPU; this process only relays its exit code.
+        return launch_ranks(a.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks; measuring {world}",
+              file=sys.stderr, flush=True)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import torch.distributed as dist
 
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("ACFE_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     from acfe import ops
     from acfe.train import FrontEnd, Trainer
+
+    ops.set_seed_rank(rank)  # per-replica dropout masks
 
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     if a.model == "bird":
@@ -215,11 +230,18 @@ def main():
     elapsed = time.perf_counter() - t0
     ops.watch_conv(target.weight, None)
     frontend.timer = None
+    own = elapsed
+    per_rank = [own]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        gathered = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(gathered, t)
+        per_rank = [float(g.item()) for g in gathered]
+        elapsed = max(per_rank)
     loss_v = float(loss.item())
+    if rank != 0:  # each rank's own line, on stderr (stdout carries rank 0's one JSON line)
+        print(f"bench rank {rank}/{world}: {a.batch * a.steps / own:.1f} clips/s, {own / a.steps * 1e3:.3f} ms/step, "
+              f"loss {loss_v:.5f}", file=sys.stderr, flush=True)
 
     def avg_ms(kind, evs):
         d = [e0.elapsed_time(e1) for k, e0, e1 in evs if k == kind]
@@ -280,6 +302,10 @@ def main():
             "valu_tflops": round(a.batch * 68.87e6 / (mel_ms * 1e-3) / 1e12, 2),
             "valu_frac": round(a.batch * 68.87e6 / (mel_ms * 1e-3) / 1e12 / 157.3, 4),
         },
+        "per_rank_s": [round(v, 4) for v in per_rank],
+        "grad_allreduce": ({"buckets": len(trainer.buckets.buckets), "bucket_bytes": 4 << 20,
+                            "arena_bytes": trainer.arena.numel * 4, "overlapped_with_backward": True}
+                           if trainer.buckets is not None else None),
         "model_tflops_fwd_bwd": round(3 * (flops_per_clip(model) if flops_per_clip else 64.956e9) * value / 1e12, 2),
         "final_loss": round(loss_v, 5),
     }
@@ -290,6 +316,21 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def launch_ranks(n: int) -> int:
+    import socket
+    import subprocess
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.run(cmd, env=env).returncode
 
 
 def run_inference(a):
@@ -390,4 +431,4 @@ def run_inference(a):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -22,8 +22,9 @@ bf16 compute, vs the oracle with the same bf16 storage points (storage="bf16"):
     (floor measured between fp32- and fp64-accumulating bf16 oracles:
      1.2e-3 / 8.8e-3);
   training-mode BN on a 2-clip batch is chaotic at init -- the same two
-    oracles differ by 3.6% (logits) and 61% (gradients) -- so only
-    rel-L2(logits) <= 0.15 and finiteness are asserted there.
+    oracles differ by 3.6% (logits) and 61% (gradients) -- so logits are held
+    to rel-L2 <= 0.15 and every parameter gradient to the accuracy class of
+    the bf16 emulation against exact float64 math (see the test body).
 """
 import math
 
@@ -88,7 +89,7 @@ def test_model_step_parity(cuda, kind, prec, training):
 
     storage = "bf16" if dtype == torch.bfloat16 else None
 
-    def oracle(dt):
+    def oracle(dt, storage=storage):
         p = {k: v.detach().to(dt).cpu().clone() for k, v in m.state_dict().items()}
         prm = {k: v.requires_grad_(True) for k, v in p.items() if "moving" not in k}
         st = {k: v for k, v in p.items() if "moving" in k}
@@ -98,7 +99,7 @@ def test_model_step_parity(cuda, kind, prec, training):
         return z_, l_, prm, st
 
     z_ref, loss_ref, params, state = oracle(torch.float64)
-    _, _, params32, _ = oracle(torch.float32)
+    _z32, _, params32, _ = oracle(torch.float32)
     # device
     from acfe import ops
 
@@ -136,7 +137,25 @@ def test_model_step_parity(cuda, kind, prec, training):
     elif not training:
         assert rel(g_dev, g_ref) < 5e-2, rel(g_dev, g_ref)
     else:
+        # Training-mode BN in bf16 at init is dominated by rounding noise (the
+        # bf16-storage oracle itself is 0.6-1.0 rel-L2 from exact math on most
+        # conv gradients), so each parameter is held to the accuracy class of
+        # a faithful bf16 emulation: rel(dev, exact) <= 2 x the worse of the
+        # two bf16-storage oracles (f32 / f64 accumulation) + 0.02.  The head
+        # and Dense gradients, where the emulation is within 0.01-0.2 of exact,
+        # are bounded tightly; a wrong kernel is off by O(1) everywhere.
         assert torch.isfinite(g_dev).all()
+        z_ex, _, p_ex, _ = oracle(torch.float64, storage=None)
+        assert rel(z, z_ex) <= 2 * max(rel(z_ref, z_ex), rel(_z32, z_ex)) + 0.01
+        gnorm = torch.cat([p_ex[n].grad.reshape(-1) for n in names]).norm().item()
+        for n, q in m.named_parameters():
+            ex = p_ex[n].grad
+            if ex.norm().item() < 1e-9 * gnorm:  # zero in exact arithmetic (bias feeding a BN)
+                lim = 4 * max(params[n].grad.norm().item(), params32[n].grad.norm().item()) + 1e-6 * gnorm
+                assert q.grad.double().norm().item() <= lim, n
+                continue
+            e_or = max(rel(params[n].grad, ex), rel(params32[n].grad, ex))
+            assert rel(q.grad, ex) <= 2 * e_or + 0.02, (n, rel(q.grad, ex), e_or)
     # moving statistics updated like Keras (momentum 0.99)
     for k, v in state.items():
         assert rel(m.state_dict()[k], v) < (1e-4 if dtype == torch.float32 else 3e-2), k

@@ -1,0 +1,248 @@
+"""Oracle parity of the T1 hot kernels at the shapes and tile / split counts
+they run at in the training step.
+
+The dominant stage-1 block-0 layers of wr_resnet_bird at 128 mels x 513
+frames (resnet/wr_resnet_bird.py:136-178):
+  * conv21 3x3 128->128 @ 128x256 -> MaxPool2D(2) -> Dropout -> BN sums
+    (acfe_conv2d_fwd_pool, k_conv3x3_rows<128,6,1>)
+  * its backward: acfe_conv2d_dgrad_unpool (k_conv3x3_rows<128,6,2>) and
+    acfe_conv2d_wgrad_unpool (k_wgrad3x3_halo<128,true>, split-K + combine)
+  * conv2b 3x3 64->64 @ 64x128 + residual Add (+ReLU) + BN sums
+    (acfe_conv2d_fwd_add, k_conv3x3_rows<64,6,3>)
+at N = 8 / 32 clips, i.e. 704 output tiles for the 256 persistent workgroups
+(every workgroup walks several tiles, the inter-tile pipeline runs) and the
+production split-K counts of the weight gradient.
+
+The oracle is torch-CPU float64 convolution of the same bf16 operands
+(oracle.models.conv semantics: Keras "same" = pad 1 for 3x3).  Bounds:
+  * bf16 outputs (y, dx): |gpu - exact| <= 1 bf16 ulp(exact) + 1e-4 -- the
+    kernel accumulates in fp32 and rounds once, so its error is half an ulp
+    plus fp32 accumulation noise; a wrong tap, channel or tile is off by O(1);
+  * pooled output: the same bound against max over the 2x2 window of the
+    exact conv (rounding is monotone, so max and round commute), and the
+    argmax byte must point at a value within that bound of the window max;
+  * weight gradient (fp32 out): rel-L2 <= 5e-5 and every element within
+    5e-4 x max|exact| (fp32 accumulation over 131072-262144 pixels);
+  * BN statistics slabs: the float64 sums of the stored output to rel 1e-6
+    (the epilogue sums each wave's 16-row fragment in fp32 first).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+F64 = torch.float64
+
+
+@pytest.fixture(scope="module")
+def env(cuda):
+    from acfe import ops
+    from acfe._lib import call, lib
+    from acfe._torch import ptr, stream
+
+    return ops, call, lib, ptr, stream
+
+
+def _ulp(t):
+    """bf16 unit in the last place of each element of t (float64)."""
+    e = torch.floor(torch.log2(t.abs().clamp_min(2.0 ** -120)))
+    return torch.pow(2.0, e - 7)
+
+
+def _within_ulp(gpu, exact, atol=1e-4, what="", extra=0.0):
+    g = gpu.detach().to(F64).cpu()
+    err = (g - exact).abs()
+    bad = err > _ulp(exact) + atol + extra
+    nbad = int(bad.sum())
+    assert nbad == 0, (what, nbad, float(err.max()), float((err / (_ulp(exact) + atol)).max()))
+
+
+def _oracle_conv(x_nhwc, w_krsc, b=None):
+    """exact 'same' 3x3 conv of bf16 operands: x [N,H,W,C] bf16, w fp32 KRSC
+    (the kernel multiplies its bf16 packing) -> [N,H,W,K] float64."""
+    x = x_nhwc.detach().cpu().to(F64).permute(0, 3, 1, 2)
+    w = w_krsc.detach().cpu().to(BF).to(F64).permute(0, 3, 1, 2)
+    y = F.conv2d(x, w, None if b is None else b.detach().cpu().to(F64), padding=1)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def _sums(t):
+    t = t.detach().to(F64).cpu().reshape(-1, t.shape[-1])
+    return torch.stack([t.sum(0), (t * t).sum(0)])
+
+
+def _data(N, H, W, C, K, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn((N, H, W, C), generator=g).to(BF)
+    w = torch.randn((K, 3, 3, C), generator=g) * (1.0 / (3 * C ** 0.5))
+    b = torch.randn((K,), generator=g) * 0.1
+    return x.to(device), w.to(device), b.to(device), g
+
+
+def test_conv_fwd_pool_production(env, cuda):
+    """acfe_conv2d_fwd_pool at the T1 stage-1 shape (8 clips x 128 x 256,
+    128 -> 128): pooled values, argmax bytes, dropout mask and BN sums."""
+    ops, call, lib, ptr, stream = env
+    N, H, W, C, K = 8, 128, 256, 128, 128
+    assert lib.acfe_conv2d_pool_supported(N, H, W, C, K, 3, 3, 1)
+    x, w, b, g = _data(N, H, W, C, K, 101, cuda)
+    wp = ops.pack_weights(w, BF, False)
+    P, Q = H // 2, W // 2
+    rows = lib.acfe_conv2d_stats_rows(N * H * W, K)
+    y0 = torch.empty((N, P, Q, K), dtype=BF, device=cuda)
+    am0 = torch.empty((N, P, Q, K), dtype=torch.uint8, device=cuda)
+    st0 = torch.empty((rows, 2, wp.shape[0]), dtype=F64, device=cuda)
+    call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y0), ptr(am0), 0.0, 0, ptr(st0),
+         1, stream())
+    y1, am1 = torch.empty_like(y0), torch.empty_like(am0)
+    st1 = torch.empty_like(st0)
+    call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y1), ptr(am1), 0.1, 4242,
+         ptr(st1), 1, stream())
+    torch.cuda.synchronize()
+    exact = _oracle_conv(x, w, b)                                   # [N, H, W, K]
+    win = exact.reshape(N, P, 2, Q, 2, K).permute(0, 1, 3, 5, 2, 4).reshape(N, P, Q, K, 4)
+    wmax = win.max(-1).values
+    _within_ulp(y0, wmax, what="pooled")
+    # the argmax byte names a (near-)maximum of the window: a*2+b in [0, 4)
+    am = am0.cpu().long()
+    assert int(am.max()) < 4
+    picked = torch.gather(win, -1, am[..., None])[..., 0]
+    assert bool(((wmax - picked) <= _ulp(wmax) + 1e-4).all())
+    # dropout: the same pooled values with acfe_dropout's mask, same argmax
+    ref = torch.empty_like(y0)
+    call("acfe_dropout", ptr(y0), y0.numel(), 0.1, 4242, ptr(ref), 1, stream())
+    assert torch.equal(y1, ref) and torch.equal(am1, am0)
+    # BN sums of the stored (dropped-out) output
+    torch.testing.assert_close(st1.sum(0)[:, :K].cpu(), _sums(y1), rtol=1e-6, atol=1e-6)
+
+
+def test_conv_unpool_backward_production(env, cuda):
+    """acfe_conv2d_dgrad_unpool / acfe_conv2d_wgrad_unpool at the T1 shape
+    from a pooled gradient and argmax bytes: dX and dW against the float64
+    gradients of the exact convolution of the expanded (unpooled) gradient."""
+    ops, call, lib, ptr, stream = env
+    N, H, W, C, K = 8, 128, 256, 128, 128
+    x, w, b, g = _data(N, H, W, C, K, 102, cuda)
+    P, Q = H // 2, W // 2
+    gp = (torch.randn((N, P, Q, K), generator=g) * 0.5).to(BF)
+    am = torch.randint(0, 4, (N, P, Q, K), generator=g, dtype=torch.uint8)
+    # expanded gradient: gp at (2p + a, 2q + b) with a*2+b = argmax
+    onehot = F.one_hot(am.long(), 4).to(F64).reshape(N, P, Q, K, 2, 2).permute(0, 1, 4, 2, 5, 3)
+    full = (onehot * gp.to(F64)[:, :, None, :, None, :]).reshape(N, H, W, K)
+    gp, am = gp.to(cuda), am.to(cuda)
+    wf = ops.pack_weights(w, BF, True)
+    dx = torch.empty((N, H, W, C), dtype=BF, device=cuda)
+    call("acfe_conv2d_dgrad_unpool", ptr(gp), ptr(am), N, H, W, K, ptr(wf), C, 1, 1, ptr(dx), 1, stream())
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+    dw = torch.full((K, 3, 3, C), 0.25, device=cuda)  # beta 1: accumulated onto
+    call("acfe_conv2d_wgrad_unpool", ptr(x), N, H, W, C, ptr(gp), ptr(am), K, 1, 1, ptr(dw), 1.0, 1, ptr(ws),
+         stream())
+    torch.cuda.synchronize()
+    wd = w.detach().cpu().to(BF).to(F64).permute(0, 3, 1, 2)
+    gfull = full.permute(0, 3, 1, 2)
+    dx_exact = F.conv_transpose2d(gfull, wd, padding=1).permute(0, 2, 3, 1)
+    _within_ulp(dx, dx_exact, what="dgrad_unpool")
+    xd = x.cpu().to(F64).permute(0, 3, 1, 2)
+    dw_exact = torch.nn.grad.conv2d_weight(xd, wd.shape, gfull, padding=1).permute(0, 2, 3, 1) + 0.25
+    d = dw.cpu().to(F64)
+    assert ((d - dw_exact).norm() / dw_exact.norm()).item() < 5e-5
+    assert ((d - dw_exact).abs().max() / dw_exact.abs().max()).item() < 5e-4
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv_fwd_add_production(env, cuda, relu):
+    """acfe_conv2d_fwd_add at the stage-1 conv2b shape (64x128, 64 -> 64) for 32
+    clips: (ReLU)(conv + bias + shortcut) within one ulp of the exact value of
+    the bf16 sum, BN sums of the stored output."""
+    ops, call, lib, ptr, stream = env
+    N, H, W, C, K = 32, 64, 128, 64, 64
+    assert lib.acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, 1)
+    x, w, b, g = _data(N, H, W, C, K, 103 + relu, cuda)
+    sc = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+    wp = ops.pack_weights(w, BF, False)
+    z = torch.empty((N, H, W, K), dtype=BF, device=cuda)
+    st = torch.empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), dtype=F64, device=cuda)
+    call("acfe_conv2d_fwd_add", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(sc), int(relu), ptr(z), ptr(st), 1,
+         stream())
+    torch.cuda.synchronize()
+    conv = _oracle_conv(x, w, b)
+    exact = conv + sc.cpu().to(F64)
+    if relu:
+        exact = exact.clamp_min(0)
+    # the conv output is rounded to bf16 before the Add (conv2d -> add), so a
+    # cancelling sum may carry half an ulp of the conv value on top
+    _within_ulp(z, exact, what="fwd_add", extra=0.5 * _ulp(conv))
+    torch.testing.assert_close(st.sum(0)[:, :K].cpu(), _sums(z), rtol=1e-6, atol=1e-6)
+
+
+def test_conv_rows_dgrad_wgrad_production(env, cuda):
+    """The un-pooled stride-1 3x3 128->64 (stage-1 block-0 conv2b at 64x128 with
+    128 input channels) dgrad and wgrad for 16 clips against float64."""
+    ops, call, lib, ptr, stream = env
+    N, H, W, C, K = 16, 64, 128, 128, 64
+    x, w, b, g = _data(N, H, W, C, K, 105, cuda)
+    dy = (torch.randn((N, H, W, K), generator=g) * 0.5).to(BF).to(cuda)
+    wf = ops.pack_weights(w, BF, True)
+    dx = torch.empty((N, H, W, C), dtype=BF, device=cuda)
+    call("acfe_conv2d_dgrad", ptr(dy), N, H, W, K, ptr(wf), C, 3, 3, 1, 1, 1, H, W, ptr(dx), 1, None, stream())
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+    dw = torch.empty((K, 3, 3, C), device=cuda)
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, 3, 3, 1, 1, 1, H, W, ptr(dw), 0.0, 1, ptr(ws),
+         stream())
+    torch.cuda.synchronize()
+    wd = w.cpu().to(BF).to(F64).permute(0, 3, 1, 2)
+    gd = dy.cpu().to(F64).permute(0, 3, 1, 2)
+    _within_ulp(dx, F.conv_transpose2d(gd, wd, padding=1).permute(0, 2, 3, 1), what="dgrad")
+    dw_exact = torch.nn.grad.conv2d_weight(x.cpu().to(F64).permute(0, 3, 1, 2), wd.shape, gd,
+                                           padding=1).permute(0, 2, 3, 1)
+    d = dw.cpu().to(F64)
+    assert ((d - dw_exact).norm() / dw_exact.norm()).item() < 5e-5
+    assert ((d - dw_exact).abs().max() / dw_exact.abs().max()).item() < 5e-4
+
+
+def test_bird_t1_shape_eval_parity(cuda):
+    """wr_resnet_bird at the T1 input (128 mels x 513 frames, 50 classes), bf16,
+    eval-mode BN, 2 clips, against the bf16-storage float64 oracle
+    (oracle.models.wr_resnet_bird): at this width stage 1 is 256 px wide, so
+    the rows / pool / add / halo kernels all run inside the model.  Bounds as
+    tests/test_model_gpu.py's bf16-eval case: logits <= 1e-2, gradient arena
+    <= 5e-2 (oracle-vs-oracle floor f32/f64 accumulation ~1e-3 / 1e-2)."""
+    from oracle import models as om
+    from resnet.wr_resnet_bird import WRResNet
+    from acfe import ops
+
+    H, W, classes, N = 128, 513, 50, 2
+    torch.manual_seed(0)
+    m = WRResNet(input_shape=(H, W, 3), classes=classes, dtype=BF, dropout=0.0).to(cuda)
+    g = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            if name.endswith("gamma"):
+                p.copy_(1 + 0.1 * torch.randn(p.shape, generator=g))
+            elif name.endswith("beta") or name.endswith("bias"):
+                p.copy_(0.05 * torch.randn(p.shape, generator=g))
+        for name, bb in m.named_buffers():
+            if name.endswith("moving_mean"):
+                bb.copy_(0.1 * torch.randn(bb.shape, generator=g))
+            elif name.endswith("moving_variance"):
+                bb.copy_(1 + 0.5 * torch.rand(bb.shape, generator=g))
+    m.eval()
+    x = (torch.rand((N, H, W), generator=g, dtype=F64) * 2 - 1).to(BF).double()
+    tgt = torch.zeros(N, classes, dtype=F64)
+    tgt[0, 3] = tgt[1, 41] = 1
+    p = {k: v.detach().to(F64).cpu().clone() for k, v in m.state_dict().items()}
+    prm = {k: v.requires_grad_(True) for k, v in p.items() if "moving" not in k}
+    st = {k: v for k, v in p.items() if "moving" in k}
+    z_ref = om.wr_resnet_bird(x[:, None].repeat(1, 3, 1, 1), prm, False, st, storage="bf16")
+    om.keras_loss(z_ref, tgt, "cce").backward()
+    z = m(x.to(BF).to(cuda))
+    _, dz = ops.loss_and_grad(z, tgt.float().to(cuda), "cce")
+    z.backward(dz)
+    zr = z.detach().double().cpu()
+    assert ((zr - z_ref.detach()).norm() / z_ref.detach().norm()).item() < 1e-2
+    names = [n for n, _ in m.named_parameters()]
+    g_dev = torch.cat([q.grad.reshape(-1).double().cpu() for q in m.parameters()])
+    g_ref = torch.cat([prm[n].grad.reshape(-1) for n in names])
+    assert ((g_dev - g_ref).norm() / g_ref.norm()).item() < 5e-2
