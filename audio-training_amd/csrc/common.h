@@ -94,5 +94,21 @@ template <typename T>
 __device__ __forceinline__ float drop_apply(const Drop& d, uint64_t idx, float v) {
   return hash_u32(d.seed, idx) >= d.thr ? rnd(v * d.scl, T()) : 0.f;
 }
+// The same mask for an index known to be < 2^32 (hash_u32 with idx >> 32 == 0),
+// without the 64-bit index arithmetic.
+__device__ __forceinline__ uint32_t hash_u32_lo(uint64_t seed, uint32_t idx) {
+  uint32_t h = idx * 0x9E3779B1u + (uint32_t)seed;
+  h ^= (uint32_t)(seed >> 32);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+template <typename T>
+__device__ __forceinline__ float drop_apply32(const Drop& d, uint32_t idx, float v) {
+  return hash_u32_lo(d.seed, idx) >= d.thr ? rnd(v * d.scl, T()) : 0.f;
+}
 
 }  // namespace acfe

@@ -45,6 +45,7 @@ struct ConvGeom {
   int dbg;           // diagnostics (ACFE_CONV_DBG=8: loop-segment cycle stamps), 0 in production
   const uint16_t* res;  // k_conv3x3_rows PM 3: residual added in the epilogue (same layout as Y)
   int res_relu;         // PM 3: ReLU after the residual add
+  int idx32;            // M * K < 2^32: output element (dropout) indices fit 32 bits
 };
 
 // 64 bytes of zeros in global memory: im2col taps that fall into the padding
@@ -869,7 +870,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
                int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
   static_assert(PM != 1 || TR % 2 == 0, "2x2 pooling needs row pairs");
   using T = uint16_t;
-  constexpr int SEGW = 64, HWX = SEGW + 2, XRB = 144;           // pixels per row, halo row bytes
+  // pixels per row, halo row bytes: 160-B rows make the fragment reads
+  // conflict-free under ds_read_b128's lane grouping at every tap shift (144-B
+  // rows had 2-way conflicts: a third of the LDS cycles, rocprofv3 r02c)
+  constexpr int SEGW = 64, HWX = SEGW + 2, XRB = 160;
   constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
   constexpr int NBUF = TR <= 3 ? 2 : 1;                          // LDS buffers (single: store after a barrier)
   // 6-row tiles: weights by LDS-DMA into a double buffer (no staging VGPRs,
@@ -881,10 +885,9 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   constexpr int XPT = (XG + 511) / 512, WPT = WG / 512;
   static_assert(WG % 512 == 0, "weight granules per thread");
   constexpr int OFF_W2 = WDMA ? XBYTES + 2 * WBYTES : 0;           // WDMA layout: [X][W0][W1]
-  constexpr int OFF_STAT = WDMA ? OFF_W2 : NBUF * BUFB, OFF_BIAS = OFF_STAT + 2 * KB * 8;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_BIAS + KB * 4];
+  constexpr int OFF_STAT = WDMA ? OFF_W2 : NBUF * BUFB;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_STAT + 2 * KB * 8];
   double* sstat = reinterpret_cast<double*>(smem + OFF_STAT);
-  float* sbias = reinterpret_cast<float*>(smem + OFF_BIAS);
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = wid >> 2, wp = wid & 3;
@@ -892,7 +895,11 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   const int tpi = tiles_h * tiles_w;
   const T* zp = reinterpret_cast<const T*>(g_zero_page);
   for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
-  for (int i = tid; i < KB; i += 512) sbias[i] = bias ? bias[i] : 0.f;
+  // this lane's bias quads are loaded (f4, L2-resident) at each epilogue: no
+  // LDS copy (the 160-B image fills the LDS at K = 128) and no registers held
+  // across the main loop (the K = 128 variants sit at the 256-VGPR limit)
+  const float* bq = bias ? bias + wk * (KB / 2) + (lane >> 4) * 4 : reinterpret_cast<const float*>(g_zero_page);
+  const int bfs = bias ? 16 : 0;
   const TileWalk walk(ntiles);
   const int ntl = walk.tm < walk.end ? (walk.end - walk.tm + walk.step - 1) / walk.step : 0;
   const int L = ntl * nsteps_t;
@@ -924,58 +931,113 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
     for (int j = 0; j < (WDMA ? WPW : 0); ++j) bldsx4(voffW[j], dw, lb + j * 1024);
   };
-  auto gload = [&](int t) __attribute__((always_inline)) {
-    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
+  // Input staging without per-step address arithmetic: granule i of this
+  // thread is halo row xrow[i], halo pixel xpix[i], 16-B channel slot gr of the
+  // 64-channel chunk -- fixed for the whole kernel.  When the staged tile
+  // changes, each granule's byte offset inside its image (filter row 0, chunk
+  // 0) and a 3-bit mask of the filter rows r for which it lies inside the image
+  // are computed once; a step then adds the wave-uniform (r, chunk) delta and
+  // selects an out-of-range offset for masked granules, whose buffer loads
+  // return zeros (no branches, no 64-bit math).
+  const int gr = tid & 7;
+  // PM 2 (K = 128 sits at the register limit with the argmax bytes in flight)
+  // keeps no per-granule state: its offsets are recomputed per step from the
+  // wave-uniform tile origin (sh0, sw0)
+  int xoffs[PM == 2 ? 1 : XPT];
+  int sh0 = 0, sw0 = 0;       // PM 2: input row / column of halo pixel (0, 0) at filter row 0 (wave-uniform)
+  unsigned xm = 0;            // 4 mask bits per granule: filter rows 0..2 inside the image, (PM 2) column parity
+  int stl = -1;  // walk index of the tile the offsets belong to
+  __amdgpu_buffer_rsrc_t xrs, ars;
+  const int CB = g.C * 2;  // bytes per pixel
+  auto stage_tile = [&](int tl) __attribute__((always_inline)) {
     const int tm = walk.tm + tl * walk.step;
     const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
-    const int h0 = hb * TR, w0 = wb * SEGW;
+    const int h0 = hb * TR - g.pt, w0 = wb * SEGW - g.pl;
+    sh0 = h0;
+    sw0 = w0;
+    if constexpr (PM == 2) {
+      // X = pooled gradient [N][H/2][W/2][C], amax its argmax bytes
+      const long long img = (long long)n * (g.H >> 1) * (g.W >> 1) * g.C;
+      const int nb = (g.H >> 1) * (g.W >> 1) * g.C;
+      xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + img), (short)0, nb * 2, 0x00020000);
+      ars = __builtin_amdgcn_make_buffer_rsrc((void*)(amax + img), (short)0, nb, 0x00020000);
+    } else {
+      const long long img = (long long)n * g.H * g.W * g.C;
+      xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + img), (short)0, g.H * g.W * CB, 0x00020000);
+    }
+    xm = 0;
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
+    for (int i = 0; i < (PM == 2 ? 0 : XPT); ++i) {
       const int idx = tid + 512 * i;
-      const int row = idx / (HWX * 8), r2 = idx - row * (HWX * 8), hp = r2 >> 3, gr = r2 & 7;
-      const int hin = h0 + row + r - g.pt, win = w0 + hp - g.pl;
-      const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
-      if constexpr (PM == 2) {
-        const long long e =
-            (((long long)n * (g.H >> 1) + (hin >> 1)) * (g.W >> 1) + (win >> 1)) * g.C + cc * 64 + gr * 8;
-        rx[i] = *reinterpret_cast<const u32x4*>(ok ? X + e : zp);
-        ra[i] = *reinterpret_cast<const uint2*>(ok ? amax + e : reinterpret_cast<const uint8_t*>(zp));
+      const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
+      const int hin = h0 + xrow, win = w0 + xpix;
+      const bool ok = idx < XG && (unsigned)win < (unsigned)g.W;
+      unsigned m = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) m |= ((unsigned)(hin + r) < (unsigned)g.H ? 1u : 0u) << r;
+      m = ok ? m : 0u;
+      xoffs[i] = (hin * g.W + win) * CB + gr * 16;
+      xm |= m << (4 * i);
+    }
+  };
+  auto gload = [&](int t) __attribute__((always_inline)) {
+    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
+    if (tl != stl) {
+      stage_tile(tl);
+      stl = tl;
+    }
+    if constexpr (PM == 2) {
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int idx = tid + 512 * i;
+        const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
+        const int hin = sh0 + xrow + r, win = sw0 + xpix;
+        const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
+        const int e = ((hin >> 1) * (g.W >> 1) + (win >> 1)) * g.C + gr * 8 + cc * 64;
+        rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? e * 2 : 0x80000000, 0, 0);
+        const auto a8 = __builtin_amdgcn_raw_buffer_load_b64(ars, ok ? e : 0x80000000, 0, 0);
+        ra[i] = uint2{a8[0], a8[1]};
         if (i == 0) rpos = 0;
-        rpos |= (unsigned)(((hin & 1) << 1) | (win & 1)) << (2 * i);
-      } else {
-        rx[i] = *reinterpret_cast<const u32x4*>(
-            ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + gr * 8 : zp);
+        rpos |= (((unsigned)(hin & 1) << 1) | ((unsigned)win & 1u)) << (2 * i);
+      }
+    } else {
+      const int delta = r * g.W * CB + cc * 128;
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const bool ok = (xm >> (4 * i + r)) & 1u;
+        rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xoffs[i] + delta : 0x80000000, 0, 0);
       }
     }
     if constexpr (!WDMA) {
 #pragma unroll
       for (int i = 0; i < WPT; ++i) {
         const int idx = tid + 512 * i;
-        const int s = idx / (KB * 8), r2 = idx - s * (KB * 8), k = r2 >> 3, gr = r2 & 7;
-        rw[i] = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + (r * 3 + s) * g.C + cc * 64 + gr * 8);
+        const int s = idx / (KB * 8), r2 = idx - s * (KB * 8), k = r2 >> 3, gw = r2 & 7;
+        rw[i] = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + (r * 3 + s) * g.C + cc * 64 + gw * 8);
       }
     }
   };
+  // LDS image slot of granule i: halo pixel (tid >> 3) + 64 i, channel slot gr
+  const int xsto = (tid >> 3) * XRB + gr * 16;
   auto sstore = [&](int buf) __attribute__((always_inline)) {
     unsigned char* Xl = smem + buf * BUFB;
     unsigned char* Wl = Xl + XBYTES;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + 512 * i;
-      const int row = idx >> 3, gr = idx & 7;  // row = halo row * HWX + pixel
       if constexpr (PM == 2) {
         if (idx < XG)
-          *reinterpret_cast<u32x4*>(Xl + row * XRB + gr * 16) = rx[i] & unpool_mask(ra[i], (rpos >> (2 * i)) & 3u);
+          *reinterpret_cast<u32x4*>(Xl + xsto + i * 64 * XRB) = rx[i] & unpool_mask(ra[i], (rpos >> (2 * i)) & 3u);
       } else {
-        if (idx < XG) *reinterpret_cast<u32x4*>(Xl + row * XRB + gr * 16) = rx[i];
+        if (idx < XG) *reinterpret_cast<u32x4*>(Xl + xsto + i * 64 * XRB) = rx[i];
       }
     }
     if constexpr (!WDMA) {
 #pragma unroll
       for (int i = 0; i < WPT; ++i) {
         const int idx = tid + 512 * i;
-        const int row = idx >> 3, gr = idx & 7;  // row = s * KB + k
-        *reinterpret_cast<u32x4*>(Wl + row * 128 + ((gr ^ (row & 7)) << 4)) = rw[i];
+        const int row = idx >> 3, gw = idx & 7;  // row = s * KB + k
+        *reinterpret_cast<u32x4*>(Wl + row * 128 + ((gw ^ (row & 7)) << 4)) = rw[i];
       }
     }
   };
@@ -1024,50 +1086,74 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     float sv[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) sv[i] = 0.f;
+    // bias quad of fragment column fn (PM 2, the dgrad, has none)
+    auto bias4 = [&](int fn) __attribute__((always_inline)) {
+      return PM == 2 ? f4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f4*>(bq + fn * bfs);
+    };
     if constexpr (PM == 1) {
-      // 2x2 windows: rows (2i, 2i+1) in this lane's fragments, columns (l16, l16^1)
-      // in the neighbouring lane; window order (0,0),(0,1),(1,0),(1,1), first max wins
+      // 2x2 windows: rows (2i, 2i+1) in this lane's fragments, columns (l16,
+      // l16 ^ 1) in the neighbouring lane.  The lane pair splits each channel
+      // quad: the even lane pools channels 0-1, the odd lane 2-3, each getting
+      // the partner's column by one DPP swap per row -- half the max / argmax /
+      // dropout work of both lanes pooling all four.  Window order (0,0),(0,1),
+      // (1,0),(1,1), first maximum wins (acfe_maxpool2d_fused's argmax bytes).
       const int P2 = g.P >> 1, Q2 = g.Q >> 1;
       const int wq = (wb * SEGW + wp * 16 + l16) >> 1;
-      const bool evn = (l16 & 1) == 0;
+      const bool odd = (l16 & 1) != 0;
 #pragma unroll
       for (int i = 0; i < TR / 2; ++i) {
         const int hp2 = ((hb * TR) >> 1) + i;
-        const bool inb = evn && hp2 < P2 && wq < Q2;
-        const long long pp = ((long long)n * P2 + hp2) * Q2 + wq;
+        const bool inb = hp2 < P2 && wq < Q2;
+        const unsigned pp = ((unsigned)n * P2 + hp2) * Q2 + wq;  // < 2^32 (acfe_conv2d_pool_supported)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
-          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
-          uint16_t hv[4];
+          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4 + (odd ? 2 : 0);
+          const f4 rb = bias4(fn);
+          float hv[2];
           unsigned amb = 0;
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const float a0 = bf2f(f2bf(acc[2 * i][fn][jj] + sbias[c + jj]));
-            const float a2 = bf2f(f2bf(acc[2 * i + 1][fn][jj] + sbias[c + jj]));
-            const float a1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a0), 0xB1, 0xF, 0xF, false));
-            const float a3 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a2), 0xB1, 0xF, 0xF, false));
-            float m = -INFINITY;
+          for (int jp = 0; jp < 2; ++jp) {
+            // conv outputs rounded to the storage type (conv -> maxpool), own and partner channel
+            const float e0 = bf2f(f2bf(acc[2 * i][fn][jp] + rb[jp]));
+            const float e1 = bf2f(f2bf(acc[2 * i + 1][fn][jp] + rb[jp]));
+            const float u0 = bf2f(f2bf(acc[2 * i][fn][jp + 2] + rb[jp + 2]));
+            const float u1 = bf2f(f2bf(acc[2 * i + 1][fn][jp + 2] + rb[jp + 2]));
+            const float o0 = odd ? u0 : e0, o1 = odd ? u1 : e1;   // this lane's channel
+            const float s0 = odd ? e0 : u0, s1 = odd ? e1 : u1;   // the partner's channel
+            const float r0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s0), 0xB1, 0xF, 0xF, false));
+            const float r1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s1), 0xB1, 0xF, 0xF, false));
+            const float a0 = odd ? r0 : o0, a1 = odd ? o0 : r0;   // row 0: left, right column
+            const float a2 = odd ? r1 : o1, a3 = odd ? o1 : r1;   // row 1
+            float m = a0;
             unsigned am = 0;
-            if (a0 > m) m = a0, am = 0;
             if (a1 > m) m = a1, am = 1;
             if (a2 > m) m = a2, am = 2;
             if (a3 > m) m = a3, am = 3;
-            if (g.drop.on) m = drop_apply<T>(g.drop, (uint64_t)pp * g.K + c + jj, m);
-            hv[jj] = f2bf(m);
-            const float f = inb ? bf2f(hv[jj]) : 0.f;
-            sv[fn * 4 + jj] += f;
-            sv[FN * 4 + fn * 4 + jj] += f * f;
-            amb |= am << (8 * jj);
+            if (g.drop.on) m = drop_apply32<T>(g.drop, pp * (unsigned)g.K + c + jp, m);
+            hv[jp] = m;
+            const float f = inb ? m : 0.f;
+            sv[fn * 4 + jp] += f;
+            sv[FN * 4 + fn * 4 + jp] += f * f;
+            amb |= am << (8 * jp);
           }
           if (inb) {
-            uint2 v;
-            v.x = (unsigned)hv[0] | ((unsigned)hv[1] << 16);
-            v.y = (unsigned)hv[2] | ((unsigned)hv[3] << 16);
-            *reinterpret_cast<uint2*>(Y + pp * g.ldy + c) = v;
-            *reinterpret_cast<unsigned*>(amax + pp * g.K + c) = amb;
+            *reinterpret_cast<unsigned*>(Y + (size_t)pp * g.ldy + c) =
+                (unsigned)f2bf(hv[0]) | ((unsigned)f2bf(hv[1]) << 16);
+            *reinterpret_cast<uint16_t*>(amax + (size_t)pp * g.K + c) = (uint16_t)amb;
           }
           acc[2 * i][fn] = acc[2 * i + 1][fn] = f4{0.f, 0.f, 0.f, 0.f};
         }
+      }
+      // odd lanes hold channels 2-3 of each quad in slots 0-1: move them to the
+      // slots of the butterfly's channel order
+#pragma unroll
+      for (int k = 0; k < 2 * FN; ++k) {
+        const int b = (k / FN) * FN * 4 + (k % FN) * 4;
+        const float x0 = sv[b], x1 = sv[b + 1];
+        sv[b] = odd ? 0.f : x0;
+        sv[b + 1] = odd ? 0.f : x1;
+        sv[b + 2] = odd ? x0 : 0.f;
+        sv[b + 3] = odd ? x1 : 0.f;
       }
     }
 #pragma unroll
@@ -1079,14 +1165,17 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
+        const f4 rb = bias4(fn);
         uint16_t hv[4];
         uint2 rv = {0u, 0u};
         if constexpr (RPRE) rv = rres[fm][fn];
         else if constexpr (PM == 3) rv = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          hv[jj] = f2bf(acc[fm][fn][jj] + sbias[c + jj]);
-          if (g.drop.on) hv[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(hv[jj])));
+          hv[jj] = f2bf(acc[fm][fn][jj] + rb[jj]);
+          if (g.drop.on)
+            hv[jj] = f2bf(g.idx32 ? drop_apply32<T>(g.drop, (unsigned)pix * (unsigned)g.K + c + jj, bf2f(hv[jj]))
+                                  : drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(hv[jj])));
           if constexpr (PM == 3) {
             const unsigned rw = jj < 2 ? rv.x : rv.y;
             float z = bf2f(hv[jj]) + __uint_as_float((jj & 1) ? (rw & 0xffff0000u) : (rw << 16));
@@ -1903,6 +1992,7 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.drop = make_drop(0.f, 0);
   g.res = nullptr;
   g.res_relu = 0;
+  g.idx32 = g.M * K < (1ll << 32) ? 1 : 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
   return g;
@@ -2265,7 +2355,8 @@ ACFE_API int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R
   static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS") || getenv_flag("ACFE_CONV_NO_POOL");
   return !no_rows && dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
          (K == 64 || K == 128) && W > 0 && W % 64 == 0 && H >= 2 && H % 2 == 0 &&
-         (long long)N * ((H + 5) / 6) * (W / 64) < (1ll << 31) && (long long)N * H * (W / 64) < (1ll << 31);
+         (long long)N * ((H + 5) / 6) * (W / 64) < (1ll << 31) && (long long)N * H * (W / 64) < (1ll << 31) &&
+         (long long)N * (H / 2) * (W / 2) * (C > K ? C : K) < (1ll << 32);  // 32-bit pooled element index
 }
 
 ACFE_API int acfe_conv2d_fwd_pool(const void* x, int N, int H, int W, int C, const void* wpacked, int K,

@@ -177,7 +177,8 @@ class TFRecordWriter:
     """tf.io.TFRecordWriter(path, options="GZIP") equivalent (audiowriter.py:259-277)."""
 
     def __init__(self, path, compression: str | None = "GZIP"):
-        self._f = gzip.open(path, "wb") if compression == "GZIP" else open(path, "wb")
+        # zlib level 6 = Z_DEFAULT_COMPRESSION, what TF's GZIP writer uses
+        self._f = gzip.open(path, "wb", compresslevel=6) if compression == "GZIP" else open(path, "wb")
 
     def write(self, record: bytes):
         self._f.write(frame(record))

@@ -174,6 +174,8 @@ def main():
     if world != a.gpus and rank == 0:
         print(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks; measuring {world}",
               file=sys.stderr, flush=True)
+    # ranks beyond the visible GPUs share them (the gloo rehearsal on one GPU)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import torch.distributed as dist

@@ -27,3 +27,26 @@ def pcen_torch(mel_btm: torch.Tensor, params: torch.Tensor, eps: float = 1e-6) -
     mx, mn = torch.amax(y), torch.amin(y)
     out = 2 * ((y - mn) / (mx - mn)) - 1
     return out.transpose(1, 2)
+
+
+def frontend_port(raw, weights, params, n_fft=4096, hop=281):
+    """The reference front end as BASELINE.md 3 specifies the CPU baseline:
+    normalize (tfdataset.py:1916-1934) -> tf.signal.stft(pad_end) restated as
+    torch.stft(center=False) on the end-padded clip with a periodic Hann window
+    (:2026-2034) -> |X|^2 -> the DENSE batch_dot with the filterbank tiled over
+    the batch (:2044-2051) -> PCEN + normalize_minmax (tfpcen.py).  raw [B, N]
+    float32 -> [B, M, T] float32."""
+    x = raw.to(torch.float32)
+    x = x - x.amin(dim=-1, keepdim=True)
+    x = x / x.amax(dim=-1, keepdim=True) + 1e-6
+    x = (x - 0.5) * 2
+    b, n = x.shape
+    t = -(-n // hop)
+    x = torch.nn.functional.pad(x, (0, (t - 1) * hop + n_fft - n))
+    win = torch.hann_window(n_fft, periodic=True, dtype=torch.float32)
+    spec = torch.stft(x, n_fft, hop, n_fft, win, center=False, return_complex=True)  # [B, F, T]
+    power = spec.real ** 2 + spec.imag ** 2
+    w = torch.as_tensor(weights, dtype=torch.float32)
+    mel = torch.bmm(w.expand(b, -1, -1), power)                                        # [B, M, T]
+    with torch.no_grad():
+        return pcen_torch(mel.transpose(1, 2).contiguous(), params.to(torch.float32))

@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""CPU baseline rows of BASELINE.md 3, timed on the host cores of the box the
+command runs on (the GPU box's 16-thread share by default: OMP_NUM_THREADS).
+
+The reference TF path cannot run (no TensorFlow / librosa in the image, and its
+sources never travel to the GPU box), so every row times the repository's own
+faithful CPU restatement (oracle/: kind "port"):
+  * front end  -- normalize, torch.stft on the pad_end-padded clip, |X|^2, the
+                  DENSE tiled-filterbank batch_dot, sequential PCEN scan +
+                  batch min/max (oracle.torch_ref.frontend_port); clips/s and
+                  GB/s of the 838 656 algorithmic bytes per clip;
+  * inference  -- front end + wr_resnet forward, fp32, batch 256 (config I);
+  * training   -- front end + wr_resnet_bird (50 classes) forward/backward +
+                  Keras Adam, fp32, batch 128 (config T1 at the largest batch
+                  that stays well inside host memory);
+  * config P   -- 256-clip synthetic 2-class TFRecord set (build.py), read by
+                  tfdataset.AudioDataset, wr_resnet training at batch 8.
+Medians over the timed repetitions; the sample of each row is stated.
+usage: python tools/cpu_baseline.py [--out profiles/r02_cpu_baseline.json] [--quick]"""
+import argparse
+import json
+import os
+import platform
+import statistics
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "audio-training_amd"), str(ROOT)]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+FRONTEND_BYTES = 144000 * 4 + 128 * 513 * 4
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def median_time(fn, reps, warm=1):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), ts
+
+
+def model_params(kind, classes):
+    """A random-init model's parameters (the product module's state_dict layout,
+    fp32 CPU tensors) for the oracle graphs."""
+    torch.manual_seed(0)
+    if kind == "bird":
+        from resnet.wr_resnet_bird import WRResNet
+    else:
+        from resnet.wr_resnet import WRResNet
+    m = WRResNet(input_shape=(128, 513, 3), classes=classes, dropout=0.0)
+    p = {k: v.detach().float().clone() for k, v in m.state_dict().items()}
+    names = [n for n, _ in m.named_parameters()]
+    return p, names
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r02_cpu_baseline.json"))
+    ap.add_argument("--quick", action="store_true", help="small samples (smoke run)")
+    a = ap.parse_args()
+    from oracle import frontend as of
+    from oracle import models as om
+    from oracle.torch_ref import frontend_port
+    from bench import synth_bank
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    q = a.quick
+    weights = torch.from_numpy(of.mel_f(48000, 128, 100, 11000, 4096, 1000))
+    pc = torch.tensor([0.98, 2.0, 2.0, 0.04])
+    rows = {}
+
+    # ---- front end
+    B = 8 if q else 64
+    raw = torch.from_numpy(synth_bank(B, seed=11))
+    t, ts = median_time(lambda: frontend_port(raw, weights, pc), 2 if q else 10)
+    rows["frontend"] = {"value": round(B / t, 3), "unit": "clips/s", "GBps": round(B * FRONTEND_BYTES / t / 1e9, 4),
+                        "cores": cores, "kind": "port",
+                        "sample": f"median of {len(ts)} batches of {B} clips (after 1 warm-up): {t:.3f} s/batch"}
+    print(json.dumps({"frontend": rows["frontend"]}), flush=True)
+
+    # ---- inference, config I
+    B = 4 if q else 256
+    p, names = model_params("wrn", 2)
+    raw = torch.from_numpy(np.tile(synth_bank(64, seed=12), (B // 64 + 1, 1))[:B])
+
+    def infer():
+        with torch.no_grad():
+            f = frontend_port(raw, weights, pc)
+            return om.wr_resnet(f[:, None].repeat(1, 3, 1, 1), p, False, {k: v for k, v in p.items() if "moving" in k})
+
+    t, ts = median_time(infer, 1 if q else 3)
+    rows["inference"] = {"value": round(B / t, 3), "unit": "clips/s", "cores": cores, "kind": "port",
+                         "sample": f"median of {len(ts)} batches of {B} clips (after 1 warm-up), front end + "
+                                   f"wr_resnet forward fp32: {t:.2f} s/batch"}
+    print(json.dumps({"inference": rows["inference"]}), flush=True)
+
+    # ---- training, config T1 (fp32 on the CPU)
+    B = 2 if q else 128
+    p, names = model_params("bird", 50)
+    trainable = [p[n].requires_grad_(True) for n in names]
+    state = {k: v for k, v in p.items() if "moving" in k}
+    mv = [torch.zeros_like(x) for x in trainable]
+    vv = [torch.zeros_like(x) for x in trainable]
+    raw = torch.from_numpy(np.tile(synth_bank(64, seed=13), (B // 64 + 1, 1))[:B])
+    y = torch.zeros(B, 50)
+    y[torch.arange(B), torch.arange(B) % 50] = 1
+    it = [0]
+
+    def train():
+        it[0] += 1
+        f = frontend_port(raw, weights, pc)
+        z = om.wr_resnet_bird(f[:, None].repeat(1, 3, 1, 1), p, True, state)
+        loss = om.keras_loss(z, y, "cce")
+        loss.backward()
+        with torch.no_grad():
+            new, _, _ = om.keras_adam([x.detach() for x in trainable], [x.grad for x in trainable], mv, vv, it[0])
+            for x, nx in zip(trainable, new):
+                x.copy_(nx)
+                x.grad = None
+
+    t, ts = median_time(train, 1 if q else 5)
+    rows["training"] = {"value": round(B / t, 3), "unit": "clips/s", "cores": cores, "kind": "port",
+                        "sample": f"median of {len(ts)} steps of {B} clips (after 1 warm-up): front end + "
+                                  f"wr_resnet_bird fwd/bwd fp32 + Keras Adam, {t:.2f} s/step"}
+    print(json.dumps({"training": rows["training"]}), flush=True)
+
+    # ---- config P: 256-clip TFRecord set -> wr_resnet, batch 8
+    import build
+    import tfdataset
+
+    n_clips = 16 if q else 256
+    with tempfile.TemporaryDirectory() as tmp:
+        t0 = time.perf_counter()
+        build.main([str(Path(tmp) / "ds"), "--synthetic", str(n_clips), "--labels", "bird,noise", "--shards", "4"])
+        t_build = time.perf_counter() - t0
+        td = Path(tmp) / "ds" / "training-data"
+        ds = tfdataset.AudioDataset(tfdataset._files(td / "train"), ["bird", "noise"], batch_size=8, shuffle=True,
+                                    device="cpu", threads=4, drop_remainder=True)
+        p, names = model_params("wrn", 2)
+        trainable = [p[n].requires_grad_(True) for n in names]
+        state = {k: v for k, v in p.items() if "moving" in k}
+        mv = [torch.zeros_like(x) for x in trainable]
+        vv = [torch.zeros_like(x) for x in trainable]
+        steps, clips = 0, 0
+        max_steps = 2 if q else 12
+        t0 = time.perf_counter()
+        for x, yy in ds:
+            f = frontend_port(x, weights, pc)
+            z = om.wr_resnet(f[:, None].repeat(1, 3, 1, 1), p, True, state)
+            om.keras_loss(z, yy, "cce").backward()
+            with torch.no_grad():
+                new, _, _ = om.keras_adam([v.detach() for v in trainable], [v.grad for v in trainable], mv, vv,
+                                          steps + 1)
+                for v, nv in zip(trainable, new):
+                    v.copy_(nv)
+                    v.grad = None
+            steps += 1
+            clips += x.shape[0]
+            if steps >= max_steps:
+                break
+        dt = time.perf_counter() - t0
+    rows["config_p"] = {"value": round(clips / dt, 3), "unit": "clips/s", "cores": cores, "kind": "port",
+                        "sample": f"{steps} training steps of 8 clips read from the {n_clips}-clip GZIP TFRecord set "
+                                  f"(build.py --synthetic, written in {t_build:.1f} s): loader + front end + "
+                                  f"wr_resnet fwd/bwd fp32 + Keras Adam, {dt:.1f} s"}
+    print(json.dumps({"config_p": rows["config_p"]}), flush=True)
+    out = {"cpu": cpu_model(), "threads": cores, "torch": torch.__version__, "rows": rows}
+    if not q:
+        Path(a.out).write_text(json.dumps(out, indent=1) + "\n")
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
