@@ -31,6 +31,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_normalize_apply": [P, I64, I32, I32, P, P, P],
     "acfe_mixup": [P, P, P, P, P, I32, I32, P, P],
     "acfe_mel_fwd": [P, P, I64, I32, I32, P, I32, I32, P, I32, P],
+    "acfe_mel_from_spec": [P, P, I64, I32, I32, I32, I32, P, I32, P],
     "acfe_pcen_partials": [I32, I32],
     "acfe_pcen_fwd": [P, I32, I32, I32, P, F32, P, P, P],
     "acfe_pcen_normalize": [P, I64, P, I32, P, P, I32, P, P],

@@ -93,6 +93,33 @@ class MelPlan:
         return out
 
 
+    def mel_from_spec(self, spec: torch.Tensor, power=1, layout="btm", out: torch.Tensor | None = None,
+                      timer: list | None = None) -> torch.Tensor:
+        """Stored magnitude spectrograms [B, F, T] fp32 (F = 1 + n_fft/2, the
+        record's audio/spectogram reshaped (2049, 513), tfdataset.py:1082) ->
+        mel = W . S^power [B,T,M] ("btm") or [B,M,T] ("bmt") (tfdataset.py:1089)."""
+        require_cuda(spec)
+        if spec.dtype != torch.float32 or spec.dim() != 3 or not spec.is_contiguous():
+            raise TypeError("spectrograms must be contiguous float32 [B, F, T]")
+        b, f, t = spec.shape
+        if f != self.n_fft // 2 + 1:
+            raise ValueError(f"expected {self.n_fft // 2 + 1} frequency bins, got {f}")
+        shape = (b, t, self.n_mels) if layout == "btm" else (b, self.n_mels, t)
+        if out is None:
+            out = torch.empty(shape, dtype=torch.float32, device=spec.device)
+        e0 = None
+        if timer is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        call("acfe_mel_from_spec", self._h, ptr(spec), f * t, b, f, t, int(power), ptr(out),
+             _lib.LAYOUT_BTM if layout == "btm" else _lib.LAYOUT_BMT, stream())
+        if timer is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            timer.append(("mel", e0, e1))
+        return out
+
+
 def normalize_stats(x: torch.Tensor, n: int | None = None, clip_stride: int | None = None,
                     batch: int | None = None) -> torch.Tensor:
     """Per-clip {min, max(x-min)} (tfdataset.normalize reductions)."""

@@ -30,8 +30,12 @@ class FrontEnd(nn.Module):
     the feature, as in the reference's raw_to_mel output (tfdataset.py:2049-2053)."""
 
     def __init__(self, n_mels=128, n_fft=4096, hop=281, sr=48000, fmin=100, fmax=11000, break_freq=1000,
-                 pcen=True, dtype=torch.bfloat16, device=None, weights=None):
+                 pcen=True, dtype=torch.bfloat16, device=None, weights=None, power=2):
         super().__init__()
+        # |X|^power of the raw-audio paths: 2 in raw_to_mel (tfdataset.py:2044) and
+        # get_spect (predict_utils.py:215); 1 for a model trained on the stored
+        # magnitude spectrograms (tfdataset.py:1085-1089), as its metadata records
+        self.power = power
         self.plan = fe.MelPlan(sr, n_fft, hop, n_mels, fmin, fmax, break_freq, weights=weights, device=device)
         self.pcen = fe.PCEN(out_dtype=dtype) if pcen else None
         self.dtype = dtype
@@ -49,11 +53,19 @@ class FrontEnd(nn.Module):
         # normalising on load inside the STFT repeats the divide per frame).
         src = fe.normalize_apply(src, st, out=src if src is not x1 else None)
         if self.pcen is not None:
-            mel = self.plan.mel(src, None, pad_mode=pad_mode, layout="btm", timer=self.timer)
+            mel = self.plan.mel(src, None, pad_mode=pad_mode, power=self.power, layout="btm", timer=self.timer)
             return self.pcen(mel, scope_minmax)
-        mel = self.plan.mel(src, None, pad_mode=pad_mode, layout="bmt", timer=self.timer)
+        mel = self.plan.mel(src, None, pad_mode=pad_mode, power=self.power, layout="bmt", timer=self.timer)
         return ops.cast(mel, self.dtype)
 
+
+    def forward_spec(self, spec, scope_minmax=None):
+        """Model input from stored magnitude spectrograms [B, F, T] (the
+        load_raw=False records, tfdataset.py:1065-1102): banded mel of the
+        magnitude (power 1), then PCEN when enabled, else the mel itself."""
+        if self.pcen is not None:
+            return self.pcen(self.plan.mel_from_spec(spec, power=1, layout="btm", timer=self.timer), scope_minmax)
+        return ops.cast(self.plan.mel_from_spec(spec, power=1, layout="bmt", timer=self.timer), self.dtype)
 
     def forward_windows(self, rec, first, count, n=144000, hop=72000, pad_mode="constant", scope_minmax=None):
         """Features of `count` overlapping windows of one device recording `rec`
@@ -63,11 +75,11 @@ class FrontEnd(nn.Module):
         view = rec[first * hop:]
         st = fe.normalize_stats(view, n=n, clip_stride=hop, batch=count)
         if self.pcen is not None:
-            mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="btm", n=n, clip_stride=hop, batch=count,
-                                timer=self.timer)
+            mel = self.plan.mel(view, st, pad_mode=pad_mode, power=self.power, layout="btm", n=n, clip_stride=hop,
+                                batch=count, timer=self.timer)
             return self.pcen(mel, scope_minmax)
-        mel = self.plan.mel(view, st, pad_mode=pad_mode, layout="bmt", n=n, clip_stride=hop, batch=count,
-                            timer=self.timer)
+        mel = self.plan.mel(view, st, pad_mode=pad_mode, power=self.power, layout="bmt", n=n, clip_stride=hop,
+                            batch=count, timer=self.timer)
         return ops.cast(mel, self.dtype)
 
 
@@ -110,7 +122,10 @@ class Trainer:
         return self
 
     def step(self, x1, y, x2=None, lam=None):
-        feats = self.frontend(x1, x2, lam)
+        """One training iteration.  x1 [B, N] raw clips (x2 / lam: mix_up
+        partner and weights), or [B, F, T] stored magnitude spectrograms (the
+        load_raw=False path, no mix_up: tfdataset.py:503-504)."""
+        feats = self.frontend.forward_spec(x1) if x1.dim() == 3 else self.frontend(x1, x2, lam)
         z = self.model(feats)
         loss, dz = ops.loss_and_grad(z, y, self.loss_mode)
         self.arena.zero_grad()
@@ -132,6 +147,7 @@ class Trainer:
     def predict(self, x, pad_mode="end"):
         self.holder.eval()
         try:
-            return ops.sigmoid(self.model(self.frontend(x, pad_mode=pad_mode)))
+            f = self.frontend.forward_spec(x) if x.dim() == 3 else self.frontend(x, pad_mode=pad_mode)
+            return ops.sigmoid(self.model(f))
         finally:
             self.holder.train()

@@ -79,7 +79,8 @@ def evaluate(trainer, dataset, multi_label, group=None):
     tot = torch.zeros(3, dtype=torch.float64, device=dev)  # loss sum, correct, count
     with torch.no_grad():
         for x, y in dp.synced_batches(dataset, group=group):
-            z = trainer.model(trainer.frontend(x))
+            f = trainer.frontend.forward_spec(x) if x.dim() == 3 else trainer.frontend(x)
+            z = trainer.model(f)
             loss, _ = ops.loss_and_grad(z, y, trainer.loss_mode)
             b = x.shape[0]
             if multi_label:
@@ -169,15 +170,16 @@ def train_model(args):
         sd = torch.load(args.weights, map_location="cpu", weights_only=True)
         trainer.holder.load_state_dict(sd)
     files, rshard = shard_files(tfdataset._files(td / "train"), rank, world)
+    load_raw = bool(args.load_raw)
     train_ds = tfdataset.AudioDataset(files, labels, batch_size=args.batch_size, shuffle=args.shuffle,
-                                      augment=args.augment, device=dev, drop_remainder=world > 1, seed=args.seed,
-                                      record_shard=rshard)
+                                      augment=args.augment and load_raw, device=dev, drop_remainder=world > 1,
+                                      seed=args.seed, record_shard=rshard, load_raw=load_raw)
     val_dir = td / "validation"
     val_ds = None
     if val_dir.exists() and tfdataset._files(val_dir):
         vfiles, vshard = shard_files(tfdataset._files(val_dir), rank, world)
         val_ds = tfdataset.AudioDataset(vfiles, labels, batch_size=args.batch_size, shuffle=False, device=dev,
-                                        record_shard=vshard)
+                                        record_shard=vshard, load_raw=load_raw)
     history = {"loss": [], "val_loss": [], "val_accuracy": [], "clips_per_s": []}
     out_dir = Path(args.checkpoint_dir) / args.name
     best = float("inf")
@@ -192,7 +194,7 @@ def train_model(args):
 
     for epoch in range(args.epochs):
         t0 = time.perf_counter()
-        n, lsum, steps = train_epoch(train_ds, step, args.augment, args.steps_per_epoch, mixup, ctrl)
+        n, lsum, steps = train_epoch(train_ds, step, args.augment and load_raw, args.steps_per_epoch, mixup, ctrl)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         n_all, lsum_all = dp.allreduce_sums([n, lsum], device=dev)
@@ -214,8 +216,8 @@ def train_model(args):
     if rank == 0:
         meta_out = dict(meta)
         meta_out.update(name=args.model_name, ebird_labels=labels, labels=labels, n_mels=n_mels, fmin=fmin,
-                        fmax=fmax, n_fft=n_fft, break_freq=brk, hop_length=281, power=2, pcen=args.pcen,
-                        multi_label=args.multi_label, loss_fn="bce" if args.multi_label else "cce",
+                        fmax=fmax, n_fft=n_fft, break_freq=brk, hop_length=281, power=2 if load_raw else 1, pcen=args.pcen,
+                        multi_label=args.multi_label, loss_fn="bce" if args.multi_label else "cce", load_raw=load_raw,
                         dtype=args.dtype, training_date=str(time.time()), magv2=True)
         save_checkpoint(out_dir, trainer, meta_out, history)
         print(json.dumps({"run": args.name, "epochs": args.epochs, "final_loss": history["loss"][-1],
@@ -232,7 +234,9 @@ def parse_args(argv=None):
     p.add_argument("-d", "--dataset-dir", required=True)
     p.add_argument("--epochs", type=int, default=100)
     p.add_argument("--model-name", default="wr-resnet", choices=sorted(MODEL_NAMES))
-    p.add_argument("--load-raw", default=True, type=str2bool, help="raw audio records (the only supported input)")
+    p.add_argument("--load-raw", default=0, action="count",
+                   help="train on the records' raw audio (GPU STFT / mel / mix_up) instead of their stored magnitude "
+                        "spectrogram (audiomodel.py:2344-2349: count flag, default the spectrogram path)")
     p.add_argument("--multi-label", type=str2bool, default=False)
     p.add_argument("--n_mels", type=int, default=None)
     p.add_argument("--fmin", type=float, default=None)

@@ -95,11 +95,35 @@ def split_by_recording(samples, fractions=(0.8, 0.1, 0.1), seed=0):
     return {k: [s for s in samples if s[0] in v] for k, v in parts.items()}
 
 
-def write_split(samples, out_dir, shards=4):
+def normalize_data(x):
+    """audiodataset.normalize_data (audiodataset.py:1334-1341)."""
+    x = x - np.min(x, -1, keepdims=True)
+    x = x / np.max(x, -1, keepdims=True) + 0.000001
+    return (x - 0.5) * 2
+
+
+def stft_magnitude(clip, n_fft=4096, hop=281):
+    """The stored spectrogram of audiodataset.load_data (:1302-1303):
+    |librosa.stft(normalize_data(clip), n_fft, hop)| with librosa's defaults
+    (center=True, constant padding as of librosa 0.10, periodic Hann window)
+    -> float32 [1 + n_fft // 2, 1 + len // hop]."""
+    x = normalize_data(np.asarray(clip, np.float64))
+    x = np.pad(x, (n_fft // 2, n_fft // 2))
+    t = 1 + (len(x) - n_fft) // hop
+    win = 0.5 - 0.5 * np.cos(2.0 * np.pi * np.arange(n_fft) / n_fft)
+    out = np.empty((n_fft // 2 + 1, t), np.float32)
+    for a in range(0, t, 64):  # bounded frame blocks (64 x 4096 doubles)
+        idx = np.arange(a, min(t, a + 64))[:, None] * hop + np.arange(n_fft)[None, :]
+        out[:, a:a + idx.shape[0]] = np.abs(np.fft.rfft(x[idx] * win, axis=-1)).T
+    return out
+
+
+def write_split(samples, out_dir, shards=4, spectrogram=True):
     out_dir.mkdir(parents=True, exist_ok=True)
     writers = [tfr.TFRecordWriter(out_dir / f"{i:05d}.tfrecord") for i in range(max(1, shards))]
     for i, (rec, lab, start, raw) in enumerate(samples):
-        writers[i % len(writers)].write(tfr.audio_example(raw, rec, i, lab, lab, start_s=start))
+        spec = stft_magnitude(raw) if spectrogram else None
+        writers[i % len(writers)].write(tfr.audio_example(raw, rec, i, lab, lab, start_s=start, spectrogram=spec))
     for w in writers:
         w.close()
 
@@ -118,6 +142,9 @@ def main(argv=None):
     ap.add_argument("--fmax", type=float, default=11000)
     ap.add_argument("--shards", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-spectrogram", action="store_true",
+                    help="store audio/raw only (the reference also stores audio/spectogram, audiowriter.py:131-134, "
+                         "which the default load_raw=False training path reads)")
     a = ap.parse_args(argv)
     if a.synthetic:
         samples = synthetic_samples(a.synthetic, a.labels.split(","), seed=20260227 + a.seed)
@@ -132,7 +159,7 @@ def main(argv=None):
     base = Path(a.out) / "training-data"
     counts, recs = {}, {}
     for name, ss in splits.items():
-        write_split(ss, base / name, a.shards)
+        write_split(ss, base / name, a.shards, spectrogram=not a.no_spectrogram)
         rc = defaultdict(set)
         for s in ss:
             rc[s[1]].add(s[0])

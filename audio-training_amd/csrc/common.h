@@ -81,18 +81,27 @@ struct Drop {
   unsigned long long seed;
   bool on;
 };
-inline Drop make_drop(float rate, unsigned long long seed) {
+// Dropout mask: element idx is kept iff its 16-bit slice of the hash of its
+// PAIR, hash(seed, idx >> 1) (low half for even idx, high half for odd), is
+// >= rate * 2^16 -- one hash per two elements, so the conv epilogues (whose
+// lanes own consecutive channel pairs) pay half the hashing; every kernel that
+// applies or regenerates a mask goes through drop_keep*, so they all agree.
+__host__ __device__ inline Drop make_drop(float rate, unsigned long long seed) {
   Drop d;
   d.on = rate > 0.f;
-  const float t = rate * 4294967296.0f;  // exact (power-of-two scale); saturate like v_cvt_u32_f32
-  d.thr = t >= 4294967296.0f ? 0xFFFFFFFFu : (uint32_t)t;
+  const float t = rate * 65536.0f;  // exact (power-of-two scale)
+  d.thr = t >= 65536.0f ? 65536u : (uint32_t)t;
   d.scl = 1.0f / (1.0f - rate);
   d.seed = seed;
   return d;
 }
+__device__ __forceinline__ bool drop_keep(const Drop& d, uint64_t idx) {
+  const uint32_t h = hash_u32(d.seed, idx >> 1);
+  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= d.thr;
+}
 template <typename T>
 __device__ __forceinline__ float drop_apply(const Drop& d, uint64_t idx, float v) {
-  return hash_u32(d.seed, idx) >= d.thr ? rnd(v * d.scl, T()) : 0.f;
+  return drop_keep(d, idx) ? rnd(v * d.scl, T()) : 0.f;
 }
 // The same mask for an index known to be < 2^32 (hash_u32 with idx >> 32 == 0),
 // without the 64-bit index arithmetic.
@@ -106,9 +115,16 @@ __device__ __forceinline__ uint32_t hash_u32_lo(uint64_t seed, uint32_t idx) {
   h ^= h >> 16;
   return h;
 }
+// pair hash of an even element index e < 2^32 (elements e and e + 1):
+// keep(e) = (h & 0xFFFF) >= thr, keep(e + 1) = (h >> 16) >= thr
+__device__ __forceinline__ uint32_t drop_pair_hash32(const Drop& d, uint32_t e) {
+  return hash_u32_lo(d.seed, e >> 1);
+}
+__device__ __forceinline__ uint32_t drop_pair_hash(const Drop& d, uint64_t e) { return hash_u32(d.seed, e >> 1); }
 template <typename T>
 __device__ __forceinline__ float drop_apply32(const Drop& d, uint32_t idx, float v) {
-  return hash_u32_lo(d.seed, idx) >= d.thr ? rnd(v * d.scl, T()) : 0.f;
+  const uint32_t h = hash_u32_lo(d.seed, idx >> 1);
+  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= d.thr ? rnd(v * d.scl, T()) : 0.f;
 }
 
 }  // namespace acfe

@@ -24,6 +24,8 @@
 //                 weights over Cin; exact up to fp reassociation).
 #include "common.h"
 
+#include <type_traits>
+
 using namespace acfe;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -844,7 +846,8 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 
 // ------------------------------------------------------------------ 3x3 stride-1 conv, row-halo steps
 // Forward (and stride-1 dgrad) of the 3x3 layers with C % 64 == 0,
-// K in {64, 128}, Q % 64 == 0.  Built like k_wgrad3x3_halo, whose measured
+// K in {64, 128} (a partial last 64-pixel column tile is masked: wr_resnet's
+// 513- / 257-wide stages).  Built like k_wgrad3x3_halo, whose measured
 // lesson is that each pipeline step carries a fixed ~1 us of non-MFMA time,
 // so the matrix work per step has to be large: a workgroup owns 3 output rows
 // x 64 pixels x K channels, and one step = one 64-channel chunk x one filter
@@ -856,7 +859,8 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 // with the k & 7 XOR swizzle.  Operands swapped (weights x pixels) so the
 // epilogue is k_conv_fwd_p's: 8-byte channel quads straight from registers,
 // bias from LDS, fused Dropout, DPP-butterfly BatchNormalization sums.
-// PM (epilogue mode): 0 plain; 3 = z = (ReLU)(conv + residual g.res) as
+// PM (epilogue mode): 0 plain; 4 = plain + Dropout (its own instantiation:
+// the dropout epilogue's registers would spill the K = 128 dgrad); 3 = z = (ReLU)(conv + residual g.res) as
 // ops.add stores it, BN sums of z; 1 = the output feeds MaxPool2D(2, 2) -> Dropout:
 // the epilogue pools row pairs x column pairs (waves own 16-column strips of
 // all TR rows), stores only the pooled values, their first-maximum argmax byte
@@ -870,31 +874,48 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
                int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
   static_assert(PM != 1 || TR % 2 == 0, "2x2 pooling needs row pairs");
   using T = uint16_t;
+  constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
+  // 6-row tiles: weights by LDS-DMA into a double buffer (no staging VGPRs,
+  // which spilled at K = 128), input rows register-staged.  LDS buffers of the
+  // input image: two (the next step's rows are stored right after this step's
+  // MFMAs, one barrier per step) where they fit -- K = 64 and the 3-row tiles --,
+  // else one (stored between two barriers, the MFMA pipe idle meanwhile).
+  constexpr bool WDMA = TR > 3;
+  constexpr int NBUF = (TR <= 3 || KB == 64) ? 2 : 1;
   // pixels per row, halo row bytes: 160-B rows make the fragment reads
   // conflict-free under ds_read_b128's lane grouping at every tap shift (144-B
-  // rows had 2-way conflicts: a third of the LDS cycles, rocprofv3 r02c)
-  constexpr int SEGW = 64, HWX = SEGW + 2, XRB = 160;
-  constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
-  constexpr int NBUF = TR <= 3 ? 2 : 1;                          // LDS buffers (single: store after a barrier)
-  // 6-row tiles: weights by LDS-DMA into a double buffer (no staging VGPRs,
-  // which spilled at K = 128), input rows register-staged into one buffer
-  constexpr bool WDMA = TR > 3;
+  // rows had 2-way conflicts: a third of the LDS cycles, rocprofv3 r02c); the
+  // double-buffered K = 64 image only fits with 144-B rows
+  constexpr int SEGW = 64, HWX = SEGW + 2, XRB = (WDMA && NBUF == 2) ? 144 : 160;
   constexpr int NV = 8 * FN;
   constexpr int XBYTES = TR * HWX * XRB, WBYTES = 3 * KB * 128, BUFB = XBYTES + WBYTES;
   constexpr int XG = TR * HWX * 8, WG = 3 * KB * 8;             // 16-B granules per step
   constexpr int XPT = (XG + 511) / 512, WPT = WG / 512;
   static_assert(WG % 512 == 0, "weight granules per thread");
-  constexpr int OFF_W2 = WDMA ? XBYTES + 2 * WBYTES : 0;           // WDMA layout: [X][W0][W1]
-  constexpr int OFF_STAT = WDMA ? OFF_W2 : NBUF * BUFB;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_STAT + 2 * KB * 8];
-  double* sstat = reinterpret_cast<double*>(smem + OFF_STAT);
+  // WDMA layout [X0 (X1)][W0][W1]; else [X0 W0][X1 W1]
+  constexpr int WBASE = WDMA ? NBUF * XBYTES : XBYTES;
+  constexpr int SMEM0 = WDMA ? NBUF * XBYTES + 2 * WBYTES : NBUF * BUFB;
+  // BN sums: K = 64 (LDS full with the double buffer) keeps per-lane double
+  // partials in registers, reduced over the waves once at the end; K = 128 (at
+  // the register limit) accumulates them with LDS double atomics per tile
+  constexpr bool REGSTAT = KB == 64;
+  constexpr int SMEM = SMEM0 + (REGSTAT ? 0 : 2 * KB * 8);
+  static_assert(SMEM <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  double* sstat = reinterpret_cast<double*>(smem + SMEM0);
+  auto xbuf = [&](int b) __attribute__((always_inline)) { return smem + (WDMA ? b * XBYTES : b * BUFB); };
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = wid >> 2, wp = wid & 3;
   const int nch = g.C / 64, nsteps_t = nch * 3;
   const int tpi = tiles_h * tiles_w;
   const T* zp = reinterpret_cast<const T*>(g_zero_page);
-  for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
+  constexpr int NV16 = 8 * FN / 16;
+  double dstat[REGSTAT ? NV16 : 1];
+#pragma unroll
+  for (int k = 0; k < (REGSTAT ? NV16 : 1); ++k) dstat[k] = 0.0;
+  if constexpr (!REGSTAT)
+    for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
   // this lane's bias quads are loaded (f4, L2-resident) at each epilogue: no
   // LDS copy (the 160-B image fills the LDS at K = 128) and no registers held
   // across the main loop (the K = 128 variants sit at the 256-VGPR limit)
@@ -927,7 +948,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
     const long long base = (long long)(uintptr_t)Wp + ((long long)r * 3 * g.C + cc * 64) * 2;
     const i4 dw = {(int)(unsigned)base, (int)(unsigned)(base >> 32), (int)0x80000000u, 0x00020000};
-    const unsigned lb = lds0 + XBYTES + wb * WBYTES + wid * WPW * 1024;
+    const unsigned lb = lds0 + WBASE + wb * WBYTES + wid * WPW * 1024;
 #pragma unroll
     for (int j = 0; j < (WDMA ? WPW : 0); ++j) bldsx4(voffW[j], dw, lb + j * 1024);
   };
@@ -1020,8 +1041,8 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // LDS image slot of granule i: halo pixel (tid >> 3) + 64 i, channel slot gr
   const int xsto = (tid >> 3) * XRB + gr * 16;
   auto sstore = [&](int buf) __attribute__((always_inline)) {
-    unsigned char* Xl = smem + buf * BUFB;
-    unsigned char* Wl = Xl + XBYTES;
+    unsigned char* Xl = xbuf(buf);
+    unsigned char* Wl = Xl + XBYTES;  // (register-staged weights: non-WDMA layout)
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + 512 * i;
@@ -1111,6 +1132,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
           const f4 rb = bias4(fn);
           float hv[2];
           unsigned amb = 0;
+          uint32_t dh = 0;
 #pragma unroll
           for (int jp = 0; jp < 2; ++jp) {
             // conv outputs rounded to the storage type (conv -> maxpool), own and partner channel
@@ -1129,7 +1151,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
             if (a1 > m) m = a1, am = 1;
             if (a2 > m) m = a2, am = 2;
             if (a3 > m) m = a3, am = 3;
-            if (g.drop.on) m = drop_apply32<T>(g.drop, pp * (unsigned)g.K + c + jp, m);
+            if (g.drop.on) {
+              if (jp == 0) dh = drop_pair_hash32(g.drop, pp * (unsigned)g.K + c);  // channels c, c + 1
+              m = ((jp ? dh >> 16 : dh & 0xFFFFu) >= g.drop.thr) ? bf2f(f2bf(m * g.drop.scl)) : 0.f;
+            }
             hv[jp] = m;
             const float f = inb ? m : 0.f;
             sv[fn * 4 + jp] += f;
@@ -1156,44 +1181,65 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
         sv[b + 3] = odd ? x1 : 0.f;
       }
     }
+    // PM 0 / 3: per (fragment row, channel quad) -- bias, rounding to the
+    // storage type, Dropout with one hash per channel pair, the residual Add
+    // (+ReLU), BN sums; rounded values are bf16-exact, so packing is a bit move.
+    // Templated on (dropout on, 32-bit index) so the per-element work has no
+    // uniform branches and the dgrad / eval paths carry no dropout code.
+    auto epi03 = [&](auto dropc, auto idxc) __attribute__((always_inline)) {
+      constexpr bool DRP = decltype(dropc)::value, I32 = decltype(idxc)::value;
 #pragma unroll
-    for (int fm = 0; fm < (PM == 1 ? 0 : FM); ++fm) {
-      const int p = wp * (TR * 16) + fm * 16;
-      const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
-      const bool inb = h < g.P && w < g.Q;
-      const long long pix = ((long long)n * g.P + h) * g.Q + w;
+      for (int fm = 0; fm < FM; ++fm) {
+        const int p = wp * (TR * 16) + fm * 16;
+        const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+        const bool inb = h < g.P && w < g.Q;
+        const long long pix = ((long long)n * g.P + h) * g.Q + w;
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
-        const f4 rb = bias4(fn);
-        uint16_t hv[4];
-        uint2 rv = {0u, 0u};
-        if constexpr (RPRE) rv = rres[fm][fn];
-        else if constexpr (PM == 3) rv = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
+        for (int fn = 0; fn < FN; ++fn) {
+          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
+          const f4 rb = bias4(fn);
+          float r[4];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          hv[jj] = f2bf(acc[fm][fn][jj] + rb[jj]);
-          if (g.drop.on)
-            hv[jj] = f2bf(g.idx32 ? drop_apply32<T>(g.drop, (unsigned)pix * (unsigned)g.K + c + jj, bf2f(hv[jj]))
-                                  : drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(hv[jj])));
-          if constexpr (PM == 3) {
-            const unsigned rw = jj < 2 ? rv.x : rv.y;
-            float z = bf2f(hv[jj]) + __uint_as_float((jj & 1) ? (rw & 0xffff0000u) : (rw << 16));
-            if (g.res_relu) z = fmaxf(z, 0.f);
-            hv[jj] = f2bf(z);
+          for (int jj = 0; jj < 4; ++jj) r[jj] = bf2f(f2bf(acc[fm][fn][jj] + rb[jj]));
+          if constexpr (DRP) {
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+              uint32_t hh;
+              if constexpr (I32) hh = drop_pair_hash32(g.drop, (unsigned)pix * (unsigned)g.K + c + 2 * pr);
+              else hh = drop_pair_hash(g.drop, (uint64_t)pix * g.K + c + 2 * pr);
+              r[2 * pr] = (hh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(r[2 * pr] * g.drop.scl)) : 0.f;
+              r[2 * pr + 1] = (hh >> 16) >= g.drop.thr ? bf2f(f2bf(r[2 * pr + 1] * g.drop.scl)) : 0.f;
+            }
           }
-          const float f = inb ? bf2f(hv[jj]) : 0.f;
-          sv[fn * 4 + jj] += f;
-          sv[FN * 4 + fn * 4 + jj] += f * f;
+          if constexpr (PM == 3) {
+            uint2 rv;
+            if constexpr (RPRE) rv = rres[fm][fn];
+            else rv = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const unsigned rw = jj < 2 ? rv.x : rv.y;
+              float z = r[jj] + __uint_as_float((jj & 1) ? (rw & 0xffff0000u) : (rw << 16));
+              if (g.res_relu) z = fmaxf(z, 0.f);
+              r[jj] = bf2f(f2bf(z));
+            }
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const float f = inb ? r[jj] : 0.f;
+            sv[fn * 4 + jj] += f;
+            sv[FN * 4 + fn * 4 + jj] += f * f;
+          }
+          uint2 v;
+          v.x = (__float_as_uint(r[0]) >> 16) | (__float_as_uint(r[1]) & 0xffff0000u);
+          v.y = (__float_as_uint(r[2]) >> 16) | (__float_as_uint(r[3]) & 0xffff0000u);
+          uint2* dst = inb ? reinterpret_cast<uint2*>(Y + pix * g.ldy + c) : &g_store_sink[lane];
+          *dst = v;
+          acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
         }
-        uint2 v;
-        v.x = (unsigned)hv[0] | ((unsigned)hv[1] << 16);
-        v.y = (unsigned)hv[2] | ((unsigned)hv[3] << 16);
-        uint2* dst = inb ? reinterpret_cast<uint2*>(Y + pix * g.ldy + c) : &g_store_sink[lane];
-        *dst = v;
-        acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
       }
-    }
+    };
+    // only PM 4 carries a Dropout, launched with 32-bit element indices (launch_fwd_t)
+    if constexpr (PM != 1) epi03(std::bool_constant<PM == 4>{}, std::true_type{});
     if (stats) {
       butterfly_step<NV, 8, 0x128>(sv, lane);
       butterfly_step<NV / 2, 4, 0x141>(sv, lane);
@@ -1202,10 +1248,14 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       const int b0 = ((l16 >> 3) & 1) * (NV / 2) + ((l16 >> 2) & 1) * (NV / 4) + ((l16 >> 1) & 1) * (NV / 8) +
                      (l16 & 1) * (NV / 16);
 #pragma unroll
-      for (int k = 0; k < NV / 16; ++k) {
-        const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
-        const int col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
-        atomicAdd(&sstat[st * KB + col], (double)sv[k]);
+      for (int k = 0; k < NV16; ++k) {
+        if constexpr (REGSTAT) {
+          dstat[k] += (double)sv[k];
+        } else {
+          const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
+          const int col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+          atomicAdd(&sstat[st * KB + col], (double)sv[k]);
+        }
       }
     }
   };
@@ -1227,8 +1277,8 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     if constexpr (RPRE) {
       if (cst + 1 == nsteps_t) rload(ctm);
     }
-    const unsigned char* Xl = smem + buf * BUFB;
-    const unsigned char* Wl = WDMA ? smem + XBYTES + (t & 1) * WBYTES : Xl + XBYTES;
+    const unsigned char* Xl = xbuf(buf);
+    const unsigned char* Wl = WDMA ? smem + WBASE + (t & 1) * WBYTES : Xl + XBYTES;
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
@@ -1253,6 +1303,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       epilogue(ctm);
       ctm += walk.step;
     }
+    if constexpr (WDMA && NBUF == 2) wait_vmcnt<0>();  // next step's weight pieces landed
     __syncthreads();
     if (NBUF == 2) {
       buf ^= 1;
@@ -1262,11 +1313,36 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       __syncthreads();
     }
   }
-  if (stats) {
+  if (stats && !REGSTAT) {
     for (int c = tid; c < KB; c += 512) {
       stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = sstat[c];
       stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = sstat[KB + c];
     }
+  }
+  if (stats && REGSTAT) {
+    // the 4 waves of one channel half (wid = wk * 4 + wp) hold partials of the
+    // same (channel, sum / sum-of-squares) slots in the same lanes: fixed-order
+    // sum through LDS (free after the main loop), wave wp = 0 writes the row
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(smem);
+#pragma unroll
+    for (int k = 0; k < NV16; ++k) red[(wid * 64 + lane) * NV16 + k] = dstat[k];
+    __syncthreads();
+    if (wp == 0) {
+      const int b0 = ((l16 >> 3) & 1) * (NV / 2) + ((l16 >> 2) & 1) * (NV / 4) + ((l16 >> 1) & 1) * (NV / 8) +
+                     (l16 & 1) * (NV / 16);
+#pragma unroll
+      for (int k = 0; k < NV16; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v += red[((wk * 4 + q) * 64 + lane) * NV16 + k];
+        const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
+        const int col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+        stats[((long long)blockIdx.x * 2 + st) * g.Kp + col] = v;
+      }
+    }
+  }
+  if (stats) {
     for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
       for (int c = tid; c < 2 * KB; c += 512) stats[((long long)rr * 2 + (c / KB)) * g.Kp + (c % KB)] = 0.0;
   }
@@ -1754,7 +1830,8 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 // `rep` input channels for the folded stem)
 // ------------------------------------------------------------------ wgrad, 3x3 stride 1, halo-staged
 // dW[k][r][s][c] for the 3x3 stride-1 layers with C % 64 == 0, K in {64, 128}
-// and Q % 64 == 0 (wr_resnet_bird stages 1-2: ~70 % of the step's wgrad time).
+// (wr_resnet_bird stages 1-2: ~70 % of the step's wgrad time; a partial last
+// 64-pixel segment of a row reads zeros past Q).
 // A workgroup owns one 64-channel chunk and ALL nine taps (output tile
 // K x 576) and reduces over a contiguous range of 64-pixel output-row segments
 // (split-K over pixels, slabs combined by k_wgrad_reduce).  Per segment it
@@ -1785,7 +1862,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   const int cc = bi % nchunk, split = (bi / nchunk) * 8 + xcd;
   const int sbeg = split * segs_per_split;
   const int send = sbeg + segs_per_split < nseg ? sbeg + segs_per_split : nseg;
-  const int QS = g.Q / SEGW;
+  const int QS = (g.Q + SEGW - 1) / SEGW;  // the last segment of a row may be partial
   const T16* zp = reinterpret_cast<const T16*>(g_zero_page);
 
   u32x4 rd[DPT], rx[XPT];
@@ -1801,13 +1878,14 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       const int px = idx / DGR, cg = idx - px * DGR;
       if constexpr (UNP) {
         const int w = w0 + px;
+        const bool okd = idx < DG && w < g.Q;
         const long long e = (((long long)n * (g.P >> 1) + (h >> 1)) * (g.Q >> 1) + (w >> 1)) * g.K + cg * 8;
-        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG ? dY + e : zp);
-        rda[i] = *reinterpret_cast<const uint2*>(idx < DG ? amax + e : reinterpret_cast<const uint8_t*>(zp));
+        rd[i] = *reinterpret_cast<const u32x4*>(okd ? dY + e : zp);
+        rda[i] = *reinterpret_cast<const uint2*>(okd ? amax + e : reinterpret_cast<const uint8_t*>(zp));
         if (i == 0) dpos = 0;
         dpos |= (unsigned)(((h & 1) << 1) | (w & 1)) << (2 * i);
       } else {
-        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG ? dyrow + px * g.K + cg * 8 : zp);
+        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG && w0 + px < g.Q ? dyrow + px * g.K + cg * 8 : zp);
       }
     }
 #pragma unroll
@@ -2015,25 +2093,30 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
   if constexpr (sizeof(T) == 2 && BN >= 64) {
     static const bool no_pipe = getenv_flag("ACFE_CONV_NO_PIPE");
     static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS");
-    if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && g.Q % 64 == 0 && !no_rows) {
+    if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && !no_rows && (!g.drop.on || g.idx32)) {
       // 6 output rows per tile halves the weight traffic per pixel, but at K = 128
       // its register staging spills (measured 1.4x slower): 3 rows there
       static const int rows_tr = getenv("ACFE_CONV_ROWS_TR") ? atoi(getenv("ACFE_CONV_ROWS_TR")) : 0;
       const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr : 6;
-      const int tiles_h = (g.P + tr - 1) / tr, tiles_w = g.Q / 64;
+      const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + 63) / 64;  // partial last column tile
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
         int gp = 256;
         if (gp > nt) gp = (int)nt;
         if (gp >= 64) gp &= ~7;
-        if (tr == 3)
-          hipLaunchKernelGGL((k_conv3x3_rows<BN, 3, 0>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
-                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m,
-                             nullptr);
-        else
-          hipLaunchKernelGGL((k_conv3x3_rows<BN, 6, 0>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
-                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m,
-                             nullptr);
+        // each workgroup writes statistics slab row blockIdx.x: never more
+        // workgroups than the caller's slab rows (narrow images have more
+        // 6 x 64 tiles than 128-pixel slab rows)
+        if (stats && gp > grid_m) gp = grid_m;
+#define ROWS(TR_, PM_)                                                                                   \
+  hipLaunchKernelGGL((k_conv3x3_rows<BN, TR_, PM_>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,      \
+                     (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m, nullptr)
+        if (tr == 3) {
+          if (g.drop.on) ROWS(3, 4); else ROWS(3, 0);
+        } else {
+          if (g.drop.on) ROWS(6, 4); else ROWS(6, 0);
+        }
+#undef ROWS
         return launch_rc("acfe_conv2d_fwd");
       }
     }
@@ -2268,7 +2351,7 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
 // 0): split count within the planned workspace (`splits`), returned in *used.
 static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
                              long long splits, hipStream_t s, int* used) {
-  const int nchunk = g.C / 64, nseg = (int)((long long)g.N * g.P * (g.Q / 64));
+  const int nchunk = g.C / 64, nseg = (int)((long long)g.N * g.P * ((g.Q + 63) / 64));
   int sp = 256 / nchunk;
   if (sp > splits) sp = (int)splits;
   sp &= ~7;
@@ -2306,7 +2389,7 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   int rc;
   static const bool no_halo_w = getenv_flag("ACFE_WGRAD_NO_HALO");
   if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 && C % 64 == 0 && (K == 64 || K == 128) &&
-      Q % 64 == 0 && (long long)N * P * (Q / 64) < (1ll << 31) && !no_halo_w) {
+      (long long)N * P * ((Q + 63) / 64) < (1ll << 31) && !no_halo_w) {
     // halo-staged kernel; its split count stays within the planned workspace
     int used = 0;
     rc = wgrad_halo_launch(g, x, dy, nullptr, workspace, splits, strm(stream), &used);
@@ -2341,11 +2424,12 @@ template <int KB, int PM>
 static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                        int srows, uint8_t* amax, hipStream_t s, const char* what) {
   constexpr int TR = 6;
-  const int tiles_h = (g.P + TR - 1) / TR, tiles_w = g.Q / 64;
+  const int tiles_h = (g.P + TR - 1) / TR, tiles_w = (g.Q + 63) / 64;
   const long long nt = (long long)g.N * tiles_h * tiles_w;
   int gp = 256;
   if (gp > nt) gp = (int)nt;
   if (gp >= 64) gp &= ~7;
+  if (stats && gp > srows) gp = srows;  // one statistics slab row per workgroup
   hipLaunchKernelGGL((k_conv3x3_rows<KB, TR, PM>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
   return launch_rc(what);
@@ -2354,8 +2438,9 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
 ACFE_API int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {
   static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS") || getenv_flag("ACFE_CONV_NO_POOL");
   return !no_rows && dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
-         (K == 64 || K == 128) && W > 0 && W % 64 == 0 && H >= 2 && H % 2 == 0 &&
-         (long long)N * ((H + 5) / 6) * (W / 64) < (1ll << 31) && (long long)N * H * (W / 64) < (1ll << 31) &&
+         (K == 64 || K == 128) && W >= 2 && W % 2 == 0 && H >= 2 && H % 2 == 0 &&
+         (long long)N * ((H + 5) / 6) * ((W + 63) / 64) < (1ll << 31) &&
+         (long long)N * H * ((W + 63) / 64) < (1ll << 31) &&
          (long long)N * (H / 2) * (W / 2) * (C > K ? C : K) < (1ll << 32);  // 32-bit pooled element index
 }
 
@@ -2419,8 +2504,7 @@ ACFE_API int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C,
 ACFE_API int acfe_conv2d_rows_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {
   static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS") || getenv_flag("ACFE_CONV_NO_ADD");
   return !no_rows && dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
-         (K == 64 || K == 128) && W > 0 && W % 64 == 0 && H > 0 &&
-         (long long)N * ((H + 5) / 6) * (W / 64) < (1ll << 31);
+         (K == 64 || K == 128) && W > 0 && H > 0 && (long long)N * ((H + 5) / 6) * ((W + 63) / 64) < (1ll << 31);
 }
 
 ACFE_API int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,

@@ -744,6 +744,63 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   return launch_rc("acfe_mel_fwd");
 }
 
+// ------------------------------------------------------------ stored spectrogram -> mel
+// The load_raw=False path (tfdataset.py:1065-1102): a record holds the
+// magnitude |STFT| [F = 1 + n_fft/2][T] written by audiodataset.load_data
+// (:1302-1303); the model input is tensordot(MEL_WEIGHTS, S^power) [M][T]
+// (power 1: the reference keeps the magnitude for PCEN, :1085-1089).  A
+// 256-thread workgroup owns 64 frames of one clip: lanes = frames (S rows are
+// frame-contiguous, so every tap is one coalesced 256-B load), the 4 waves
+// take interleaved mel bands (m = wave + 4j) of the plan's banded filterbank;
+// overlapping bands re-read a row from L1/L2, never from HBM.  [B][T][M]
+// output goes through an LDS tile so its rows are written contiguously.
+__global__ void __launch_bounds__(256) k_mel_spec(const float* __restrict__ spec, int64_t cs, int F, int T,
+                                                  int power, const int* __restrict__ band,
+                                                  const float* __restrict__ vals, int M, float* __restrict__ out,
+                                                  int layout) {
+  extern __shared__ float tile[];  // [64][M + 1] for layout btm
+  const int b = blockIdx.y, t0 = blockIdx.x * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = t0 + lane;
+  const bool ok = t < T;
+  const float* S = spec + (int64_t)b * cs + (ok ? t : 0);
+  for (int m = w; m < M; m += 4) {
+    const int st = band[3 * m], len = band[3 * m + 1], off = band[3 * m + 2];
+    float acc = 0.f;
+    for (int k = 0; k < len; ++k) {
+      float v = S[(int64_t)(st + k) * T];
+      if (power == 2) v *= v;
+      acc = fmaf(vals[off + k], v, acc);
+    }
+    if (layout == 1) {
+      if (ok) out[((int64_t)b * M + m) * T + t] = acc;
+    } else {
+      tile[lane * (M + 1) + m] = acc;
+    }
+  }
+  if (layout == 0) {
+    __syncthreads();
+    const int nt = min(64, T - t0);
+    for (int i = threadIdx.x; i < nt * M; i += 256) {
+      const int r = i / M, m = i - r * M;
+      out[((int64_t)b * T + t0 + r) * M + m] = tile[r * (M + 1) + m];
+    }
+  }
+}
+
+ACFE_API int acfe_mel_from_spec(acfe_plan_t p, const float* spec, int64_t cs, int batch, int n_bins, int T,
+                                int power, float* out, int layout, void* stream) {
+  if (batch == 0 && p && T > 0) return ACFE_OK;
+  if (!p || !spec || !out || batch < 0 || batch > 65535 || T <= 0 || n_bins != p->n_bins ||
+      (power != 1 && power != 2) || (layout != 0 && layout != 1) || cs < (int64_t)n_bins * T)
+    return ACFE_E_INVAL;
+  const size_t shm = layout == 0 ? sizeof(float) * 64 * (p->n_mels + 1) : 0;
+  if (shm > 65536) return ACFE_E_INVAL;
+  hipLaunchKernelGGL(k_mel_spec, dim3(cdiv(T, 64), batch), dim3(256), shm, strm(stream), spec, cs, n_bins, T,
+                     power, p->d_band, p->d_vals, p->n_mels, out, layout);
+  return launch_rc("acfe_mel_from_spec");
+}
+
 // ------------------------------------------------------------ PCEN
 // Thread per (b, m) row; the EMA recurrence runs sequentially over T (the
 // reference's tf.scan), reading mel [B][T][M] coalesced across threads.

@@ -751,27 +751,27 @@ ACFE_API int acfe_relu_bwd_sum(const void* dy, const void* y, long long rows, in
 }
 
 // Dropout (tf.keras.layers.Dropout: keep with prob 1-rate, scale 1/(1-rate)).
-// Mask = hash(seed, i) >= rate * 2^32, regenerated in the backward.
+// Mask: drop_keep (common.h), regenerated in the backward.
 template <typename T>
 __global__ void k_dropout(const T* __restrict__ x, long long n, float rate, unsigned long long seed,
                           T* __restrict__ y) {
-  const uint32_t thr = (uint32_t)fminf(rate * 4294967296.0f, 4294967295.0f);
-  const float scl = 1.0f / (1.0f - rate);
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const bool keep = hash_u32(seed, (uint64_t)i) >= thr;
-    st(y, i, keep ? ld(x, i) * scl : 0.f);
-  }
+  const Drop d = make_drop(rate, seed);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    st(y, i, drop_keep(d, (uint64_t)i) ? ld(x, i) * d.scl : 0.f);
 }
 template <typename T>
 __global__ void k_dropout8(const T* __restrict__ x, unsigned nvec, float rate, unsigned long long seed,
                            T* __restrict__ y) {
-  const uint32_t thr = (uint32_t)fminf(rate * 4294967296.0f, 4294967295.0f);
-  const float scl = 1.0f / (1.0f - rate);
+  const Drop d = make_drop(rate, seed);
   for (unsigned v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
     float f[8];
     ld8(x + (size_t)v * 8, f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = hash_u32(seed, (uint64_t)v * 8 + j) >= thr ? f[j] * scl : 0.f;
+    for (int j = 0; j < 8; j += 2) {
+      const uint32_t h = drop_pair_hash(d, (uint64_t)v * 8 + j);
+      f[j] = (h & 0xFFFFu) >= d.thr ? f[j] * d.scl : 0.f;
+      f[j + 1] = (h >> 16) >= d.thr ? f[j + 1] * d.scl : 0.f;
+    }
     st8(y + (size_t)v * 8, f);
   }
 }

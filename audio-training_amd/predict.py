@@ -63,7 +63,7 @@ class Predictor:
         self.frontend = FrontEnd(n_mels=n_mels, n_fft=self.meta.get("n_fft", 4096), hop=self.meta.get("hop_length", 281),
                                  fmin=self.meta.get("fmin", 100), fmax=self.meta.get("fmax", 11000),
                                  break_freq=self.meta.get("break_freq", 1000), pcen=self.meta.get("pcen", True),
-                                 dtype=dt, device=self.device)
+                                 dtype=dt, device=self.device, power=self.meta.get("power", 2))
         holder = torch.nn.ModuleList([self.frontend, self.model])
         sd = torch.load(d / "model.pt", map_location="cpu", weights_only=True)
         holder.load_state_dict(sd)

@@ -34,15 +34,20 @@ class BasicBlock(nn.Module):
 
     def forward(self, x, x_stats=None):
         """x -> (block output, its BN statistics slab in training else None);
-        conv2a + Dropout + bn2b run as one fused node (ops.conv_dropout_bn)."""
+        conv2a + Dropout + bn2b run as one fused node (ops.conv_dropout_bn),
+        conv2b + the residual Add + ReLU (+ the next BN's statistics) as
+        another (ops.conv_add: the rows kernel's Add epilogue where it covers
+        the shape, else conv2d -> add).  A conv shortcut's gradient reaches x
+        through autograd's accumulation; the gradient-tensor tags the fused
+        nodes rely on are version-checked (ops._tag)."""
         link = ops.ResidualLink.make() if self.shortcut is None else None
         y = self.bn2a(x, relu=True, stats=x_stats, link=link)
         y = conv_dropout_bn(self.conv2a, self.bn2b, y, self.dropout)
-        y = self.conv2b(y)
         sc = x if self.shortcut is None else self.shortcut(x)
-        if self.training and ops.FUSE:
-            return ops.add(y, sc, relu=True, want_stats=True, link=link)
-        return ops.add(y, sc, relu=True, link=link), None
+        want = self.training and ops.FUSE
+        z, st = ops.conv_add(y, self.conv2b.weight, self.conv2b.bias, sc, relu=True, want_stats=want, link=link,
+                             stride=self.conv2b.strides, padding=self.conv2b.padding)
+        return z, (st if want else None)
 
 
 class WRResNet(nn.Module):

@@ -33,12 +33,18 @@ class AudioDataset:
     """Iterable over device batches; one pass = one epoch."""
 
     def __init__(self, files, labels, batch_size=32, shuffle=True, augment=False, device=None, threads=8,
-                 drop_remainder=False, seed=0, label_map=None, record_shard=None):
+                 drop_remainder=False, seed=0, label_map=None, record_shard=None, load_raw=True):
         """record_shard=(rank, world): keep only the records whose (file index
         + record index) % world == rank -- data-parallel sharding when there
-        are fewer shard files than ranks (otherwise ranks take whole files)."""
+        are fewer shard files than ranks (otherwise ranks take whole files).
+        load_raw=False: batches of the stored magnitude spectrograms
+        [B, 2049, 513] (audio/spectogram, tfdataset.py:1032-1034, 1081-1082);
+        there is no mix_up on that path (tfdataset.py:503-504)."""
         self.files, self.labels = list(files), list(labels)
         self.record_shard = record_shard
+        self.load_raw = load_raw
+        if not load_raw:
+            augment = False
         self.batch_size, self.shuffle, self.augment = batch_size, shuffle, augment
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.threads, self.drop_remainder, self.seed = threads, drop_remainder, seed
@@ -64,13 +70,14 @@ class AudioDataset:
                 for r, rec in enumerate(tfr.read_records(files[i], ignore_errors=True)):  # tfdataset.py:226
                     if shard is not None and (stable.get(files[i], i) + r) % shard[1] != shard[0]:
                         continue
-                    ex = tfr.parse_audio_example(rec)
-                    if not np.all(np.isfinite(ex["raw"])):  # NaN/Inf filter, tfdataset.py:297
+                    ex = tfr.parse_audio_example(rec, load_raw=self.load_raw)
+                    x = ex["raw"] if self.load_raw else ex["spectrogram"]
+                    if not np.all(np.isfinite(x)):  # NaN/Inf filter, tfdataset.py:297
                         continue
                     lab = self.label_map.get(ex["text"], ex["text"])
                     if lab not in self.label_index:
                         continue
-                    q.put((ex["raw"], self.label_index[lab]))
+                    q.put((x, self.label_index[lab]))
 
         ts = [threading.Thread(target=worker, daemon=True) for _ in range(min(self.threads, max(1, len(files))))]
         for t in ts:
@@ -110,7 +117,7 @@ class AudioDataset:
     def _to_device(self, items):
         b = len(items)
         pin = torch.device(self.device).type == "cuda"
-        x = torch.empty((b, N_SAMPLES), dtype=torch.float32, pin_memory=pin)
+        x = torch.empty((b,) + tuple(items[0][0].shape), dtype=torch.float32, pin_memory=pin)
         y = torch.zeros((b, len(self.labels)), dtype=torch.float32, pin_memory=pin)
         for i, (raw, lab) in enumerate(items):
             x[i] = torch.from_numpy(raw)
@@ -126,7 +133,8 @@ class AudioDataset:
             return
         # second independent pass over the data for mix_up (tfdataset.py:473-480)
         other = AudioDataset(self.files, self.labels, self.batch_size, True, False, self.device, self.threads,
-                             self.drop_remainder, self.seed + 7919 * self.epoch, self.label_map, self.record_shard)
+                             self.drop_remainder, self.seed + 7919 * self.epoch, self.label_map, self.record_shard,
+                             self.load_raw)
         for a, b in zip(it, other._batches()):
             if len(a) != len(b):
                 break
@@ -166,6 +174,6 @@ def get_dataset(dir, labels, global_epoch=None, **args):
     ds = AudioDataset(files, labels, batch_size=args.get("batch_size", 32), shuffle=args.get("shuffle", True),
                       augment=args.get("augment", False), device=args.get("device"),
                       threads=args.get("threads", 8), seed=args.get("seed", 0),
-                      label_map=args.get("label_map"))
+                      label_map=args.get("label_map"), load_raw=args.get("load_raw", True))
     logging.info("dataset %s: %d shards, %d labels", dir, len(files), len(labels))
     return ds, remapped, epoch_size, labels, {}

@@ -156,10 +156,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8)
     ap.add_argument("--cpu-steps", type=int, default=10)
-    ap.add_argument("--workload", choices=["train", "infer", "stream"], default="train",
+    ap.add_argument("--clips", type=int, default=4096, help="e2e: clips written to the TFRecord set")
+    ap.add_argument("--workload", choices=["train", "infer", "stream", "e2e"], default="train",
                     help="train = T1/T8 (the driver's line); infer = config I (B=256 fp32 wr_resnet fwd); "
                          "stream = config S (60-min recording, 3 s / 1.5 s windows, batch 1024)")
     a = ap.parse_args()
+    if a.workload == "e2e":
+        return run_e2e(a)
     if a.workload != "train":
         return run_inference(a)
 
@@ -333,6 +336,95 @@ def launch_ranks(n: int) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
     return subprocess.run(cmd, env=env).returncode
+
+
+def _write_shard(args):
+    path, first, count, classes = args
+    sys.path[:0] = [str(ROOT / "audio-training_amd")]
+    import tfrecord as tfr
+
+    bank = synth_bank(64, seed=20260227)
+    rng = np.random.default_rng(first)
+    with tfr.TFRecordWriter(path) as w:
+        for i in range(first, first + count):
+            raw = np.roll(bank[i % 64], int(rng.integers(0, N_SAMPLES)))
+            lab = f"c{i % classes:02d}"
+            w.write(tfr.audio_example(raw, f"r{i}", i, lab, lab))
+    return count
+
+
+def run_e2e(a):
+    """T1 training fed END TO END from GZIP TFRecords (SURVEY 8d's "second run
+    with the TFRecord loader"): `--clips` synthetic clips in the reference
+    schema are written to 16 shards in a temp dir (not timed), then
+    tfdataset.AudioDataset (reader threads: GZIP inflate + protobuf parse into
+    pinned host batches, mix_up pairs) feeds acfe.train.Trainer.  value =
+    clips/s of the timed steps, host loading included."""
+    import tempfile
+    from concurrent.futures import ProcessPoolExecutor
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    classes = a.classes
+    labels = [f"c{i:02d}" for i in range(classes)]
+    tmp = tempfile.mkdtemp(prefix="acfe_e2e_")
+    nsh = 16
+    per = -(-a.clips // nsh)
+    jobs = [(os.path.join(tmp, f"{i:05d}.tfrecord"), i * per, min(per, a.clips - i * per), classes)
+            for i in range(nsh) if a.clips - i * per > 0]
+    t0 = time.perf_counter()
+    with ProcessPoolExecutor(min(16, len(jobs))) as ex:
+        list(ex.map(_write_shard, jobs))
+    t_write = time.perf_counter() - t0
+    import tfdataset
+    from acfe.frontend import sample_mixup_lambda
+    from acfe.train import FrontEnd, Trainer, mix_labels
+
+    if a.model == "bird":
+        from resnet.wr_resnet_bird import WRResNet
+    else:
+        from resnet.wr_resnet import WRResNet
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    torch.manual_seed(1234)
+    model = WRResNet(input_shape=(128, 513, 3), classes=classes, dtype=dtype).to(dev)
+    frontend = FrontEnd(n_mels=128, dtype=dtype, device=dev).to(dev)
+    trainer = Trainer(model, frontend, lr=0.01, loss="cce", device=dev)
+    ds = tfdataset.AudioDataset(tfdataset._files(tmp), labels, batch_size=a.batch, shuffle=True, augment=True,
+                                device=dev, threads=16, drop_remainder=True)
+    def epochs():
+        while True:
+            yield from ds
+
+    it = epochs()
+
+    def step():
+        (x1, y1), (x2, y2) = next(it)
+        lam = sample_mixup_lambda(x1.shape[0], 0.5, 0.25, device=dev)
+        return trainer.step(x1, mix_labels(y1, y2, lam), x2, lam)[0]
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    for _ in range(a.steps):
+        loss = step()
+        n += 1
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    import shutil
+
+    shutil.rmtree(tmp, ignore_errors=True)
+    out = {"metric": "clips/sec training end to end from GZIP TFRecords (3s@48kHz)", "value": round(n * a.batch / el, 2),
+           "unit": "clips/s", "n_gpus": 1, "steps": n, "warmup": a.warmup,
+           "ms_per_step": round(el / max(n, 1) * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+           "data": f"synthetic clips written as {len(jobs)} GZIP TFRecord shards ({a.clips} clips, {t_write:.1f} s to "
+                   f"write, not timed), read by tfdataset.AudioDataset (16 reader threads, mix_up pairs)",
+           "config": {"workload": "T1 end to end: TFRecord loader + training step",
+                      "model": "wr_resnet_bird" if a.model == "bird" else "wr_resnet", "classes": classes,
+                      "batch": a.batch}, "final_loss": round(float(loss.item()), 5)}
+    print(json.dumps(out), flush=True)
 
 
 def run_inference(a):

@@ -106,6 +106,15 @@ int acfe_mel_fwd(acfe_plan_t plan, const float* raw, int64_t clip_stride, int ba
                  const float* stats, int pad_mode, int power, float* out, int layout,
                  void* stream);
 
+/* Stored-spectrogram path (load_raw=False): mel = W . S^power of the magnitude
+ * spectrogram each record holds, S = |librosa.stft| [n_bins][T] fp32 (clip b at
+ * spec + b*clip_stride, frame-contiguous rows), through the plan's banded
+ * filterbank; out [B][T][M] (layout 0) or [B][M][T] (layout 1).  Replaces the
+ * per-example tf.tensordot(MEL_WEIGHTS, spectogram) of tfdataset.py:1082-1090
+ * (power 1 there: the magnitude is kept for PCEN, :1085-1089). */
+int acfe_mel_from_spec(acfe_plan_t plan, const float* spec, int64_t clip_stride, int batch, int n_bins, int T,
+                       int power, float* out, int layout, void* stream);
+
 /* PCEN forward on mel [B][T][M] fp32 (tfpcen.py:89-95):
  *   a_t = w x_t + (1-w) a_{t-1}, a_{-1} = x_0,  w = clip(smooth, 0, 1)
  *   y   = (x/(eps + a)^min(gain,1) + bias)^(1/max(root,1)) - bias^(1/max(root,1))

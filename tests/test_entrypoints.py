@@ -9,10 +9,12 @@ import pytest
 from conftest import PKG
 
 
-def _build(tmp_path, n=24):
+def _build(tmp_path, n=24, spectrogram=True):
     import build
 
-    assert build.main([str(tmp_path / "ds"), "--synthetic", str(n), "--labels", "bird,noise", "--shards", "2"]) == 0
+    extra = [] if spectrogram else ["--no-spectrogram"]
+    assert build.main([str(tmp_path / "ds"), "--synthetic", str(n), "--labels", "bird,noise", "--shards", "2"]
+                      + extra) == 0
     return tmp_path / "ds" / "training-data"
 
 
@@ -31,6 +33,8 @@ def test_build_synthetic_records(tmp_path):
             for rec in tfr.read_records(f):
                 ex = tfr.parse_audio_example(rec)
                 assert ex["raw"].shape == (144000,) and ex["text"] in ("bird", "noise")
+                sp = tfr.parse_audio_example(rec, load_raw=False)["spectrogram"]
+                assert sp.shape == (2049, 513) and sp.dtype == np.float32
                 seen.setdefault(ex["rec_id"], set()).add(split)
                 n += 1
         assert n == sum(meta["counts"][split]["sample_counts"].values())
@@ -39,19 +43,40 @@ def test_build_synthetic_records(tmp_path):
     assert all(len(v) == 1 for v in seen.values())  # no recording in two splits
 
 
+def test_stored_spectrogram_matches_oracle():
+    """build.stft_magnitude = the audio/spectogram audiodataset.load_data stores
+    (:1302-1303: |librosa.stft(normalize_data(clip))|, center=True, constant
+    padding) against the float64 oracle restatement (oracle.frontend.stft_center)."""
+    import build
+    from oracle import frontend as of
+
+    clip = build.synth_clip(np.random.default_rng(5), False)
+    got = build.stft_magnitude(clip)
+    ref = np.abs(of.stft_center(of.normalize(clip)[None], 4096, 281, "constant"))[0]
+    assert got.shape == ref.shape == (2049, 513)
+    assert np.abs(got - ref).max() <= 2e-6 * np.abs(ref).max()
+
+
 @pytest.mark.gpu
-def test_train_checkpoint_predict(tmp_path, cuda):
+@pytest.mark.parametrize("load_raw", [False, True], ids=["spectrogram", "raw"])
+def test_train_checkpoint_predict(tmp_path, cuda, load_raw):
+    """The default CLI path trains on the stored spectrograms (--load-raw is a
+    count flag defaulting to off, audiomodel.py:2344-2349); --load-raw trains on
+    the raw audio with the GPU STFT and mix_up."""
     import audiomodel
     import predict
     from scipy.io import wavfile
 
     td = _build(tmp_path, 16)
     args = audiomodel.parse_args(["run1", "-d", str(td), "--epochs", "1", "--batch-size", "4", "--model-name",
-                                  "wr-resnet-bird", "--n_mels", "128", "--checkpoint-dir", str(tmp_path / "ck")])
+                                  "wr-resnet-bird", "--n_mels", "128", "--checkpoint-dir", str(tmp_path / "ck")]
+                                 + (["--load-raw"] if load_raw else []))
     hist = audiomodel.train_model(args)
     assert np.isfinite(hist["loss"][0])
     ck = tmp_path / "ck" / "run1"
-    assert (ck / "model.pt").exists() and json.loads((ck / "metadata.txt").read_text())["labels"] == ["bird", "noise"]
+    meta = json.loads((ck / "metadata.txt").read_text())
+    assert (ck / "model.pt").exists() and meta["labels"] == ["bird", "noise"]
+    assert meta["power"] == (2 if load_raw else 1) and meta["load_raw"] == load_raw
     # 10 s synthetic recording -> 8 windows at 1 s stride
     import build
 
@@ -75,12 +100,13 @@ def test_config_p_plumbing(tmp_path, cuda):
     import audiomodel
 
     t0 = time.perf_counter()
-    td = _build(tmp_path, 256)
+    td = _build(tmp_path, 256, spectrogram=False)
     t_build = time.perf_counter() - t0
     meta = json.loads((td / "training-meta.json").read_text())
     n_train = sum(meta["counts"]["train"]["sample_counts"].values())
     args = audiomodel.parse_args(["p", "-d", str(td), "--epochs", "1", "--batch-size", "8", "--model-name",
-                                  "wr-resnet", "--n_mels", "128", "--checkpoint-dir", str(tmp_path / "ck")])
+                                  "wr-resnet", "--n_mels", "128", "--load-raw", "--checkpoint-dir",
+                                  str(tmp_path / "ck")])
     hist = audiomodel.train_model(args)
     assert np.isfinite(hist["loss"][0]) and np.isfinite(hist["val_loss"][0])
     assert 0.0 <= hist["val_accuracy"][0] <= 1.0

@@ -138,3 +138,58 @@ def test_pcen_backward(fe, cuda, params):
     (ref * g).sum().backward()
     gg, gr = p.grad.cpu().double().numpy(), pr.grad.numpy()
     np.testing.assert_allclose(gg, gr, rtol=2e-3, atol=2e-3 * np.abs(gr).max())
+
+
+@pytest.mark.parametrize("power", [1, 2])
+def test_mel_from_spec_golden(fe, cuda, power):
+    """acfe_mel_from_spec (the load_raw=False path, tfdataset.py:1082-1090) on the
+    golden |S| fixtures against the reference custommel.mel_spec output
+    (tests/golden/mel_spec_p{1,2}.npz, generated from the reference itself):
+    three clips at a clip stride, both output layouts; the plan's own
+    filterbank is pinned separately (bit-exact mel_f goldens)."""
+    import numpy as np
+    from conftest import GOLDEN
+
+    d = np.load(GOLDEN / f"mel_spec_p{power}.npz")
+    S, ref = d["S"].astype(np.float32), d["mel"].astype(np.float64)   # [2049, T], [128, T]
+    T = S.shape[1]
+    plan = fe.MelPlan(n_mels=128)
+    spec = torch.from_numpy(np.stack([S, 0.5 * S, S[:, ::-1].copy()])).to(cuda)
+    refs = [ref, 0.5 ** power * ref, None]
+    for layout in ("btm", "bmt"):
+        out = plan.mel_from_spec(spec, power=power, layout=layout).double().cpu().numpy()
+        if layout == "btm":
+            out = out.transpose(0, 2, 1)
+        for b, r in enumerate(refs):
+            if r is None:  # time-reversed clip: same weights, reversed frames
+                r = out[0][:, ::-1] * 1.0
+                assert np.allclose(out[b], r, rtol=1e-6, atol=1e-6 * np.abs(r).max())
+                continue
+            assert np.abs(out[b] - r).max() <= 2e-6 * np.abs(r).max(), (b, layout)
+
+
+def test_stored_spectrogram_path_matches_raw_path(fe, cuda):
+    """The stored spectrogram of build.py (|centre-padded STFT| of the
+    normalised clip, audiodataset.py:1302-1303) through acfe_mel_from_spec
+    equals the fused raw-audio kernel run with the same framing
+    (acfe_mel_fwd, centre / constant padding, power 1), and the full
+    FrontEnd.forward_spec (PCEN) equals PCEN of the oracle mel."""
+    import numpy as np
+    import build
+    from acfe.train import FrontEnd
+    from oracle import frontend as of
+
+    rng = np.random.default_rng(9)
+    clips = np.stack([build.synth_clip(rng, i == 1) for i in range(3)])
+    spec = torch.from_numpy(np.stack([build.stft_magnitude(c) for c in clips])).to(cuda)
+    plan = fe.MelPlan(n_mels=128)
+    a = plan.mel_from_spec(spec, power=1, layout="btm")
+    x = torch.from_numpy(clips).to(cuda)
+    b = plan.mel(x, fe.normalize_stats(x), pad_mode="constant", power=1, layout="btm")
+    rel = ((a - b).norm() / b.norm()).item()
+    assert rel < 1e-5, rel
+    front = FrontEnd(n_mels=128, dtype=torch.float32, device=cuda).to(cuda)
+    got = front.forward_spec(spec).detach().double().cpu().numpy()
+    mel = np.einsum("mf,bft->btm", plan.weights.astype(np.float64), spec.double().cpu().numpy())
+    ref = of.pcen(mel).transpose(0, 2, 1)
+    assert np.abs(got - ref).max() < 5e-5

@@ -246,3 +246,72 @@ def test_bird_t1_shape_eval_parity(cuda):
     g_dev = torch.cat([q.grad.reshape(-1).double().cpu() for q in m.parameters()])
     g_ref = torch.cat([prm[n].grad.reshape(-1) for n in names])
     assert ((g_dev - g_ref).norm() / g_ref.norm()).item() < 5e-2
+
+
+@pytest.mark.parametrize("W", [130, 513], ids=["W130", "W513"])
+def test_conv_rows_partial_column_tile(env, cuda, W):
+    """wr_resnet's 513- / 257-wide stages run the rows / halo kernels with a
+    partial last 64-pixel column tile (masked loads past Q, masked stores):
+    fwd (+ BN sums), stride-1 dgrad and wgrad through the generic entry points
+    against float64, and the pooled forward at an even width."""
+    ops, call, lib, ptr, stream = env
+    N, H, C, K = 4, 20, 64, 64
+    x, w, b, g = _data(N, H, W, C, K, 107, cuda)
+    assert lib.acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, 1)
+    wp, wf = ops.pack_weights(w, BF, False), ops.pack_weights(w, BF, True)
+    y = torch.empty((N, H, W, K), dtype=BF, device=cuda)
+    st = torch.empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), dtype=F64, device=cuda)
+    call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b), ptr(y), 1, ptr(st), stream())
+    dy = (torch.randn((N, H, W, K), generator=g) * 0.5).to(BF).to(cuda)
+    dx = torch.empty_like(x)
+    call("acfe_conv2d_dgrad", ptr(dy), N, H, W, K, ptr(wf), C, 3, 3, 1, 1, 1, H, W, ptr(dx), 1, None, stream())
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+    dw = torch.empty((K, 3, 3, C), device=cuda)
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, 3, 3, 1, 1, 1, H, W, ptr(dw), 0.0, 1, ptr(ws),
+         stream())
+    torch.cuda.synchronize()
+    _within_ulp(y, _oracle_conv(x, w, b), what="fwd partial")
+    torch.testing.assert_close(st.sum(0)[:, :K].cpu(), _sums(y), rtol=1e-6, atol=1e-6)
+    wd = w.cpu().to(BF).to(F64).permute(0, 3, 1, 2)
+    gd = dy.cpu().to(F64).permute(0, 3, 1, 2)
+    _within_ulp(dx, F.conv_transpose2d(gd, wd, padding=1).permute(0, 2, 3, 1), what="dgrad partial")
+    dw_exact = torch.nn.grad.conv2d_weight(x.cpu().to(F64).permute(0, 3, 1, 2), wd.shape, gd,
+                                           padding=1).permute(0, 2, 3, 1)
+    d = dw.cpu().to(F64)
+    assert ((d - dw_exact).norm() / dw_exact.norm()).item() < 5e-5
+    if W % 2 == 0:
+        assert lib.acfe_conv2d_pool_supported(N, H, W, C, K, 3, 3, 1)
+        P, Q = H // 2, W // 2
+        yp = torch.empty((N, P, Q, K), dtype=BF, device=cuda)
+        am = torch.empty((N, P, Q, K), dtype=torch.uint8, device=cuda)
+        call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(yp), ptr(am), 0.0, 0, None,
+             1, stream())
+        torch.cuda.synchronize()
+        win = _oracle_conv(x, w, b).reshape(N, P, 2, Q, 2, K).permute(0, 1, 3, 5, 2, 4).reshape(N, P, Q, K, 4)
+        _within_ulp(yp, win.max(-1).values, what="pool partial")
+
+
+def test_conv_rows_narrow_image_stats(env, cuda):
+    """A narrow image (W = 16: one partial 64-pixel column tile per 6 rows) has
+    more rows-kernel tiles than 128-pixel statistics slab rows; the launch
+    caps its grid at the slab rows (each workgroup owns slab row blockIdx.x).
+    Forward with dropout + BN sums (acfe_conv2d_fwd_dropout) against float64."""
+    ops, call, lib, ptr, stream = env
+    N, H, W, C, K = 2, 64, 16, 64, 64
+    x, w, b, g = _data(N, H, W, C, K, 108, cuda)
+    wp = ops.pack_weights(w, BF, False)
+    rows = lib.acfe_conv2d_stats_rows(N * H * W, K)
+    # slab padded with sentinel rows: nothing may be written past `rows`
+    st = torch.full((rows + 4, 2, wp.shape[0]), 7.0, dtype=F64, device=cuda)
+    y0, y1 = (torch.empty((N, H, W, K), dtype=BF, device=cuda) for _ in range(2))
+    call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b), ptr(y0), 1, None, stream())
+    call("acfe_conv2d_fwd_dropout", ptr(x), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b), ptr(y1), 1,
+         ptr(st), 0.1, 31, stream())
+    torch.cuda.synchronize()
+    _within_ulp(y0, _oracle_conv(x, w, b), what="narrow fwd")
+    ref = torch.empty_like(y0)
+    call("acfe_dropout", ptr(y0), y0.numel(), 0.1, 31, ptr(ref), 1, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y1, ref)
+    torch.testing.assert_close(st[:rows].sum(0)[:, :K].cpu(), _sums(y1), rtol=1e-6, atol=1e-6)
+    assert bool((st[rows:] == 7.0).all())
