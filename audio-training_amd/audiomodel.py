@@ -60,8 +60,13 @@ def load_meta(data_dir):
 
 
 def save_checkpoint(out_dir: Path, trainer, meta: dict, history: dict | None = None):
+    """model.pt (front end + model state) and the model's weights in the Keras 3
+    `*.weights.h5` layout the reference's checkpoints use (audiomodel.py:878-938)."""
+    from keras_weights import save_keras_weights
+
     out_dir.mkdir(parents=True, exist_ok=True)
     torch.save({k: v.detach().cpu() for k, v in trainer.holder.state_dict().items()}, out_dir / "model.pt")
+    save_keras_weights(trainer.model, out_dir / "model.weights.h5")
     m = dict(meta)
     if history:
         m["history"] = history
@@ -167,8 +172,13 @@ def train_model(args):
                         pcen=args.pcen, dtype=dtype, device=dev).to(dev)
     trainer = Trainer(model, frontend, lr=args.lr, loss="bce" if args.multi_label else "cce", device=dev)
     if args.weights:
-        sd = torch.load(args.weights, map_location="cpu", weights_only=True)
-        trainer.holder.load_state_dict(sd)
+        if str(args.weights).endswith((".h5", ".keras")):  # reference checkpoints (audiomodel.py:569-595)
+            from keras_weights import load_keras_weights
+
+            load_keras_weights(model, args.weights)
+        else:
+            sd = torch.load(args.weights, map_location="cpu", weights_only=True)
+            trainer.holder.load_state_dict(sd)
     files, rshard = shard_files(tfdataset._files(td / "train"), rank, world)
     load_raw = bool(args.load_raw)
     train_ds = tfdataset.AudioDataset(files, labels, batch_size=args.batch_size, shuffle=args.shuffle,
@@ -243,7 +253,7 @@ def parse_args(argv=None):
     p.add_argument("--fmax", type=float, default=None)
     p.add_argument("--n_fft", type=int, default=None)
     p.add_argument("--break-freq", type=float, default=None)
-    p.add_argument("-w", "--weights", help="model.pt to start from")
+    p.add_argument("-w", "--weights", help="model.pt, or a Keras *.weights.h5 / .keras file, to start from")
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--batch-size", type=int, default=32)
     p.add_argument("--shuffle", type=str2bool, default=True)

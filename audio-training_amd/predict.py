@@ -65,8 +65,16 @@ class Predictor:
                                  break_freq=self.meta.get("break_freq", 1000), pcen=self.meta.get("pcen", True),
                                  dtype=dt, device=self.device, power=self.meta.get("power", 2))
         holder = torch.nn.ModuleList([self.frontend, self.model])
-        sd = torch.load(d / "model.pt", map_location="cpu", weights_only=True)
-        holder.load_state_dict(sd)
+        if (d / "model.pt").exists():
+            sd = torch.load(d / "model.pt", map_location="cpu", weights_only=True)
+            holder.load_state_dict(sd)
+        else:  # a reference checkpoint dir: {run}.keras / *.weights.h5 (predict.py:746-789)
+            from keras_weights import load_keras_weights
+
+            cands = sorted(d.glob("*.keras")) + sorted(d.glob("*.weights.h5"))
+            if not cands:
+                raise FileNotFoundError(f"{d}: no model.pt, *.keras or *.weights.h5")
+            load_keras_weights(self.model, cands[0])
         holder.to(self.device).eval()
 
     @torch.no_grad()

@@ -30,6 +30,7 @@ class BasicBlock(nn.Module):
         if cin != F2:
             # Keras default padding "valid", default (unseeded) GlorotUniform
             self.shortcut = Conv2D(cin, F2, 1, stride, "valid", name=f"conv2d_shortcut_{stage}{block}", seed=seed + 1)
+            self.shortcut.keras_auto = True  # unnamed in the reference (:84-86): Keras auto-names it
         self.out_channels = F2
 
     def forward(self, x, x_stats=None):

@@ -42,6 +42,7 @@ class BasicBlock(nn.Module):
         self.shortcut = None
         if cin != filters:
             self.shortcut = Conv2D(cin, filters, 1, 1, "same", name=f"conv2d_shortcut_{stage}{block}", seed=seed)
+            self.shortcut.keras_auto = True  # unnamed in the reference (:169-174): Keras auto-names it
         self.relu_out = stage + sub_id > 1
         self.out_channels = filters
         self.out_height = height // stride if stride > 1 else height
@@ -92,6 +93,7 @@ class WRResNet(nn.Module):
         n = int((depth - 4) / 6)
         self.conv1_1 = StemConv2D(cin, filters[0], (5, 5), name="conv1_1", seed=seed, out_dtype=dtype)
         self.bn_stem = BatchNormalization(filters[0], "batch_normalization")
+        self.bn_stem.keras_auto = True
         h, w, c = H, W // 2, filters[0]
         blocks = []
         for stage in range(1, len(filters)):
@@ -112,6 +114,10 @@ class WRResNet(nn.Module):
         self.head_conv3 = Conv2D(FILTERS[-1] * 2, classes, 1, 1, "same", name="conv2d_head_3", seed=seed)
         self.prediction = Dense(w, classes, name="prediction", seed=seed)
         self.feature_hw = (h, w)
+        # layers the reference leaves unnamed (:47-70): matched by class and
+        # creation order when Keras weight files are read (keras_weights.py)
+        for m in (self.head_conv1, self.head_bn1, self.head_conv2, self.head_bn2, self.head_conv3):
+            m.keras_auto = True
 
     def forward(self, x):
         if x.dim() == 4:

@@ -5,6 +5,7 @@ import sys
 
 import numpy as np
 import pytest
+import torch
 
 from conftest import PKG
 
@@ -76,6 +77,7 @@ def test_train_checkpoint_predict(tmp_path, cuda, load_raw):
     ck = tmp_path / "ck" / "run1"
     meta = json.loads((ck / "metadata.txt").read_text())
     assert (ck / "model.pt").exists() and meta["labels"] == ["bird", "noise"]
+    assert (ck / "model.weights.h5").exists()  # Keras 3 layout, as the reference's checkpoints
     assert meta["power"] == (2 if load_raw else 1) and meta["load_raw"] == load_raw
     # 10 s synthetic recording -> 8 windows at 1 s stride
     import build
@@ -87,6 +89,18 @@ def test_train_checkpoint_predict(tmp_path, cuda, load_raw):
     r = p.predict_file(tmp_path / "rec.wav", stride=1.0, batch_size=4)
     assert r["windows"] == 8
     assert set(r["mean"]) == {"bird", "noise"} and all(0 <= v <= 1 for v in r["mean"].values())
+    # the same checkpoint read through its Keras weights file (no model.pt):
+    # identical model outputs (PCEN at its default init on both sides is not
+    # compared: the reference's wr-resnet models carry no PCEN)
+    import shutil
+
+    kd = tmp_path / "keras_ck"
+    kd.mkdir()
+    shutil.copy(ck / "metadata.txt", kd / "metadata.txt")
+    shutil.copy(ck / "model.weights.h5", kd / "model.weights.h5")
+    pk = predict.Predictor(kd)
+    for (n1, t1), (n2, t2) in zip(p.model.state_dict().items(), pk.model.state_dict().items()):
+        assert n1 == n2 and torch.equal(t1.cpu(), t2.cpu()), n1
 
 
 @pytest.mark.gpu

@@ -45,14 +45,15 @@ def cpu_model():
     return platform.processor()
 
 
-def median_time(fn, reps, warm=1):
+def median_time(fn, reps, warm=1, what=""):
     for _ in range(warm):
         fn()
     ts = []
-    for _ in range(reps):
+    for i in range(reps):
         t0 = time.perf_counter()
         fn()
         ts.append(time.perf_counter() - t0)
+        print(f"  {what} rep {i + 1}/{reps}: {ts[-1]:.2f} s", flush=True)  # progress (a silent minute looks hung)
     return statistics.median(ts), ts
 
 
@@ -90,7 +91,7 @@ def main():
     # ---- front end
     B = 8 if q else 64
     raw = torch.from_numpy(synth_bank(B, seed=11))
-    t, ts = median_time(lambda: frontend_port(raw, weights, pc), 2 if q else 10)
+    t, ts = median_time(lambda: frontend_port(raw, weights, pc), 2 if q else 10, what="frontend")
     rows["frontend"] = {"value": round(B / t, 3), "unit": "clips/s", "GBps": round(B * FRONTEND_BYTES / t / 1e9, 4),
                         "cores": cores, "kind": "port",
                         "sample": f"median of {len(ts)} batches of {B} clips (after 1 warm-up): {t:.3f} s/batch"}
@@ -106,7 +107,7 @@ def main():
             f = frontend_port(raw, weights, pc)
             return om.wr_resnet(f[:, None].repeat(1, 3, 1, 1), p, False, {k: v for k, v in p.items() if "moving" in k})
 
-    t, ts = median_time(infer, 1 if q else 3)
+    t, ts = median_time(infer, 1 if q else 3, what="inference")
     rows["inference"] = {"value": round(B / t, 3), "unit": "clips/s", "cores": cores, "kind": "port",
                          "sample": f"median of {len(ts)} batches of {B} clips (after 1 warm-up), front end + "
                                    f"wr_resnet forward fp32: {t:.2f} s/batch"}
@@ -136,7 +137,7 @@ def main():
                 x.copy_(nx)
                 x.grad = None
 
-    t, ts = median_time(train, 1 if q else 5)
+    t, ts = median_time(train, 1 if q else 5, what="training")
     rows["training"] = {"value": round(B / t, 3), "unit": "clips/s", "cores": cores, "kind": "port",
                         "sample": f"median of {len(ts)} steps of {B} clips (after 1 warm-up): front end + "
                                   f"wr_resnet_bird fwd/bwd fp32 + Keras Adam, {t:.2f} s/step"}
@@ -174,6 +175,7 @@ def main():
                     v.grad = None
             steps += 1
             clips += x.shape[0]
+            print(f"  config P step {steps}", flush=True)
             if steps >= max_steps:
                 break
         dt = time.perf_counter() - t0
