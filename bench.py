@@ -260,8 +260,9 @@ def main():
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
     traffic = None
-    pmc = ROOT / "profiles" / "pmc_dominant_r01l.json"
-    if pmc.exists():
+    pmc = next((q for q in (ROOT / "profiles" / f"pmc_dominant_{t}.json" for t in ("r02", "r01l")) if q.exists()),
+               None)
+    if pmc is not None:
         try:
             traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
         except Exception:
@@ -316,6 +317,13 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps, a.model, a.classes)
+        suite = ROOT / "profiles" / "r02_cpu_baseline.json"
+        if suite.exists():  # the other workloads' CPU rows (tools/cpu_baseline.py, same host type)
+            try:
+                out["cpu_baseline"]["suite"] = {"source": "profiles/r02_cpu_baseline.json",
+                                                **json.loads(suite.read_text())["rows"]}
+            except (ValueError, KeyError):
+                pass
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

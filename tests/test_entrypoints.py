@@ -89,6 +89,17 @@ def test_train_checkpoint_predict(tmp_path, cuda, load_raw):
     r = p.predict_file(tmp_path / "rec.wav", stride=1.0, batch_size=4)
     assert r["windows"] == 8
     assert set(r["mean"]) == {"bird", "noise"} and all(0 <= v <= 1 for v in r["mean"].values())
+    # track mode gathers windows on the host: the same windows read in place
+    # by the fused front end give the same probabilities
+    wins = np.stack([rec[k * 48000:(k + 3) * 48000] for k in range(8)])
+    a, b = p.predict_clips(wins, batch_size=8), p.predict_windows(rec, 1.0, batch_size=8)
+    assert np.abs(a - b).max() < 2e-3
+    tracks, end = p.predict_tracks(rec, batch_size=4, rng=np.random.RandomState(0))
+    assert end == pytest.approx(len(rec) / 48000)
+    for t in tracks:
+        (res,) = t.predictions
+        assert res.labels or res.raw_tag in ("bird", "noise")
+    predict.main([str(ck), "--file", str(tmp_path / "rec.wav"), "--mode", "tracks"])
     # the same checkpoint read through its Keras weights file (no model.pt):
     # identical model outputs (PCEN at its default init on both sides is not
     # compared: the reference's wr-resnet models carry no PCEN)

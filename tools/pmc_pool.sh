@@ -5,7 +5,7 @@
 # Then tools/pmc_traffic.py folds the passes into profiles/pmc_dominant_<tag>.json.
 # usage: tools/pmc_pool.sh [tag]
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-TAG=${1:-r01l}
+TAG=${1:-r02}
 O=gpurun_out/pmc_pool
 mkdir -p $O
 i=0
@@ -18,3 +18,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE"; do
   fi
   i=$((i+1))
 done
+python tools/pmc_traffic.py $O $TAG pool

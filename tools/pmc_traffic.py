@@ -36,16 +36,25 @@ def per_dispatch(d):
 
 def main():
     d, tag = sys.argv[1], sys.argv[2]
+    pool = len(sys.argv) > 3 and sys.argv[3] == "pool"
     agg = {}
     for p in sorted(glob.glob(f"{d}/p*/")):
         agg.update(per_dispatch(p))
     fetch = agg.get("FETCH_SIZE", 0.0) * 1024 * 2       # KiB -> B, x2 gfx950 correction
     write = agg.get("WRITE_SIZE", 0.0) * 1024
     B, H, W, C, K = 512, 128, 256, 128, 128
-    algo = (B * H * W * C + B * H * W * K) * 2 + K * 9 * C * 2
+    if pool:  # input + pooled output + 1-byte argmax per pooled output (weights negligible)
+        algo = B * H * W * C * 2 + B * (H // 2) * (W // 2) * K * 3 + K * 9 * C * 2
+        kern = ("k_conv3x3_rows<128,6,1> (s1b0 conv21 3x3 128->128 @128x256 + 2x2 max-pool/dropout/BN-sums "
+                "epilogue, batch 512)")
+        src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes inside bench.py (tools/pmc_pool.sh)"
+    else:
+        algo = (B * H * W * C + B * H * W * K) * 2 + K * 9 * C * 2
+        kern = "k_conv3x3_rows<128,3> (s1b0 conv21 3x3 128->128 @128x256, batch 512)"
+        src = "rocprofv3 --pmc, separate passes (tools/pmc_traffic.sh), conv_bench --layers 0 --passes fwd"
     res = {
-        "kernel": "k_conv3x3_rows<128,3> (s1b0 conv21 3x3 128->128 @128x256, batch 512)",
-        "source": "rocprofv3 --pmc, separate passes (tools/pmc_traffic.sh), conv_bench --layers 0 --passes fwd",
+        "kernel": kern,
+        "source": src,
         "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
         "hbm_bytes_per_launch": fetch + write,
         "algorithmic_bytes_per_launch": algo,
