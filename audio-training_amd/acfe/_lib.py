@@ -10,7 +10,8 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libacfe.so"
+# ACFE_LIB: an alternative build of the same library (A/B experiments, tools/ab_lib.sh)
+LIB_PATH = Path(os.environ.get("ACFE_LIB") or Path(__file__).resolve().parent / "libacfe.so")
 
 P = C.c_void_p
 I32 = C.c_int

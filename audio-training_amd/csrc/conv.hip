@@ -1279,6 +1279,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     }
     const unsigned char* Xl = xbuf(buf);
     const unsigned char* Wl = WDMA ? smem + WBASE + (t & 1) * WBYTES : Xl + XBYTES;
+    // K = 64: let the scheduler interleave the fragment reads with the MFMAs
+    // (fwd_add 128->64 1.084 -> 1.013 ms, dropout 64->64 0.649 -> 0.625 ms;
+    // at K = 128 the same hint spills: fwd_pool 4.96 -> 5.35 ms, r02o)
+    if constexpr (KB == 64) __builtin_amdgcn_iglp_opt(0);
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
@@ -1992,6 +1996,158 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     }
 }
 
+// ------------------------------------------------------------------ wgrad, R x S stride 1, one filter row per workgroup
+// dW[k][r][s][c] of the wide-kernel layer of wr_resnet_bird's head (Conv2D
+// (4, 10) 256 -> 128 at 16 x 32, resnet/wr_resnet_bird.py:47-52), whose
+// im2col wgrad re-reads every input pixel 40 times (k_conv_wgrad: 500
+// TFLOP/s).  A workgroup owns one filter row r, one 64-channel chunk and ALL
+// S taps of that row (output tile K x S*64) and reduces over a contiguous
+// range of SEGW-pixel output-row segments, NSEG per pipeline step: per step
+// it stages dY[NSEG x SEGW px][K] and the matching input rows (row h + r - pt)
+// as NSEG halo strips of SEGW + S - 1 pixels x 64 channels ONCE; the S taps
+// are shifted views of a strip.  8 waves = 2 halves of K x 4 groups of S
+// (tap, 16-channel) blocks; per step each wave runs NSEG * (SEGW / 32) *
+// (K / 32) * S MFMAs (160 for the head).  LDS images and fragment reads as in
+// k_wgrad3x3_halo (pixel-major, 288-B / 160-B padded rows read by
+// ds_read_b64_tr_b16), register-staged double buffer, one barrier per step;
+// split-K slabs combined by k_wgrad_reduce_g.
+template <int KB, int S, int SEGW, int NSEG>
+__global__ void __launch_bounds__(512, 1)
+k_wgrad_row_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
+                 float* __restrict__ ws, int ngroups, int nchunk, int nseg, int segs_per_split) {
+  constexpr int HWX = SEGW + S - 1;
+  constexpr int LDD = KB + 16, LDX = 64 + 16;
+  constexpr int DS = NSEG * SEGW * LDD, XS = NSEG * HWX * LDX;
+  constexpr int FM = KB / 32, FN = S;  // 4 wave groups x S blocks = S taps x 4 channel blocks
+  constexpr int DGR = KB / 8, DG = NSEG * SEGW * DGR, XG = NSEG * HWX * 8;
+  constexpr int DPT = (DG + 511) / 512, XPT = (XG + 511) / 512;
+  static_assert(SEGW % 32 == 0, "segment = whole 32-pixel MFMA k-chunks");
+  static_assert(2 * (DS + XS) * 2 <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (DS + XS)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wid >> 2, wc = wid & 3;
+  const int xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
+  const int grp = bi % ngroups, split = (bi / ngroups) * 8 + xcd;
+  const int r = grp / nchunk, cc = grp - r * nchunk;
+  const int sbeg = split * segs_per_split;
+  const int send = sbeg + segs_per_split < nseg ? sbeg + segs_per_split : nseg;
+  const int QS = (g.Q + SEGW - 1) / SEGW;
+  const T16* zp = reinterpret_cast<const T16*>(g_zero_page);
+
+  u32x4 rd[DPT], rx[XPT];
+  auto gload = [&](int s0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int px = idx / DGR, cg = idx - px * DGR;
+      const int sg = px / SEGW, pxs = px - sg * SEGW;
+      const int seg = s0 + sg;
+      const int n = seg / (g.P * QS), rem = seg - n * (g.P * QS);
+      const int h = rem / QS, w = (rem - h * QS) * SEGW + pxs;
+      const bool ok = idx < DG && seg < send && w < g.Q;
+      rd[i] = *reinterpret_cast<const u32x4*>(ok ? dY + (((long long)n * g.P + h) * g.Q + w) * g.K + cg * 8 : zp);
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx >> 3, cg = idx & 7;
+      const int sg = row / HWX, hp = row - sg * HWX;
+      const int seg = s0 + sg;
+      const int n = seg / (g.P * QS), rem = seg - n * (g.P * QS);
+      const int h = rem / QS, w0 = (rem - h * QS) * SEGW;
+      const int hin = h + r - g.pt, win = w0 - g.pl + hp;
+      const bool ok = idx < XG && seg < send && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
+      rx[i] = *reinterpret_cast<const u32x4*>(
+          ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + cg * 8 : zp);
+    }
+  };
+  auto sstore = [&](int buf) __attribute__((always_inline)) {
+    uint16_t* Ds = smem + buf * (DS + XS);
+    uint16_t* Xh = Ds + DS;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int idx = tid + 512 * i;
+      const int px = idx / DGR, cg = idx - px * DGR;
+      if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i;
+      if (idx < XG) *reinterpret_cast<u32x4*>(Xh + (idx >> 3) * LDX + (idx & 7) * 8) = rx[i];
+    }
+  };
+
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // this wave's S blocks: block b = wc * S + fn -> tap b / 4, channels (b % 4) * 16
+  const int grp4 = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  typedef __attribute__((address_space(3))) bf4* lp;
+
+  if (sbeg < send) {
+    gload(sbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int s0 = sbeg; s0 < send; s0 += NSEG) {
+    const bool more = s0 + NSEG < send;
+    if (more) gload(s0 + NSEG);
+    const uint16_t* Ds = smem + buf * (DS + XS);
+    const uint16_t* Xh = Ds + DS;
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg)
+#pragma unroll
+      for (int kc = 0; kc < SEGW / 32; ++kc) {
+        const int rb = sg * SEGW + kc * 32;  // dY pixel row of this 32-pixel chunk
+        const int xb0 = sg * HWX + kc * 32;  // halo pixel of tap 0
+        bf8 af[FM];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int col = wk * (KB / 2) + fm * 16 + 4 * pp;
+          const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(Ds + (rb + 4 * grp4 + q) * LDD + col)));
+          const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(Ds + (rb + 16 + 4 * grp4 + q) * LDD + col)));
+          af[fm] = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int b = wc * FN + fn, t = b >> 2;
+          const uint16_t* xb = Xh + (xb0 + t) * LDX + (b & 3) * 16 + 4 * pp;
+          const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(xb + (4 * grp4 + q) * LDX)));
+          const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lp)(reinterpret_cast<const __bf16*>(xb + (16 + 4 * grp4 + q) * LDX)));
+          const bf8 bv = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int fm = 0; fm < FM; ++fm)
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bv, acc[fm][fn], 0, 0, 0);
+        }
+      }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // slab write: D[k][c] -> ws[split][k][(r * S + tap) * C + cc * 64 + c]
+  const long long kd = (long long)g.R * S * g.C;
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int b = wc * FN + fn, t = b >> 2;
+      const int col = (r * S + t) * g.C + cc * 64 + (b & 3) * 16 + (lane & 15);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int k = wk * (KB / 2) + fm * 16 + (lane >> 4) * 4 + jj;
+        ws[((long long)split * g.K + k) * kd + col] = acc[fm][fn][jj];
+      }
+    }
+}
+
 // Deterministic split-K combine: dw = beta*dw + sum_z ws[z].  Each thread owns
 // four consecutive outputs (16-B loads) and keeps eight slab loads in flight
 // (independent partial sums, fixed combine order), so the pass runs at HBM
@@ -2372,6 +2528,25 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   return launch_rc(amax ? "acfe_conv2d_wgrad_unpool" : "acfe_conv2d_wgrad(halo)");
 }
 
+// k_wgrad_row_halo launch (the (4, 10) head conv: bf16, stride 1, K = 128,
+// C % 64 == 0): split count within the planned workspace, returned in *used.
+static int wgrad_row_halo_launch(const ConvGeom& g, const void* x, const void* dy, float* ws, long long splits,
+                                 hipStream_t s, int* used) {
+  constexpr int SEGW = 32, NSEG = 3;
+  const int nchunk = g.C / 64, ngroups = g.R * nchunk;
+  const int nseg = (int)((long long)g.N * g.P * ((g.Q + SEGW - 1) / SEGW));
+  // one 126-KB workgroup per CU: about one grid-wave of workgroups
+  int sp = (256 / ngroups) & ~7;
+  if (sp < 8) sp = 8;
+  if (sp > splits) sp = (int)splits;  // splits is a multiple of 8 (wgrad_plan)
+  int per = (nseg + sp - 1) / sp;
+  per = (per + NSEG - 1) / NSEG * NSEG;  // whole steps per split
+  hipLaunchKernelGGL((k_wgrad_row_halo<128, 10, SEGW, NSEG>), dim3(ngroups * sp), dim3(512), 0, s, g,
+                     (const uint16_t*)x, (const uint16_t*)dy, ws, ngroups, nchunk, nseg, per);
+  *used = sp;
+  return launch_rc("acfe_conv2d_wgrad(row halo)");
+}
+
 // dW[k][r][s][c] (fp32, KRSC) = sum over pixels.  beta: dW = beta*dW + grad.
 ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy, int K, int R, int S,
                                int stride, int pad_top, int pad_left, int P, int Q, float* dw, float beta,
@@ -2393,6 +2568,12 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
     // halo-staged kernel; its split count stays within the planned workspace
     int used = 0;
     rc = wgrad_halo_launch(g, x, dy, nullptr, workspace, splits, strm(stream), &used);
+    if (rc) return rc;
+    splits = used;
+  } else if (dtype == ACFE_DTYPE_BF16 && S == 10 && stride == 1 && C % 64 == 0 && K == 128 &&
+             (long long)N * P * ((Q + 31) / 32) < (1ll << 31) && !no_halo_w) {
+    int used = 0;
+    rc = wgrad_row_halo_launch(g, x, dy, workspace, splits, strm(stream), &used);
     if (rc) return rc;
     splits = used;
   } else if (dtype == ACFE_DTYPE_BF16) {

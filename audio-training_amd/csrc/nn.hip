@@ -112,14 +112,26 @@ __device__ __forceinline__ void slab_sum(const double* __restrict__ part, int nr
       b[u & 7] += part[((long long)r * 2 + 1) * ld + c];
     }
   }
-  tmp[rg][0][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  tmp[rg][1][cl] = ((b[0] + b[1]) + (b[2] + b[3])) + ((b[4] + b[5]) + (b[6] + b[7]));
+  double ta = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  double tb = ((b[0] + b[1]) + (b[2] + b[3])) + ((b[4] + b[5]) + (b[6] + b[7]));
+  // fixed-order pairwise tree over the 128 row groups in LDS (7 barriers); a
+  // 128-long serial sum of dependent LDS loads was the finalizers' 9-13 us
+  tmp[rg][0][cl] = ta;
+  tmp[rg][1][cl] = tb;
   __syncthreads();
+#pragma unroll
+  for (int h = SLAB_RG / 2; h >= 1; h >>= 1) {
+    if (rg < h) {
+      ta += tmp[rg + h][0][cl];
+      tb += tmp[rg + h][1][cl];
+      tmp[rg][0][cl] = ta;
+      tmp[rg][1][cl] = tb;
+    }
+    __syncthreads();
+  }
   if (threadIdx.x < 2 * SLAB_CH) {
     const int ch = threadIdx.x % SLAB_CH, w = threadIdx.x / SLAB_CH;
-    double x = 0.0;
-    for (int i = 0; i < SLAB_RG; ++i) x += tmp[i][w][ch];
-    s[w][ch] = x;
+    s[w][ch] = tmp[0][w][ch];
   }
   __syncthreads();
 }

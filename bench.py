@@ -267,6 +267,16 @@ def main():
             traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    counters = None
+    sq = ROOT / "profiles" / "sq_dominant_r02.json"
+    if sq.exists():  # SQ counters of the same kernel (tools/pmc_sq.sh, separate rocprofv3 --pmc passes)
+        try:
+            d = json.loads(sq.read_text())
+            counters = {k: d[k] for k in ("mfma_busy_per_simd", "wave_time_waiting", "valu_insts_per_mfma",
+                                          "lds_bank_conflict_share")}
+            counters["source"] = "profiles/sq_dominant_r02.json"
+        except (ValueError, KeyError):
+            counters = None
     clips = world * a.batch * a.steps
     value = clips / elapsed
     out = {
@@ -294,6 +304,7 @@ def main():
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
+            "counters": counters,
             "dgrad_ms": round(dgrad_ms, 4), "wgrad_ms": round(wgrad_ms, 4),
             "dgrad_tflops": round(flops_launch / (dgrad_ms * 1e-3) / 1e12, 2),
             "wgrad_tflops": round(flops_launch / (wgrad_ms * 1e-3) / 1e12, 2),

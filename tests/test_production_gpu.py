@@ -315,3 +315,32 @@ def test_conv_rows_narrow_image_stats(env, cuda):
     assert torch.equal(y1, ref)
     torch.testing.assert_close(st[:rows].sum(0)[:, :K].cpu(), _sums(y1), rtol=1e-6, atol=1e-6)
     assert bool((st[rows:] == 7.0).all())
+
+
+def test_head_conv_wgrad_row_halo(env, cuda):
+    """wr_resnet_bird's head Conv2D (4, 10) 256 -> 128 at 16 x 32 (Keras
+    "same": pad top 1 / bottom 2, left 4 / right 5; wr_resnet_bird.py:47-52):
+    its weight gradient runs on k_wgrad_row_halo (one filter row x 64 channels
+    x all 10 taps per workgroup, split-K + combine) -- at 32 clips, 16 per-row
+    groups x the production split count -- against float64."""
+    ops, call, lib, ptr, stream = env
+    N, H, W, C, K, R, S = 32, 16, 32, 256, 128, 4, 10
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn((N, H, W, C), generator=g) * 0.5).to(BF).to(cuda)
+    dy = (torch.randn((N, H, W, K), generator=g) * 0.5).to(BF).to(cuda)
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, R, S, H, W),), device=cuda)
+    dw = torch.full((K, R, S, C), 7.0, device=cuda)
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, 1, 1, 4, H, W, ptr(dw), 0.0, 1, ptr(ws),
+         stream())
+    torch.cuda.synchronize()
+    xp = F.pad(x.cpu().to(F64).permute(0, 3, 1, 2), (4, 5, 1, 2))
+    gd = dy.cpu().to(F64).permute(0, 3, 1, 2)
+    dw_exact = torch.nn.grad.conv2d_weight(xp, (K, C, R, S), gd).permute(0, 2, 3, 1)
+    d = dw.cpu().to(F64)
+    assert ((d - dw_exact).norm() / dw_exact.norm()).item() < 5e-5
+    assert ((d - dw_exact).abs().max() / dw_exact.abs().max()).item() < 5e-4
+    # beta = 1 accumulates onto the previous gradient
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, R, S, 1, 1, 4, H, W, ptr(dw), 1.0, 1, ptr(ws),
+         stream())
+    torch.cuda.synchronize()
+    assert ((dw.cpu().to(F64) - 2 * dw_exact).norm() / (2 * dw_exact).norm()).item() < 5e-5
