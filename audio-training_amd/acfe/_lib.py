@@ -39,6 +39,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_pcen_bwd": [P, I32, I32, I32, P, F32, P, P, I32, P, P, P],
     "acfe_conv2d_packed_shape": [I32, I32, I32, I32, I32, I32, P, P],
     "acfe_conv2d_pack_weights": [P, I32, I32, I32, I32, I32, I32, P, P],
+    "acfe_conv2d_pack_weights_batch": [P, I32, I64, I32, P],
     "acfe_conv2d_stats_rows": [I64, I32],
     "acfe_conv2d_fwd": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P, P],
     "acfe_conv2d_fwd_dropout": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P, F32,
@@ -67,6 +68,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_wgrad_unpool": [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, F32, I32, P, P],
     "acfe_bn_bwd_apply_pool": [P, I32, P, I32, I32, I32, I32, I32, P, P, I32, P, P, I32, P, I32, P, P],
     "acfe_conv2d_rows_supported": [I32, I32, I32, I32, I32, I32, I32, I32],
+    "acfe_conv2d_fwd_add_supported": [I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_fwd_add": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, I32, P, P, I32, P],
     "acfe_c1bn_supported": [I32, I32],
     "acfe_c1bn_workspace": [I64, I32, I32],

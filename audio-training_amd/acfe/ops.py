@@ -49,13 +49,67 @@ def packed_shape(K, R, S, C, dt, flip):
     return rp.value, cp.value
 
 
+# WeightPacker state: while a packer is active (inside Trainer.step) the packed
+# forms it produced are returned instead of packing again; a list in
+# _PACK_LOG records what a step packs (the packer is built from it)
+_PACK_ACTIVE: dict | None = None
+_PACK_LOG: list | None = None
+
+
 def pack_weights(w: torch.Tensor, dtype: torch.dtype, flip: bool) -> torch.Tensor:
     K, R, S, C = w.shape
     dt = dtype_code(dtype)
+    key = (w.data_ptr(), dt, int(flip))
+    if _PACK_ACTIVE is not None:
+        hit = _PACK_ACTIVE.get(key)
+        if hit is not None:
+            return hit
+    if _PACK_LOG is not None:
+        _PACK_LOG.append((w, dtype, bool(flip)))
     rp, cp = packed_shape(K, R, S, C, dt, int(flip))
     out = _empty((rp, cp), dtype, w.device)
     call("acfe_conv2d_pack_weights", ptr(w), K, R, S, C, dt, int(flip), ptr(out), stream())
     return out
+
+
+class WeightPacker:
+    """Every packed conv weight a training step uses, produced by ONE launch
+    (acfe_conv2d_pack_weights_batch) at the start of the step instead of one
+    acfe_conv2d_pack_weights launch per conv and orientation (52 per
+    wr_resnet_bird step).  Built from the (weight, dtype, flip) list a step
+    records in _PACK_LOG; the weights must keep their storage (arena views)."""
+
+    def __init__(self, entries, device):
+        import numpy as np
+
+        seen, self.entries = set(), []
+        for w, dtype, flip in entries:
+            key = (w.data_ptr(), dtype_code(dtype), int(flip))
+            if key not in seen:
+                seen.add(key)
+                self.entries.append((w, dtype, flip, key))
+        dts = {dtype_code(d) for _, d, _, _ in self.entries}
+        if len(dts) != 1 or not self.entries or len(self.entries) > 256:
+            raise ValueError("WeightPacker: one dtype, 1..256 packings")
+        self.dt = dts.pop()
+        rec = np.zeros(len(self.entries), dtype=np.dtype(
+            {"names": ["w", "out", "begin", "K", "R", "S", "C", "flip", "rows_p", "cols_p", "pad"],
+             "formats": ["<u8", "<u8", "<i8"] + ["<i4"] * 8, "offsets": [0, 8, 16, 24, 28, 32, 36, 40, 44, 48, 52],
+             "itemsize": 56}))
+        self.out, total = {}, 0
+        for i, (w, dtype, flip, key) in enumerate(self.entries):
+            K, R, S, C = w.shape
+            rp, cp = packed_shape(K, R, S, C, self.dt, int(flip))
+            o = _empty((rp, cp), dtype, device)
+            self.out[key] = o
+            rec[i] = (w.data_ptr(), o.data_ptr(), total, K, R, S, C, int(flip), rp, cp, 0)
+            total += rp * cp
+        self.total = total
+        self.table = torch.from_numpy(rec.view(np.uint8).copy()).to(device)
+
+    def pack(self):
+        call("acfe_conv2d_pack_weights_batch", ptr(self.table), len(self.entries), self.total, self.dt, stream())
+        return self.out
 
 
 def _no_stats(dev):
@@ -638,7 +692,8 @@ def _conv_add_ok(x, w, sc, stride, padding) -> bool:
     K, R, S, _ = w.shape
     return (FUSE and x.dtype == torch.bfloat16 and stride == 1 and padding == "same" and x.is_contiguous()
             and x.data_ptr() % 16 == 0 and sc.dtype == x.dtype and tuple(sc.shape) == (N, H, W, K)
-            and bool(lib.acfe_conv2d_rows_supported(N, H, W, C, K, R, S, dtype_code(x.dtype))))
+            and sc.is_contiguous() and sc.data_ptr() % 16 == 0
+            and (R, S) == (3, 3) and bool(lib.acfe_conv2d_fwd_add_supported(N, H, W, C, K, dtype_code(x.dtype))))
 
 
 class _ConvAddFn(torch.autograd.Function):

@@ -95,7 +95,7 @@ class Trainer:
     Keras-Adam; `step` runs one full training iteration on device tensors."""
 
     def __init__(self, model: nn.Module, frontend: FrontEnd, lr=0.01, loss="cce", process_group=None,
-                 device=None, bucket_bytes=dp.BUCKET_BYTES):
+                 device=None, bucket_bytes=dp.BUCKET_BYTES, pack_once=True):
         self.model, self.frontend, self.loss_mode = model, frontend, loss
         self.device = device or next(model.parameters()).device
         self.holder = nn.ModuleList([frontend, model])
@@ -103,6 +103,8 @@ class Trainer:
         self.opt = Adam(self.arena, lr=lr)
         self.pg = process_group
         self.world = dp.world_size(process_group)
+        self.packer = None  # ops.WeightPacker, built from the first step's packings
+        self.pack_once = pack_once
         self.buckets = None
         if self.world > 1:
             self.buckets = dp.GradBuckets(self.arena.grad, self.arena.params, self.arena.offsets, bucket_bytes,
@@ -125,21 +127,38 @@ class Trainer:
         """One training iteration.  x1 [B, N] raw clips (x2 / lam: mix_up
         partner and weights), or [B, F, T] stored magnitude spectrograms (the
         load_raw=False path, no mix_up: tfdataset.py:503-504)."""
-        feats = self.frontend.forward_spec(x1) if x1.dim() == 3 else self.frontend(x1, x2, lam)
-        z = self.model(feats)
-        loss, dz = ops.loss_and_grad(z, y, self.loss_mode)
-        self.arena.zero_grad()
-        if self.buckets is None:
-            z.backward(dz)
-            scale = 1.0
-        else:
-            self.buckets.begin()
-            ops.set_grad_ready(self.buckets.ready)
-            try:
+        # the conv weights change only in the Adam step: all their packed forms
+        # for this step come from one launch (the first step records them)
+        if self.packer is not None:
+            ops._PACK_ACTIVE = self.packer.pack()
+        elif self.pack_once:
+            ops._PACK_LOG = []
+        try:
+            feats = self.frontend.forward_spec(x1) if x1.dim() == 3 else self.frontend(x1, x2, lam)
+            z = self.model(feats)
+            loss, dz = ops.loss_and_grad(z, y, self.loss_mode)
+            self.arena.zero_grad()
+            if self.buckets is None:
                 z.backward(dz)
-            finally:
-                ops.set_grad_ready(None)
-            scale = self.buckets.finish()
+                scale = 1.0
+            else:
+                self.buckets.begin()
+                ops.set_grad_ready(self.buckets.ready)
+                try:
+                    z.backward(dz)
+                finally:
+                    ops.set_grad_ready(None)
+                scale = self.buckets.finish()
+        finally:
+            ops._PACK_ACTIVE = None
+            log, ops._PACK_LOG = ops._PACK_LOG, None
+        if self.packer is None and log and self.pack_once:
+            # arena weights only (their storage is fixed); derived weights keep
+            # the per-call packing
+            arena_ptrs = {p.data_ptr() for p in self.arena.params}
+            log = [e for e in log if e[0].data_ptr() in arena_ptrs]
+            if log and len({d for _, d, _ in log}) == 1:
+                self.packer = ops.WeightPacker(log, self.device)
         self.opt.step(grad_scale=scale)
         return loss, z
 

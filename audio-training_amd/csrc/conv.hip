@@ -354,7 +354,7 @@ constexpr int conv_g_smem() {
   return a > b ? a : b;
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, int WM, int WN, bool RES = false>
 __global__ void __launch_bounds__(256, 2)
 k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, const float* __restrict__ bias,
              T* __restrict__ Y, double* __restrict__ stats, int tiles_m) {
@@ -469,6 +469,11 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
 #undef CONV_G_COMPUTE
 #undef CONV_G_ISSUE
     // ---- epilogue: +bias, round, BN statistics of the rounded values, LDS-staged 16-B row stores
+    // (g.res: the residual Add (+ReLU) of ops.conv_add is applied in the row
+    // stores and the statistics are those of z = (ReLU)(y + res))
+    constexpr bool res = RES && sizeof(T) == 2;
+    constexpr int GPR = BN / GR, NR = BM * GPR / 256;
+    u32x4 rvs[NR];
     T* Cs = reinterpret_cast<T*>(smem);
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
@@ -491,7 +496,7 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
             t2 += f * f;
           }
         }
-      if (stats) {
+      if (stats && !res) {
         t1 += __shfl_xor(t1, 16, 64);
         t1 += __shfl_xor(t1, 32, 64);
         t2 += __shfl_xor(t2, 16, 64);
@@ -502,8 +507,68 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
         }
       }
     }
+    if constexpr (res) {
+      // the residual rows of this thread's stores are requested before the
+      // barrier, all at once (rows past M read the zero page)
+#pragma unroll
+      for (int u = 0; u < NR; ++u) {
+        const long long m = m0 + (tid + 256 * u) / GPR;
+        rvs[u] = *reinterpret_cast<const u32x4*>(m < g.M ? reinterpret_cast<const uint16_t*>(g.res) + m * g.ldy +
+                                                               n0 + (tid % GPR) * GR
+                                                         : reinterpret_cast<const uint16_t*>(g_zero_page));
+      }
+    }
     __syncthreads();
-    constexpr int GPR = BN / GR;
+    if constexpr (res && 256 % GPR == 0) {
+      {
+        // z = bf16((ReLU)(y + r)) for 8 channels per thread; the thread's
+        // channel group cg is fixed (256 % GPR == 0), so its statistics stay in
+        // registers over its rows and are combined across the lanes holding the
+        // same cg, then one LDS f64 atomic per value (the caller guarantees
+        // n0 + BN <= K and 16-B rows)
+        float z1[GR], z2[GR];
+#pragma unroll
+        for (int j = 0; j < GR; ++j) z1[j] = z2[j] = 0.f;
+        const int cg = tid % GPR;
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+          const int row = (tid + 256 * u) / GPR;
+          const long long m = m0 + row;
+          if (m < g.M) {
+            const u32x4 yv = *reinterpret_cast<const u32x4*>(Cs + row * LC + cg * GR);
+            const u32x4 rv = rvs[u];
+            u32x4 zv;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float a = __uint_as_float(yv[q] << 16) + __uint_as_float(rv[q] << 16);
+              float c = __uint_as_float(yv[q] & 0xffff0000u) + __uint_as_float(rv[q] & 0xffff0000u);
+              if (g.res_relu) a = fmaxf(a, 0.f), c = fmaxf(c, 0.f);
+              const unsigned ba = f2bf(a), bc = f2bf(c);
+              zv[q] = ba | (bc << 16);
+              const float fa = __uint_as_float(ba << 16), fc = __uint_as_float(bc << 16);
+              z1[2 * q] += fa, z2[2 * q] += fa * fa;
+              z1[2 * q + 1] += fc, z2[2 * q + 1] += fc * fc;
+            }
+            *reinterpret_cast<u32x4*>(Y + m * g.ldy + n0 + cg * GR) = zv;
+          }
+        }
+        if (stats) {
+#pragma unroll
+          for (int off = GPR; off < 64; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < GR; ++j) z1[j] += __shfl_xor(z1[j], off, 64), z2[j] += __shfl_xor(z2[j], off, 64);
+          if (lane < GPR) {
+#pragma unroll
+            for (int j = 0; j < GR; ++j) {
+              atomicAdd(&sstat[0][cg * GR + j], (double)z1[j]);
+              atomicAdd(&sstat[1][cg * GR + j], (double)z2[j]);
+            }
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+    }
     if (n0 + BN <= g.K && (g.ldy % GR) == 0) {
       for (int idx = tid; idx < BM * GPR; idx += 256) {
         const int row = idx / GPR, cg = idx - (idx / GPR) * GPR;
@@ -1519,6 +1584,46 @@ __global__ void k_pack_w(const float* __restrict__ w, int K, int R, int S, int C
   }
 }
 
+// All conv weights of a training step in one launch (acfe_conv2d_pack_weights_batch):
+// the descriptor table lists each (weight, orientation) with its packed
+// geometry and its first element in the concatenated index space; a thread
+// finds its descriptor by binary search over the table's start offsets (in LDS).
+struct PackDesc {
+  const float* w;
+  void* out;
+  long long begin;
+  int K, R, S, C, flip, rows_p, cols_p, pad;
+};
+static_assert(sizeof(PackDesc) == 56, "PackDesc layout (acfe/ops.py WeightPacker)");
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_pack_w_batch(const PackDesc* __restrict__ d, int n, long long total) {
+  __shared__ long long beg[257];
+  for (int i = threadIdx.x; i <= n; i += 256) beg[i] = i < n ? d[i].begin : total;
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (beg[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const PackDesc& p = d[lo];
+    const long long e = i - beg[lo];
+    const int row = (int)(e / p.cols_p), col = (int)(e - (e / p.cols_p) * p.cols_p);
+    float v = 0.f;
+    if (!p.flip) {
+      if (row < p.K && col < p.R * p.S * p.C) v = p.w[(long long)row * p.R * p.S * p.C + col];
+    } else {
+      if (row < p.C && col < p.R * p.S * p.K) {
+        const int k = col % p.K, rs = col / p.K, r = rs / p.S, s = rs % p.S;
+        v = p.w[(((long long)k * p.R + (p.R - 1 - r)) * p.S + (p.S - 1 - s)) * p.C + row];
+      }
+    }
+    reinterpret_cast<T*>(p.out)[e] = cvt_out(v, T());
+  }
+}
+
 // ------------------------------------------------------------------ zero insertion (strided dgrad)
 template <typename T>
 __global__ void k_zero_insert(const T* __restrict__ dy, int N, int P, int Q, int K, int st, int Hu, int Wu,
@@ -2370,6 +2475,19 @@ ACFE_API int acfe_conv2d_pack_weights(const float* w, int K, int R, int S, int C
   return launch_rc("acfe_conv2d_pack_weights");
 }
 
+ACFE_API int acfe_conv2d_pack_weights_batch(const void* descs, int n, long long total, int dtype, void* stream) {
+  if (!descs || n <= 0 || n > 256 || total <= 0 || (dtype != 0 && dtype != 1)) return ACFE_E_INVAL;
+  long long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (dtype == ACFE_DTYPE_BF16)
+    hipLaunchKernelGGL(k_pack_w_batch<uint16_t>, dim3((unsigned)g), dim3(256), 0, strm(stream),
+                       (const PackDesc*)descs, n, total);
+  else
+    hipLaunchKernelGGL(k_pack_w_batch<float>, dim3((unsigned)g), dim3(256), 0, strm(stream), (const PackDesc*)descs,
+                       n, total);
+  return launch_rc("acfe_conv2d_pack_weights_batch");
+}
+
 ACFE_API int acfe_conv2d_stats_rows(long long M, int K) {
   return grid_m_for(M, (K + pick_bn(K) - 1) / pick_bn(K));
 }
@@ -2688,12 +2806,35 @@ ACFE_API int acfe_conv2d_rows_supported(int N, int H, int W, int C, int K, int R
          (K == 64 || K == 128) && W > 0 && H > 0 && (long long)N * ((H + 5) / 6) * ((W + 63) / 64) < (1ll << 31);
 }
 
+// Shapes the generic (C % 8 == 0) kernel takes with the Add in its row stores:
+// wr_resnet_bird's stage-2/3 conv2b (32 -> 128, 16 / 32 -> 256 channels).
+static bool fwd_add_generic_ok(int N, int H, int W, int C, int K, int dtype) {
+  return dtype == ACFE_DTYPE_BF16 && N > 0 && H > 0 && W > 0 && C % 8 == 0 && C % 64 != 0 && K % 128 == 0 &&
+         pick_bn(K) == 128 && (long long)N * H * W < (1ll << 31);
+}
+
+ACFE_API int acfe_conv2d_fwd_add_supported(int N, int H, int W, int C, int K, int dtype) {
+  return acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, dtype) || fwd_add_generic_ok(N, H, W, C, K, dtype);
+}
+
 ACFE_API int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
                                  int pad_left, const float* bias, const void* res, int relu, void* y,
                                  double* stats_partial, int dtype, void* stream) {
-  if (!x || !wpacked || !y || !res || !acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, dtype) ||
+  if (!x || !wpacked || !y || !res || !acfe_conv2d_fwd_add_supported(N, H, W, C, K, dtype) ||
       ((uintptr_t)y & 7) || ((uintptr_t)res & 7))
     return ACFE_E_INVAL;
+  if (!acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, dtype)) {
+    // generic kernel: 16-B residual / output rows
+    if (((uintptr_t)y & 15) || ((uintptr_t)res & 15)) return ACFE_E_INVAL;
+    ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, 128);
+    g.res = (const uint16_t*)res;
+    g.res_relu = relu ? 1 : 0;
+    const int ny = g.Kp / 128, gm = grid_m_for(g.M, ny);
+    const int tiles_m = (int)((g.M + 127) / 128);
+    hipLaunchKernelGGL((k_conv_fwd_g<uint16_t, 128, 128, 2, 2, true>), dim3(gm, ny), dim3(256), 0, strm(stream), g,
+                       (const uint16_t*)x, (const uint16_t*)wpacked, bias, (uint16_t*)y, stats_partial, tiles_m);
+    return launch_rc("acfe_conv2d_fwd_add(generic)");
+  }
   ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
   g.res = (const uint16_t*)res;
   g.res_relu = relu ? 1 : 0;

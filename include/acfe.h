@@ -153,6 +153,12 @@ int acfe_pcen_bwd(const float* mel_btm, int batch, int t, int m, const float* pa
 int acfe_conv2d_packed_shape(int K, int R, int S, int C, int dtype, int flip, int* rows_p, int* cols_p);
 int acfe_conv2d_pack_weights(const float* w_krsc, int K, int R, int S, int C, int dtype, int flip,
                              void* out, void* stream);
+/* All of a step's packings in one launch: descs = device array of n (<= 256)
+ * records {const float* w; void* out; int64 begin; int K, R, S, C, flip,
+ * rows_p, cols_p, pad} (56 B, the arguments of acfe_conv2d_pack_weights with
+ * the record's first element in the concatenated index space [0, total),
+ * begin ascending); dtype as acfe_conv2d_pack_weights, one for all records. */
+int acfe_conv2d_pack_weights_batch(const void* descs, int n, long long total, int dtype, void* stream);
 /* Rows of the per-channel statistics slab written by acfe_conv2d_fwd
  * (stats_partial: double[rows][2][rows_p of the forward packing]). */
 int acfe_conv2d_stats_rows(long long M, int K);
@@ -265,8 +271,12 @@ int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C, const vo
 /* Conv2D 3x3 "same" stride 1 followed by the residual Add (+ReLU) of the block
  * (res{s}{b}_branch2b + Add, resnet/wr_resnet_bird.py:173-178): y = (ReLU)(conv(x)
  * + res), res/y [N][H][W][K] bf16, BN statistics of y into stats_partial (rows =
- * acfe_conv2d_stats_rows(N*H*W, K), nullable).  Shapes: acfe_conv2d_rows_supported. */
+ * acfe_conv2d_stats_rows(N*H*W, K), nullable).  Shapes: acfe_conv2d_fwd_add_supported
+ * (the rows kernel's, plus C % 8 == 0 / K % 128 == 0 bf16 layers -- the stage-2/3
+ * conv2b -- on the generic kernel with the Add in its row stores; 16-B aligned
+ * res / y there). */
 int acfe_conv2d_rows_supported(int N, int H, int W, int C, int K, int R, int S, int dtype);
+int acfe_conv2d_fwd_add_supported(int N, int H, int W, int C, int K, int dtype);
 int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
                         int pad_left, const float* bias, const void* res, int relu, void* y, double* stats_partial,
                         int dtype, void* stream);

@@ -423,11 +423,13 @@ def test_pool_link(env, cuda):
 
 
 @pytest.mark.parametrize("relu", [False, True])
-@pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128)])
+@pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128), (32, 128), (16, 256), (32, 256)])
 def test_conv_add_node(env, cuda, relu, C, K):
     """(ReLU)(conv 3x3 + shortcut) with the Add in the conv epilogue
-    (acfe_conv2d_fwd_add) == conv2d -> add: z bit-exact, statistics to 1e-6,
-    gradients of x, w, b and the shortcut identical up to summation order."""
+    (acfe_conv2d_fwd_add: the rows kernel, or for the stage-2/3 conv2b shapes
+    C = 16 / 32, K = 128 / 256 the generic kernel with the Add in its row
+    stores) == conv2d -> add: z bit-exact, statistics to 1e-6, gradients of x,
+    w, b and the shortcut identical up to summation order."""
     ops = env[0]
     N, H, W = 2, 14, 128
     g = torch.Generator(device="cpu").manual_seed(41)

@@ -212,3 +212,37 @@ def test_arena_gradients_match_autograd(cuda, kind, training):
     for n, a, b in zip(names, grads[1], again):
         if not training:  # training-mode BN statistics move between the two forwards
             torch.testing.assert_close(b, 2 * a, rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.parametrize("kind", ["bird", "wrn"])
+def test_weight_packer_matches_per_call_packing(cuda, kind):
+    """Trainer packs every conv weight of a step with ONE launch
+    (acfe_conv2d_pack_weights_batch) from the second step on: each packed form
+    is bit-identical to acfe_conv2d_pack_weights of the same weight, the
+    packer covers both orientations of every arena conv weight the step used,
+    and a step with the packer gives the same loss as a step without."""
+    from acfe import ops
+    from acfe.train import FrontEnd, Trainer
+
+    H, W, classes, N = 128, 513, 10, 2
+    m = _build(kind, (H, W, 3), classes, torch.bfloat16, cuda)
+    fe = FrontEnd(n_mels=H, dtype=torch.bfloat16, device=cuda, pcen=False).to(cuda)
+    tr = Trainer(m, fe, lr=0.0, loss="cce", device=cuda)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((N, 144000), generator=g).clamp(-1, 1).to(cuda)
+    y = torch.zeros(N, classes, device=cuda)
+    y[0, 1] = y[1, 2] = 1
+    l1, _ = tr.step(x, y)
+    assert tr.packer is not None
+    flips = {(e[0].data_ptr(), e[2]) for e in tr.packer.entries}
+    convs = [p for n, p in m.named_parameters() if p.dim() == 4 and n.endswith("weight")]
+    assert len(tr.packer.entries) >= len(convs)
+    outs = tr.packer.pack()
+    for w, dtype, flip, key in tr.packer.entries:
+        ops._PACK_ACTIVE = None
+        ref = ops.pack_weights(w, dtype, flip)
+        assert torch.equal(outs[key], ref), (tuple(w.shape), flip)
+    l2, _ = tr.step(x, y)  # lr 0: same weights, packed by the batch kernel now
+    torch.cuda.synchronize()
+    assert abs(float(l2) - float(l1)) <= 1e-5 * max(1.0, abs(float(l1)))
+    assert len(flips) == len(tr.packer.entries)
