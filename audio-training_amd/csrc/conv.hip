@@ -1417,6 +1417,212 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   }
 }
 
+// ------------------------------------------------------------------ 3x3 stride 1, narrow output (K in {16, 32})
+// wr_resnet_bird's stage-2/3 branch21 convolutions whose output channel count
+// is the feature height (resnet/wr_resnet_bird.py:139: 128 -> 32 at 32 x 64,
+// 256 -> 16 at 16 x 32) and the dgrads of the branch2b convolutions (32 / 16
+// output channels).  With K <= 32 an im2col GEMM tile does 4-8 MFMAs per
+// K-tile and wave (k_conv_fwd_g: 125-310 TFLOP/s).  Here the whole packed
+// weight matrix (9 taps x C x K <= 72 KB) stays in LDS for the workgroup's
+// lifetime, and one pipeline step stages a 64-channel chunk of the input halo
+// (TR + 2 rows x SEGW + 2 pixels, TR x SEGW = 128 output pixels) ONCE for all
+// nine taps: 4 waves x 32 pixels x K, 36 x K / 16 MFMAs per wave per step.
+// Fragment reads as k_conv3x3_rows (160-B pixel pitch, XOR-swizzled 128-B
+// weight rows), register-staged double buffer, one barrier per step; epilogue:
+// bias, bf16 rounding, the pair-hash Dropout (PM 4's), BN sums through
+// 16-lane shuffles and LDS f64 atomics.  Persistent, XCD-aware tile walk.
+template <int KB, int SEGW, bool DROP>
+__global__ void __launch_bounds__(256, 1)
+k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+                 const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
+                 int tiles_w, int ntiles, int srows) {
+  constexpr int TR = 128 / SEGW, HWX = SEGW + 2, XR = TR + 2, XRB = 160;
+  constexpr int FM = 2, FN = KB / 16;
+  constexpr int XBYTES = XR * HWX * XRB, WBYTES = 576 * 128;
+  constexpr int XG = XR * HWX * 8, XPT = (XG + 255) / 256;
+  constexpr int SMEM = 2 * XBYTES + WBYTES + 2 * KB * 8;
+  static_assert(SMEM <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  unsigned char* Wl = smem + 2 * XBYTES;
+  double* sstat = reinterpret_cast<double*>(smem + 2 * XBYTES + WBYTES);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nch = g.C / 64, tpi = tiles_h * tiles_w;
+  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
+  for (int i = tid; i < 2 * KB; i += 256) sstat[i] = 0.0;
+  // resident weights: row (t * nch + cc) * KB + k = W[k][tap t][chunk cc], granule gw at slot gw ^ (k & 7)
+  {
+    const int wrows = 9 * nch * KB;
+    for (int gi = tid; gi < wrows * 8; gi += 256) {
+      const int row = gi >> 3, gw = gi & 7;
+      const int k = row % KB, tc = row / KB, cc = tc % nch, t = tc / nch;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + t * g.C + cc * 64 + gw * 8);
+      *reinterpret_cast<u32x4*>(Wl + row * 128 + ((gw ^ (k & 7)) << 4)) = v;
+    }
+  }
+  const TileWalk walk(ntiles);
+  const int ntl = walk.tm < walk.end ? (walk.end - walk.tm + walk.step - 1) / walk.step : 0;
+  const int L = ntl * nch;
+  // two register sets: step t + 2 is requested while step t computes, so a
+  // load has two steps of MFMA work to land (one wave per SIMD hides nothing)
+  u32x4 ra[XPT], rb[XPT];
+  auto gload = [&](u32x4 (&rx)[XPT], int t) __attribute__((always_inline)) {
+    const int tl = t / nch, cc = t - tl * nch;
+    const int tm = walk.tm + tl * walk.step;
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    const int h0 = hb * TR - g.pt, w0 = wb * SEGW - g.pl;
+    const uint16_t* img = X + (long long)n * g.H * g.W * g.C + cc * 64;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 256 * i;
+      const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3, gr = idx & 7;
+      const int hin = h0 + xrow, win = w0 + xpix;
+      const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
+      rx[i] = *reinterpret_cast<const u32x4*>(ok ? img + ((long long)hin * g.W + win) * g.C + gr * 8 : zp);
+    }
+  };
+  auto sstore = [&](const u32x4 (&rx)[XPT], int buf) __attribute__((always_inline)) {
+    unsigned char* Xl = smem + buf * XBYTES;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 256 * i;
+      if (idx < XG) *reinterpret_cast<u32x4*>(Xl + (idx >> 3) * XRB + (idx & 7) * 16) = rx[i];
+    }
+  };
+  f4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // this wave's two 16-pixel fragments: tile pixel wid * 32 + fm * 16 + l16 = (row, col)
+  // this lane's bias quads, loaded once
+  f4 bq[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn)
+    bq[fn] = bias ? *reinterpret_cast<const f4*>(bias + fn * 16 + (lane >> 4) * 4) : f4{0.f, 0.f, 0.f, 0.f};
+  int xoff[FM];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int p = wid * 32 + fm * 16;
+    xoff[fm] = ((p / SEGW) * HWX + (p % SEGW) + l16) * XRB + (lane >> 4) * 16;
+  }
+  auto epilogue = [&](int tm) __attribute__((always_inline)) {
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    float s1[FN][4], s2[FN][4];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s1[fn][j] = s2[fn][j] = 0.f;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int p = wid * 32 + fm * 16 + l16;
+      const int h = hb * TR + p / SEGW, w = wb * SEGW + p % SEGW;
+      const bool inb = h < g.P && w < g.Q;
+      const unsigned pix = ((unsigned)n * g.P + h) * g.Q + w;  // < 2^32: launch checks M * K < 2^32
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int c = fn * 16 + (lane >> 4) * 4;
+        float r[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = bf2f(f2bf(acc[fm][fn][j] + bq[fn][j]));
+        if constexpr (DROP) {
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const uint32_t hh = drop_pair_hash32(g.drop, pix * (unsigned)g.K + c + 2 * pr);
+            r[2 * pr] = (hh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(r[2 * pr] * g.drop.scl)) : 0.f;
+            r[2 * pr + 1] = (hh >> 16) >= g.drop.thr ? bf2f(f2bf(r[2 * pr + 1] * g.drop.scl)) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float f = inb ? r[j] : 0.f;
+          s1[fn][j] += f;
+          s2[fn][j] += f * f;
+        }
+        uint2 v;
+        v.x = (__float_as_uint(r[0]) >> 16) | (__float_as_uint(r[1]) & 0xffff0000u);
+        v.y = (__float_as_uint(r[2]) >> 16) | (__float_as_uint(r[3]) & 0xffff0000u);
+        uint2* dst = inb ? reinterpret_cast<uint2*>(Y + (size_t)pix * g.ldy + c) : &g_store_sink[lane];
+        *dst = v;
+        acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if (stats) {
+      // sum over the 16 pixels (lanes l16) of each channel, then one LDS atomic per value
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) {
+            s1[fn][j] += __shfl_xor(s1[fn][j], off, 64);
+            s2[fn][j] += __shfl_xor(s2[fn][j], off, 64);
+          }
+          if (l16 == 0) {
+            const int c = fn * 16 + (lane >> 4) * 4 + j;
+            atomicAdd(&sstat[c], (double)s1[fn][j]);
+            atomicAdd(&sstat[KB + c], (double)s2[fn][j]);
+          }
+        }
+    }
+  };
+
+  if (L > 0) {
+    gload(ra, 0);
+    sstore(ra, 0);
+  }
+  if (L > 1) gload(rb, 1);
+  __syncthreads();
+  int cst = 0, ctm = walk.tm;
+  // at entry of step t: LDS buffer t & 1 holds step t, rnext holds (in flight) step t + 1
+  auto step = [&](int t, const u32x4 (&rnext)[XPT], u32x4 (&rfree)[XPT]) __attribute__((always_inline)) {
+    if (t + 2 < L) gload(rfree, t + 2);
+    const int cc = t % nch;
+    const unsigned char* Xl = smem + (t & 1) * XBYTES;
+    __builtin_amdgcn_iglp_opt(0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int r = tap / 3, s = tap - 3 * (tap / 3);
+        uint4 wf[FN], xf[FM];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int k = fn * 16 + l16;
+          const int row = (tap * nch + cc) * KB + k;
+          wf[fn] = *reinterpret_cast<const uint4*>(Wl + row * 128 + (((kk * 4 + (lane >> 4)) ^ (k & 7)) << 4));
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          xf[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + (r * HWX + s) * XRB + kk * 64);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], wf[fn], xf[fm], uint16_t());
+      }
+    if (t + 1 < L) sstore(rnext, (t + 1) & 1);
+    if (++cst == nch) {
+      cst = 0;
+      epilogue(ctm);
+      ctm += walk.step;
+    }
+    __syncthreads();
+  };
+  for (int t = 0; t < L; t += 2) {
+    step(t, rb, ra);
+    if (t + 1 < L) step(t + 1, ra, rb);
+  }
+  if (stats) {
+    __syncthreads();
+    for (int c = tid; c < g.Kp; c += 256) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = c < KB ? sstat[c] : 0.0;
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = c < KB ? sstat[KB + c] : 0.0;
+    }
+    for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
+      for (int c = tid; c < 2 * g.Kp; c += 256) stats[((long long)rr * 2 + (c / g.Kp)) * g.Kp + (c % g.Kp)] = 0.0;
+  }
+}
+
 // ------------------------------------------------------------------ 1x1 conv, register-resident weights
 // 1x1 stride-1 convolutions with few input or few output channels (C or K <= 32:
 // the 16->128 stage-1 entry conv, the 16->64 shortcut, and their dgrads
@@ -1953,20 +2159,28 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 // distinct banks; register-staged double buffer, one barrier per step.
 // UNP: dY is the 2x2 max-pool backward of the pooled gradient dY (argmax bytes
 // amax), expanded while staging.
-template <int KB, bool UNP>
+template <int KB, bool UNP, int CW = 64>
 __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
                 float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
   constexpr int SEGW = 64, HW = SEGW + 2;
-  constexpr int LDD = KB + 16, LDX = 64 + 16;
+  // CW-channel chunks (C = 16 / 32 layers: the stage-2/3 branch2b): the 8 waves
+  // are WC = CW / 16 channel blocks x WK = 8 / WC slices of K; a wave's nine
+  // blocks are the nine taps of its channel block (CW = 64: 2 K halves x 4
+  // groups of 9 (tap, block) pairs)
+  static_assert(CW == 64 || (CW == 32 && !UNP) || (CW == 16 && !UNP), "chunk");
+  constexpr int WC = CW == 64 ? 4 : CW / 16, WK = 8 / WC;
+  constexpr int LDD = KB + 16, LDX = CW + 16;
   constexpr int DS = SEGW * LDD, XS = 3 * HW * LDX;
-  constexpr int FM = KB / 32, FN = 9;
-  constexpr int DGR = KB / 8, DG = SEGW * DGR, XG = 3 * HW * 8;
+  constexpr int FM = KB / (16 * WK), FN = 9;
+  static_assert(FM >= 1, "K slice");
+  constexpr int XGR = CW / 8;
+  constexpr int DGR = KB / 8, DG = SEGW * DGR, XG = 3 * HW * XGR;
   constexpr int DPT = (DG + 511) / 512, XPT = (XG + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (DS + XS)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = wid >> 2, wc = wid & 3;
+  const int wk = wid / WC, wc = wid - (wid / WC) * WC;
   const int xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
   const int cc = bi % nchunk, split = (bi / nchunk) * 8 + xcd;
   const int sbeg = split * segs_per_split;
@@ -2000,11 +2214,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + 512 * i;
-      const int hr = idx / (HW * 8), r2 = idx - hr * (HW * 8), hp = r2 >> 3, cg = r2 & 7;
+      const int hr = idx / (HW * XGR), r2 = idx - hr * (HW * XGR), hp = r2 / XGR, cg = r2 - hp * XGR;
       const int hin = h - g.pt + hr, win = w0 - g.pl + hp;
       const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
       rx[i] = *reinterpret_cast<const u32x4*>(
-          ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * 64 + cg * 8 : zp);
+          ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * CW + cg * 8 : zp);
     }
   };
   auto sstore = [&](int buf) __attribute__((always_inline)) {
@@ -2024,7 +2238,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + 512 * i;
-      const int row = idx >> 3, cg = idx & 7;  // row = hr * HW + hp
+      const int row = idx / XGR, cg = idx - row * XGR;  // row = hr * HW + hp
       if (idx < XG) *reinterpret_cast<u32x4*>(Xh + row * LDX + cg * 8) = rx[i];
     }
   };
@@ -2038,8 +2252,8 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   int boff[FN];
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
-    const int b = wc * 9 + fn, t = b >> 2;
-    boff[fn] = ((t / 3) * HW + (t % 3)) * LDX + (b & 3) * 16;
+    const int b = wc * 9 + fn, t = CW == 64 ? b >> 2 : fn, cb = CW == 64 ? b & 3 : wc;
+    boff[fn] = ((t / 3) * HW + (t % 3)) * LDX + cb * 16;
   }
   const int grp = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   typedef __attribute__((address_space(3))) bf4* lp;
@@ -2061,7 +2275,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       bf8 af[FM];
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
-        const int col = wk * (KB / 2) + fm * 16 + 4 * pp;
+        const int col = wk * (KB / WK) + fm * 16 + 4 * pp;
         const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
             (lp)(reinterpret_cast<const __bf16*>(Ds + (rb + 4 * grp + q) * LDD + col)));
         const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
@@ -2091,11 +2305,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      const int b = wc * 9 + fn, t = b >> 2;
-      const int col = t * g.C + cc * 64 + (b & 3) * 16 + (lane & 15);
+      const int b = wc * 9 + fn, t = CW == 64 ? b >> 2 : fn, cb = CW == 64 ? b & 3 : wc;
+      const int col = t * g.C + cc * CW + cb * 16 + (lane & 15);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int k = wk * (KB / 2) + fm * 16 + (lane >> 4) * 4 + jj;
+        const int k = wk * (KB / WK) + fm * 16 + (lane >> 4) * 4 + jj;
         ws[((long long)split * g.K + k) * kd + col] = acc[fm][fn][jj];
       }
     }
@@ -2429,6 +2643,30 @@ static int launch_fwd(const ConvGeom& g, const void* x, const void* wp, const fl
 #undef L1
   }
 general:
+  if constexpr (sizeof(T) == 2) {
+    static const bool no_narrow = getenv_flag("ACFE_CONV_NO_NARROW");
+    if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W &&
+        g.C % 64 == 0 && (g.K == 32 || g.K == 16) && g.C * g.K <= 4096 && g.ldy == g.K &&
+        g.M * g.K < (1ll << 32) && !no_narrow) {
+      const int segw = g.Q <= 32 ? 32 : 64, tr = 128 / segw;
+      const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + segw - 1) / segw;
+      const long long nt = (long long)g.N * tiles_h * tiles_w;
+      if (nt < (1ll << 31)) {
+        int gp = 256;
+        if (gp > nt) gp = (int)nt;
+        if (gp >= 64) gp &= ~7;
+        if (stats && gp > grid_m) gp = grid_m;  // one statistics slab row per workgroup
+#define NARROW(KB_, SW_)                                                                                           do {                                                                                                               if (g.drop.on)                                                                                                     hipLaunchKernelGGL((k_conv3x3_narrow<KB_, SW_, true>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,                            (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);         else                                                                                                               hipLaunchKernelGGL((k_conv3x3_narrow<KB_, SW_, false>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,                           (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);       } while (0)
+        if (g.K == 32) {
+          if (segw == 64) NARROW(32, 64); else NARROW(32, 32);
+        } else {
+          if (segw == 64) NARROW(16, 64); else NARROW(16, 32);
+        }
+#undef NARROW
+        return launch_rc("acfe_conv2d_fwd(narrow)");
+      }
+    }
+  }
   const int bn = pick_bn(g.K);
   if (bn == 32) return launch_fwd_t<T, 32, 4, 1>(g, x, wp, bias, y, stats, grid_m, s);
   if (bn == 64) return launch_fwd_t<T, 64, 2, 2>(g, x, wp, bias, y, stats, grid_m, s);
@@ -2625,7 +2863,8 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
 // 0): split count within the planned workspace (`splits`), returned in *used.
 static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
                              long long splits, hipStream_t s, int* used) {
-  const int nchunk = g.C / 64, nseg = (int)((long long)g.N * g.P * ((g.Q + 63) / 64));
+  const int cw = g.C % 64 == 0 ? 64 : g.C;  // 16 / 32-channel layers: one chunk of C
+  const int nchunk = g.C / cw, nseg = (int)((long long)g.N * g.P * ((g.Q + 63) / 64));
   int sp = 256 / nchunk;
   if (sp > splits) sp = (int)splits;
   sp &= ~7;
@@ -2636,11 +2875,21 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
 #define WH(KB_, U_)                                                                                              \
   hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, U_>), gr, dim3(512), 0, s, g, (const uint16_t*)x, (const uint16_t*)dy, \
                      ws, nchunk, nseg, per, amax)
-  if (g.K == 128) {
+#define WHC(KB_, CW_)                                                                                              \
+  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_>), gr, dim3(512), 0, s, g, (const uint16_t*)x,               \
+                     (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
+  if (cw == 32) {  // the stage-2/3 branch2b (32 -> 128 / 256)
+    if (g.K == 128) WHC(128, 32); else WHC(256, 32);
+  } else if (cw == 16) {  // stage 3 (16 -> 256)
+    WHC(256, 16);
+  } else if (g.K == 128) {
     if (amax) WH(128, true); else WH(128, false);
-  } else {
+  } else if (g.K == 64) {
     if (amax) WH(64, true); else WH(64, false);
+  } else {
+    WH(32, false);  // the stage-2 branch21 (128 -> 32): 18 MFMAs per wave per segment
   }
+#undef WHC
 #undef WH
   *used = sp;
   return launch_rc(amax ? "acfe_conv2d_wgrad_unpool" : "acfe_conv2d_wgrad(halo)");
@@ -2681,7 +2930,10 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   g.ldy = K;
   int rc;
   static const bool no_halo_w = getenv_flag("ACFE_WGRAD_NO_HALO");
-  if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 && C % 64 == 0 && (K == 64 || K == 128) &&
+  static const bool halo32 = !getenv_flag("ACFE_WGRAD_NO_HALO32");
+  if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 &&
+      ((C % 64 == 0 && (K == 64 || K == 128 || (K == 32 && halo32))) ||
+       (halo32 && ((C == 32 && (K == 128 || K == 256)) || (C == 16 && K == 256)))) &&
       (long long)N * P * ((Q + 63) / 64) < (1ll << 31) && !no_halo_w) {
     // halo-staged kernel; its split count stays within the planned workspace
     int used = 0;

@@ -344,3 +344,69 @@ def test_head_conv_wgrad_row_halo(env, cuda):
          stream())
     torch.cuda.synchronize()
     assert ((dw.cpu().to(F64) - 2 * dw_exact).norm() / (2 * dw_exact).norm()).item() < 5e-5
+
+
+@pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (256, 16, 16, 32), (64, 32, 20, 70)],
+                         ids=["s2-128to32", "s3-256to16", "ragged"])
+def test_conv_narrow_production(env, cuda, C, K, H, W):
+    """k_conv3x3_narrow (resident weights, halo staged once for all nine taps)
+    at wr_resnet_bird's stage-2/3 branch21 shapes (128 -> 32 at 32 x 64,
+    256 -> 16 at 16 x 32; 32 clips: more tiles than workgroups) and a ragged
+    one (partial row and column tiles): outputs within 1 bf16 ulp of the
+    float64 conv, BN sums of the stored values to 1e-6, the fused Dropout's
+    mask equal to acfe_dropout's, and the dgrad of the matching branch2b
+    (dY K' = C channels -> dX K channels) through the same kernel."""
+    ops, call, lib, ptr, stream = env
+    N = 32 if H * W <= 2048 else 8
+    x, w, b, g = _data(N, H, W, C, K, 211 + K, cuda)
+    wp = ops.pack_weights(w, BF, False)
+    rows = lib.acfe_conv2d_stats_rows(N * H * W, K)
+    y = torch.empty((N, H, W, K), dtype=BF, device=cuda)
+    st = torch.full((rows, 2, wp.shape[0]), 3.0, dtype=F64, device=cuda)
+    call("acfe_conv2d_fwd", ptr(x), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b), ptr(y), 1, ptr(st),
+         stream())
+    yd = torch.empty_like(y)
+    std = torch.empty_like(st)
+    call("acfe_conv2d_fwd_dropout", ptr(x), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b), ptr(yd), 1,
+         ptr(std), 0.1, 977, stream())
+    ref_drop = torch.empty_like(y)
+    call("acfe_dropout", ptr(y), y.numel(), 0.1, 977, ptr(ref_drop), 1, stream())
+    torch.cuda.synchronize()
+    _within_ulp(y, _oracle_conv(x, w, b), what="narrow fwd")
+    torch.testing.assert_close(st.sum(0)[:, :K].cpu(), _sums(y), rtol=1e-6, atol=1e-6)
+    assert float(st[:, :, K:].abs().max()) == 0.0 if wp.shape[0] > K else True
+    assert torch.equal(yd, ref_drop)
+    torch.testing.assert_close(std.sum(0)[:, :K].cpu(), _sums(yd), rtol=1e-6, atol=1e-6)
+    # dgrad of a K -> C... i.e. of the conv C' = K -> K' = C (branch2b): output K channels
+    w2 = (torch.randn((C, 3, 3, K), generator=g) / (3 * K ** 0.5)).to(cuda)
+    dy = (torch.randn((N, H, W, C), generator=g) * 0.5).to(BF).to(cuda)
+    wf = ops.pack_weights(w2, BF, True)
+    dx = torch.empty((N, H, W, K), dtype=BF, device=cuda)
+    call("acfe_conv2d_dgrad", ptr(dy), N, H, W, C, ptr(wf), K, 3, 3, 1, 1, 1, H, W, ptr(dx), 1, None, stream())
+    torch.cuda.synchronize()
+    wd = w2.cpu().to(BF).to(F64).permute(0, 3, 1, 2)
+    gd = dy.cpu().to(F64).permute(0, 3, 1, 2)
+    _within_ulp(dx, F.conv_transpose2d(gd, wd, padding=1).permute(0, 2, 3, 1), what="narrow dgrad")
+
+
+@pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (32, 128, 32, 64), (32, 256, 16, 32), (16, 256, 16, 32)],
+                         ids=["s2-21", "s2-2b", "s3-2b-b6", "s3-2b"])
+def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
+    """k_wgrad3x3_halo for the stage-2/3 layers whose channel count is the
+    feature height: K = 32 (branch21 128 -> 32) and the 16 / 32-channel
+    chunks (branch2b 32 -> 128 / 256, 16 -> 256), at 32 clips and the
+    production split count, against float64."""
+    ops, call, lib, ptr, stream = env
+    N = 32
+    x, w, b, g = _data(N, H, W, C, K, 307, cuda)
+    dy = (torch.randn((N, H, W, K), generator=g) * 0.5).to(BF).to(cuda)
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+    dw = torch.empty((K, 3, 3, C), device=cuda)
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, 3, 3, 1, 1, 1, H, W, ptr(dw), 0.0, 1, ptr(ws),
+         stream())
+    torch.cuda.synchronize()
+    dw_exact = torch.nn.grad.conv2d_weight(x.cpu().to(F64).permute(0, 3, 1, 2), (K, C, 3, 3),
+                                           dy.cpu().to(F64).permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    d = dw.cpu().to(F64)
+    assert ((d - dw_exact).norm() / dw_exact.norm()).item() < 5e-5
+    assert ((d - dw_exact).abs().max() / dw_exact.abs().max()).item() < 5e-4
