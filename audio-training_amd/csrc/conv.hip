@@ -951,7 +951,15 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // conflict-free under ds_read_b128's lane grouping at every tap shift (144-B
   // rows had 2-way conflicts: a third of the LDS cycles, rocprofv3 r02c); the
   // double-buffered K = 64 image only fits with 144-B rows
-  constexpr int SEGW = 64, HWX = SEGW + 2, XRB = (WDMA && NBUF == 2) ? 144 : 160;
+  // 160-B pixel pitch wherever the LDS allows it (conflict-free fragment reads);
+  // 144 B only for the 6-row K = 64 double buffer (37 % of its LDS cycles are
+  // bank conflicts, SQ counters r02z; the conflict-free 5-row variant,
+  // ACFE_ROWS64_TR=5, measured the same: those kernels are not LDS-bound)
+  constexpr int SEGW = 64, HWX = SEGW + 2;
+  constexpr int WB_ = 3 * KB * 128;
+  constexpr int SMEM160 = (WDMA ? NBUF * TR * HWX * 160 + 2 * WB_ : NBUF * (TR * HWX * 160 + WB_)) +
+                          (KB == 64 ? 0 : 2 * KB * 8);
+  constexpr int XRB = SMEM160 <= 163840 ? 160 : 144;
   constexpr int NV = 8 * FN;
   constexpr int XBYTES = TR * HWX * XRB, WBYTES = 3 * KB * 128, BUFB = XBYTES + WBYTES;
   constexpr int XG = TR * HWX * 8, WG = 3 * KB * 8;             // 16-B granules per step
@@ -2560,6 +2568,8 @@ static bool getenv_flag(const char* name) {
 
 static int pick_bn(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
+static int rows64_tr();
+
 template <typename T, int BN, int WM, int WN>
 static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                         double* stats, int grid_m, hipStream_t s) {
@@ -2572,7 +2582,7 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
       // 6 output rows per tile halves the weight traffic per pixel, but at K = 128
       // its register staging spills (measured 1.4x slower): 3 rows there
       static const int rows_tr = getenv("ACFE_CONV_ROWS_TR") ? atoi(getenv("ACFE_CONV_ROWS_TR")) : 0;
-      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr : 6;
+      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr : (BN == 64 ? rows64_tr() : 6);
       const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + 63) / 64;  // partial last column tile
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
@@ -2586,10 +2596,19 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
 #define ROWS(TR_, PM_)                                                                                   \
   hipLaunchKernelGGL((k_conv3x3_rows<BN, TR_, PM_>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,      \
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m, nullptr)
-        if (tr == 3) {
-          if (g.drop.on) ROWS(3, 4); else ROWS(3, 0);
-        } else {
-          if (g.drop.on) ROWS(6, 4); else ROWS(6, 0);
+        bool done = false;
+        if constexpr (BN == 64) {
+          if (tr == 5) {
+            if (g.drop.on) ROWS(5, 4); else ROWS(5, 0);
+            done = true;
+          }
+        }
+        if (!done) {
+          if (tr == 3) {
+            if (g.drop.on) ROWS(3, 4); else ROWS(3, 0);
+          } else {
+            if (g.drop.on) ROWS(6, 4); else ROWS(6, 0);
+          }
         }
 #undef ROWS
         return launch_rc("acfe_conv2d_fwd");
@@ -2971,10 +2990,18 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
 // output is never written; the backward reads the pooled gradient + argmax
 // bytes and expands them in its input staging (dgrad: k_conv3x3_rows<C, 6, 2>,
 // wgrad: k_wgrad3x3_halo<K, true>).
-template <int KB, int PM>
-static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
-                       int srows, uint8_t* amax, hipStream_t s, const char* what) {
-  constexpr int TR = 6;
+static int rows64_tr() {  // output rows per tile of the K = 64 rows kernels (ACFE_ROWS64_TR: 5 or 6)
+  static const int v = [] {
+    const char* e = getenv("ACFE_ROWS64_TR");
+    const int t = e ? atoi(e) : 0;
+    return t == 5 || t == 6 ? t : 6;  // 5 rows (conflict-free 160-B pitch) measured within 2 % of 6 (r02aa)
+  }();
+  return v;
+}
+
+template <int KB, int PM, int TR>
+static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
+                          double* stats, int srows, uint8_t* amax, hipStream_t s, const char* what) {
   const int tiles_h = (g.P + TR - 1) / TR, tiles_w = (g.Q + 63) / 64;
   const long long nt = (long long)g.N * tiles_h * tiles_w;
   int gp = 256;
@@ -2984,6 +3011,16 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
   hipLaunchKernelGGL((k_conv3x3_rows<KB, TR, PM>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
   return launch_rc(what);
+}
+
+template <int KB, int PM>
+static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+                       int srows, uint8_t* amax, hipStream_t s, const char* what) {
+  // pooling (PM 1 / 2) needs row pairs: 6 rows
+  if constexpr (KB == 64 && PM != 1 && PM != 2) {
+    if (rows64_tr() == 5) return launch_rows_tr<KB, PM, 5>(g, x, wp, bias, y, stats, srows, amax, s, what);
+  }
+  return launch_rows_tr<KB, PM, 6>(g, x, wp, bias, y, stats, srows, amax, s, what);
 }
 
 ACFE_API int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {

@@ -694,6 +694,184 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
 }
 
+// Two waves per frame (128 threads): the same radix-16/16/8 Stockham passes,
+// twiddles, post-processing and band sums as k_mel_w -- every value is
+// computed by the same operations in the same order, so the output is
+// bit-identical -- with each lane holding half the butterflies, so a wave
+// needs <= 128 VGPRs and the 18 KB frame buffer is shared by two waves:
+// 16 waves per CU (k_mel_w: 8, limited by LDS and 206+ VGPRs; its waves sat
+// waiting 41 % of their time, rocprofv3 SQ counters r02n).
+#ifndef ACFE_MEL_W2_WPE
+#define ACFE_MEL_W2_WPE 3
+#endif
+// k_mel_w2's LDS index: one float2 of padding per 16 points (k_mel_w pads one
+// per 8): pass-1 rows (stride 17), pass-2/3 stores (16-lane groups of
+// consecutive points) are bank-conflict free; the 32-lane reads keep one
+// colliding lane pair either way (k_mel_w: 50 % of its LDS cycles were
+// conflicts, SQ counters r02n)
+__device__ __forceinline__ int padx16(int i) { return i + (i >> 4); }
+
+template <int NC, int R, int NS, int NT>
+__device__ __forceinline__ void stockham_pass_t(float2* buf, const float2 (*bw)[4], int tid) {
+  constexpr int NB = NC / R, PER = NB / NT;
+  static_assert(NB % NT == 0 && NB % 8 == 0 && NS % 8 == 0, "pass shape");
+  float2 v[PER][R];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int j = tid + NT * p;
+    const float2* src = buf + padx16(j);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[p][r] = src[r * (NB + NB / 16)];
+    float2 w[R];
+    twiddle_pows<R>(bw[p], w);
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[p][r] = cmul(v[p][r], w[r]);
+  }
+  __syncthreads();  // every lane's reads precede the in-place writes of the other wave
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int j = tid + NT * p, jm = j & (NS - 1);
+    dft<R>(v[p]);
+    float2* dst = buf + padx16((j / NS) * NS * R + jm);
+#pragma unroll
+    for (int r = 0; r < R; ++r) dst[r * (NS + NS / 16)] = v[p][r];
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ACFE_MEL_W2_WPE)))
+k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restrict__ stats, int pad_mode, int power,
+         int n_frames, int fpw, int hop, const float2* __restrict__ tw, const float2* __restrict__ rtw,
+         const float* __restrict__ win, const int* __restrict__ band, const float* __restrict__ vals, int n_mels,
+         int kmin, int kmax, float* __restrict__ out, int layout) {
+  constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16, NT = 128;
+  extern __shared__ float2 wbuf[];
+  const int nk = kmax - kmin + 1;
+  const bool alias = nk <= 1024;
+  float* pw = alias ? reinterpret_cast<float*>(wbuf) : reinterpret_cast<float*>(wbuf + NC + NC / 16);
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const float* xb = raw + (int64_t)b * cs;
+  const bool do_norm = stats != nullptr;
+  const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
+  const int f0 = blockIdx.x * fpw;
+  // base twiddles: pass 2 (jm = j & 15), pass 3 (jm = j, two butterflies per lane)
+  float2 bw2[1][4], bw3[2][4];
+  {
+    const int t = (tid & 15) * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bw2[0][q] = tw[(t << q) & (NC - 1)];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) bw3[p][q] = tw[((tid + NT * p) << q) & (NC - 1)];
+      bw3[p][3] = make_float2(1.f, 0.f);
+    }
+  }
+  for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
+    int zo;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
+    const float* winf = win + zo;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      asm volatile("" : "+v"(bw2[0][q].x), "+v"(bw2[0][q].y));
+#pragma unroll
+      for (int p = 0; p < 2; ++p) asm volatile("" : "+v"(bw3[p][q].x), "+v"(bw3[p][q].y));
+    }
+    const int start = (pad_mode == ACFE_PAD_END) ? f * hop : f * hop - L / 2;
+    const bool inb = start >= 0 && start + L <= n;
+    __syncthreads();  // the previous frame's readers of wbuf / pw are done
+    {
+      const int j = tid;
+      float xa[16], xc[16], wa[16], wc[16];
+      const float* ws = winf + 2 * j;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wa[r] = ws[2 * r * NB0], wc[r] = ws[2 * r * NB0 + 1];
+      if (inb) {
+        const float* xs = xb + start + 2 * j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xa[r] = xs[2 * r * NB0], xc[r] = xs[2 * r * NB0 + 1];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int nn = 2 * (j + r * NB0);
+          xa[r] = fetch(xb, n, start + nn, pad_mode, false, 0.f, 1.f);
+          xc[r] = fetch(xb, n, start + nn + 1, pad_mode, false, 0.f, 1.f);
+        }
+      }
+      float2 v[16];
+      if (do_norm) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int nn = 2 * (j + r * NB0);
+          const bool ia = inb || in_sig(start + nn, n, pad_mode), ic = inb || in_sig(start + nn + 1, n, pad_mode);
+          v[r] = make_float2(ia ? norm1(xa[r], mn, rng) * wa[r] : 0.f, ic ? norm1(xc[r], mn, rng) * wc[r] : 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = make_float2(xa[r] * wa[r], xc[r] * wc[r]);
+      }
+      dft<16>(v);
+      float2* dst = wbuf + j * 17;  // padx16(16 j + r) = 17 j + r
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[r] = v[r];
+    }
+    __syncthreads();
+    stockham_pass_t<NC, 16, 16, NT>(wbuf, bw2, tid);
+    stockham_pass_t<NC, 8, 256, NT>(wbuf, bw3, tid);
+    for (int i0 = 0; i0 < nk; i0 += 1024) {  // uniform: every thread reaches the barrier
+      float2 rt[8];
+      float pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + tid + NT * u;
+        rt[u] = i < nk ? rtw[kmin + i] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + tid + NT * u;
+        pv[u] = 0.f;
+        if (i < nk) {
+          const int k = kmin + i;
+          const float2 zk = wbuf[padx16(k & (NC - 1))];
+          const float2 zm = wbuf[padx16((NC - k) & (NC - 1))];
+          const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+          const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
+          const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
+          const float2 X = cadd(E, cmul(rt[u], O));
+          pv[u] = X.x * X.x + X.y * X.y;
+        }
+      }
+      if (alias) __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + tid + NT * u < nk) pw[i0 + tid + NT * u] = pv[u];
+    }
+    if (tid < 8) pw[nk + tid] = 0.f;
+    if (power != 2) {
+      __syncthreads();
+      for (int k = tid; k < nk; k += NT) pw[k] = sqrtf(pw[k]);
+    }
+    __syncthreads();
+    // band pairs (m, n_mels-1-m): wave 0 the low band, wave 1 the high band
+    for (int q = tid & 63; q < (n_mels + 1) / 2; q += 64) {
+      const int m = tid < 64 ? q : n_mels - 1 - q;
+      if (tid >= 64 && m == q) continue;
+      const int s0 = band[3 * m], pl = (band[3 * m + 1] + 7) & ~7, off = band[3 * m + 2];
+      const float4* v0 = reinterpret_cast<const float4*>(vals + off);
+      const float* p0 = pw + (s0 - kmin);
+      float acc = 0.f;
+      for (int i0 = 0; i0 < pl; i0 += 8) {
+        const float4 a = v0[i0 / 4], c = v0[i0 / 4 + 1];
+        acc += a.x * p0[i0] + a.y * p0[i0 + 1] + a.z * p0[i0 + 2] + a.w * p0[i0 + 3] + c.x * p0[i0 + 4] +
+               c.y * p0[i0 + 5] + c.z * p0[i0 + 6] + c.w * p0[i0 + 7];
+      }
+      out[layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m : ((size_t)b * n_mels + m) * n_frames + f] =
+          acc;
+    }
+  }
+}
+
 static bool mel_wave_path() {
   static const int v = [] {
     const char* e = getenv("ACFE_MEL_BLOCK");
@@ -721,9 +899,18 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
     const int fpw = fpw_env;
     const int nk = p->kmax - p->kmin + 1;
     const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + (nk <= 1024 ? 0 : sizeof(float) * (nk + 8));
-    hipLaunchKernelGGL(k_mel_w, dim3(cdiv(T, fpw), batch), dim3(64), shm, strm(stream), raw, cs, n, stats,
-                       pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
-                       p->n_mels, p->kmin, p->kmax, out, layout);
+    const size_t shm2 = sizeof(float2) * (2048 + 2048 / 16) + (nk <= 1024 ? 0 : sizeof(float) * (nk + 8));
+    // ACFE_MEL_W1=1: the one-wave-per-frame kernel (read per call: the A/B test flips it)
+    const char* w1 = getenv("ACFE_MEL_W1");
+    const bool one_wave = w1 && atoi(w1);
+    if (one_wave)
+      hipLaunchKernelGGL(k_mel_w, dim3(cdiv(T, fpw), batch), dim3(64), shm, strm(stream), raw, cs, n, stats,
+                         pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
+                         p->n_mels, p->kmin, p->kmax, out, layout);
+    else
+      hipLaunchKernelGGL(k_mel_w2, dim3(cdiv(T, fpw), batch), dim3(128), shm2, strm(stream), raw, cs, n, stats,
+                         pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
+                         p->n_mels, p->kmin, p->kmax, out, layout);
     return launch_rc("acfe_mel_fwd");
   }
   const int fpb = 4;
