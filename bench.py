@@ -262,7 +262,7 @@ def main():
     traffic = None
     pmc = next((q for q in (ROOT / "profiles" / f"pmc_dominant_{t}.json" for t in ("r02", "r01l")) if q.exists()),
                None)
-    if pmc is not None:
+    if pmc is not None and a.batch == 512 and a.model == "bird":  # measured on this launch's shape
         try:
             traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
         except Exception:
@@ -310,7 +310,7 @@ def main():
             "wgrad_tflops": round(flops_launch / (wgrad_ms * 1e-3) / 1e12, 2),
         },
         "mel_pipeline": {
-            "kernel": "k_mel_w (wave per frame: frame+Hann+4096 rFFT+|X|^2+banded mel)",
+            "kernel": "k_mel_w2 (two waves per frame: frame+Hann+4096 rFFT+|X|^2+banded mel)",
             "avg_launch_ms": round(mel_ms, 4),
             "GBps": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2),
             "hbm_frac": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9 / MI355X_PEAK_HBM_GBS, 4),
