@@ -1433,35 +1433,39 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 // K-tile and wave (k_conv_fwd_g: 125-310 TFLOP/s).  Here the whole packed
 // weight matrix (9 taps x C x K <= 72 KB) stays in LDS for the workgroup's
 // lifetime, and one pipeline step stages a 64-channel chunk of the input halo
-// (TR + 2 rows x SEGW + 2 pixels, TR x SEGW = 128 output pixels) ONCE for all
-// nine taps: 4 waves x 32 pixels x K, 36 x K / 16 MFMAs per wave per step.
+// (TR + 2 rows x SEGW + 2 pixels, TR x SEGW = NW x 32 output pixels) ONCE for
+// all nine taps: NW waves x 32 pixels x K, 36 x K / 16 MFMAs per wave per step.
 // Fragment reads as k_conv3x3_rows (160-B pixel pitch, XOR-swizzled 128-B
 // weight rows), register-staged double buffer, one barrier per step; epilogue:
 // bias, bf16 rounding, the pair-hash Dropout (PM 4's), BN sums through
 // 16-lane shuffles and LDS f64 atomics.  Persistent, XCD-aware tile walk.
-template <int KB, int SEGW, bool DROP>
-__global__ void __launch_bounds__(256, 1)
+template <int KB, int SEGW, bool DROP, int NW>
+__global__ void __launch_bounds__(NW * 64, 1)
 k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
                  const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
                  int tiles_w, int ntiles, int srows) {
-  constexpr int TR = 128 / SEGW, HWX = SEGW + 2, XR = TR + 2, XRB = 160;
+  // NW = 4: 128-pixel tiles, double-buffered input image (one wave per SIMD);
+  // NW = 8: 256-pixel tiles, one image buffer stored between two barriers
+  // (two waves per SIMD hide each other's latency)
+  constexpr int NT = NW * 64, NXB = NW == 8 ? 1 : 2;
+  constexpr int TR = NW * 32 / SEGW, HWX = SEGW + 2, XR = TR + 2, XRB = 160;
   constexpr int FM = 2, FN = KB / 16;
   constexpr int XBYTES = XR * HWX * XRB, WBYTES = 576 * 128;
-  constexpr int XG = XR * HWX * 8, XPT = (XG + 255) / 256;
-  constexpr int SMEM = 2 * XBYTES + WBYTES + 2 * KB * 8;
+  constexpr int XG = XR * HWX * 8, XPT = (XG + NT - 1) / NT;
+  constexpr int SMEM = NXB * XBYTES + WBYTES + 2 * KB * 8;
   static_assert(SMEM <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
-  unsigned char* Wl = smem + 2 * XBYTES;
-  double* sstat = reinterpret_cast<double*>(smem + 2 * XBYTES + WBYTES);
+  unsigned char* Wl = smem + NXB * XBYTES;
+  double* sstat = reinterpret_cast<double*>(smem + NXB * XBYTES + WBYTES);
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nch = g.C / 64, tpi = tiles_h * tiles_w;
   const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
-  for (int i = tid; i < 2 * KB; i += 256) sstat[i] = 0.0;
+  for (int i = tid; i < 2 * KB; i += NT) sstat[i] = 0.0;
   // resident weights: row (t * nch + cc) * KB + k = W[k][tap t][chunk cc], granule gw at slot gw ^ (k & 7)
   {
     const int wrows = 9 * nch * KB;
-    for (int gi = tid; gi < wrows * 8; gi += 256) {
+    for (int gi = tid; gi < wrows * 8; gi += NT) {
       const int row = gi >> 3, gw = gi & 7;
       const int k = row % KB, tc = row / KB, cc = tc % nch, t = tc / nch;
       const u32x4 v = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + t * g.C + cc * 64 + gw * 8);
@@ -1482,7 +1486,7 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
     const uint16_t* img = X + (long long)n * g.H * g.W * g.C + cc * 64;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3, gr = idx & 7;
       const int hin = h0 + xrow, win = w0 + xpix;
       const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
@@ -1493,7 +1497,7 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
     unsigned char* Xl = smem + buf * XBYTES;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       if (idx < XG) *reinterpret_cast<u32x4*>(Xl + (idx >> 3) * XRB + (idx & 7) * 16) = rx[i];
     }
   };
@@ -1586,7 +1590,7 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   auto step = [&](int t, const u32x4 (&rnext)[XPT], u32x4 (&rfree)[XPT]) __attribute__((always_inline)) {
     if (t + 2 < L) gload(rfree, t + 2);
     const int cc = t % nch;
-    const unsigned char* Xl = smem + (t & 1) * XBYTES;
+    const unsigned char* Xl = smem + (NXB == 2 ? (t & 1) * XBYTES : 0);
     __builtin_amdgcn_iglp_opt(0);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap)
@@ -1608,13 +1612,21 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
 #pragma unroll
           for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], wf[fn], xf[fm], uint16_t());
       }
-    if (t + 1 < L) sstore(rnext, (t + 1) & 1);
+    if constexpr (NXB == 2) {
+      if (t + 1 < L) sstore(rnext, (t + 1) & 1);
+    }
     if (++cst == nch) {
       cst = 0;
       epilogue(ctm);
       ctm += walk.step;
     }
     __syncthreads();
+    if constexpr (NXB == 1) {
+      if (t + 1 < L) {  // every wave is done with the image: restage it
+        sstore(rnext, 0);
+        __syncthreads();
+      }
+    }
   };
   for (int t = 0; t < L; t += 2) {
     step(t, rb, ra);
@@ -1622,12 +1634,12 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   }
   if (stats) {
     __syncthreads();
-    for (int c = tid; c < g.Kp; c += 256) {
+    for (int c = tid; c < g.Kp; c += NT) {
       stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = c < KB ? sstat[c] : 0.0;
       stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = c < KB ? sstat[KB + c] : 0.0;
     }
     for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
-      for (int c = tid; c < 2 * g.Kp; c += 256) stats[((long long)rr * 2 + (c / g.Kp)) * g.Kp + (c % g.Kp)] = 0.0;
+      for (int c = tid; c < 2 * g.Kp; c += NT) stats[((long long)rr * 2 + (c / g.Kp)) * g.Kp + (c % g.Kp)] = 0.0;
   }
 }
 
@@ -2570,6 +2582,36 @@ static int pick_bn(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
 static int rows64_tr();
 
+// waves per k_conv3x3_narrow workgroup (ACFE_NARROW_WAVES: 4 or 8)
+static int narrow_waves() {
+  const char* e = getenv("ACFE_NARROW_WAVES");
+  const int v = e ? atoi(e) : 0;
+  return v == 4 || v == 8 ? v : 8;
+}
+
+template <int KB, int SW>
+static void launch_narrow(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
+                          double* stats, int tiles_h, int tiles_w, long long nt, int grid_m, int gp, int nw,
+                          hipStream_t s) {
+  const uint16_t *xx = (const uint16_t*)x, *ww = (const uint16_t*)wp;
+  uint16_t* yy = (uint16_t*)y;
+  if (nw == 8) {
+    if (g.drop.on)
+      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, true, 8>), dim3(gp), dim3(512), 0, s, g, xx, ww, bias, yy, stats,
+                         tiles_h, tiles_w, (int)nt, grid_m);
+    else
+      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, false, 8>), dim3(gp), dim3(512), 0, s, g, xx, ww, bias, yy, stats,
+                         tiles_h, tiles_w, (int)nt, grid_m);
+  } else {
+    if (g.drop.on)
+      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, true, 4>), dim3(gp), dim3(256), 0, s, g, xx, ww, bias, yy, stats,
+                         tiles_h, tiles_w, (int)nt, grid_m);
+    else
+      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, false, 4>), dim3(gp), dim3(256), 0, s, g, xx, ww, bias, yy, stats,
+                         tiles_h, tiles_w, (int)nt, grid_m);
+  }
+}
+
 template <typename T, int BN, int WM, int WN>
 static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                         double* stats, int grid_m, hipStream_t s) {
@@ -2667,7 +2709,9 @@ general:
     if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W &&
         g.C % 64 == 0 && (g.K == 32 || g.K == 16) && g.C * g.K <= 4096 && g.ldy == g.K &&
         g.M * g.K < (1ll << 32) && !no_narrow) {
-      const int segw = g.Q <= 32 ? 32 : 64, tr = 128 / segw;
+      static const int nw = narrow_waves();
+      // tiles of nw * 32 pixels: segw columns x tr rows
+      const int segw = g.Q <= 32 ? 32 : 64, tr = nw * 32 / segw;
       const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + segw - 1) / segw;
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
@@ -2675,13 +2719,13 @@ general:
         if (gp > nt) gp = (int)nt;
         if (gp >= 64) gp &= ~7;
         if (stats && gp > grid_m) gp = grid_m;  // one statistics slab row per workgroup
-#define NARROW(KB_, SW_)                                                                                           do {                                                                                                               if (g.drop.on)                                                                                                     hipLaunchKernelGGL((k_conv3x3_narrow<KB_, SW_, true>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,                            (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);         else                                                                                                               hipLaunchKernelGGL((k_conv3x3_narrow<KB_, SW_, false>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,                           (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);       } while (0)
         if (g.K == 32) {
-          if (segw == 64) NARROW(32, 64); else NARROW(32, 32);
+          if (segw == 64) launch_narrow<32, 64>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
+          else launch_narrow<32, 32>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
         } else {
-          if (segw == 64) NARROW(16, 64); else NARROW(16, 32);
+          if (segw == 64) launch_narrow<16, 64>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
+          else launch_narrow<16, 32>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
         }
-#undef NARROW
         return launch_rc("acfe_conv2d_fwd(narrow)");
       }
     }
