@@ -923,7 +923,9 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 // fragment read hit distinct banks at any tap shift); weight rows are 128 B
 // with the k & 7 XOR swizzle.  Operands swapped (weights x pixels) so the
 // epilogue is k_conv_fwd_p's: 8-byte channel quads straight from registers,
-// bias from LDS, fused Dropout, DPP-butterfly BatchNormalization sums.
+// bias gathered by ds_bpermute, fused Dropout, DPP-butterfly BatchNormalization
+// sums.  XRES (K = 128: 4 rows, K = 64: 6 rows) stages the TR + 2 halo rows of
+// a chunk once for its three filter-row steps (see the XROWS comment below).
 // PM (epilogue mode): 0 plain; 4 = plain + Dropout (its own instantiation:
 // the dropout epilogue's registers would spill the K = 128 dgrad); 3 = z = (ReLU)(conv + residual g.res) as
 // ops.add stores it, BN sums of z; 1 = the output feeds MaxPool2D(2, 2) -> Dropout:
@@ -932,7 +934,7 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 // (amax) and their BN statistics; 2 = dgrad whose dY is the 2x2 max-pool
 // backward of X = the pooled gradient with argmax bytes amax (expanded while
 // staging, the full-resolution dY is never stored).
-template <int KB, int TR, int PM>
+template <int KB, int TR, int PM, bool XRES = false>
 __global__ void __launch_bounds__(512, 1)
 k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
                const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
@@ -946,7 +948,13 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // MFMAs, one barrier per step) where they fit -- K = 64 and the 3-row tiles --,
   // else one (stored between two barriers, the MFMA pipe idle meanwhile).
   constexpr bool WDMA = TR > 3;
-  constexpr int NBUF = (TR <= 3 || KB == 64) ? 2 : 1;
+  // XRES: the TR + 2 halo rows of a 64-channel chunk are staged once and serve
+  // its three filter-row steps (single buffer, restaged between two barriers
+  // once per chunk instead of once per step: a third of the LDS stores and of
+  // the input reads); the steps in between only wait for their weight pieces
+  constexpr int XROWS = XRES ? TR + 2 : TR;
+  constexpr int NBUF = XRES ? 1 : (TR <= 3 || KB == 64) ? 2 : 1;
+  static_assert(!XRES || WDMA, "XRES needs the weight DMA");
   // pixels per row, halo row bytes: 160-B rows make the fragment reads
   // conflict-free under ds_read_b128's lane grouping at every tap shift (144-B
   // rows had 2-way conflicts: a third of the LDS cycles, rocprofv3 r02c); the
@@ -957,12 +965,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // ACFE_ROWS64_TR=5, measured the same: those kernels are not LDS-bound)
   constexpr int SEGW = 64, HWX = SEGW + 2;
   constexpr int WB_ = 3 * KB * 128;
-  constexpr int SMEM160 = (WDMA ? NBUF * TR * HWX * 160 + 2 * WB_ : NBUF * (TR * HWX * 160 + WB_)) +
+  constexpr int SMEM160 = (WDMA ? NBUF * XROWS * HWX * 160 + 2 * WB_ : NBUF * (XROWS * HWX * 160 + WB_)) +
                           (KB == 64 ? 0 : 2 * KB * 8);
   constexpr int XRB = SMEM160 <= 163840 ? 160 : 144;
   constexpr int NV = 8 * FN;
-  constexpr int XBYTES = TR * HWX * XRB, WBYTES = 3 * KB * 128, BUFB = XBYTES + WBYTES;
-  constexpr int XG = TR * HWX * 8, WG = 3 * KB * 8;             // 16-B granules per step
+  constexpr int XBYTES = XROWS * HWX * XRB, WBYTES = 3 * KB * 128, BUFB = XBYTES + WBYTES;
+  constexpr int XG = XROWS * HWX * 8, WG = 3 * KB * 8;          // 16-B granules per step
   constexpr int XPT = (XG + 511) / 512, WPT = WG / 512;
   static_assert(WG % 512 == 0, "weight granules per thread");
   // WDMA layout [X0 (X1)][W0][W1]; else [X0 W0][X1 W1]
@@ -989,11 +997,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   for (int k = 0; k < (REGSTAT ? NV16 : 1); ++k) dstat[k] = 0.0;
   if constexpr (!REGSTAT)
     for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
-  // this lane's bias quads are loaded (f4, L2-resident) at each epilogue: no
-  // LDS copy (the 160-B image fills the LDS at K = 128) and no registers held
-  // across the main loop (the K = 128 variants sit at the 256-VGPR limit)
-  const float* bq = bias ? bias + wk * (KB / 2) + (lane >> 4) * 4 : reinterpret_cast<const float*>(g_zero_page);
-  const int bfs = bias ? 16 : 0;
+  // bias: lane l holds channel wk * KB/2 + (l mod KB/2), one VGPR across the
+  // main loop (the K = 128 variants sit at the 256-VGPR limit; no LDS left for
+  // a copy); each epilogue gathers its quads with ds_bpermute, once per
+  // fragment column (a global f4 load per fragment waited on its full L2
+  // latency twelve times per tile)
+  const float blane = (bias && PM != 2) ? bias[wk * (KB / 2) + (lane & (KB / 2 - 1))] : 0.f;
   const TileWalk walk(ntiles);
   const int ntl = walk.tm < walk.end ? (walk.end - walk.tm + walk.step - 1) / walk.step : 0;
   const int L = ntl * nsteps_t;
@@ -1039,7 +1048,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // wave-uniform tile origin (sh0, sw0)
   int xoffs[PM == 2 ? 1 : XPT];
   int sh0 = 0, sw0 = 0;       // PM 2: input row / column of halo pixel (0, 0) at filter row 0 (wave-uniform)
-  unsigned xm = 0;            // 4 mask bits per granule: filter rows 0..2 inside the image, (PM 2) column parity
+  // mask bits per granule: filter rows 0..2 inside the image (XRES: row 0 only)
+  constexpr int MB = XRES ? 1 : 4;
+  static_assert(MB * XPT <= 32, "granule mask bits");
+  unsigned xm = 0;
   int stl = -1;  // walk index of the tile the offsets belong to
   __amdgpu_buffer_rsrc_t xrs, ars;
   const int CB = g.C * 2;  // bytes per pixel
@@ -1071,11 +1083,11 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       for (int r = 0; r < 3; ++r) m |= ((unsigned)(hin + r) < (unsigned)g.H ? 1u : 0u) << r;
       m = ok ? m : 0u;
       xoffs[i] = (hin * g.W + win) * CB + gr * 16;
-      xm |= m << (4 * i);
+      xm |= (XRES ? m & 1u : m) << (MB * i);
     }
   };
   auto gload = [&](int t) __attribute__((always_inline)) {
-    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
+    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = XRES ? 0 : st - cc * 3;
     if (tl != stl) {
       stage_tile(tl);
       stl = tl;
@@ -1098,7 +1110,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       const int delta = r * g.W * CB + cc * 128;
 #pragma unroll
       for (int i = 0; i < XPT; ++i) {
-        const bool ok = (xm >> (4 * i + r)) & 1u;
+        const bool ok = (xm >> (MB * i + r)) & 1u;
         rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xoffs[i] + delta : 0x80000000, 0, 0);
       }
     }
@@ -1156,7 +1168,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 
   // PM 3 with K = 64: the tile's residual quads are loaded at the start of its
   // last step (in flight during that step's MFMAs) instead of in the epilogue
-  constexpr bool RPRE = PM == 3 && KB == 64;
+  constexpr bool RPRE = PM == 3 && KB == 64 && FM <= 6;  // (8 rows: its registers spill)
   uint2 rres[RPRE ? FM : 1][RPRE ? FN : 1];
   auto rload = [&](int tm) __attribute__((always_inline)) {
     if constexpr (RPRE) {
@@ -1182,7 +1194,14 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     for (int i = 0; i < NV; ++i) sv[i] = 0.f;
     // bias quad of fragment column fn (PM 2, the dgrad, has none)
     auto bias4 = [&](int fn) __attribute__((always_inline)) {
-      return PM == 2 ? f4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f4*>(bq + fn * bfs);
+      f4 r = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (PM != 2) {
+        const int src = fn * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          r[j] = __int_as_float(__builtin_amdgcn_ds_bpermute((src + j) * 4, __float_as_int(blane)));
+      }
+      return r;
     };
     if constexpr (PM == 1) {
       // 2x2 windows: rows (2i, 2i+1) in this lane's fragments, columns (l16,
@@ -1195,14 +1214,14 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       const int wq = (wb * SEGW + wp * 16 + l16) >> 1;
       const bool odd = (l16 & 1) != 0;
 #pragma unroll
-      for (int i = 0; i < TR / 2; ++i) {
-        const int hp2 = ((hb * TR) >> 1) + i;
-        const bool inb = hp2 < P2 && wq < Q2;
-        const unsigned pp = ((unsigned)n * P2 + hp2) * Q2 + wq;  // < 2^32 (acfe_conv2d_pool_supported)
+      for (int fn = 0; fn < FN; ++fn) {
+        const f4 rb = bias4(fn);
+        const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4 + (odd ? 2 : 0);
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4 + (odd ? 2 : 0);
-          const f4 rb = bias4(fn);
+        for (int i = 0; i < TR / 2; ++i) {
+          const int hp2 = ((hb * TR) >> 1) + i;
+          const bool inb = hp2 < P2 && wq < Q2;
+          const unsigned pp = ((unsigned)n * P2 + hp2) * Q2 + wq;  // < 2^32 (acfe_conv2d_pool_supported)
           float hv[2];
           unsigned amb = 0;
           uint32_t dh = 0;
@@ -1262,15 +1281,15 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     auto epi03 = [&](auto dropc, auto idxc) __attribute__((always_inline)) {
       constexpr bool DRP = decltype(dropc)::value, I32 = decltype(idxc)::value;
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const int p = wp * (TR * 16) + fm * 16;
-        const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
-        const bool inb = h < g.P && w < g.Q;
-        const long long pix = ((long long)n * g.P + h) * g.Q + w;
+      for (int fn = 0; fn < FN; ++fn) {
+        const f4 rb = bias4(fn);
+        const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
-          const f4 rb = bias4(fn);
+        for (int fm = 0; fm < FM; ++fm) {
+          const int p = wp * (TR * 16) + fm * 16;
+          const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+          const bool inb = h < g.P && w < g.Q;
+          const long long pix = ((long long)n * g.P + h) * g.Q + w;
           float r[4];
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) r[jj] = bf2f(f2bf(acc[fm][fn][jj] + rb[jj]));
@@ -1343,15 +1362,18 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   int buf = 0, cst = 0, ctm = walk.tm;
   for (int t = 0; t < L; ++t) {
     const bool more = t + 1 < L;
+    // XRES: filter row of this step and whether the next one starts a chunk
+    const int rs = XRES ? cst - 3 * (cst / 3) : 0;
+    const bool xnext = more && (!XRES || rs == 2);
     if (more) {
-      gload(t + 1);
+      if (xnext) gload(t + 1);
       if constexpr (WDMA) wdma(t + 1, (t + 1) & 1);
     }
     if constexpr (RPRE) {
       if (cst + 1 == nsteps_t) rload(ctm);
     }
-    const unsigned char* Xl = xbuf(buf);
-    const unsigned char* Wl = WDMA ? smem + WBASE + (t & 1) * WBYTES : Xl + XBYTES;
+    const unsigned char* Xl = xbuf(buf) + rs * (HWX * XRB);
+    const unsigned char* Wl = WDMA ? smem + WBASE + (t & 1) * WBYTES : xbuf(buf) + XBYTES;
     // K = 64: let the scheduler interleave the fragment reads with the MFMAs
     // (fwd_add 128->64 1.084 -> 1.013 ms, dropout 64->64 0.649 -> 0.625 ms;
     // at K = 128 the same hint spills: fwd_pool 4.96 -> 5.35 ms, r02o)
@@ -1381,10 +1403,13 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       ctm += walk.step;
     }
     if constexpr (WDMA && NBUF == 2) wait_vmcnt<0>();  // next step's weight pieces landed
+    if constexpr (XRES) {
+      if (!xnext) wait_vmcnt<0>();
+    }
     __syncthreads();
     if (NBUF == 2) {
       buf ^= 1;
-    } else if (more) {
+    } else if (xnext) {
       sstore(0);  // single buffer: every wave has finished reading it
       if constexpr (WDMA) wait_vmcnt<0>();  // next step's weight pieces landed
       __syncthreads();
@@ -2581,6 +2606,8 @@ static bool getenv_flag(const char* name) {
 static int pick_bn(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
 static int rows64_tr();
+static bool rows128_xres();
+static int rows64_xres();
 
 // waves per k_conv3x3_narrow workgroup (ACFE_NARROW_WAVES: 4 or 8)
 static int narrow_waves() {
@@ -2624,7 +2651,11 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
       // 6 output rows per tile halves the weight traffic per pixel, but at K = 128
       // its register staging spills (measured 1.4x slower): 3 rows there
       static const int rows_tr = getenv("ACFE_CONV_ROWS_TR") ? atoi(getenv("ACFE_CONV_ROWS_TR")) : 0;
-      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr : (BN == 64 ? rows64_tr() : 6);
+      const int xr64 = BN == 64 && rows_tr == 0 ? rows64_xres() : 0;
+      const bool xres = (BN == 128 && rows_tr == 0 && rows128_xres()) || xr64 != 0;
+      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr
+                     : BN == 64 ? (xr64 ? xr64 : rows64_tr())
+                                : (xres ? 4 : 6);
       const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + 63) / 64;  // partial last column tile
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
@@ -2635,10 +2666,25 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
         // workgroups than the caller's slab rows (narrow images have more
         // 6 x 64 tiles than 128-pixel slab rows)
         if (stats && gp > grid_m) gp = grid_m;
-#define ROWS(TR_, PM_)                                                                                   \
-  hipLaunchKernelGGL((k_conv3x3_rows<BN, TR_, PM_>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,      \
+#define ROWS(TR_, PM_, ...)                                                                                   \
+  hipLaunchKernelGGL((k_conv3x3_rows<BN, TR_, PM_, ##__VA_ARGS__>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x, \
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m, nullptr)
         bool done = false;
+        if constexpr (BN == 128) {
+          if (xres) {
+            if (g.drop.on) ROWS(4, 4, true); else ROWS(4, 0, true);
+            done = true;
+          }
+        } else {
+          if (xres) {
+            if (tr == 8) {
+              if (g.drop.on) ROWS(8, 4, true); else ROWS(8, 0, true);
+            } else {
+              if (g.drop.on) ROWS(6, 4, true); else ROWS(6, 0, true);
+            }
+            done = true;
+          }
+        }
         if constexpr (BN == 64) {
           if (tr == 5) {
             if (g.drop.on) ROWS(5, 4); else ROWS(5, 0);
@@ -3034,6 +3080,28 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
 // output is never written; the backward reads the pooled gradient + argmax
 // bytes and expands them in its input staging (dgrad: k_conv3x3_rows<C, 6, 2>,
 // wgrad: k_wgrad3x3_halo<K, true>).
+// K = 128 rows kernels: 4-row tiles with chunk-resident halo rows
+// (ACFE_ROWS_XRES=0: the 6-row per-step staging; r02z: fwd_pool 4.97 -> 4.89 ms,
+// dgrad_unpool 5.19 -> 4.75 ms)
+static bool rows128_xres() {
+  static const bool v = [] {
+    const char* e = getenv("ACFE_ROWS_XRES");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+// K = 64 rows kernels with chunk-resident halo rows: the tile rows (6, 8) or 0
+// (off: the per-step staging with a double-buffered image), ACFE_ROWS64_XRES;
+// r02z on the 64x128 layers: 6 rows fwd_add 128->64 1.037 -> 0.968 ms, 64->64
+// 0.717 -> 0.658 ms, fwd_dropout 0.614 -> 0.544 ms (8 rows: 1.003 / 0.678 / 0.525)
+static int rows64_xres() {
+  static const int v = [] {
+    const char* e = getenv("ACFE_ROWS64_XRES");
+    const int t = e ? atoi(e) : 6;
+    return t == 6 || t == 8 ? t : 0;
+  }();
+  return v;
+}
 static int rows64_tr() {  // output rows per tile of the K = 64 rows kernels (ACFE_ROWS64_TR: 5 or 6)
   static const int v = [] {
     const char* e = getenv("ACFE_ROWS64_TR");
@@ -3043,7 +3111,7 @@ static int rows64_tr() {  // output rows per tile of the K = 64 rows kernels (AC
   return v;
 }
 
-template <int KB, int PM, int TR>
+template <int KB, int PM, int TR, bool XR = false>
 static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                           double* stats, int srows, uint8_t* amax, hipStream_t s, const char* what) {
   const int tiles_h = (g.P + TR - 1) / TR, tiles_w = (g.Q + 63) / 64;
@@ -3052,7 +3120,7 @@ static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, cons
   if (gp > nt) gp = (int)nt;
   if (gp >= 64) gp &= ~7;
   if (stats && gp > srows) gp = srows;  // one statistics slab row per workgroup
-  hipLaunchKernelGGL((k_conv3x3_rows<KB, TR, PM>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+  hipLaunchKernelGGL((k_conv3x3_rows<KB, TR, PM, XR>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
   return launch_rc(what);
 }
@@ -3060,7 +3128,15 @@ static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, cons
 template <int KB, int PM>
 static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                        int srows, uint8_t* amax, hipStream_t s, const char* what) {
-  // pooling (PM 1 / 2) needs row pairs: 6 rows
+  // pooling (PM 1 / 2) needs row pairs: 6 rows (or 4 chunk-resident rows)
+  if constexpr (KB == 128) {
+    if (rows128_xres()) return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+  }
+  if constexpr (KB == 64) {
+    const int xr = rows64_xres();
+    if (xr == 6) return launch_rows_tr<KB, PM, 6, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+    if (xr == 8) return launch_rows_tr<KB, PM, 8, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+  }
   if constexpr (KB == 64 && PM != 1 && PM != 2) {
     if (rows64_tr() == 5) return launch_rows_tr<KB, PM, 5>(g, x, wp, bias, y, stats, srows, amax, s, what);
   }

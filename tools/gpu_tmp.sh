@@ -1,6 +1,9 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-timeout -k 10 600 python -u -m pytest tests/test_ops_gpu.py tests/test_fused_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-for tr in 6 3; do
-echo "== TR $tr"
-ACFE_CONV_ROWS_TR=$tr timeout -k 10 300 python tools/conv_bench.py --iters 5 --layers 0,2,3 --passes fwd,dgrad 2>&1 | grep -v amdgpu.ids || exit 1
+mkdir -p gpurun_out/xres
+timeout -k 10 300 python -u tools/layer_profile.py > gpurun_out/xres/lp.log 2>&1 || exit 1
+cat gpurun_out/xres/lp.log | grep -v amdgpu.ids
+for v in new old new old; do
+  if [ $v = old ]; then lib=$PWD/abtest/old.so; else lib=""; fi
+  ACFE_LIB=$lib timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/xres/b_$v.json 2>gpurun_out/xres/b_$v.err || exit 1
+  python -c "import json,sys; d=json.loads(open('gpurun_out/xres/b_$v.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'])"
 done
