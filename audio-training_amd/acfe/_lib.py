@@ -70,6 +70,9 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_rows_supported": [I32, I32, I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_fwd_add_supported": [I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_fwd_add": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, I32, P, P, I32, P],
+    "acfe_conv2d_bn_prologue_supported": [I32, I32, I32, I32, I32, I32],
+    "acfe_conv2d_fwd_bn": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, P, F32, C.c_uint64, P, P, I32, P, I32, P],
+    "acfe_conv2d_fwd_add_bn": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, I32, P, P, P, P, I32, P, I32, P],
     "acfe_c1bn_supported": [I32, I32],
     "acfe_c1bn_workspace": [I64, I32, I32],
     "acfe_c1bn_stats": [P, I64, I32, P, I32, P, P, P, P, P],

@@ -72,16 +72,18 @@ class BatchNormalization(nn.Module):
         self.register_buffer("moving_mean", torch.zeros(channels))
         self.register_buffer("moving_variance", torch.ones(channels))
 
-    def forward(self, x, relu=False, stats=None, link=None):
+    def forward(self, x, relu=False, stats=None, link=None, defer=False):
+        """defer: the output comes back pending for a consuming conv's BN
+        prologue (ops.batch_norm)."""
         return ops.batch_norm(x, self.gamma, self.beta, self.moving_mean, self.moving_variance, self.training,
-                              relu, stats, self.eps, self.momentum, link)
+                              relu, stats, self.eps, self.momentum, link, defer)
 
 
-def conv_dropout_bn(conv: Conv2D, bn: BatchNormalization, x, rate, relu=True):
+def conv_dropout_bn(conv: Conv2D, bn: BatchNormalization, x, rate, relu=True, defer=False):
     """bn(Dropout(rate)(conv(x))) (+ReLU) as one fused node (ops.conv_dropout_bn)."""
     return ops.conv_dropout_bn(x, conv.weight, conv.bias, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance,
                                bn.training, rate, relu=relu, stride=conv.strides, padding=conv.padding,
-                               eps=bn.eps, momentum=bn.momentum)
+                               eps=bn.eps, momentum=bn.momentum, defer=defer)
 
 
 def conv_bn(conv: Conv2D, bn: BatchNormalization, x, relu=True):
@@ -97,12 +99,12 @@ def maxpool_dropout_bn(x, kh, kw, bn: BatchNormalization, rate, relu=True):
                                   rate, relu=relu, eps=bn.eps, momentum=bn.momentum)
 
 
-def conv_maxpool_dropout_bn(conv: Conv2D, x, k, bn: BatchNormalization, rate, relu=True):
+def conv_maxpool_dropout_bn(conv: Conv2D, x, k, bn: BatchNormalization, rate, relu=True, defer=False):
     """bn(Dropout(rate)(MaxPool2D((k, k))(conv(x)))) (+ReLU) as one fused node
     (the pooling runs in the conv epilogue when the kernel covers the shape)."""
     return ops.conv_maxpool_dropout_bn(x, conv.weight, conv.bias, conv.strides, conv.padding, k, k, bn.gamma, bn.beta,
                                        bn.moving_mean, bn.moving_variance, bn.training, rate, relu=relu, eps=bn.eps,
-                                       momentum=bn.momentum)
+                                       momentum=bn.momentum, defer=defer)
 
 
 class Dense(nn.Module):

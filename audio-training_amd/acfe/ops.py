@@ -24,6 +24,9 @@ FUSE = os.environ.get("ACFE_FUSE", "1") != "0"
 # backward and runs the plain dgrad / wgrad instead of expanding it in their
 # input staging (A/B switch).
 UNPOOL = os.environ.get("ACFE_UNPOOL", "1") != "0"
+# ACFE_BN_PROLOGUE=0: every BatchNormalization writes its output in its own
+# apply pass instead of handing it to the consuming conv's input staging.
+PROLOGUE = os.environ.get("ACFE_BN_PROLOGUE", "1") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -148,7 +151,13 @@ class _Timed:
 
 # ------------------------------------------------------------------ conv
 def _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats, drop=None):
-    """acfe_conv2d_fwd[_dropout] -> (y, stats_partial)."""
+    """acfe_conv2d_fwd[_dropout] -> (y, stats_partial); a pending BN output x
+    (bn_prologue_ok's shapes) is convolved through the BN prologue."""
+    if _pending(x) is not None:
+        if stride == 1 and (P, Q, pt, pl) == (x.shape[1], x.shape[2], 1, 1) and \
+                bn_prologue_ok(x.shape, x.dtype, w):
+            return _conv_fwd_bn(x, w, b, want_stats, drop)
+        materialize(x)
     N, H, W, C = x.shape
     K, R, S, Cw = w.shape
     assert Cw == C, (Cw, C)
@@ -393,8 +402,11 @@ class ResidualLink:
         return p
 
 
-def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype):
-    """Batch statistics (given slab or acfe_bn_stats) -> finalize -> apply. Returns (y, saved)."""
+def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, defer=False):
+    """Batch statistics (given slab or acfe_bn_stats) -> finalize -> apply. Returns (y, saved).
+    defer: y is returned unwritten, marked pending (x, scale, shift, relu); the
+    consuming conv applies the BN in its input staging and fills y, or
+    materialize(y) runs the apply pass."""
     C = x.shape[-1]
     rows = x.numel() // C
     dt = dtype_code(x.dtype)
@@ -419,8 +431,66 @@ def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, o
     if out_dtype is None:  # affine only: the caller applies it (bn_max_pool)
         return None, (scale, shift, mean, invstd)
     y = _empty(x.shape, out_dtype, dev)
+    if defer and out_dtype == x.dtype:
+        y._acfe_bn_pending = (x, scale, shift, bool(relu))
+        return y, (scale, shift, mean, invstd)
     call("acfe_bn_apply", ptr(x), dt, rows, C, ptr(scale), ptr(shift), int(relu), ptr(y), dtype_code(out_dtype), s)
     return y, (scale, shift, mean, invstd)
+
+
+# ------------------------------------------------------------------ BN prologue (deferred BN apply)
+def bn_prologue_ok(x_shape, dtype, w) -> bool:
+    """Can a conv with weights w [K][3][3][C] take its BN (+ReLU) input as a
+    prologue (acfe_conv2d_fwd_bn / acfe_conv2d_fwd_add_bn)?"""
+    if not (FUSE and PROLOGUE and dtype == torch.bfloat16 and len(x_shape) == 4):
+        return False
+    N, H, W, C = x_shape
+    K, R, S, Cw = w.shape
+    return (R, S) == (3, 3) and Cw == C and bool(lib.acfe_conv2d_bn_prologue_supported(N, H, W, C, K, 1))
+
+
+def _pending(t):
+    return getattr(t, "_acfe_bn_pending", None)
+
+
+def materialize(t: torch.Tensor) -> torch.Tensor:
+    """Write a pending BN output with acfe_bn_apply (no-op for other tensors)."""
+    p = _pending(t)
+    if p is None:
+        return t
+    x, scale, shift, relu = p
+    C = x.shape[-1]
+    call("acfe_bn_apply", ptr(x), dtype_code(x.dtype), x.numel() // C, C, ptr(scale), ptr(shift), int(relu), ptr(t),
+         dtype_code(t.dtype), stream())
+    t._acfe_bn_pending = None
+    return t
+
+
+def _prologue_args(xb):
+    """(BN input, scale, shift, relu) of the pending BN output xb, which the
+    kernel about to run fills; xb stops being pending."""
+    x, scale, shift, relu = _pending(xb)
+    assert x.is_contiguous() and x.data_ptr() % 16 == 0 and xb.data_ptr() % 16 == 0
+    xb._acfe_bn_pending = None
+    return x, scale, shift, relu
+
+
+def _conv_fwd_bn(xb, w, b, want_stats, drop):
+    """_conv_fwd of a pending BN output xb: acfe_conv2d_fwd_bn (3x3 "same" stride 1)."""
+    N, H, W, C = xb.shape
+    K = w.shape[0]
+    x, scale, shift, relu = _prologue_args(xb)
+    wp = pack_weights(w, xb.dtype, False)
+    y = _empty((N, H, W, K), xb.dtype, xb.device)
+    stats = _no_stats(xb.device)
+    if want_stats:
+        stats = _empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), F64, xb.device)
+    rate, seed = drop if drop is not None and drop[0] > 0.0 else (0.0, 0)
+    with _Timed(w, "fwd"):
+        call("acfe_conv2d_fwd_bn", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y),
+             ptr(stats) if want_stats else None, float(rate), int(seed), ptr(scale), ptr(shift), int(relu), ptr(xb),
+             dtype_code(xb.dtype), stream())
+    return y, stats
 
 
 def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None, params=None):
@@ -488,9 +558,9 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
 
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, link):
+    def forward(ctx, x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, link, defer):
         ctx.gb = (gamma, beta)
-        y, saved = _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype)
+        y, saved = _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, defer)
         ctx.save_for_backward(x, *saved)
         ctx.conf = (relu, training, link)
         ctx.mask_in = FUSE and getattr(x, "_acfe_relu_out", False)
@@ -507,12 +577,15 @@ class _BNFn(torch.autograd.Function):
                 raise RuntimeError("ResidualLink: the shortcut gradient was not delivered before this BN's backward")
         dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool,
                                     params=ctx.gb)
-        return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
 
 
-def batch_norm(x, gamma, beta, mmean, mvar, training, relu=False, stats=None, eps=1e-3, momentum=0.99, link=None):
+def batch_norm(x, gamma, beta, mmean, mvar, training, relu=False, stats=None, eps=1e-3, momentum=0.99, link=None,
+               defer=False):
+    """defer: return the output pending (see _bn_fwd) -- only for a consumer
+    that takes it through bn_prologue_ok's path or materialize()s it."""
     return _BNFn.apply(x, gamma, beta, stats, mmean, mvar, bool(training), bool(relu), float(eps),
-                       float(momentum), x.dtype, link)
+                       float(momentum), x.dtype, link, bool(defer))
 
 
 class _ConvDropBNFn(torch.autograd.Function):
@@ -524,11 +597,11 @@ class _ConvDropBNFn(torch.autograd.Function):
     def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
         ctx.bias = b
         ctx.gb = (gamma, beta)
-        stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum = conf
+        stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum, defer = conf
         drop = (rate, seed) if training and rate > 0.0 else None
         u, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, training, drop)
         y, saved = _bn_fwd(u, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
-                           u.dtype)
+                           u.dtype, defer)
         ctx.save_for_backward(x, w, u, *saved)
         ctx.conf = conf
         ctx.has_b = b is not None
@@ -538,7 +611,7 @@ class _ConvDropBNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, u, *saved = ctx.saved_tensors
-        stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum = ctx.conf
+        stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum, _ = ctx.conf
         g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop, params=ctx.gb)
         dx, dw, db = _conv_bwd(x, w, g, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                                ctx.has_b and ctx.needs_input_grad[2], bias=ctx.bias)
@@ -546,8 +619,9 @@ class _ConvDropBNFn(torch.autograd.Function):
 
 
 def conv_dropout_bn(x, w, b, gamma, beta, mmean, mvar, training, rate=0.0, seed=None, relu=True, stride=1,
-                    padding="same", eps=1e-3, momentum=0.99):
-    """BN(Dropout(Conv2D(x))) (+ReLU), Keras semantics of each layer."""
+                    padding="same", eps=1e-3, momentum=0.99, defer=False):
+    """BN(Dropout(Conv2D(x))) (+ReLU), Keras semantics of each layer; defer:
+    the BN output is returned pending (batch_norm)."""
     if not FUSE:
         u, _ = conv2d(x, w, b, stride, padding)
         u = dropout(u, rate, training, seed)
@@ -562,7 +636,7 @@ def conv_dropout_bn(x, w, b, gamma, beta, mmean, mvar, training, rate=0.0, seed=
     if training and rate > 0.0 and seed is None:
         seed = next_seed()
     conf = (stride, pt, pl, P, Q, float(rate), int(seed or 0), bool(training), bool(relu), float(eps),
-            float(momentum))
+            float(momentum), bool(defer))
     return _ConvDropBNFn.apply(x, w, b, gamma, beta, mmean, mvar, conf)
 
 
@@ -714,9 +788,18 @@ class _ConvAddFn(torch.autograd.Function):
         stats = _no_stats(x.device)
         if want_stats:
             stats = _empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), F64, x.device)
+        pro = _pending(x) is not None and bn_prologue_ok(x.shape, x.dtype, w)
+        if not pro:
+            materialize(x)
         with _Timed(w, "fwd"):
-            call("acfe_conv2d_fwd_add", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(sc), int(relu), ptr(z),
-                 ptr(stats) if want_stats else None, dtype_code(x.dtype), stream())
+            if pro:  # x is a pending BN output: convolve it through the prologue, which also writes it
+                xr, scale, shift, brelu = _prologue_args(x)
+                call("acfe_conv2d_fwd_add_bn", ptr(xr), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(sc), int(relu),
+                     ptr(z), ptr(stats) if want_stats else None, ptr(scale), ptr(shift), int(brelu), ptr(x),
+                     dtype_code(x.dtype), stream())
+            else:
+                call("acfe_conv2d_fwd_add", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(sc), int(relu),
+                     ptr(z), ptr(stats) if want_stats else None, dtype_code(x.dtype), stream())
         ctx.save_for_backward(x, w, z if relu else None)
         ctx.conf = (pt, pl, relu, b is not None, link)
         if relu:
@@ -978,7 +1061,8 @@ class _ConvPoolBNFn(torch.autograd.Function):
     def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
         ctx.bias = b
         ctx.gb = (gamma, beta)
-        pt, pl, rate, seed, training, relu, eps, momentum = conf
+        pt, pl, rate, seed, training, relu, eps, momentum, defer = conf
+        materialize(x)
         N, H, W, C = x.shape
         K = w.shape[0]
         dev = x.device
@@ -991,7 +1075,7 @@ class _ConvPoolBNFn(torch.autograd.Function):
         with _Timed(w, "fwd"):
             call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(u), ptr(amax),
                  float(r_), int(s_), ptr(stats), dtype_code(x.dtype), stream())
-        y, saved = _bn_fwd(u, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, u.dtype)
+        y, saved = _bn_fwd(u, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, u.dtype, defer)
         ctx.save_for_backward(x, w, u, amax, *saved)
         ctx.conf, ctx.drop, ctx.has_b = conf, drop, b is not None
         return y
@@ -999,7 +1083,7 @@ class _ConvPoolBNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, u, amax, *saved = ctx.saved_tensors
-        pt, pl, rate, seed, training, relu, eps, momentum = ctx.conf
+        pt, pl, rate, seed, training, relu, eps, momentum, _ = ctx.conf
         N, H, W, C = x.shape
         K = w.shape[0]
         dev, s = x.device, stream()
@@ -1036,7 +1120,7 @@ class _ConvPoolBNFn(torch.autograd.Function):
 
 
 def conv_maxpool_dropout_bn(x, w, b, stride, padding, kh, kw, gamma, beta, mmean, mvar, training, rate=0.0,
-                            seed=None, relu=True, eps=1e-3, momentum=0.99):
+                            seed=None, relu=True, eps=1e-3, momentum=0.99, defer=False):
     """BN(Dropout(MaxPool2D((kh, kw))(Conv2D(x)))) (+ReLU): one node with the
     pooling in the conv epilogue when the kernel covers the shape, else the
     conv followed by maxpool_dropout_bn."""
@@ -1048,7 +1132,8 @@ def conv_maxpool_dropout_bn(x, w, b, stride, padding, kh, kw, gamma, beta, mmean
     K, R, S, _ = w.shape
     _, pt = same_padding(x.shape[1], R, 1)
     _, pl = same_padding(x.shape[2], S, 1)
-    conf = (pt, pl, float(rate), int(seed or 0), bool(training), bool(relu), float(eps), float(momentum))
+    conf = (pt, pl, float(rate), int(seed or 0), bool(training), bool(relu), float(eps), float(momentum),
+            bool(defer))
     return _ConvPoolBNFn.apply(x, w, b, gamma, beta, mmean, mvar, conf)
 
 

@@ -48,6 +48,13 @@ struct ConvGeom {
   const uint16_t* res;  // k_conv3x3_rows PM 3: residual added in the epilogue (same layout as Y)
   int res_relu;         // PM 3: ReLU after the residual add
   int idx32;            // M * K < 2^32: output element (dropout) indices fit 32 bits
+  // k_conv3x3_rows PRO: BatchNormalization (+ReLU) of the input applied while
+  // staging it, x' = (ReLU)(x * pro_sc[c] + pro_sh[c]) (acfe_bn_apply's
+  // arithmetic); x' is also stored to pro_out (nullable) for the backward
+  const float* pro_sc;
+  const float* pro_sh;
+  int pro_relu;
+  uint16_t* pro_out;
 };
 
 // 64 bytes of zeros in global memory: im2col taps that fall into the padding
@@ -934,7 +941,7 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 // (amax) and their BN statistics; 2 = dgrad whose dY is the 2x2 max-pool
 // backward of X = the pooled gradient with argmax bytes amax (expanded while
 // staging, the full-resolution dY is never stored).
-template <int KB, int TR, int PM, bool XRES = false>
+template <int KB, int TR, int PM, bool XRES = false, bool PRO = false>
 __global__ void __launch_bounds__(512, 1)
 k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
                const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
@@ -955,6 +962,8 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   constexpr int XROWS = XRES ? TR + 2 : TR;
   constexpr int NBUF = XRES ? 1 : (TR <= 3 || KB == 64) ? 2 : 1;
   static_assert(!XRES || WDMA, "XRES needs the weight DMA");
+  // PRO: the BatchNormalization (+ReLU) prologue on the staged input (C <= 256)
+  static_assert(!PRO || (XRES && (PM == 0 || PM == 3 || PM == 4)), "prologue: chunk-resident forward");
   // pixels per row, halo row bytes: 160-B rows make the fragment reads
   // conflict-free under ds_read_b128's lane grouping at every tap shift (144-B
   // rows had 2-way conflicts: a third of the LDS cycles, rocprofv3 r02c); the
@@ -980,10 +989,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // partials in registers, reduced over the waves once at the end; K = 128 (at
   // the register limit) accumulates them with LDS double atomics per tile
   constexpr bool REGSTAT = KB == 64;
-  constexpr int SMEM = SMEM0 + (REGSTAT ? 0 : 2 * KB * 8);
+  constexpr int SMEMS = SMEM0 + (REGSTAT ? 0 : 2 * KB * 8);
+  constexpr int SMEM = SMEMS + (PRO ? 2 * 256 * 4 : 0);
   static_assert(SMEM <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   double* sstat = reinterpret_cast<double*>(smem + SMEM0);
+  float* pss = reinterpret_cast<float*>(smem + SMEMS);  // PRO: scale[256], shift[256]
   auto xbuf = [&](int b) __attribute__((always_inline)) { return smem + (WDMA ? b * XBYTES : b * BUFB); };
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -997,6 +1008,8 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   for (int k = 0; k < (REGSTAT ? NV16 : 1); ++k) dstat[k] = 0.0;
   if constexpr (!REGSTAT)
     for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
+  if constexpr (PRO)
+    for (int i = tid; i < g.C; i += 512) pss[i] = g.pro_sc[i], pss[256 + i] = g.pro_sh[i];
   // bias: lane l holds channel wk * KB/2 + (l mod KB/2), one VGPR across the
   // main loop (the K = 128 variants sit at the 256-VGPR limit; no LDS left for
   // a copy); each epilogue gathers its quads with ds_bpermute, once per
@@ -1048,11 +1061,13 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // wave-uniform tile origin (sh0, sw0)
   int xoffs[PM == 2 ? 1 : XPT];
   int sh0 = 0, sw0 = 0;       // PM 2: input row / column of halo pixel (0, 0) at filter row 0 (wave-uniform)
-  // mask bits per granule: filter rows 0..2 inside the image (XRES: row 0 only)
-  constexpr int MB = XRES ? 1 : 4;
+  // mask bits per granule: filter rows 0..2 inside the image (XRES: row 0
+  // only; PRO: + the granule is one of the tile's own pixels, stored to pro_out)
+  constexpr int MB = XRES ? (PRO ? 2 : 1) : 4;
   static_assert(MB * XPT <= 32, "granule mask bits");
   unsigned xm = 0;
   int stl = -1;  // walk index of the tile the offsets belong to
+  long long pimg = 0;  // PRO: byte offset of the staged tile's image
   __amdgpu_buffer_rsrc_t xrs, ars;
   const int CB = g.C * 2;  // bytes per pixel
   auto stage_tile = [&](int tl) __attribute__((always_inline)) {
@@ -1070,6 +1085,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     } else {
       const long long img = (long long)n * g.H * g.W * g.C;
       xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + img), (short)0, g.H * g.W * CB, 0x00020000);
+      pimg = img * 2;
     }
     xm = 0;
 #pragma unroll
@@ -1083,7 +1099,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       for (int r = 0; r < 3; ++r) m |= ((unsigned)(hin + r) < (unsigned)g.H ? 1u : 0u) << r;
       m = ok ? m : 0u;
       xoffs[i] = (hin * g.W + win) * CB + gr * 16;
-      xm |= (XRES ? m & 1u : m) << (MB * i);
+      unsigned mm = XRES ? m & 1u : m;
+      if constexpr (PRO) {
+        const bool own = xrow >= 1 && xrow <= TR && xpix >= 1 && xpix <= SEGW;
+        mm |= (own && (m & 1u)) ? 2u : 0u;
+      }
+      xm |= mm << (MB * i);
     }
   };
   auto gload = [&](int t) __attribute__((always_inline)) {
@@ -1144,6 +1165,40 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
         const int idx = tid + 512 * i;
         const int row = idx >> 3, gw = idx & 7;  // row = s * KB + k
         *reinterpret_cast<u32x4*>(Wl + row * 128 + ((gw ^ (row & 7)) << 4)) = rw[i];
+      }
+    }
+  };
+  // PRO: rx (chunk cc of the staged tile) -> (ReLU)(x * scale + shift) in
+  // bf16 (FMA, max, round to nearest even: acfe_bn_apply's values), zero for
+  // granules outside the image (the conv's padding is applied after the BN);
+  // the tile's own pixels also go to pro_out
+  auto xform = [&](int cc) __attribute__((always_inline)) {
+    if constexpr (PRO) {
+      typedef float f2v __attribute__((ext_vector_type(2)));
+      typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+      const f4* ps = reinterpret_cast<const f4*>(pss + cc * 64 + gr * 8);
+      const f4 sc0 = ps[0], sc1 = ps[1], sh0 = ps[64], sh1 = ps[65];
+      const float scv[8] = {sc0[0], sc0[1], sc0[2], sc0[3], sc1[0], sc1[1], sc1[2], sc1[3]};
+      const float shv[8] = {sh0[0], sh0[1], sh0[2], sh0[3], sh1[0], sh1[1], sh1[2], sh1[3]};
+      const bool relu = g.pro_relu != 0;
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        u32x4 v = rx[i];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          float lo = __builtin_fmaf(__uint_as_float(v[d] << 16), scv[2 * d], shv[2 * d]);
+          float hi = __builtin_fmaf(__uint_as_float(v[d] & 0xffff0000u), scv[2 * d + 1], shv[2 * d + 1]);
+          if (relu) {
+            lo = fmaxf(lo, 0.f);
+            hi = fmaxf(hi, 0.f);
+          }
+          const b2v pk = __builtin_convertvector((f2v){lo, hi}, b2v);
+          v[d] = __builtin_bit_cast(unsigned, pk);
+        }
+        const bool in = (xm >> (MB * i)) & 1u;
+        rx[i] = in ? v : u32x4{0u, 0u, 0u, 0u};
+        if (g.pro_out && ((xm >> (MB * i + 1)) & 1u))
+          *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(g.pro_out) + pimg + xoffs[i] + cc * 128) = v;
       }
     }
   };
@@ -1352,9 +1407,11 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     }
   };
 
+  if constexpr (PRO) __syncthreads();  // pss
   if (L > 0) {
     gload(0);
     if constexpr (WDMA) wdma(0, 0);
+    xform(0);
     sstore(0);
   }
   if constexpr (WDMA) wait_vmcnt<0>();
@@ -1363,11 +1420,23 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   for (int t = 0; t < L; ++t) {
     const bool more = t + 1 < L;
     // XRES: filter row of this step and whether the next one starts a chunk
+    // (XRES: the next chunk's rows are requested one step early, at rs == 1,
+    // and land by that step's closing wait; PRO transforms them during rs == 2)
     const int rs = XRES ? cst - 3 * (cst / 3) : 0;
     const bool xnext = more && (!XRES || rs == 2);
+    if constexpr (XRES) {
+      if (rs == 1 && t + 2 < L) gload(t + 2);
+    } else {
+      if (more) gload(t + 1);
+    }
     if (more) {
-      if (xnext) gload(t + 1);
       if constexpr (WDMA) wdma(t + 1, (t + 1) & 1);
+    }
+    if constexpr (PRO) {
+      if (xnext) {
+        const int st1 = (t + 1) % nsteps_t;
+        xform(st1 / 3);
+      }
     }
     if constexpr (RPRE) {
       if (cst + 1 == nsteps_t) rload(ctm);
@@ -2590,6 +2659,9 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.drop = make_drop(0.f, 0);
   g.res = nullptr;
   g.res_relu = 0;
+  g.pro_sc = g.pro_sh = nullptr;
+  g.pro_relu = 0;
+  g.pro_out = nullptr;
   g.idx32 = g.M * K < (1ll << 32) ? 1 : 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
@@ -3111,7 +3183,7 @@ static int rows64_tr() {  // output rows per tile of the K = 64 rows kernels (AC
   return v;
 }
 
-template <int KB, int PM, int TR, bool XR = false>
+template <int KB, int PM, int TR, bool XR = false, bool PR = false>
 static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                           double* stats, int srows, uint8_t* amax, hipStream_t s, const char* what) {
   const int tiles_h = (g.P + TR - 1) / TR, tiles_w = (g.Q + 63) / 64;
@@ -3120,7 +3192,7 @@ static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, cons
   if (gp > nt) gp = (int)nt;
   if (gp >= 64) gp &= ~7;
   if (stats && gp > srows) gp = srows;  // one statistics slab row per workgroup
-  hipLaunchKernelGGL((k_conv3x3_rows<KB, TR, PM, XR>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+  hipLaunchKernelGGL((k_conv3x3_rows<KB, TR, PM, XR, PR>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
   return launch_rc(what);
 }
@@ -3131,6 +3203,10 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
   // pooling (PM 1 / 2) needs row pairs: 6 rows (or 4 chunk-resident rows)
   if constexpr (KB == 128) {
     if (rows128_xres()) return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+  }
+  if constexpr (KB == 64 && (PM == 0 || PM == 3 || PM == 4)) {
+    // BatchNormalization prologue (acfe_conv2d_bn_prologue_supported): 6 chunk-resident rows
+    if (g.pro_sc) return launch_rows_tr<KB, PM, 6, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
   }
   if constexpr (KB == 64) {
     const int xr = rows64_xres();
@@ -3253,6 +3329,64 @@ ACFE_API int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, cons
                                "acfe_conv2d_fwd_add");
   return launch_rows<64, 3>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
                             "acfe_conv2d_fwd_add");
+}
+
+// ------------------------------------------------------------------ BatchNormalization (+ReLU) prologue
+// The pre-activation BN -> ReLU -> Conv2D 3x3 of wr_resnet_bird's blocks
+// (resnet/wr_resnet_bird.py:136-145 bn2a -> conv21, :152-161 bn2b -> conv2b)
+// as one pass: the conv reads the BN input x and stages x' = (ReLU)(x * scale
+// + shift) (acfe_bn_apply's values), so no separate apply pass reads x and
+// writes x'; x' is still written (x_bn_out, nullable) for the weight gradient,
+// from the staging registers of the tile's own pixels.  Shapes: K = 64, C % 64
+// == 0, C <= 256, 3x3 stride-1 "same" bf16 (the stage-1 layers).
+ACFE_API int acfe_conv2d_bn_prologue_supported(int N, int H, int W, int C, int K, int dtype) {
+  return acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, dtype) && K == 64 && C <= 256 &&
+         (long long)N * H * W * K < (1ll << 32);
+}
+
+static bool pro_args_ok(const float* sc, const float* sh, const void* xo) {
+  return sc && sh && ((uintptr_t)sc & 15) == 0 && ((uintptr_t)sh & 15) == 0 && ((uintptr_t)xo & 15) == 0;
+}
+
+ACFE_API int acfe_conv2d_fwd_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                                int pad_left, const float* bias, void* y, double* stats_partial, float drop_rate,
+                                unsigned long long seed, const float* bn_scale, const float* bn_shift, int bn_relu,
+                                void* x_bn_out, int dtype, void* stream) {
+  if (!x || !wpacked || !y || !acfe_conv2d_bn_prologue_supported(N, H, W, C, K, dtype) ||
+      !pro_args_ok(bn_scale, bn_shift, x_bn_out) || ((uintptr_t)x & 15) || drop_rate < 0.f || drop_rate >= 1.f)
+    return ACFE_E_INVAL;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
+  g.drop = make_drop(drop_rate, seed);
+  g.pro_sc = bn_scale;
+  g.pro_sh = bn_shift;
+  g.pro_relu = bn_relu ? 1 : 0;
+  g.pro_out = (uint16_t*)x_bn_out;
+  const int srows = grid_m_for(g.M, 1);
+  if (g.drop.on)
+    return launch_rows<64, 4>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
+                              "acfe_conv2d_fwd_bn");
+  return launch_rows<64, 0>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
+                            "acfe_conv2d_fwd_bn");
+}
+
+ACFE_API int acfe_conv2d_fwd_add_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K,
+                                    int pad_top, int pad_left, const float* bias, const void* res, int relu, void* y,
+                                    double* stats_partial, const float* bn_scale, const float* bn_shift, int bn_relu,
+                                    void* x_bn_out, int dtype, void* stream) {
+  if (!x || !wpacked || !y || !res || !acfe_conv2d_bn_prologue_supported(N, H, W, C, K, dtype) ||
+      !pro_args_ok(bn_scale, bn_shift, x_bn_out) || ((uintptr_t)x & 15) || ((uintptr_t)y & 7) ||
+      ((uintptr_t)res & 7))
+    return ACFE_E_INVAL;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
+  g.res = (const uint16_t*)res;
+  g.res_relu = relu ? 1 : 0;
+  g.pro_sc = bn_scale;
+  g.pro_sh = bn_shift;
+  g.pro_relu = bn_relu ? 1 : 0;
+  g.pro_out = (uint16_t*)x_bn_out;
+  const int srows = grid_m_for(g.M, 1);
+  return launch_rows<64, 3>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
+                            "acfe_conv2d_fwd_add_bn");
 }
 
 // ------------------------------------------------------------------ stem (C = 1)

@@ -42,8 +42,11 @@ class BasicBlock(nn.Module):
         through autograd's accumulation; the gradient-tensor tags the fused
         nodes rely on are version-checked (ops._tag)."""
         link = ops.ResidualLink.make() if self.shortcut is None else None
-        y = self.bn2a(x, relu=True, stats=x_stats, link=link)
-        y = conv_dropout_bn(self.conv2a, self.bn2b, y, self.dropout)
+        # BN outputs come back pending: the 3x3 convs apply them in their input
+        # staging where ops.bn_prologue_ok covers the shape
+        defer = ops.FUSE and ops.PROLOGUE
+        y = self.bn2a(x, relu=True, stats=x_stats, link=link, defer=defer)
+        y = conv_dropout_bn(self.conv2a, self.bn2b, y, self.dropout, defer=defer)
         sc = x if self.shortcut is None else self.shortcut(x)
         want = self.training and ops.FUSE
         z, st = ops.conv_add(y, self.conv2b.weight, self.conv2b.bias, sc, relu=True, want_stats=want, link=link,

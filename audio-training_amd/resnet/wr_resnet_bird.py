@@ -57,14 +57,18 @@ class BasicBlock(nn.Module):
         # identity shortcut: the Add's gradient for x, conv shortcut: the pooled
         # gradient of its AveragePooling2D, both summed inside the BN reading x
         link = ops.ResidualLink.make()
+        # BN -> ReLU -> 3x3 conv: the BN output comes back pending and the conv
+        # applies it in its input staging (ops.bn_prologue_ok shapes; other
+        # consumers write it with the apply pass first)
+        defer = ops.FUSE and ops.PROLOGUE
         y = x
         if self.stride > 1:
             y = self.bn2a0(y, relu=True, stats=x_stats, link=link)
             y = conv_bn(self.conv2a0, self.bn2a, y, relu=True)
-            y = conv_maxpool_dropout_bn(self.conv21, y, self.stride, self.bn2b, self.dropout)
+            y = conv_maxpool_dropout_bn(self.conv21, y, self.stride, self.bn2b, self.dropout, defer=defer)
         else:
-            y = self.bn2a(y, relu=True, stats=x_stats, link=link)
-            y = conv_dropout_bn(self.conv21, self.bn2b, y, self.dropout)
+            y = self.bn2a(y, relu=True, stats=x_stats, link=link, defer=defer)
+            y = conv_dropout_bn(self.conv21, self.bn2b, y, self.dropout, defer=defer)
         # the shortcut is built after the residual branch (its backward then runs
         # first, delivering the linked gradient before the BN reading x needs it)
         sc = x

@@ -281,6 +281,28 @@ int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, const void* w
                         int pad_left, const float* bias, const void* res, int relu, void* y, double* stats_partial,
                         int dtype, void* stream);
 
+/* BatchNormalization (+ReLU) prologue of the pre-activation blocks
+ * (resnet/wr_resnet_bird.py:136-145 bn2a -> ReLU -> res{s}{b}_branch21,
+ * :152-161 bn2b -> ReLU -> branch2b; the SURVEY §8b conv ABI's `bn_scale_shift`
+ * argument): the conv reads the BN INPUT x and convolves x' = (ReLU)(x *
+ * bn_scale[c] + bn_shift[c]) (acfe_bn_apply's values; zero padding applies to
+ * x'), replacing acfe_bn_apply + the conv.  x' is written to x_bn_out
+ * (nullable, [N][H][W][C] bf16) for the weight gradient.  bn_scale / bn_shift:
+ * fp32 [C] from acfe_bn_finalize, 16-B aligned.  Shapes:
+ * acfe_conv2d_bn_prologue_supported (3x3 stride-1 "same" bf16, C % 64 == 0,
+ * C <= 256, K = 64).  acfe_conv2d_fwd_bn = acfe_conv2d_fwd_dropout (drop_rate
+ * 0: none) with the prologue, acfe_conv2d_fwd_add_bn = acfe_conv2d_fwd_add
+ * with the prologue. */
+int acfe_conv2d_bn_prologue_supported(int N, int H, int W, int C, int K, int dtype);
+int acfe_conv2d_fwd_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                       int pad_left, const float* bias, void* y, double* stats_partial, float drop_rate,
+                       unsigned long long seed, const float* bn_scale, const float* bn_shift, int bn_relu,
+                       void* x_bn_out, int dtype, void* stream);
+int acfe_conv2d_fwd_add_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                           int pad_left, const float* bias, const void* res, int relu, void* y, double* stats_partial,
+                           const float* bn_scale, const float* bn_shift, int bn_relu, void* x_bn_out, int dtype,
+                           void* stream);
+
 /* Conv2D(1x1, 16 -> K in {64, 128}, bias) -> BatchNormalization -> (ReLU) as one
  * node whose conv output A = W x + b is never stored (csrc/c1bn.hip;
  * res{s}b0_branch2a0 + bn{s}b0_branch2a of resnet/wr_resnet_bird.py:121-131).

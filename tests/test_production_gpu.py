@@ -26,6 +26,8 @@ The oracle is torch-CPU float64 convolution of the same bf16 operands
   * BN statistics slabs: the float64 sums of the stored output to rel 1e-6
     (the epilogue sums each wave's 16-row fragment in fp32 first).
 """
+import itertools
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -410,3 +412,96 @@ def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
     d = dw.cpu().to(F64)
     assert ((d - dw_exact).norm() / dw_exact.norm()).item() < 5e-5
     assert ((d - dw_exact).abs().max() / dw_exact.abs().max()).item() < 5e-4
+
+
+def _bn_affine(C, seed, device):
+    """scale / shift of a trained-looking BN (mixed signs so the ReLU cuts)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    sc = (torch.rand(C, generator=g) * 1.5 + 0.25) * torch.where(torch.rand(C, generator=g) < 0.1, -1.0, 1.0)
+    sh = torch.randn(C, generator=g) * 0.5
+    return sc.to(device), sh.to(device)
+
+
+@pytest.mark.parametrize("N,H,W,C,mode", [(8, 64, 128, 64, "drop"), (8, 64, 128, 128, "add"),
+                                          (4, 64, 128, 64, "plain"), (3, 14, 100, 64, "add"),
+                                          (2, 9, 70, 128, "drop")])
+def test_conv_bn_prologue(env, cuda, N, H, W, C, mode):
+    """acfe_conv2d_fwd_bn / acfe_conv2d_fwd_add_bn (BatchNormalization + ReLU
+    applied while staging the conv input, resnet/wr_resnet_bird.py:136-161)
+    against the unfused chain acfe_bn_apply -> acfe_conv2d_fwd_dropout /
+    acfe_conv2d_fwd_add: the conv output, its BN statistics and the written BN
+    output x' all bit-identical; x' also against the float64 BN of x within one
+    bf16 ulp.  Shapes: the stage-1 layers (K = 64, C = 64 / 128) at production
+    tile counts, plus partial 6-row / 64-column tiles."""
+    ops, call, lib, ptr, stream = env
+    K = 64
+    assert lib.acfe_conv2d_bn_prologue_supported(N, H, W, C, K, 1)
+    x, w, b, g = _data(N, H, W, C, K, 131 + C + H, cuda)
+    sc, sh = _bn_affine(C, 7 + C, cuda)
+    wp = ops.pack_weights(w, BF, False)
+    rows = lib.acfe_conv2d_stats_rows(N * H * W, K)
+    res = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+
+    def run(fused):
+        xb = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+        y = torch.empty((N, H, W, K), dtype=BF, device=cuda)
+        st = torch.empty((rows, 2, wp.shape[0]), dtype=F64, device=cuda)
+        if not fused:
+            call("acfe_bn_apply", ptr(x), 1, N * H * W, C, ptr(sc), ptr(sh), 1, ptr(xb), 1, stream())
+        if mode == "add":
+            if fused:
+                call("acfe_conv2d_fwd_add_bn", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(res), 1, ptr(y),
+                     ptr(st), ptr(sc), ptr(sh), 1, ptr(xb), 1, stream())
+            else:
+                call("acfe_conv2d_fwd_add", ptr(xb), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(res), 1, ptr(y),
+                     ptr(st), 1, stream())
+        else:
+            rate = 0.1 if mode == "drop" else 0.0
+            if fused:
+                call("acfe_conv2d_fwd_bn", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y), ptr(st), rate, 77,
+                     ptr(sc), ptr(sh), 1, ptr(xb), 1, stream())
+            else:
+                call("acfe_conv2d_fwd_dropout", ptr(xb), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b),
+                     ptr(y), 1, ptr(st), rate, 77, stream())
+        torch.cuda.synchronize()
+        return xb, y, st
+
+    xb0, y0, st0 = run(False)
+    xb1, y1, st1 = run(True)
+    assert torch.equal(xb1.view(torch.int16), xb0.view(torch.int16)), "BN output"
+    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16)), "conv output"
+    assert torch.equal(st1[:, :, :K], st0[:, :, :K]), "BN statistics"
+    exact = (x.cpu().to(F64) * sc.cpu().to(F64) + sh.cpu().to(F64)).clamp_min(0)
+    _within_ulp(xb1, exact, atol=1e-6, what="x'")
+
+
+def test_model_bn_prologue_matches_unfused(env, cuda):
+    """A wr_resnet_bird training step with the BN prologue (the stage-1 BN ->
+    ReLU -> conv pairs on acfe_conv2d_fwd_bn / fwd_add_bn) against the same
+    step with every BN output written by its apply pass (ops.PROLOGUE off):
+    identical loss, logits and gradients."""
+    ops = env[0]
+    from acfe.train import FrontEnd, Trainer
+    from resnet.wr_resnet_bird import WRResNet
+    import bench
+
+    B = 4
+    outs = []
+    for pro in (False, True):
+        ops.PROLOGUE = pro
+        try:
+            torch.manual_seed(0)
+            model = WRResNet(input_shape=(128, 513, 3), classes=10, dtype=BF).to(cuda)
+            fe = FrontEnd(n_mels=128, dtype=BF, device=cuda).to(cuda)
+            tr = Trainer(model, fe, lr=0.01, loss="cce", device=cuda)
+            x1, x2, lam, y = bench.make_batches(B, 10, cuda, n_sets=1)[0]
+            ops._seed_counter = itertools.count()  # same dropout seeds in both runs
+            loss, z = tr.step(x1, y, x2, lam)
+            torch.cuda.synchronize()
+            outs.append((loss.detach().clone(), tr.arena.grad.detach().clone(), tr.arena.flat.detach().clone()))
+        finally:
+            ops.PROLOGUE = True
+    (l0, g0, p0), (l1, g1, p1) = outs
+    assert torch.equal(l0, l1)
+    assert torch.equal(g0, g1)
+    assert torch.equal(p0, p1)
