@@ -72,12 +72,17 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_fwd_add": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, I32, P, P, I32, P],
     "acfe_conv2d_bn_prologue_supported": [I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_fwd_bn": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, P, F32, C.c_uint64, P, P, I32, P, I32, P],
+    "acfe_conv2d_fwd_pool_bn": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, P, F32, C.c_uint64, P, P, P, I32, P,
+                                I32, P],
     "acfe_conv2d_fwd_add_bn": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, I32, P, P, P, P, I32, P, I32, P],
     "acfe_c1bn_supported": [I32, I32],
     "acfe_c1bn_workspace": [I64, I32, I32],
     "acfe_c1bn_stats": [P, I64, I32, P, I32, P, P, P, P, P],
     "acfe_c1bn_apply": [P, I64, I32, P, I32, P, P, P, I32, P, P],
     "acfe_c1bn_bwd": [P, P, I64, I32, P, I32, P, P, P, P, P, I32, F64, P, P, P, P, P, P, P, P],
+    "acfe_c1bn_stats_bn": [P, I64, I32, P, I32, P, P, P, P, P, P, I32, P],
+    "acfe_c1bn_apply_bn": [P, I64, I32, P, I32, P, P, P, I32, P, P, P, I32, P],
+    "acfe_c1bn_bwd_bn": [P, P, I64, I32, P, I32, P, P, P, P, P, I32, F64, P, P, P, P, P, P, P, P, P, I32, P],
     "acfe_channel_sum": [P, I64, I32, I32, P, P, F32, P],
     "acfe_add": [P, P, I64, I32, P, I32, P],
     "acfe_add_stats": [P, P, I64, I32, I32, P, I32, P, P],

@@ -86,11 +86,12 @@ def conv_dropout_bn(conv: Conv2D, bn: BatchNormalization, x, rate, relu=True, de
                                eps=bn.eps, momentum=bn.momentum, defer=defer)
 
 
-def conv_bn(conv: Conv2D, bn: BatchNormalization, x, relu=True):
+def conv_bn(conv: Conv2D, bn: BatchNormalization, x, relu=True, defer=False):
     """bn(conv(x)) (+ReLU) as one node (ops.conv_bn: the recomputing 1x1 node
     when the conv has 16 input channels)."""
     return ops.conv_bn(x, conv.weight, conv.bias, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance, bn.training,
-                       relu=relu, stride=conv.strides, padding=conv.padding, eps=bn.eps, momentum=bn.momentum)
+                       relu=relu, stride=conv.strides, padding=conv.padding, eps=bn.eps, momentum=bn.momentum,
+                       defer=defer)
 
 
 def maxpool_dropout_bn(x, kh, kw, bn: BatchNormalization, rate, relu=True):

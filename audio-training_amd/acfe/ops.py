@@ -27,6 +27,11 @@ UNPOOL = os.environ.get("ACFE_UNPOOL", "1") != "0"
 # ACFE_BN_PROLOGUE=0: every BatchNormalization writes its output in its own
 # apply pass instead of handing it to the consuming conv's input staging.
 PROLOGUE = os.environ.get("ACFE_BN_PROLOGUE", "1") != "0"
+# per-consumer switches of the prologue (A/B): the pooled 3x3 conv; the 1x1 + BN
+# node (off by default: its four streaming passes each redo the BN of x, which
+# measured 1 % slower per T1 step than the one apply pass it saves, r02ab)
+PRO_POOL = os.environ.get("ACFE_BN_PROLOGUE_POOL", "1") != "0"
+PRO_C1 = os.environ.get("ACFE_BN_PROLOGUE_C1", "0") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -650,7 +655,9 @@ def _c1bn_ok(x, w, stride) -> bool:
 class _C1BNFn(torch.autograd.Function):
     """BatchNormalization(+ReLU) of a 1x1 Conv2D with 16 input channels as one
     node (csrc/c1bn.hip): the conv output is never stored; its statistics come
-    from the 16x16 Gram matrix of x, the backward's sums from g^T x."""
+    from the 16x16 Gram matrix of x, the backward's sums from g^T x.  A pending
+    BN output x (the block's bn2a0) is never written: every pass reads the BN
+    input and applies the BN (+ReLU) itself (acfe_c1bn_*_bn)."""
 
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
@@ -661,11 +668,22 @@ class _C1BNFn(torch.autograd.Function):
         K = w.shape[0]
         M = N * H * W
         dev, s = x.device, stream()
+        pend = _pending(x)
+        if pend is not None and not (PRO_C1 and pend[0].is_contiguous() and pend[0].data_ptr() % 16 == 0
+                                     and pend[0].shape == x.shape):
+            materialize(x)
+            pend = None
+        # (x stays pending: a later reader would materialize it)
+        xr, xsc, xsh, xrelu = pend if pend is not None else (x, None, None, False)
         scale, shift, mean, invstd = (_empty((K,), F32, dev) for _ in range(4))
         ws = _empty((lib.acfe_c1bn_workspace(M, C, K),), F32, dev)
         gram = _empty((272,), F32, dev)
         part = _empty((1, 2, K), F64, dev)
-        call("acfe_c1bn_stats", ptr(x), M, C, ptr(w), K, ptr(b), ptr(part), ptr(gram), ptr(ws), s)
+        if pend is not None:
+            call("acfe_c1bn_stats_bn", ptr(xr), M, C, ptr(w), K, ptr(b), ptr(part), ptr(gram), ptr(ws), ptr(xsc),
+                 ptr(xsh), int(xrelu), s)
+        else:
+            call("acfe_c1bn_stats", ptr(x), M, C, ptr(w), K, ptr(b), ptr(part), ptr(gram), ptr(ws), s)
         if training:
             call("acfe_bn_finalize", ptr(part), 1, K, K, float(M), ptr(gamma), ptr(beta), eps, momentum,
                  ptr(mmean), ptr(mvar), 1, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
@@ -673,14 +691,20 @@ class _C1BNFn(torch.autograd.Function):
             call("acfe_bn_finalize", None, 0, K, K, 0.0, ptr(gamma), ptr(beta), eps, momentum, ptr(mmean),
                  ptr(mvar), 0, ptr(scale), ptr(shift), ptr(mean), ptr(invstd), s)
         y = _empty((N, H, W, K), x.dtype, dev)
-        call("acfe_c1bn_apply", ptr(x), M, C, ptr(w), K, ptr(b), ptr(scale), ptr(shift), int(relu), ptr(y), s)
-        ctx.save_for_backward(x, w, b, scale, shift, mean, invstd, gram)
+        if pend is not None:
+            call("acfe_c1bn_apply_bn", ptr(xr), M, C, ptr(w), K, ptr(b), ptr(scale), ptr(shift), int(relu), ptr(y),
+                 ptr(xsc), ptr(xsh), int(xrelu), s)
+            ctx.save_for_backward(xr, w, b, scale, shift, mean, invstd, gram, xsc, xsh)
+        else:
+            call("acfe_c1bn_apply", ptr(x), M, C, ptr(w), K, ptr(b), ptr(scale), ptr(shift), int(relu), ptr(y), s)
+            ctx.save_for_backward(x, w, b, scale, shift, mean, invstd, gram, None, None)
         ctx.conf = conf
+        ctx.xrelu = bool(xrelu)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, b, scale, shift, mean, invstd, gram = ctx.saved_tensors
+        x, w, b, scale, shift, mean, invstd, gram, xsc, xsh = ctx.saved_tensors
         training, relu, eps, momentum = ctx.conf
         N, H, W, C = x.shape
         K = w.shape[0]
@@ -693,23 +717,28 @@ class _C1BNFn(torch.autograd.Function):
         dgamma, dbeta = _empty((K,), F32, dev), _empty((K,), F32, dev)
         ws = _empty((lib.acfe_c1bn_workspace(M, C, K),), F32, dev)
         # eval mode: statistics are constants -> count -> inf removes the mean terms
-        call("acfe_c1bn_bwd", ptr(dy), ptr(x), M, C, ptr(w), K, ptr(b), ptr(scale), ptr(shift), ptr(mean),
-             ptr(invstd), int(relu), float(M) if training else 1e300, ptr(gram), ptr(dx), ptr(dw), ptr(db),
-             ptr(dgamma), ptr(dbeta), ptr(ws), stream())
+        args = (ptr(dy), ptr(x), M, C, ptr(w), K, ptr(b), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), int(relu),
+                float(M) if training else 1e300, ptr(gram), ptr(dx), ptr(dw), ptr(db), ptr(dgamma), ptr(dbeta),
+                ptr(ws))
+        if xsc is not None:  # x is the BN input of the prologue; dx is the gradient for its output
+            call("acfe_c1bn_bwd_bn", *args, ptr(xsc), ptr(xsh), int(ctx.xrelu), stream())
+        else:
+            call("acfe_c1bn_bwd", *args, stream())
         return dx, dw, db, dgamma, dbeta, None, None, None
 
 
 def conv_bn(x, w, b, gamma, beta, mmean, mvar, training, relu=True, stride=1, padding="same", eps=1e-3,
-            momentum=0.99):
+            momentum=0.99, defer=False):
     """BatchNormalization(Conv2D(x)) (+ReLU), Keras semantics of each layer.  A
     bf16 1x1 conv with 16 input channels runs as the recomputing node _C1BNFn;
-    anything else as the two layers (conv epilogue statistics -> BN)."""
+    anything else as the two layers (conv epilogue statistics -> BN; defer:
+    the BN output is returned pending, batch_norm)."""
     if _c1bn_ok(x, w, stride):
         return _C1BNFn.apply(x, w, b, gamma, beta, mmean, mvar,
                              (bool(training), bool(relu), float(eps), float(momentum)))
     u, st = conv2d(x, w, b, stride, padding, want_stats=bool(training))
     return batch_norm(u, gamma, beta, mmean, mvar, training, relu=relu, stats=st if training else None, eps=eps,
-                      momentum=momentum)
+                      momentum=momentum, defer=defer)
 
 
 # ------------------------------------------------------------------ elementwise / pooling
@@ -1062,7 +1091,9 @@ class _ConvPoolBNFn(torch.autograd.Function):
         ctx.bias = b
         ctx.gb = (gamma, beta)
         pt, pl, rate, seed, training, relu, eps, momentum, defer = conf
-        materialize(x)
+        pro = PRO_POOL and _pending(x) is not None and bn_prologue_ok(x.shape, x.dtype, w)
+        if not pro:
+            materialize(x)
         N, H, W, C = x.shape
         K = w.shape[0]
         dev = x.device
@@ -1073,8 +1104,14 @@ class _ConvPoolBNFn(torch.autograd.Function):
         stats = _empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), F64, dev) if training else None
         r_, s_ = drop if drop is not None else (0.0, 0)
         with _Timed(w, "fwd"):
-            call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(u), ptr(amax),
-                 float(r_), int(s_), ptr(stats), dtype_code(x.dtype), stream())
+            if pro:  # x is a pending BN output: the conv applies it while staging and writes it
+                xr, scale, shift, brelu = _prologue_args(x)
+                call("acfe_conv2d_fwd_pool_bn", ptr(xr), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(u), ptr(amax),
+                     float(r_), int(s_), ptr(stats), ptr(scale), ptr(shift), int(brelu), ptr(x), dtype_code(x.dtype),
+                     stream())
+            else:
+                call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(u), ptr(amax),
+                     float(r_), int(s_), ptr(stats), dtype_code(x.dtype), stream())
         y, saved = _bn_fwd(u, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, u.dtype, defer)
         ctx.save_for_backward(x, w, u, amax, *saved)
         ctx.conf, ctx.drop, ctx.has_b = conf, drop, b is not None

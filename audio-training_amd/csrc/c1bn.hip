@@ -81,9 +81,48 @@ __device__ __forceinline__ void load_wa(const float* __restrict__ w, int l16, in
   }
 }
 
-__device__ __forceinline__ uint4 load_x(const uint16_t* __restrict__ X, long long px, long long M, int q) {
+// Optional BatchNormalization (+ReLU) prologue on x (the block's bn2a0 ->
+// ReLU in front of the 1x1 conv, resnet/wr_resnet_bird.py:121-127): every
+// pass reads the BN input and forms x' = (ReLU)(x * scale + shift) of its
+// lane's 8 channels (acfe_bn_apply's arithmetic), so x' is never stored.
+struct XPro {
+  float sc[8], sh[8];
+  bool on;
+  bool relu;
+};
+__device__ __forceinline__ XPro make_xpro(const float* __restrict__ xsc, const float* __restrict__ xsh, int xrelu,
+                                          int q) {
+  XPro p;
+  p.on = xsc != nullptr;
+  p.relu = xrelu != 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    p.sc[j] = p.on && q < 2 ? xsc[q * 8 + j] : 0.f;
+    p.sh[j] = p.on && q < 2 ? xsh[q * 8 + j] : 0.f;
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint4 load_x(const uint16_t* __restrict__ X, long long px, long long M, int q,
+                                        const XPro& pro) {
   const uint16_t* zp = reinterpret_cast<const uint16_t*>(c1_zero);
-  return *reinterpret_cast<const uint4*>((px < M && q < 2) ? X + px * CIN + q * 8 : zp);
+  const bool in = px < M && q < 2;
+  uint4 v = *reinterpret_cast<const uint4*>(in ? X + px * CIN + q * 8 : zp);
+  if (pro.on) {
+    unsigned d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float lo = __builtin_fmaf(__uint_as_float(d[i] << 16), pro.sc[2 * i], pro.sh[2 * i]);
+      float hi = __builtin_fmaf(__uint_as_float(d[i] & 0xffff0000u), pro.sc[2 * i + 1], pro.sh[2 * i + 1]);
+      if (pro.relu) {
+        lo = fmaxf(lo, 0.f);
+        hi = fmaxf(hi, 0.f);
+      }
+      d[i] = in ? pack2(lo, hi) : 0u;
+    }
+    v = uint4{d[0], d[1], d[2], d[3]};
+  }
+  return v;
 }
 
 __device__ __forceinline__ bf8 tr8(const uint16_t* t, int ld, int col, int lane) {
@@ -110,19 +149,21 @@ __device__ __forceinline__ void x_tile_consts(uint16_t* tX, int l16, int q) {
 // Per block: S = sum x x^T and s = sum x over its pixels -> slab[blk][NGRAM]
 // (S[c][c'] at c*16 + c', s[c] at 256 + c).
 __global__ void __launch_bounds__(256) k_c1bn_gram(const uint16_t* __restrict__ X, long long M,
-                                                   float* __restrict__ slab) {
+                                                   float* __restrict__ slab, const float* __restrict__ xsc,
+                                                   const float* __restrict__ xsh, int xrelu) {
   __shared__ __attribute__((aligned(16))) uint16_t tiles[4][32 * LDX];
   __shared__ float red[4][NGRAM];
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
   uint16_t* tX = tiles[wid];
   x_tile_consts(tX, l16, q);
+  const XPro pro = make_xpro(xsc, xsh, xrelu, q);
   f4 a0 = f4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
   const long long nblk = (M + 15) / 16;
   const long long wstride = (long long)gridDim.x * 4 * UNR;
   for (long long b0 = ((long long)blockIdx.x * 4 + wid) * UNR; b0 < nblk; b0 += wstride) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const uint4 xb = load_x(X, (b0 + u) * 16 + l16, M, q);
+      const uint4 xb = load_x(X, (b0 + u) * 16 + l16, M, q, pro);
       if (q < 2) *reinterpret_cast<uint4*>(tX + (u * 16 + l16) * LDX + q * 8) = xb;
     }
     const bf8 xt = tr8(tX, LDX, 0, lane), ones = tr8(tX, LDX, 16, lane);
@@ -173,13 +214,15 @@ __global__ void __launch_bounds__(128) k_c1bn_gram_fin(const float* __restrict__
 template <int NKB>
 __global__ void __launch_bounds__(256)
 k_c1bn_apply(const uint16_t* __restrict__ X, const float* __restrict__ w, const float* __restrict__ bias, long long M,
-             int relu, const float* __restrict__ scale, const float* __restrict__ shift, uint16_t* __restrict__ Y) {
+             int relu, const float* __restrict__ scale, const float* __restrict__ shift, uint16_t* __restrict__ Y,
+             const float* __restrict__ xsc, const float* __restrict__ xsh, int xrelu) {
   constexpr int K = NKB * 16, TROW = K * 2 + 16;
   constexpr int LPR = K / 8, RPI = 64 / LPR;  // lanes per 16-B pixel row, rows per store instruction
   __shared__ __attribute__((aligned(16))) unsigned char stile[4 * 16 * TROW];
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
   uint4 wa[NKB];
   load_wa<NKB>(w, l16, q, wa);
+  const XPro pro = make_xpro(xsc, xsh, xrelu, q);
   float psc[NKB * 4], psh[NKB * 4];
 #pragma unroll
   for (int kb = 0; kb < NKB; ++kb)
@@ -195,7 +238,7 @@ k_c1bn_apply(const uint16_t* __restrict__ X, const float* __restrict__ w, const 
   for (long long b0 = ((long long)blockIdx.x * 4 + wid) * UNR; b0 < nblk; b0 += wstride) {
     uint4 xb[UNR];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) xb[u] = load_x(X, (b0 + u) * 16 + l16, M, q);
+    for (int u = 0; u < UNR; ++u) xb[u] = load_x(X, (b0 + u) * 16 + l16, M, q, pro);
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
 #pragma unroll
@@ -232,7 +275,8 @@ template <int NKB>
 __global__ void __launch_bounds__(256)
 k_c1bn_bsum(const uint16_t* __restrict__ X, const float* __restrict__ w, const float* __restrict__ bias, long long M,
             int relu, const uint16_t* __restrict__ dY, const float* __restrict__ scale,
-            const float* __restrict__ shift, float* __restrict__ slab) {
+            const float* __restrict__ shift, float* __restrict__ slab, const float* __restrict__ xsc,
+            const float* __restrict__ xsh, int xrelu) {
   constexpr int K = NKB * 16, LDB = K + 16, NOUT = K * 17;
   constexpr int TB = 32 * LDB, TXE = 32 * LDX, WE = TB + TXE;  // elements per wave
   constexpr int GPL = 32 * K / 8 / 64;                          // 16-B dB granules per lane per chunk
@@ -244,6 +288,7 @@ k_c1bn_bsum(const uint16_t* __restrict__ X, const float* __restrict__ w, const f
   x_tile_consts(tX, l16, q);
   uint4 wa[NKB];
   load_wa<NKB>(w, l16, q, wa);
+  const XPro pro = make_xpro(xsc, xsh, xrelu, q);
   float psc[NKB], psh[NKB];
 #pragma unroll
   for (int kb = 0; kb < NKB; ++kb) {
@@ -261,7 +306,7 @@ k_c1bn_bsum(const uint16_t* __restrict__ X, const float* __restrict__ w, const f
     const long long px0 = b0 * 16;
     uint4 xb[UNR], db[GPL];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) xb[u] = load_x(X, px0 + u * 16 + l16, M, q);
+    for (int u = 0; u < UNR; ++u) xb[u] = load_x(X, px0 + u * 16 + l16, M, q, pro);
 #pragma unroll
     for (int t = 0; t < GPL; ++t) {
       const int i = lane + 64 * t, row = i / (K / 8), cg = i - row * (K / 8);
@@ -373,11 +418,13 @@ template <int NKB>
 __global__ void __launch_bounds__(256)
 k_c1bn_dx(const uint16_t* __restrict__ X, const float* __restrict__ w, const float* __restrict__ bias, long long M,
           int relu, const uint16_t* __restrict__ dY, const float* __restrict__ scale, const float* __restrict__ shift,
-          const float* __restrict__ dxp, uint16_t* __restrict__ dX) {
+          const float* __restrict__ dxp, uint16_t* __restrict__ dX, const float* __restrict__ xsc,
+          const float* __restrict__ xsh, int xrelu) {
   constexpr int K = NKB * 16, NKS = NKB / 2;
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
   uint4 wa[NKB], wt[NKS], m2 = {0u, 0u, 0u, 0u};
   load_wa<NKB>(w, l16, q, wa);
+  const XPro pro = make_xpro(xsc, xsh, xrelu, q);
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
     float v[8];
@@ -410,7 +457,7 @@ k_c1bn_dx(const uint16_t* __restrict__ X, const float* __restrict__ w, const flo
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const long long px = (b0 + u) * 16 + l16;
-      xb[u] = load_x(X, px, M, q);
+      xb[u] = load_x(X, px, M, q, pro);
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb)
         gy[u][kb] = *reinterpret_cast<const uint2*>(px < M ? dY + px * K + kb * 16 + q * 4 : zp);
@@ -491,35 +538,39 @@ ACFE_API long long acfe_c1bn_workspace(long long M, int C, int K) {
   return fwd > bwd ? fwd : bwd;
 }
 
-ACFE_API int acfe_c1bn_stats(const void* x, long long M, int C, const float* w, int K, const float* bias,
-                             double* part, float* gram, float* workspace, void* stream) {
+static int c1bn_stats_impl(const void* x, long long M, int C, const float* w, int K, const float* bias,
+                           double* part, float* gram, float* workspace, const float* xsc, const float* xsh, int xrelu,
+                           void* stream) {
   if (!shape_ok(M, C, K, x) || !w || !part || !gram || !workspace) return ACFE_E_INVAL;
   const int grid = c1_grid(M, GRAM_GRID);
-  hipLaunchKernelGGL(k_c1bn_gram, dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, M, workspace);
+  hipLaunchKernelGGL(k_c1bn_gram, dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, M, workspace, xsc, xsh,
+                     xrelu);
   hipLaunchKernelGGL(k_c1bn_slab_sum, dim3(cdiv(NGRAM, 16)), dim3(1024), 0, strm(stream), workspace, grid, NGRAM,
                      gram);
   hipLaunchKernelGGL(k_c1bn_gram_fin, dim3(1), dim3(128), 0, strm(stream), gram, w, bias, M, K, part);
   return launch_rc("acfe_c1bn_stats");
 }
 
-ACFE_API int acfe_c1bn_apply(const void* x, long long M, int C, const float* w, int K, const float* bias,
-                             const float* scale, const float* shift, int relu, void* y, void* stream) {
+static int c1bn_apply_impl(const void* x, long long M, int C, const float* w, int K, const float* bias,
+                           const float* scale, const float* shift, int relu, void* y, const float* xsc,
+                           const float* xsh, int xrelu, void* stream) {
   if (!shape_ok(M, C, K, x) || !w || !scale || !shift || !y || (reinterpret_cast<uintptr_t>(y) & 15))
     return ACFE_E_INVAL;
   const int grid = c1_grid(M, APPLY_GRID);
   if (K == 128)
     hipLaunchKernelGGL((k_c1bn_apply<8>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, w, bias, M,
-                       relu, scale, shift, (uint16_t*)y);
+                       relu, scale, shift, (uint16_t*)y, xsc, xsh, xrelu);
   else
     hipLaunchKernelGGL((k_c1bn_apply<4>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, w, bias, M,
-                       relu, scale, shift, (uint16_t*)y);
+                       relu, scale, shift, (uint16_t*)y, xsc, xsh, xrelu);
   return launch_rc("acfe_c1bn_apply");
 }
 
-ACFE_API int acfe_c1bn_bwd(const void* dy, const void* x, long long M, int C, const float* w, int K,
-                           const float* bias, const float* scale, const float* shift, const float* mean,
-                           const float* invstd, int relu, double count, const float* gram, void* dx, float* dw,
-                           float* db, float* dgamma, float* dbeta, float* workspace, void* stream) {
+static int c1bn_bwd_impl(const void* dy, const void* x, long long M, int C, const float* w, int K,
+                         const float* bias, const float* scale, const float* shift, const float* mean,
+                         const float* invstd, int relu, double count, const float* gram, void* dx, float* dw,
+                         float* db, float* dgamma, float* dbeta, float* workspace, const float* xsc,
+                         const float* xsh, int xrelu, void* stream) {
   if (!shape_ok(M, C, K, x) || !dy || !w || !scale || !shift || !mean || !invstd || !gram || !dx || !dw ||
       !workspace || count <= 0 || (reinterpret_cast<uintptr_t>(dy) & 15) || (reinterpret_cast<uintptr_t>(dx) & 7))
     return ACFE_E_INVAL;
@@ -530,19 +581,65 @@ ACFE_API int acfe_c1bn_bwd(const void* dy, const void* x, long long M, int C, co
   hipStream_t s = strm(stream);
   if (K == 128)
     hipLaunchKernelGGL((k_c1bn_bsum<8>), dim3(gs), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, slab);
+                       (const uint16_t*)dy, scale, shift, slab, xsc, xsh, xrelu);
   else
     hipLaunchKernelGGL((k_c1bn_bsum<4>), dim3(gs), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, slab);
+                       (const uint16_t*)dy, scale, shift, slab, xsc, xsh, xrelu);
   hipLaunchKernelGGL(k_c1bn_slab_sum, dim3(cdiv(n, 16)), dim3(1024), 0, s, slab, gs, n, tot);
   hipLaunchKernelGGL(k_c1bn_bfin, dim3(1), dim3(128), 0, s, tot, gram, w, bias, scale, mean, invstd, M, count, K,
                      dgamma, dbeta, dw, db, dxp);
   const int gd = c1_grid(M, DX_GRID);
   if (K == 128)
     hipLaunchKernelGGL((k_c1bn_dx<8>), dim3(gd), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, dxp, (uint16_t*)dx);
+                       (const uint16_t*)dy, scale, shift, dxp, (uint16_t*)dx, xsc, xsh, xrelu);
   else
     hipLaunchKernelGGL((k_c1bn_dx<4>), dim3(gd), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, dxp, (uint16_t*)dx);
+                       (const uint16_t*)dy, scale, shift, dxp, (uint16_t*)dx, xsc, xsh, xrelu);
   return launch_rc("acfe_c1bn_bwd");
+}
+
+ACFE_API int acfe_c1bn_stats(const void* x, long long M, int C, const float* w, int K, const float* bias,
+                             double* part, float* gram, float* workspace, void* stream) {
+  return c1bn_stats_impl(x, M, C, w, K, bias, part, gram, workspace, nullptr, nullptr, 0, stream);
+}
+
+ACFE_API int acfe_c1bn_apply(const void* x, long long M, int C, const float* w, int K, const float* bias,
+                             const float* scale, const float* shift, int relu, void* y, void* stream) {
+  return c1bn_apply_impl(x, M, C, w, K, bias, scale, shift, relu, y, nullptr, nullptr, 0, stream);
+}
+
+ACFE_API int acfe_c1bn_bwd(const void* dy, const void* x, long long M, int C, const float* w, int K,
+                           const float* bias, const float* scale, const float* shift, const float* mean,
+                           const float* invstd, int relu, double count, const float* gram, void* dx, float* dw,
+                           float* db, float* dgamma, float* dbeta, float* workspace, void* stream) {
+  return c1bn_bwd_impl(dy, x, M, C, w, K, bias, scale, shift, mean, invstd, relu, count, gram, dx, dw, db, dgamma,
+                       dbeta, workspace, nullptr, nullptr, 0, stream);
+}
+
+// The same three passes with the BatchNormalization (+ReLU) prologue on x
+// (x_scale / x_shift: fp32 [16] from acfe_bn_finalize of the BN in front of
+// the 1x1 conv): x is the BN INPUT, x' = (ReLU)(x * x_scale + x_shift) is
+// formed in every pass and never stored; dx is the gradient for x'.
+ACFE_API int acfe_c1bn_stats_bn(const void* x, long long M, int C, const float* w, int K, const float* bias,
+                                double* part, float* gram, float* workspace, const float* x_scale,
+                                const float* x_shift, int x_relu, void* stream) {
+  if (!x_scale || !x_shift) return ACFE_E_INVAL;
+  return c1bn_stats_impl(x, M, C, w, K, bias, part, gram, workspace, x_scale, x_shift, x_relu, stream);
+}
+
+ACFE_API int acfe_c1bn_apply_bn(const void* x, long long M, int C, const float* w, int K, const float* bias,
+                                const float* scale, const float* shift, int relu, void* y, const float* x_scale,
+                                const float* x_shift, int x_relu, void* stream) {
+  if (!x_scale || !x_shift) return ACFE_E_INVAL;
+  return c1bn_apply_impl(x, M, C, w, K, bias, scale, shift, relu, y, x_scale, x_shift, x_relu, stream);
+}
+
+ACFE_API int acfe_c1bn_bwd_bn(const void* dy, const void* x, long long M, int C, const float* w, int K,
+                              const float* bias, const float* scale, const float* shift, const float* mean,
+                              const float* invstd, int relu, double count, const float* gram, void* dx, float* dw,
+                              float* db, float* dgamma, float* dbeta, float* workspace, const float* x_scale,
+                              const float* x_shift, int x_relu, void* stream) {
+  if (!x_scale || !x_shift) return ACFE_E_INVAL;
+  return c1bn_bwd_impl(dy, x, M, C, w, K, bias, scale, shift, mean, invstd, relu, count, gram, dx, dw, db, dgamma,
+                       dbeta, workspace, x_scale, x_shift, x_relu, stream);
 }

@@ -963,7 +963,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   constexpr int NBUF = XRES ? 1 : (TR <= 3 || KB == 64) ? 2 : 1;
   static_assert(!XRES || WDMA, "XRES needs the weight DMA");
   // PRO: the BatchNormalization (+ReLU) prologue on the staged input (C <= 256)
-  static_assert(!PRO || (XRES && (PM == 0 || PM == 3 || PM == 4)), "prologue: chunk-resident forward");
+  static_assert(!PRO || (XRES && PM != 2), "prologue: chunk-resident forward");
   // pixels per row, halo row bytes: 160-B rows make the fragment reads
   // conflict-free under ds_read_b128's lane grouping at every tap shift (144-B
   // rows had 2-way conflicts: a third of the LDS cycles, rocprofv3 r02c); the
@@ -2646,6 +2646,8 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------ host side
+ACFE_API int acfe_conv2d_bn_prologue_supported(int N, int H, int W, int C, int K, int dtype);
+static bool pro_args_ok(const float* sc, const float* sh, const void* xo);
 static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int st, int pt, int pl, int P,
                           int Q, int BK, int BN) {
   ConvGeom g;
@@ -3204,7 +3206,7 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
   if constexpr (KB == 128) {
     if (rows128_xres()) return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
   }
-  if constexpr (KB == 64 && (PM == 0 || PM == 3 || PM == 4)) {
+  if constexpr (KB == 64 && PM != 2) {
     // BatchNormalization prologue (acfe_conv2d_bn_prologue_supported): 6 chunk-resident rows
     if (g.pro_sc) return launch_rows_tr<KB, PM, 6, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
   }
@@ -3243,6 +3245,30 @@ ACFE_API int acfe_conv2d_fwd_pool(const void* x, int N, int H, int W, int C, con
                                "acfe_conv2d_fwd_pool");
   return launch_rows<64, 1>(g, x, wpacked, bias, y, stats_partial, srows, argmax, strm(stream),
                             "acfe_conv2d_fwd_pool");
+}
+
+// acfe_conv2d_fwd_pool with the BatchNormalization (+ReLU) prologue of
+// acfe_conv2d_fwd_bn (bn2a -> ReLU -> branch21 -> MaxPool2D of the stride-2
+// blocks, resnet/wr_resnet_bird.py:121-145).
+ACFE_API int acfe_conv2d_fwd_pool_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K,
+                                     int pad_top, int pad_left, const float* bias, void* y, uint8_t* argmax,
+                                     float drop_rate, unsigned long long seed, double* stats_partial,
+                                     const float* bn_scale, const float* bn_shift, int bn_relu, void* x_bn_out,
+                                     int dtype, void* stream) {
+  if (!x || !wpacked || !y || !argmax || drop_rate < 0.f || drop_rate >= 1.f ||
+      !acfe_conv2d_pool_supported(N, H, W, C, K, 3, 3, dtype) ||
+      !acfe_conv2d_bn_prologue_supported(N, H, W, C, K, dtype) || !pro_args_ok(bn_scale, bn_shift, x_bn_out) ||
+      ((uintptr_t)x & 15) || ((uintptr_t)y & 7) || ((uintptr_t)argmax & 3))
+    return ACFE_E_INVAL;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
+  g.drop = make_drop(drop_rate, seed);
+  g.pro_sc = bn_scale;
+  g.pro_sh = bn_shift;
+  g.pro_relu = bn_relu ? 1 : 0;
+  g.pro_out = (uint16_t*)x_bn_out;
+  const int srows = grid_m_for(g.M, 1);
+  return launch_rows<64, 1>(g, x, wpacked, bias, y, stats_partial, srows, argmax, strm(stream),
+                            "acfe_conv2d_fwd_pool_bn");
 }
 
 ACFE_API int acfe_conv2d_dgrad_unpool(const void* dyp, const uint8_t* argmax, int N, int P, int Q, int K,

@@ -63,8 +63,8 @@ class BasicBlock(nn.Module):
         defer = ops.FUSE and ops.PROLOGUE
         y = x
         if self.stride > 1:
-            y = self.bn2a0(y, relu=True, stats=x_stats, link=link)
-            y = conv_bn(self.conv2a0, self.bn2a, y, relu=True)
+            y = self.bn2a0(y, relu=True, stats=x_stats, link=link, defer=defer)
+            y = conv_bn(self.conv2a0, self.bn2a, y, relu=True, defer=defer)
             y = conv_maxpool_dropout_bn(self.conv21, y, self.stride, self.bn2b, self.dropout, defer=defer)
         else:
             y = self.bn2a(y, relu=True, stats=x_stats, link=link, defer=defer)

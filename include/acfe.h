@@ -291,13 +291,17 @@ int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, const void* w
  * fp32 [C] from acfe_bn_finalize, 16-B aligned.  Shapes:
  * acfe_conv2d_bn_prologue_supported (3x3 stride-1 "same" bf16, C % 64 == 0,
  * C <= 256, K = 64).  acfe_conv2d_fwd_bn = acfe_conv2d_fwd_dropout (drop_rate
- * 0: none) with the prologue, acfe_conv2d_fwd_add_bn = acfe_conv2d_fwd_add
- * with the prologue. */
+ * 0: none) with the prologue, acfe_conv2d_fwd_pool_bn = acfe_conv2d_fwd_pool
+ * with it, acfe_conv2d_fwd_add_bn = acfe_conv2d_fwd_add with it. */
 int acfe_conv2d_bn_prologue_supported(int N, int H, int W, int C, int K, int dtype);
 int acfe_conv2d_fwd_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
                        int pad_left, const float* bias, void* y, double* stats_partial, float drop_rate,
                        unsigned long long seed, const float* bn_scale, const float* bn_shift, int bn_relu,
                        void* x_bn_out, int dtype, void* stream);
+int acfe_conv2d_fwd_pool_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                            int pad_left, const float* bias, void* y, uint8_t* argmax, float drop_rate,
+                            unsigned long long seed, double* stats_partial, const float* bn_scale,
+                            const float* bn_shift, int bn_relu, void* x_bn_out, int dtype, void* stream);
 int acfe_conv2d_fwd_add_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
                            int pad_left, const float* bias, const void* res, int relu, void* y, double* stats_partial,
                            const float* bn_scale, const float* bn_shift, int bn_relu, void* x_bn_out, int dtype,
@@ -324,6 +328,21 @@ int acfe_c1bn_bwd(const void* dy, const void* x, long long M, int C, const float
                   const float* scale, const float* shift, const float* mean, const float* invstd, int relu,
                   double count, const float* gram, void* dx, float* dw, float* db, float* dgamma, float* dbeta,
                   float* workspace, void* stream);
+/* The three passes with a BatchNormalization (+ReLU) prologue on x (the
+ * stride-2 block's bn2a0 -> ReLU in front of branch2a0, resnet/wr_resnet_bird.py
+ * :121-127): x is the BN INPUT, every pass forms x' = (ReLU)(x * x_scale +
+ * x_shift) (fp32 [16] from acfe_bn_finalize; acfe_bn_apply's values) and x' is
+ * never stored; dx is the gradient for x'. */
+int acfe_c1bn_stats_bn(const void* x, long long M, int C, const float* w, int K, const float* bias, double* part,
+                       float* gram, float* workspace, const float* x_scale, const float* x_shift, int x_relu,
+                       void* stream);
+int acfe_c1bn_apply_bn(const void* x, long long M, int C, const float* w, int K, const float* bias,
+                       const float* scale, const float* shift, int relu, void* y, const float* x_scale,
+                       const float* x_shift, int x_relu, void* stream);
+int acfe_c1bn_bwd_bn(const void* dy, const void* x, long long M, int C, const float* w, int K, const float* bias,
+                     const float* scale, const float* shift, const float* mean, const float* invstd, int relu,
+                     double count, const float* gram, void* dx, float* dw, float* db, float* dgamma, float* dbeta,
+                     float* workspace, const float* x_scale, const float* x_shift, int x_relu, void* stream);
 
 /* acfe_bn_bwd_apply_ex whose residual term is the backward of
  * AveragePooling2D(k, strides=k, "same") applied to x (the conv shortcut of the

@@ -488,3 +488,41 @@ def test_bn_maxpool_node(env, cuda, training, dtype, W, monkeypatch):
         assert torch.equal(outs[1][5], outs[0][5]) and torch.equal(outs[1][6], outs[0][6])
     for i in (2, 3, 4):
         assert rel(outs[1][i], outs[0][i]) < 1e-5, (i, rel(outs[1][i], outs[0][i]))
+
+
+@pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
+@pytest.mark.parametrize("shape", [(3, 10, 37), (4, 64, 128)], ids=["ragged", "stage1"])
+def test_bn_prologue_conv1x1_bn_node(env, cuda, shape, training):
+    """bn2a0 -> ReLU -> (1x1 conv + BN node) with the first BN handed to the node
+    as a prologue (its output pending, never written: acfe_c1bn_*_bn) against
+    the same chain with the BN output written by acfe_bn_apply: bit-identical
+    output, input gradient, weight / bias / BN-parameter gradients and moving
+    statistics (resnet/wr_resnet_bird.py:121-131)."""
+    ops = env[0]
+    N, H, W = shape
+    C, K = 16, 128
+    g = torch.Generator(device="cpu").manual_seed(21)
+    x0 = (torch.randn((N, H, W, C), generator=g) * 2 + 0.3).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((K, 1, 1, C), generator=g) * 0.2).to(cuda)
+    b0 = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    gy = torch.randn((N, H, W, K), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    saved = ops.PRO_C1
+    ops.PRO_C1 = True  # (off by default in the model: measured slower)
+    try:
+        for defer in (False, True):
+            x = x0.clone().requires_grad_(True)
+            w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+            ga, ba, ma, va = _bn_params(C, cuda, 31)
+            gb, bb, mb, vb = _bn_params(K, cuda, 32)
+            xb = ops.batch_norm(x, ga, ba, ma, va, training, relu=True, defer=defer)
+            assert (ops._pending(xb) is not None) == defer
+            y = ops.conv_bn(xb, w, b, gb, bb, mb, vb, training, relu=True)
+            assert (ops._pending(xb) is not None) == defer  # the node never writes it
+            y.backward(gy)
+            outs.append([y, x.grad, w.grad, b.grad, ga.grad, ba.grad, gb.grad, bb.grad, ma, va, mb, vb])
+    finally:
+        ops.PRO_C1 = saved
+    names = ["y", "dx", "dw", "db", "dgamma_a", "dbeta_a", "dgamma_b", "dbeta_b", "mm_a", "mv_a", "mm_b", "mv_b"]
+    for n, a, b in zip(names, outs[0], outs[1]):
+        assert torch.equal(a, b), n

@@ -424,7 +424,8 @@ def _bn_affine(C, seed, device):
 
 @pytest.mark.parametrize("N,H,W,C,mode", [(8, 64, 128, 64, "drop"), (8, 64, 128, 128, "add"),
                                           (4, 64, 128, 64, "plain"), (3, 14, 100, 64, "add"),
-                                          (2, 9, 70, 128, "drop")])
+                                          (2, 9, 70, 128, "drop"), (8, 64, 128, 64, "pool"),
+                                          (3, 14, 100, 64, "pool")])
 def test_conv_bn_prologue(env, cuda, N, H, W, C, mode):
     """acfe_conv2d_fwd_bn / acfe_conv2d_fwd_add_bn (BatchNormalization + ReLU
     applied while staging the conv input, resnet/wr_resnet_bird.py:136-161)
@@ -444,6 +445,19 @@ def test_conv_bn_prologue(env, cuda, N, H, W, C, mode):
 
     def run(fused):
         xb = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+        if mode == "pool":
+            y = torch.empty((N, H // 2, W // 2, K), dtype=BF, device=cuda)
+            am = torch.empty((N, H // 2, W // 2, K), dtype=torch.uint8, device=cuda)
+            st = torch.empty((rows, 2, wp.shape[0]), dtype=F64, device=cuda)
+            if not fused:
+                call("acfe_bn_apply", ptr(x), 1, N * H * W, C, ptr(sc), ptr(sh), 1, ptr(xb), 1, stream())
+                call("acfe_conv2d_fwd_pool", ptr(xb), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y), ptr(am), 0.1, 91,
+                     ptr(st), 1, stream())
+            else:
+                call("acfe_conv2d_fwd_pool_bn", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y), ptr(am), 0.1,
+                     91, ptr(st), ptr(sc), ptr(sh), 1, ptr(xb), 1, stream())
+            torch.cuda.synchronize()
+            return xb, torch.cat([y.view(torch.uint8).flatten(), am.flatten()]).view(torch.int16), st
         y = torch.empty((N, H, W, K), dtype=BF, device=cuda)
         st = torch.empty((rows, 2, wp.shape[0]), dtype=F64, device=cuda)
         if not fused:
@@ -469,7 +483,7 @@ def test_conv_bn_prologue(env, cuda, N, H, W, C, mode):
     xb0, y0, st0 = run(False)
     xb1, y1, st1 = run(True)
     assert torch.equal(xb1.view(torch.int16), xb0.view(torch.int16)), "BN output"
-    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16)), "conv output"
+    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16)), "conv output (+ argmax bytes)"
     assert torch.equal(st1[:, :, :K], st0[:, :, :K]), "BN statistics"
     exact = (x.cpu().to(F64) * sc.cpu().to(F64) + sh.cpu().to(F64)).clamp_min(0)
     _within_ulp(xb1, exact, atol=1e-6, what="x'")
