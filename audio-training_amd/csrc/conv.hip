@@ -34,6 +34,7 @@ typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 // Native 16-byte vector for register staging (HIP's uint4 struct-with-union
 // defeats SROA: arrays of it were demoted to scratch).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t T16;
 
 struct ConvGeom {
@@ -645,6 +646,12 @@ __device__ __forceinline__ void bldsx4(unsigned voff, i4 desc, unsigned m0v) {
                "s"(m0v)
                : "memory", "m0");
 }
+// the same with a wave-uniform byte offset in soffset
+__device__ __forceinline__ void bldsx4s(unsigned voff, i4 desc, unsigned soff, unsigned m0v) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(desc),
+               "s"(soff), "s"(m0v)
+               : "memory", "m0");
+}
 #pragma clang diagnostic pop
 
 // ACFE_CONV_DBG=8 diagnostic: per-wave cycle totals of the conv main-loop
@@ -948,6 +955,15 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
                int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
   static_assert(PM != 1 || TR % 2 == 0, "2x2 pooling needs row pairs");
   using T = uint16_t;
+  // PM 1 with the MFMA operands in pixels x weights order: each A row block
+  // of four rows is one 2x2 window, so a lane's four accumulators are a whole
+  // window of one channel and the pooling needs no cross-lane traffic
+  // (ACFE_POOL_LANEPAIR builds the weights x pixels lane-pair epilogue instead)
+#ifdef ACFE_POOL_LANEPAIR
+  constexpr bool SWP = false;
+#else
+  constexpr bool SWP = PM == 1;
+#endif
   constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
   // 6-row tiles: weights by LDS-DMA into a double buffer (no staging VGPRs,
   // which spilled at K = 128), input rows register-staged.  LDS buffers of the
@@ -1029,23 +1045,69 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // WDMA: piece j of this wave = 8 weight rows (s*KB + k) of 128 B, granule
   // slot (lane & 7) holds global granule slot ^ (row & 7) (source-side swizzle)
   constexpr int WPW = WG / 64 / 8;  // pieces per wave per step
-  unsigned voffW[WDMA ? WPW : 1];
+  // Weight pieces.  non-SWP: LDS rows [s][k] of 128 B (one tap's 64-channel
+  // chunk), granule slot = granule ^ (k & 7); piece j = rows R0 + l8,
+  // R0 = (wid WPW + j) 8, l8 = lane >> 3, slot = lane & 7.
+  // SWP: rows [kk][s][phys(k)] of 64 B (channel half kk of the chunk), slot =
+  // granule ^ f(k); with the lane's fragment rows k = base + FN l16 + fn,
+  // phys(k) & 3 = fn ^ (l16 & 3) (FN 4; FN 2: k bit 2 into bit 0) and
+  // f = (l16 >> 2) & 2 place every ds_read_b128 lane group on 16 distinct
+  // 16-B bank slots, and kk / s are immediate offsets of the read; piece j =
+  // rows R0 + l, R0 = (wid WPW + j) 16, l = lane >> 2, slot = lane & 3.
+  // The lane-dependent part of a piece's source offset is one VGPR (vwl); the
+  // rest (its first row, tap, channel half and swizzle) is wave-uniform.
+  constexpr int LGB = FN == 4 ? 3 : 1;  // SWP: phys(k) = k ^ ((k >> 2) & LGB)
+  // piece j: wave-uniform source byte offset (its first row, tap, channel
+  // half) and the lane's SWP swizzle term
+  auto piece_so = [&](int j) __attribute__((always_inline)) {
+    if constexpr (SWP) {
+      const int R0 = (wid * WPW + j) * 16, kh = R0 / (3 * KB), rr = R0 - kh * 3 * KB;
+      const int s_ = rr / KB, kb = rr - s_ * KB;
+      return (unsigned)((kb * g.Kdp + s_ * g.C + kh * 32) * 2);
+    } else {
+      const int R0 = (wid * WPW + j) * 8, s_ = R0 / KB, kb = R0 - s_ * KB;
+      return (unsigned)((kb * g.Kdp + s_ * g.C) * 2);
+    }
+  };
+  auto piece_vx = [&](int j) __attribute__((always_inline)) {
+    if constexpr (SWP) {
+      const int R0 = (wid * WPW + j) * 16, kb = R0 % KB;
+      const unsigned fu = (unsigned)((((kb % (KB / 2)) / FN) >> 2) & 2);  // f of the piece's rows
+      return (((unsigned)lane & 3u) ^ fu) << 4;
+    } else {
+      return 0u;
+    }
+  };
+  // VOFF: each piece's full source offset held in a VGPR (no per-step
+  // scalar offset arithmetic); the 6-row K = 128 tiles, at the VGPR limit,
+  // keep one VGPR and form the rest in soffset
+  constexpr bool VOFF = !(KB == 128 && TR == 6);
+  unsigned vwo[VOFF ? WPW : 1];
+  unsigned vwl = 0;
   if constexpr (WDMA) {
+    if constexpr (SWP) {
+      const int l = lane >> 2;
+      vwl = (unsigned)((l ^ ((l >> 2) & LGB)) * g.Kdp * 2);
+    } else {
+      const int l8 = lane >> 3;
+      vwl = (unsigned)(l8 * g.Kdp * 2 + (((lane & 7) ^ l8) << 4));
+    }
+    if constexpr (VOFF) {
 #pragma unroll
-    for (int j = 0; j < WPW; ++j) {
-      const int row = (wid * WPW + j) * 8 + (lane >> 3);
-      const int s_ = row / KB, k = row - s_ * KB, gr = (lane & 7) ^ (row & 7);
-      voffW[j] = (unsigned)(((long long)k * g.Kdp + s_ * g.C + gr * 8) * 2);
+      for (int j = 0; j < WPW; ++j) vwo[j] = vwl + piece_so(j) + piece_vx(j);
     }
   }
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
-  auto wdma = [&](int t, int wb) __attribute__((always_inline)) {
-    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = st - cc * 3;
+  auto wdma = [&](int st, int wb) __attribute__((always_inline)) {
+    const int cc = st / 3, r = st - cc * 3;
     const long long base = (long long)(uintptr_t)Wp + ((long long)r * 3 * g.C + cc * 64) * 2;
     const i4 dw = {(int)(unsigned)base, (int)(unsigned)(base >> 32), (int)0x80000000u, 0x00020000};
     const unsigned lb = lds0 + WBASE + wb * WBYTES + wid * WPW * 1024;
 #pragma unroll
-    for (int j = 0; j < (WDMA ? WPW : 0); ++j) bldsx4(voffW[j], dw, lb + j * 1024);
+    for (int j = 0; j < (WDMA ? WPW : 0); ++j) {
+      if constexpr (VOFF) bldsx4(vwo[j], dw, lb + j * 1024);
+      else bldsx4s(vwl + piece_vx(j), dw, piece_so(j), lb + j * 1024);
+    }
   };
   // Input staging without per-step address arithmetic: granule i of this
   // thread is halo row xrow[i], halo pixel xpix[i], 16-B channel slot gr of the
@@ -1107,8 +1169,8 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       xm |= mm << (MB * i);
     }
   };
-  auto gload = [&](int t) __attribute__((always_inline)) {
-    const int tl = t / nsteps_t, st = t - tl * nsteps_t, cc = st / 3, r = XRES ? 0 : st - cc * 3;
+  auto gload = [&](int tl, int st) __attribute__((always_inline)) {
+    const int cc = st / 3, r = XRES ? 0 : st - cc * 3;
     if (tl != stl) {
       stage_tile(tl);
       stl = tl;
@@ -1216,10 +1278,35 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     // each lane holds both rows of its 2x2 windows
     const int p = PM == 1 ? fm * SEGW + wp * 16 : wp * (TR * 16) + fm * 16;
     xoff[fm] = ((p / SEGW) * HWX + (p % SEGW) + l16) * XRB + (lane >> 4) * 16;
+    if constexpr (SWP) {
+      // A row m = 4q + j: window q of fragment fm (row pair fm / 2, pooled
+      // column wp*8 + (fm & 1)*4 + (q ^ (q >> 1)): windows q and q ^ 3 share a
+      // ds_read_b128 lane group and sit two pooled columns apart, which makes
+      // the 16 lanes of every group hit 16 distinct 16-B bank slots at the
+      // 160-B pitch), pixel j = (dy, dx) of the window
+      const int q = l16 >> 2, j = l16 & 3;
+      const int a = wp * 8 + (fm & 1) * 4 + (q ^ (q >> 1));
+      xoff[fm] = (((fm >> 1) * 2 + (j >> 1)) * HWX + 2 * a + (j & 1)) * XRB + (lane >> 4) * 16;
+    }
   }
-  int woff[FN];
+  // weight fragment fn, column l16 = output channel woff[fn]; SWP: FN
+  // consecutive channels per lane (a lane's pooled window covers channels
+  // wk * KB/2 + FN * l16 + [0, FN)), woffp = that row's LDS row, wsw its
+  // granule swizzle
+  // wrb[fn]: byte offset of this lane's weight fragment fn in the weight
+  // buffer (non-SWP: of kk = 0 in tap 0; kk = 1 flips bit 6 -- granule
+  // kk * 4 + hi, hi < 4, XOR the swizzle; SWP: in [kk = 0][s = 0])
+  int wrb[FN];
 #pragma unroll
-  for (int fn = 0; fn < FN; ++fn) woff[fn] = wk * (KB / 2) + fn * 16 + l16;
+  for (int fn = 0; fn < FN; ++fn) {
+    if constexpr (SWP) {
+      const int k = wk * (KB / 2) + FN * l16 + fn;
+      wrb[fn] = (k ^ ((k >> 2) & LGB)) * 64 + (((lane >> 4) ^ ((l16 >> 2) & 2)) << 4);
+    } else {
+      const int k = wk * (KB / 2) + fn * 16 + l16;
+      wrb[fn] = k * 128 + (((lane >> 4) ^ (k & 7)) << 4);
+    }
+  }
 
   // PM 3 with K = 64: the tile's residual quads are loaded at the start of its
   // last step (in flight during that step's MFMAs) instead of in the epilogue
@@ -1258,7 +1345,147 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       }
       return r;
     };
-    if constexpr (PM == 1) {
+    if constexpr (SWP) {
+      // lane = (window q = lane >> 4 of each fragment, channels cf + [0, FN));
+      // accumulator j of fragment fm = pixel (dy, dx) = (j >> 1, j & 1) of
+      // that window, so the window order (0,0),(0,1),(1,0),(1,1) with the
+      // first maximum winning (acfe_maxpool2d_fused's argmax bytes) is the
+      // register order.  Lanes 2t, 2t + 1 hold channels 2 FN t + [0, 2 FN) of
+      // the same windows: one DPP swap per fragment pair gives the even lane
+      // fragment fm2's and the odd lane fragment fm2 + 1's 2 FN channels, so a
+      // tile's stores are FM / 2 x (2 FN x 2 B pooled + 2 FN argmax bytes) per
+      // lane (the per-CU store issue rate, not bytes, bounds this epilogue)
+      const int P2 = g.P >> 1, Q2 = g.Q >> 1, q = lane >> 4;
+      const int cf = wk * (KB / 2) + FN * l16;
+      const long long img = (long long)n * P2 * Q2;  // pooled pixels before this image
+      unsigned char* const yb = reinterpret_cast<unsigned char*>(Y + img * g.ldy);
+      unsigned char* const ab = amax + img * g.K;
+      const bool odd = (lane & 1) != 0;
+      constexpr int NY = FN / 2;  // dwords of a lane's FN bf16 values
+      float sb[FN], sq[FN], bch[FN];
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        sb[fn] = sq[fn] = 0.f;
+        bch[fn] = __int_as_float(__builtin_amdgcn_ds_bpermute((FN * l16 + fn) * 4, __float_as_int(blane)));
+      }
+#pragma unroll
+      for (int fm2 = 0; fm2 < FM; fm2 += 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        // fragments fm2, fm2 + 1: pooled row hp2, pooled columns wq, wq + 4
+        const int hp2 = ((hb * TR) >> 1) + (fm2 >> 1);
+        unsigned yv[2][NY], av[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int fm = fm2 + hf;
+          const int wq = ((wb * SEGW) >> 1) + wp * 8 + hf * 4 + (q ^ (q >> 1));
+          const bool inb = hp2 < P2 && wq < Q2;
+          const unsigned pp = ((unsigned)n * P2 + hp2) * Q2 + wq;  // < 2^32 (acfe_conv2d_pool_supported)
+          // Dropout keep bits of the lane's FN channels (bit fn), one pair
+          // hash per channel pair, taken before the accumulators are read
+          unsigned keep = (1u << FN) - 1u;
+          if (g.drop.on) {
+            keep = 0u;
+#pragma unroll
+            for (int pr = 0; pr < NY; ++pr) {
+              const uint32_t h = drop_pair_hash32(g.drop, pp * (unsigned)g.K + cf + 2 * pr);
+              keep |= ((h & 0xFFFFu) >= g.drop.thr ? 1u : 0u) << (2 * pr);
+              keep |= ((h >> 16) >= g.drop.thr ? 1u : 0u) << (2 * pr + 1);
+            }
+          }
+          float mv[FN];
+          av[hf] = 0u;
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) {
+            float a[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = bf2f(f2bf(acc[fm][fn][j] + bch[fn]));
+            float m = a[0];
+            unsigned am = 0;
+            if (a[1] > m) m = a[1], am = 1;
+            if (a[2] > m) m = a[2], am = 2;
+            if (a[3] > m) m = a[3], am = 3;
+            if (g.drop.on) m = ((keep >> fn) & 1u) ? bf2f(f2bf(m * g.drop.scl)) : 0.f;
+            mv[fn] = m;
+            av[hf] |= am << (8 * fn);
+            acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) {
+            const float f = inb ? mv[fn] : 0.f;
+            sb[fn] += f;
+            sq[fn] += f * f;
+          }
+          // rounded values are bf16-exact: packing is a bit move
+#pragma unroll
+          for (int pr = 0; pr < NY; ++pr)
+            yv[hf][pr] = (__float_as_uint(mv[2 * pr]) >> 16) | (__float_as_uint(mv[2 * pr + 1]) & 0xffff0000u);
+        }
+        // (no scheduling across fragment pairs: hoisting the next pair's
+        // hashes and addresses over these stores spilled at K = 128)
+        __builtin_amdgcn_sched_barrier(0);
+        // even lane: fragment fm2 (own | partner's), odd lane: fm2 + 1 (partner's | own)
+        unsigned ys[NY], yo[NY], as, ao;
+#pragma unroll
+        for (int pr = 0; pr < NY; ++pr) {
+          const unsigned send = odd ? yv[0][pr] : yv[1][pr];
+          ys[pr] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);
+          yo[pr] = odd ? yv[1][pr] : yv[0][pr];
+        }
+        {
+          const unsigned send = odd ? av[0] : av[1];
+          as = (unsigned)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);
+          ao = odd ? av[1] : av[0];
+        }
+        // stores at the image base + a 32-bit offset (out-of-image windows
+        // masked off)
+        const int hs = odd ? 1 : 0;
+        const int wq = ((wb * SEGW) >> 1) + wp * 8 + hs * 4 + (q ^ (q >> 1));
+        const bool inb = hp2 < P2 && wq < Q2;
+        const int c0 = wk * (KB / 2) + FN * (l16 & ~1);  // first of the pair's 2 FN channels
+        const unsigned pix = (unsigned)(hp2 * Q2 + wq);
+        const unsigned yo_ = (pix * (unsigned)g.ldy + c0) * 2u, ao_ = pix * (unsigned)g.K + c0;
+        if constexpr (FN == 4) {
+          const u32x4 yw = odd ? u32x4{ys[0], ys[1], yo[0], yo[1]} : u32x4{yo[0], yo[1], ys[0], ys[1]};
+          const u32x2 aw = odd ? u32x2{as, ao} : u32x2{ao, as};
+          if (inb) {
+            *reinterpret_cast<u32x4*>(yb + yo_) = yw;
+            *reinterpret_cast<u32x2*>(ab + ao_) = aw;
+          }
+        } else {
+          const u32x2 yw = odd ? u32x2{ys[0], yo[0]} : u32x2{yo[0], ys[0]};
+          const unsigned aw = odd ? ((as & 0xFFFFu) | (ao << 16)) : ((ao & 0xFFFFu) | (as << 16));
+          if (inb) {
+            *reinterpret_cast<u32x2*>(yb + yo_) = yw;
+            *reinterpret_cast<unsigned*>(ab + ao_) = aw;
+          }
+        }
+      }
+      if (stats) {
+        // sums over the four windows (lane groups), then lane group q keeps
+        // values q * NV16 + k of [sb[0..FN), sq[0..FN)]
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          sb[fn] += __shfl_xor(sb[fn], 16, 64);
+          sq[fn] += __shfl_xor(sq[fn], 16, 64);
+          sb[fn] += __shfl_xor(sb[fn], 32, 64);
+          sq[fn] += __shfl_xor(sq[fn], 32, 64);
+        }
+#pragma unroll
+        for (int k = 0; k < NV16; ++k) {
+          float v = 0.f;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int idx = qq * NV16 + k, fn = idx % FN;
+            const float vv = idx < FN ? sb[fn] : sq[fn];
+            v = q == qq ? vv : v;
+          }
+          const int idx = q * NV16 + k, st = idx / FN, col = cf + idx % FN;
+          if constexpr (REGSTAT) dstat[k] += (double)v;
+          else atomicAdd(&sstat[st * KB + col], (double)v);
+        }
+      }
+    }
+    if constexpr (PM == 1 && !SWP) {
       // 2x2 windows: rows (2i, 2i+1) in this lane's fragments, columns (l16,
       // l16 ^ 1) in the neighbouring lane.  The lane pair splits each channel
       // quad: the even lane pools channels 0-1, the odd lane 2-3, each getting
@@ -1387,7 +1614,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     };
     // only PM 4 carries a Dropout, launched with 32-bit element indices (launch_fwd_t)
     if constexpr (PM != 1) epi03(std::bool_constant<PM == 4>{}, std::true_type{});
-    if (stats) {
+    if (stats && !SWP) {
       butterfly_step<NV, 8, 0x128>(sv, lane);
       butterfly_step<NV / 2, 4, 0x141>(sv, lane);
       butterfly_step<NV / 4, 2, 0x4E>(sv, lane);
@@ -1409,7 +1636,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 
   if constexpr (PRO) __syncthreads();  // pss
   if (L > 0) {
-    gload(0);
+    gload(0, 0);
     if constexpr (WDMA) wdma(0, 0);
     xform(0);
     sstore(0);
@@ -1417,30 +1644,41 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   if constexpr (WDMA) wait_vmcnt<0>();
   __syncthreads();
   int buf = 0, cst = 0, ctm = walk.tm;
+  // ACFE_CONV_DBG=8 in a -DACFE_ROWS_STAMPS build (make stamps): per-wave
+  // cycles of issue / MFMA / epilogue / first barrier / restage + second
+  // barrier (tools/rows_stamps.py); compiled out of the production library
+#ifdef ACFE_ROWS_STAMPS
+  Stamps stp(g.dbg == 8);
+#else
+  Stamps stp(false);
+#endif
+  int ctl = 0;  // walk-local index of the current tile (step t = ctl * nsteps_t + cst)
   for (int t = 0; t < L; ++t) {
     const bool more = t + 1 < L;
+    // (tile, step) of steps t + 1 and t + 2, without divisions
+    const bool w1 = cst + 1 == nsteps_t, w2 = cst + 2 >= nsteps_t;
+    const int st1 = w1 ? 0 : cst + 1, tl1 = ctl + (w1 ? 1 : 0);
+    const int st2 = w2 ? cst + 2 - nsteps_t : cst + 2, tl2 = ctl + (w2 ? 1 : 0);
     // XRES: filter row of this step and whether the next one starts a chunk
     // (XRES: the next chunk's rows are requested one step early, at rs == 1,
     // and land by that step's closing wait; PRO transforms them during rs == 2)
     const int rs = XRES ? cst - 3 * (cst / 3) : 0;
     const bool xnext = more && (!XRES || rs == 2);
     if constexpr (XRES) {
-      if (rs == 1 && t + 2 < L) gload(t + 2);
+      if (rs == 1 && t + 2 < L) gload(tl2, st2);
     } else {
-      if (more) gload(t + 1);
+      if (more) gload(tl1, st1);
     }
     if (more) {
-      if constexpr (WDMA) wdma(t + 1, (t + 1) & 1);
+      if constexpr (WDMA) wdma(st1, (t + 1) & 1);
     }
     if constexpr (PRO) {
-      if (xnext) {
-        const int st1 = (t + 1) % nsteps_t;
-        xform(st1 / 3);
-      }
+      if (xnext) xform(st1 / 3);
     }
     if constexpr (RPRE) {
       if (cst + 1 == nsteps_t) rload(ctm);
     }
+    stp.mark(0);
     const unsigned char* Xl = xbuf(buf) + rs * (HWX * XRB);
     const unsigned char* Wl = WDMA ? smem + WBASE + (t & 1) * WBYTES : xbuf(buf) + XBYTES;
     // K = 64: let the scheduler interleave the fragment reads with the MFMAs
@@ -1453,29 +1691,35 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       for (int kk = 0; kk < 2; ++kk) {
         uint4 wf[FN], xf[FM];
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int k = woff[fn];
-          wf[fn] = *reinterpret_cast<const uint4*>(Wl + (s * KB + k) * 128 + (((kk * 4 + (lane >> 4)) ^ (k & 7)) << 4));
-        }
+        for (int fn = 0; fn < FN; ++fn)
+          wf[fn] = *reinterpret_cast<const uint4*>(SWP ? Wl + (kk * 3 + s) * KB * 64 + wrb[fn]
+                                                       : Wl + s * KB * 128 + (wrb[fn] ^ (kk << 6)));
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
           xf[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + s * XRB + kk * 64);
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], wf[fn], xf[fm], T());
+          for (int fn = 0; fn < FN; ++fn) {
+            if constexpr (SWP) mma(acc[fm][fn], xf[fm], wf[fn], T());
+            else mma(acc[fm][fn], wf[fn], xf[fm], T());
+          }
       }
+    stp.mark(1);
     if (NBUF == 2 && more) sstore(buf ^ 1);
     if (++cst == nsteps_t) {
       cst = 0;
+      ++ctl;
       epilogue(ctm);
       ctm += walk.step;
     }
+    stp.mark(2);
     if constexpr (WDMA && NBUF == 2) wait_vmcnt<0>();  // next step's weight pieces landed
     if constexpr (XRES) {
       if (!xnext) wait_vmcnt<0>();
     }
     __syncthreads();
+    stp.mark(3);
     if (NBUF == 2) {
       buf ^= 1;
     } else if (xnext) {
@@ -1483,7 +1727,9 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       if constexpr (WDMA) wait_vmcnt<0>();  // next step's weight pieces landed
       __syncthreads();
     }
+    stp.mark(4);
   }
+  stp.flush(wid);
   if (stats && !REGSTAT) {
     for (int c = tid; c < KB; c += 512) {
       stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = sstat[c];
@@ -1507,8 +1753,16 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
         double v = 0.0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) v += red[((wk * 4 + q) * 64 + lane) * NV16 + k];
-        const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
-        const int col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+        int st, col;
+        if constexpr (SWP) {
+          const int idx = (lane >> 4) * NV16 + k;
+          st = idx / FN;
+          col = wk * (KB / 2) + FN * l16 + idx % FN;
+        } else {
+          const int idx = b0 + k, rm = idx - (idx / (FN * 4)) * (FN * 4);
+          st = idx / (FN * 4);
+          col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+        }
         stats[((long long)blockIdx.x * 2 + st) * g.Kp + col] = v;
       }
     }

@@ -300,7 +300,7 @@ def main():
             "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
         },
         "roofline": {
-            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_rows<128,6,1>: 6 rows x 64 px x 128 ch per workgroup, 2x2 max-pool + dropout + BN sums in the epilogue)",
+            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_rows<128,4,1,true>: 4 rows x 64 px x 128 ch per workgroup, chunk-resident halo rows, 2x2 max-pool + dropout + BN sums in the epilogue, lanes own whole 2x2 windows)",
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
