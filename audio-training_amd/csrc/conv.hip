@@ -1082,6 +1082,11 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // scalar offset arithmetic); the 6-row K = 128 tiles, at the VGPR limit,
   // keep one VGPR and form the rest in soffset
   constexpr bool VOFF = !(KB == 128 && TR == 6);
+#ifdef ACFE_ROWS_NO_WILV
+  constexpr bool WILV = false;
+#else
+  constexpr bool WILV = WDMA && KB == 128;  // (K = 64: the iglp_opt(0) interleave is better without it)
+#endif
   unsigned vwo[VOFF ? WPW : 1];
   unsigned vwl = 0;
   if constexpr (WDMA) {
@@ -1098,16 +1103,29 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     }
   }
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
-  auto wdma = [&](int st, int wb) __attribute__((always_inline)) {
+  // weight pieces of step st into buffer wb: descriptor + LDS base, then the
+  // pieces (all at once, or one by one between the MFMA groups: WILV)
+  i4 wdw = {0, 0, 0, 0};
+  unsigned wlb = 0;
+  auto wprep = [&](int st, int wb) __attribute__((always_inline)) {
     const int cc = st / 3, r = st - cc * 3;
     const long long base = (long long)(uintptr_t)Wp + ((long long)r * 3 * g.C + cc * 64) * 2;
-    const i4 dw = {(int)(unsigned)base, (int)(unsigned)(base >> 32), (int)0x80000000u, 0x00020000};
-    const unsigned lb = lds0 + WBASE + wb * WBYTES + wid * WPW * 1024;
+    wdw = i4{(int)(unsigned)base, (int)(unsigned)(base >> 32), (int)0x80000000u, 0x00020000};
+    wlb = lds0 + WBASE + wb * WBYTES + wid * WPW * 1024;
+  };
+  auto wpiece = [&](int j) __attribute__((always_inline)) {
+    // (wave-uniform; readfirstlane keeps them in SGPRs when the piece is
+    // issued from inside the MFMA groups)
+    const i4 dw = {__builtin_amdgcn_readfirstlane(wdw[0]), __builtin_amdgcn_readfirstlane(wdw[1]),
+                   __builtin_amdgcn_readfirstlane(wdw[2]), __builtin_amdgcn_readfirstlane(wdw[3])};
+    const unsigned lb = (unsigned)__builtin_amdgcn_readfirstlane((int)(wlb + j * 1024));
+    if constexpr (VOFF) bldsx4(vwo[j], dw, lb);
+    else bldsx4s(vwl + piece_vx(j), dw, piece_so(j), lb);
+  };
+  auto wdma = [&](int st, int wb) __attribute__((always_inline)) {
+    wprep(st, wb);
 #pragma unroll
-    for (int j = 0; j < (WDMA ? WPW : 0); ++j) {
-      if constexpr (VOFF) bldsx4(vwo[j], dw, lb + j * 1024);
-      else bldsx4s(vwl + piece_vx(j), dw, piece_so(j), lb + j * 1024);
-    }
+    for (int j = 0; j < (WDMA ? WPW : 0); ++j) wpiece(j);
   };
   // Input staging without per-step address arithmetic: granule i of this
   // thread is halo row xrow[i], halo pixel xpix[i], 16-B channel slot gr of the
@@ -1670,7 +1688,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       if (more) gload(tl1, st1);
     }
     if (more) {
-      if constexpr (WDMA) wdma(st1, (t + 1) & 1);
+      if constexpr (WDMA) {
+        if constexpr (WILV) wprep(st1, (t + 1) & 1);
+        else wdma(st1, (t + 1) & 1);
+      }
     }
     if constexpr (PRO) {
       if (xnext) xform(st1 / 3);
@@ -1689,6 +1710,14 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     for (int s = 0; s < 3; ++s)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
+        // WILV: the next step's weight pieces are issued between the MFMA
+        // groups (piece j before group j * 6 / WPW), so their issue waits
+        // overlap this step's MFMAs instead of preceding them
+        if constexpr (WILV) {
+#pragma unroll
+          for (int j = 0; j < WPW; ++j)
+            if ((j * 6) / WPW == s * 2 + kk && more) wpiece(j);
+        }
         uint4 wf[FN], xf[FM];
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
