@@ -260,21 +260,22 @@ def main():
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
     traffic = None
-    pmc = next((q for q in (ROOT / "profiles" / f"pmc_dominant_{t}.json" for t in ("r02", "r01l")) if q.exists()),
-               None)
+    pmc = next((q for q in (ROOT / "profiles" / f"pmc_dominant_{t}.json" for t in ("r02b", "r02", "r01l"))
+                if q.exists()), None)
     if pmc is not None and a.batch == 512 and a.model == "bird":  # measured on this launch's shape
         try:
             traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     counters = None
-    sq = ROOT / "profiles" / "sq_dominant_r02.json"
+    sq = next((q for q in (ROOT / "profiles" / f"sq_dominant_{t}.json" for t in ("r02b", "r02")) if q.exists()),
+              ROOT / "profiles" / "sq_dominant_r02.json")
     if sq.exists():  # SQ counters of the same kernel (tools/pmc_sq.sh, separate rocprofv3 --pmc passes)
         try:
             d = json.loads(sq.read_text())
             counters = {k: d[k] for k in ("mfma_busy_per_simd", "wave_time_waiting", "valu_insts_per_mfma",
                                           "lds_bank_conflict_share")}
-            counters["source"] = "profiles/sq_dominant_r02.json"
+            counters["source"] = f"profiles/{sq.name}"
         except (ValueError, KeyError):
             counters = None
     clips = world * a.batch * a.steps

@@ -5,7 +5,7 @@
 # usage: tools/pmc_sq.sh <tag> [kernel regex]    output: gpurun_out/pmc_<tag>/
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-sq}
-RX=${2:-k_conv3x3_rows<128, 6, [12]>|k_wgrad3x3_halo<128, true>}
+RX=${2:-k_conv3x3_rows<128, 4, [12], true|k_wgrad3x3_halo<128, true>}
 O=gpurun_out/pmc_$TAG
 mkdir -p $O
 i=0

@@ -11,6 +11,7 @@ usage: tools/pmc_traffic.py <dir> <tag>"""
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -45,8 +46,8 @@ def main():
     B, H, W, C, K = 512, 128, 256, 128, 128
     if pool:  # input + pooled output + 1-byte argmax per pooled output (weights negligible)
         algo = B * H * W * C * 2 + B * (H // 2) * (W // 2) * K * 3 + K * 9 * C * 2
-        kern = ("k_conv3x3_rows<128,6,1> (s1b0 conv21 3x3 128->128 @128x256 + 2x2 max-pool/dropout/BN-sums "
-                "epilogue, batch 512)")
+        kern = (os.environ.get("KLABEL", "k_conv3x3_rows<128, 4, 1, true") +
+                "> (s1b0 conv21 3x3 128->128 @128x256 + 2x2 max-pool/dropout/BN-sums epilogue, batch 512)")
         src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes inside bench.py (tools/pmc_pool.sh)"
     else:
         algo = (B * H * W * C + B * H * W * K) * 2 + K * 9 * C * 2
