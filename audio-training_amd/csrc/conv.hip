@@ -1085,6 +1085,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #ifdef ACFE_ROWS_NO_WILV
   constexpr bool WILV = false;
 #else
+#ifndef ACFE_ROWS_WGRP
+#define ACFE_ROWS_WGRP 3
+#endif
+  constexpr int WGRP = ACFE_ROWS_WGRP;  // MFMA groups (of 6) that carry the next step's weight pieces
   constexpr bool WILV = WDMA && KB == 128;  // (K = 64: the iglp_opt(0) interleave is better without it)
 #endif
   unsigned vwo[VOFF ? WPW : 1];
@@ -1711,12 +1715,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         // WILV: the next step's weight pieces are issued between the MFMA
-        // groups (piece j before group j * 6 / WPW), so their issue waits
-        // overlap this step's MFMAs instead of preceding them
+        // groups (piece j before group j * WGRP / WPW of the six), so their
+        // issue waits overlap this step's MFMAs instead of preceding them
         if constexpr (WILV) {
 #pragma unroll
           for (int j = 0; j < WPW; ++j)
-            if ((j * 6) / WPW == s * 2 + kk && more) wpiece(j);
+            if ((j * WGRP) / WPW == s * 2 + kk && more) wpiece(j);
         }
         uint4 wf[FN], xf[FM];
 #pragma unroll
