@@ -1086,7 +1086,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   constexpr bool WILV = false;
 #else
 #ifndef ACFE_ROWS_WGRP
-#define ACFE_ROWS_WGRP 3
+#define ACFE_ROWS_WGRP 6  // r02ak same-box A/B: 6 -> fwd_pool 4.61 ms, 3 -> 4.73, 2 -> 4.61 (dgrad 4.52 / 4.57 / 4.62)
 #endif
   constexpr int WGRP = ACFE_ROWS_WGRP;  // MFMA groups (of 6) that carry the next step's weight pieces
   constexpr bool WILV = WDMA && KB == 128;  // (K = 64: the iglp_opt(0) interleave is better without it)
