@@ -683,6 +683,7 @@ struct Stamps {
 };
 
 __device__ uint2 g_store_sink[64];  // never read: target of masked-off epilogue stores
+__device__ u32x4 g_store_sink16[64];  // the same for 16-B stores
 
 // One step of a 16-lane butterfly reduce-scatter: lanes whose `BIT` is set keep
 // the upper half of v[0..CNT), the others the lower half, each adding the
@@ -964,6 +965,19 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #else
   constexpr bool SWP = PM == 1;
 #endif
+  // CPERM (weights x pixels epilogues with the weight DMA): fragment fn, A row
+  // m = output channel KB/2 wk + 4 FN (m >> 2) + 4 fn + (m & 3), so lane group
+  // q = lane >> 4 holds 4 FN consecutive channels of its pixel across the FN
+  // fragments and the epilogue stores them with FN / 2 16-B stores (not FN
+  // 8-B ones); weight LDS rows keep 128 B with the granule swizzle
+  // swzp(k) = ((k >> LQ) & 3) << 1 | ((k >> 1) & 1), which keeps the fragment
+  // reads conflict-free under the permuted rows
+#ifdef ACFE_ROWS_NO_CPERM
+  constexpr bool CPERM = false;
+#else
+  constexpr bool CPERM = !SWP && TR > 3;
+#endif
+  constexpr int LQ = KB == 128 ? 4 : 3;  // log2(4 FN), FN = KB / 32
   constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
   // 6-row tiles: weights by LDS-DMA into a double buffer (no staging VGPRs,
   // which spilled at K = 128), input rows register-staged.  LDS buffers of the
@@ -1081,7 +1095,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // VOFF: each piece's full source offset held in a VGPR (no per-step
   // scalar offset arithmetic); the 6-row K = 128 tiles, at the VGPR limit,
   // keep one VGPR and form the rest in soffset
-  constexpr bool VOFF = !(KB == 128 && TR == 6);
+  constexpr bool VOFF = !(KB == 128 && TR == 6) || CPERM;
 #ifdef ACFE_ROWS_NO_WILV
   constexpr bool WILV = false;
 #else
@@ -1103,7 +1117,15 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     }
     if constexpr (VOFF) {
 #pragma unroll
-      for (int j = 0; j < WPW; ++j) vwo[j] = vwl + piece_so(j) + piece_vx(j);
+      for (int j = 0; j < WPW; ++j) {
+        if constexpr (CPERM) {
+          const int R0 = (wid * WPW + j) * 8, s_ = R0 / KB, k = R0 - s_ * KB + (lane >> 3);
+          const int sw = (((k >> LQ) & 3) << 1) | ((k >> 1) & 1);
+          vwo[j] = (unsigned)((k * g.Kdp + s_ * g.C + (((lane & 7) ^ sw) << 3)) * 2);
+        } else {
+          vwo[j] = vwl + piece_so(j) + piece_vx(j);
+        }
+      }
     }
   }
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
@@ -1324,6 +1346,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     if constexpr (SWP) {
       const int k = wk * (KB / 2) + FN * l16 + fn;
       wrb[fn] = (k ^ ((k >> 2) & LGB)) * 64 + (((lane >> 4) ^ ((l16 >> 2) & 2)) << 4);
+    } else if constexpr (CPERM) {
+      const int k = wk * (KB / 2) + (l16 >> 2) * 4 * FN + fn * 4 + (l16 & 3);
+      const int sw = (((k >> LQ) & 3) << 1) | ((k >> 1) & 1);
+      wrb[fn] = k * 128 + (((lane >> 4) ^ sw) << 4);
     } else {
       const int k = wk * (KB / 2) + fn * 16 + l16;
       wrb[fn] = k * 128 + (((lane >> 4) ^ (k & 7)) << 4);
@@ -1345,7 +1371,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
         const long long pix = ((long long)n * g.P + h) * g.Q + w;
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
-          const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
+          const int c = wk * (KB / 2) + (CPERM ? (lane >> 4) * 4 * FN + fn * 4 : fn * 16 + (lane >> 4) * 4);
           rres[fm][fn] = *reinterpret_cast<const uint2*>(inb ? g.res + pix * g.ldy + c : zp);
         }
       }
@@ -1360,7 +1386,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     auto bias4 = [&](int fn) __attribute__((always_inline)) {
       f4 r = {0.f, 0.f, 0.f, 0.f};
       if constexpr (PM != 2) {
-        const int src = fn * 16 + (lane >> 4) * 4;
+        const int src = CPERM ? (lane >> 4) * 4 * FN + fn * 4 : fn * 16 + (lane >> 4) * 4;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           r[j] = __int_as_float(__builtin_amdgcn_ds_bpermute((src + j) * 4, __float_as_int(blane)));
@@ -1584,10 +1610,11 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     // uniform branches and the dgrad / eval paths carry no dropout code.
     auto epi03 = [&](auto dropc, auto idxc) __attribute__((always_inline)) {
       constexpr bool DRP = decltype(dropc)::value, I32 = decltype(idxc)::value;
+      uint2 vout[CPERM ? FM : 1][CPERM ? FN : 1];  // CPERM: packed values, stored per fragment row below
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const f4 rb = bias4(fn);
-        const int c = wk * (KB / 2) + fn * 16 + (lane >> 4) * 4;
+        const int c = wk * (KB / 2) + (CPERM ? (lane >> 4) * 4 * FN + fn * 4 : fn * 16 + (lane >> 4) * 4);
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {
           const int p = wp * (TR * 16) + fm * 16;
@@ -1628,9 +1655,29 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
           uint2 v;
           v.x = (__float_as_uint(r[0]) >> 16) | (__float_as_uint(r[1]) & 0xffff0000u);
           v.y = (__float_as_uint(r[2]) >> 16) | (__float_as_uint(r[3]) & 0xffff0000u);
-          uint2* dst = inb ? reinterpret_cast<uint2*>(Y + pix * g.ldy + c) : &g_store_sink[lane];
-          *dst = v;
+          if constexpr (CPERM) {
+            vout[fm][fn] = v;
+          } else {
+            uint2* dst = inb ? reinterpret_cast<uint2*>(Y + pix * g.ldy + c) : &g_store_sink[lane];
+            *dst = v;
+          }
           acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      if constexpr (CPERM) {
+        // 4 FN consecutive channels of one pixel per lane: FN / 2 16-B stores
+        const int cq = wk * (KB / 2) + (lane >> 4) * 4 * FN;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int p = wp * (TR * 16) + fm * 16;
+          const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+          const bool inb = h < g.P && w < g.Q;
+          const long long pix = ((long long)n * g.P + h) * g.Q + w;
+          u32x4* dst = inb ? reinterpret_cast<u32x4*>(Y + pix * g.ldy + cq) : &g_store_sink16[lane];
+#pragma unroll
+          for (int hq = 0; hq < FN / 2; ++hq)
+            dst[inb ? hq : 0] = u32x4{vout[fm][2 * hq].x, vout[fm][2 * hq].y, vout[fm][2 * hq + 1].x,
+                                      vout[fm][2 * hq + 1].y};
         }
       }
     };
@@ -1649,7 +1696,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
           dstat[k] += (double)sv[k];
         } else {
           const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
-          const int col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+          const int col = wk * (KB / 2) + (CPERM ? (lane >> 4) * 4 * FN + rm : (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3));
           atomicAdd(&sstat[st * KB + col], (double)sv[k]);
         }
       }
@@ -1794,7 +1841,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
         } else {
           const int idx = b0 + k, rm = idx - (idx / (FN * 4)) * (FN * 4);
           st = idx / (FN * 4);
-          col = wk * (KB / 2) + (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3);
+          col = wk * (KB / 2) + (CPERM ? (lane >> 4) * 4 * FN + rm : (rm >> 2) * 16 + (lane >> 4) * 4 + (rm & 3));
         }
         stats[((long long)blockIdx.x * 2 + st) * g.Kp + col] = v;
       }
@@ -3008,7 +3055,8 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
   if constexpr (sizeof(T) == 2 && BN >= 64) {
     static const bool no_pipe = getenv_flag("ACFE_CONV_NO_PIPE");
     static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS");
-    if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && !no_rows && (!g.drop.on || g.idx32)) {
+    if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && !no_rows && (!g.drop.on || g.idx32) &&
+        ((uintptr_t)y & 15) == 0) {  // (16-B epilogue stores)
       // 6 output rows per tile halves the weight traffic per pixel, but at K = 128
       // its register staging spills (measured 1.4x slower): 3 rows there
       static const int rows_tr = getenv("ACFE_CONV_ROWS_TR") ? atoi(getenv("ACFE_CONV_ROWS_TR")) : 0;
@@ -3475,6 +3523,7 @@ static int rows64_tr() {  // output rows per tile of the K = 64 rows kernels (AC
 template <int KB, int PM, int TR, bool XR = false, bool PR = false>
 static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                           double* stats, int srows, uint8_t* amax, hipStream_t s, const char* what) {
+  if ((uintptr_t)y & 15) return ACFE_E_INVAL;  // 16-B epilogue stores
   const int tiles_h = (g.P + TR - 1) / TR, tiles_w = (g.Q + 63) / 64;
   const long long nt = (long long)g.N * tiles_h * tiles_w;
   int gp = 256;
