@@ -2639,12 +2639,13 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   u32x4 rd[DPT], rx[XPT];
   uint2 rda[UNP ? DPT : 1];  // UNP: argmax bytes + window taps, applied at the LDS store
   unsigned dpos = 0;
-  auto gload = [&](int sg) __attribute__((always_inline)) {
+  // part bit 0: the dY granules, bit 1: the input halo granules
+  auto gload = [&](int sg, int part = 3) __attribute__((always_inline)) {
     const int n = sg / (g.P * QS), rem = sg - n * (g.P * QS);
     const int h = rem / QS, w0 = (rem - h * QS) * SEGW;
     const T16* dyrow = dY + (((long long)n * g.P + h) * g.Q + w0) * g.K;
 #pragma unroll
-    for (int i = 0; i < DPT; ++i) {
+    for (int i = 0; i < ((part & 1) ? DPT : 0); ++i) {
       const int idx = tid + 512 * i;
       const int px = idx / DGR, cg = idx - px * DGR;
       if constexpr (UNP) {
@@ -2660,7 +2661,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       }
     }
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
+    for (int i = 0; i < ((part & 2) ? XPT : 0); ++i) {
       const int idx = tid + 512 * i;
       const int hr = idx / (HW * XGR), r2 = idx - hr * (HW * XGR), hp = r2 / XGR, cg = r2 - hp * XGR;
       const int hin = h - g.pt + hr, win = w0 - g.pl + hp;
@@ -2712,13 +2713,26 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   }
   __syncthreads();
   int buf = 0;
+  // WGI: the next segment's input-halo loads are issued after the first
+  // 32-pixel half's MFMAs (their issue stalls then overlap MFMA work)
+#ifndef ACFE_WG_ILV
+#define ACFE_WG_ILV 1
+#endif
+  constexpr bool WGI = ACFE_WG_ILV != 0;
   for (int sg = sbeg; sg < send; ++sg) {
     const bool more = sg + 1 < send;
-    if (more) gload(sg + 1);
+    if (more) gload(sg + 1, WGI ? 1 : 3);
     const uint16_t* Ds = smem + buf * (DS + XS);
     const uint16_t* Xh = Ds + DS;
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
+      if constexpr (WGI) {
+        if (kc == 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (more) gload(sg + 1, 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       const int rb = kc * 32;
       bf8 af[FM];
 #pragma unroll
