@@ -1103,7 +1103,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #define ACFE_ROWS_WGRP 6  // r02ak same-box A/B: 6 -> fwd_pool 4.61 ms, 3 -> 4.73, 2 -> 4.61 (dgrad 4.52 / 4.57 / 4.62)
 #endif
   constexpr int WGRP = ACFE_ROWS_WGRP;  // MFMA groups (of 6) that carry the next step's weight pieces
-  constexpr bool WILV = WDMA && KB == 128;  // (K = 64: the iglp_opt(0) interleave is better without it)
+#ifndef ACFE_ROWS_WILV64
+#define ACFE_ROWS_WILV64 0
+#endif
+  constexpr bool WILV = WDMA && (KB == 128 || ACFE_ROWS_WILV64);  // (K = 64: the iglp_opt(0) interleave is better without it)
 #endif
   unsigned vwo[VOFF ? WPW : 1];
   unsigned vwl = 0;
@@ -1756,7 +1759,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     // K = 64: let the scheduler interleave the fragment reads with the MFMAs
     // (fwd_add 128->64 1.084 -> 1.013 ms, dropout 64->64 0.649 -> 0.625 ms;
     // at K = 128 the same hint spills: fwd_pool 4.96 -> 5.35 ms, r02o)
-    if constexpr (KB == 64) __builtin_amdgcn_iglp_opt(0);
+#ifndef ACFE_ROWS_IGLP64
+#define ACFE_ROWS_IGLP64 1
+#endif
+    if constexpr (KB == 64 && ACFE_ROWS_IGLP64) __builtin_amdgcn_iglp_opt(0);
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
