@@ -257,7 +257,11 @@ int acfe_bn_bwd_apply_ex(const void* dy, int dy_dtype, const void* x, int x_dtyp
  * The backward takes the gradient of the pooled, dropped-out values with the
  * dropout backward already applied (e.g. acfe_bn_bwd_apply_dropout):
  * acfe_conv2d_dgrad_unpool (wflip = acfe_conv2d_pack_weights(flip=1)) and
- * acfe_conv2d_wgrad_unpool (workspace as acfe_conv2d_wgrad, R = S = 3). */
+ * acfe_conv2d_wgrad_unpool (workspace as acfe_conv2d_wgrad, R = S = 3).
+ * The row-halo kernels behind these entry points (and behind acfe_conv2d_fwd_add /
+ * _fwd_bn / _fwd_add_bn / _fwd_pool_bn) store 16-byte runs: y / dx must be
+ * 16-B aligned (ACFE_E_INVAL otherwise); acfe_conv2d_fwd / _dgrad fall back to
+ * their generic kernels for a misaligned output. */
 int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R, int S, int dtype);
 int acfe_conv2d_fwd_pool(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
                          int pad_left, const float* bias, void* y, uint8_t* argmax, float drop_rate,
