@@ -1106,7 +1106,11 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #ifndef ACFE_ROWS_WILV64
 #define ACFE_ROWS_WILV64 0
 #endif
-  constexpr bool WILV = WDMA && (KB == 128 || ACFE_ROWS_WILV64);  // (K = 64: the iglp_opt(0) interleave is better without it)
+  constexpr bool WILV = WDMA && (KB == 128 || ACFE_ROWS_WILV64);
+#ifndef ACFE_ROWS_GILV
+#define ACFE_ROWS_GILV 0  // r02aq same-box A/B: fwd_pool 4.81 ms with, 4.70 without; dgrad equal
+#endif
+  constexpr bool GILV = ACFE_ROWS_GILV && XRES && WILV;  // (input-row loads spread over the MFMA groups too)  // (K = 64: the iglp_opt(0) interleave is better without it)
 #endif
   unsigned vwo[VOFF ? WPW : 1];
   unsigned vwl = 0;
@@ -1216,15 +1220,19 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       xm |= mm << (MB * i);
     }
   };
-  auto gload = [&](int tl, int st) __attribute__((always_inline)) {
+  // part < 0: every granule; else the granules i with i % 3 == part (GILV:
+  // issued one part per MFMA group of the first three -- the step's closing
+  // wait needs them; part 0 first, it carries the tile setup)
+  auto gload = [&](int tl, int st, int part = -1) __attribute__((always_inline)) {
     const int cc = st / 3, r = XRES ? 0 : st - cc * 3;
-    if (tl != stl) {
+    if (part <= 0 && tl != stl) {
       stage_tile(tl);
       stl = tl;
     }
     if constexpr (PM == 2) {
 #pragma unroll
       for (int i = 0; i < XPT; ++i) {
+        if (part >= 0 && i % 3 != part) continue;
         const int idx = tid + 512 * i;
         const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
         const int hin = sh0 + xrow + r, win = sw0 + xpix;
@@ -1240,6 +1248,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       const int delta = r * g.W * CB + cc * 128;
 #pragma unroll
       for (int i = 0; i < XPT; ++i) {
+        if (part >= 0 && i % 3 != part) continue;
         const bool ok = (xm >> (MB * i + r)) & 1u;
         rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xoffs[i] + delta : 0x80000000, 0, 0);
       }
@@ -1247,6 +1256,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     if constexpr (!WDMA) {
 #pragma unroll
       for (int i = 0; i < WPT; ++i) {
+        if (part > 0) continue;
         const int idx = tid + 512 * i;
         const int s = idx / (KB * 8), r2 = idx - s * (KB * 8), k = r2 >> 3, gw = r2 & 7;
         rw[i] = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + (r * 3 + s) * g.C + cc * 64 + gw * 8);
@@ -1736,8 +1746,9 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     // and land by that step's closing wait; PRO transforms them during rs == 2)
     const int rs = XRES ? cst - 3 * (cst / 3) : 0;
     const bool xnext = more && (!XRES || rs == 2);
+    const bool xload = XRES && rs == 1 && t + 2 < L;  // this step requests the next chunk's rows
     if constexpr (XRES) {
-      if (rs == 1 && t + 2 < L) gload(tl2, st2);
+      if (xload && !GILV) gload(tl2, st2);
     } else {
       if (more) gload(tl1, st1);
     }
@@ -1774,6 +1785,10 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
           for (int j = 0; j < WPW; ++j)
             if ((j * WGRP) / WPW == s * 2 + kk && more) wpiece(j);
+        }
+        // GILV: the next chunk's input rows, one sixth per MFMA group
+        if constexpr (GILV) {
+          if (s * 2 + kk < 3 && xload) gload(tl2, st2, s * 2 + kk);
         }
         uint4 wf[FN], xf[FM];
 #pragma unroll
