@@ -2739,7 +2739,8 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 #ifndef ACFE_WG_ILV
 #define ACFE_WG_ILV 1
 #endif
-  constexpr bool WGI = ACFE_WG_ILV != 0 && KB >= 128;  // (K = 64: 36 MFMAs per half hide less, r02ao 491 -> 517 us)
+  // (K = 64: no measurable difference, r02as: 0.518-0.522 vs 0.521-0.530 ms; ACFE_WG_ILV=2 turns it on)
+  constexpr bool WGI = ACFE_WG_ILV == 2 || (ACFE_WG_ILV != 0 && KB >= 128);
   for (int sg = sbeg; sg < send; ++sg) {
     const bool more = sg + 1 < send;
     if (more) gload(sg + 1, WGI ? 1 : 3);
