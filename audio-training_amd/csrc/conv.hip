@@ -2628,11 +2628,15 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 // distinct banks; register-staged double buffer, one barrier per step.
 // UNP: dY is the 2x2 max-pool backward of the pooled gradient dY (argmax bytes
 // amax), expanded while staging.
-template <int KB, bool UNP, int CW = 64>
+// NR: output rows per pipeline step (a "segment" = NR rows x 64 pixels, P % NR
+// == 0): NR = 2 doubles the MFMAs per barrier for K = 64 (36 -> 72 per wave),
+// the halo then being NR + 2 input rows.
+template <int KB, bool UNP, int CW = 64, int NR = 1>
 __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
                 float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
-  constexpr int SEGW = 64, HW = SEGW + 2;
+  constexpr int SEGW = 64, HW = SEGW + 2, HR = NR + 2;
+  static_assert(NR == 1 || !UNP, "row pairs: plain dY only");
   // CW-channel chunks (C = 16 / 32 layers: the stage-2/3 branch2b): the 8 waves
   // are WC = CW / 16 channel blocks x WK = 8 / WC slices of K; a wave's nine
   // blocks are the nine taps of its channel block (CW = 64: 2 K halves x 4
@@ -2640,11 +2644,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   static_assert(CW == 64 || (CW == 32 && !UNP) || (CW == 16 && !UNP), "chunk");
   constexpr int WC = CW == 64 ? 4 : CW / 16, WK = 8 / WC;
   constexpr int LDD = KB + 16, LDX = CW + 16;
-  constexpr int DS = SEGW * LDD, XS = 3 * HW * LDX;
+  constexpr int DS = NR * SEGW * LDD, XS = HR * HW * LDX;
   constexpr int FM = KB / (16 * WK), FN = 9;
   static_assert(FM >= 1, "K slice");
   constexpr int XGR = CW / 8;
-  constexpr int DGR = KB / 8, DG = SEGW * DGR, XG = 3 * HW * XGR;
+  constexpr int DGR = KB / 8, DG = NR * SEGW * DGR, XG = HR * HW * XGR;
   constexpr int DPT = (DG + 511) / 512, XPT = (XG + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (DS + XS)];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2662,8 +2666,9 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   unsigned dpos = 0;
   // part bit 0: the dY granules, bit 1: the input halo granules
   auto gload = [&](int sg, int part = 3) __attribute__((always_inline)) {
-    const int n = sg / (g.P * QS), rem = sg - n * (g.P * QS);
-    const int h = rem / QS, w0 = (rem - h * QS) * SEGW;
+    const int PR = g.P / NR;  // row groups per image
+    const int n = sg / (PR * QS), rem = sg - n * (PR * QS);
+    const int h = (rem / QS) * NR, w0 = (rem - (rem / QS) * QS) * SEGW;
     const T16* dyrow = dY + (((long long)n * g.P + h) * g.Q + w0) * g.K;
 #pragma unroll
     for (int i = 0; i < ((part & 1) ? DPT : 0); ++i) {
@@ -2678,7 +2683,9 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         if (i == 0) dpos = 0;
         dpos |= (unsigned)(((h & 1) << 1) | (w & 1)) << (2 * i);
       } else {
-        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG && w0 + px < g.Q ? dyrow + px * g.K + cg * 8 : zp);
+        const int ro = px / SEGW, pw = px - ro * SEGW;  // row of the group, pixel of the segment
+        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG && w0 + pw < g.Q
+                                                    ? dyrow + ((long long)ro * g.Q + pw) * g.K + cg * 8 : zp);
       }
     }
 #pragma unroll
@@ -2747,15 +2754,17 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     const uint16_t* Ds = smem + buf * (DS + XS);
     const uint16_t* Xh = Ds + DS;
 #pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
+    for (int kq = 0; kq < 2 * NR; ++kq) {
+      const int kc = kq & 1, ro = kq >> 1;  // 32-pixel half, output row of the group
       if constexpr (WGI) {
-        if (kc == 1) {
+        if (kq == NR) {
           __builtin_amdgcn_sched_barrier(0);
           if (more) gload(sg + 1, 2);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      const int rb = kc * 32;
+      const int rb = ro * SEGW + kc * 32;  // dY pixel row of this half
+      const int xr = kc * 32;              // its pixel offset in the halo rows (tap row + ro below)
       bf8 af[FM];
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
@@ -2768,11 +2777,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const uint16_t* xb = Xh + boff[fn] + 4 * pp;
+        const uint16_t* xb = Xh + boff[fn] + ro * HW * LDX + 4 * pp;
         const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lp)(reinterpret_cast<const __bf16*>(xb + (rb + 4 * grp + q) * LDX)));
+            (lp)(reinterpret_cast<const __bf16*>(xb + (xr + 4 * grp + q) * LDX)));
         const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lp)(reinterpret_cast<const __bf16*>(xb + (rb + 16 + 4 * grp + q) * LDX)));
+            (lp)(reinterpret_cast<const __bf16*>(xb + (xr + 16 + 4 * grp + q) * LDX)));
         const bf8 bv = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
@@ -3418,7 +3427,10 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
 static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
                              long long splits, hipStream_t s, int* used) {
   const int cw = g.C % 64 == 0 ? 64 : g.C;  // 16 / 32-channel layers: one chunk of C
-  const int nchunk = g.C / cw, nseg = (int)((long long)g.N * g.P * ((g.Q + 63) / 64));
+  // K = 64 (plain dY): two output rows per step (ACFE_WG64_NR=1: one)
+  static const int nr64 = getenv("ACFE_WG64_NR") ? atoi(getenv("ACFE_WG64_NR")) : 2;
+  const int nr = (g.K == 64 && !amax && cw == 64 && g.P % 2 == 0 && nr64 == 2) ? 2 : 1;
+  const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * ((g.Q + 63) / 64));
   int sp = 256 / nchunk;
   if (sp > splits) sp = (int)splits;
   sp &= ~7;
@@ -3439,7 +3451,11 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   } else if (g.K == 128) {
     if (amax) WH(128, true); else WH(128, false);
   } else if (g.K == 64) {
-    if (amax) WH(64, true); else WH(64, false);
+    if (amax) WH(64, true);
+    else if (nr == 2)
+      hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
+                         (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);
+    else WH(64, false);
   } else {
     WH(32, false);  // the stage-2 branch21 (128 -> 32): 18 MFMAs per wave per segment
   }

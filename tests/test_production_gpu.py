@@ -391,13 +391,17 @@ def test_conv_narrow_production(env, cuda, C, K, H, W):
     _within_ulp(dx, F.conv_transpose2d(gd, wd, padding=1).permute(0, 2, 3, 1), what="narrow dgrad")
 
 
-@pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (32, 128, 32, 64), (32, 256, 16, 32), (16, 256, 16, 32)],
-                         ids=["s2-21", "s2-2b", "s3-2b-b6", "s3-2b"])
+@pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (32, 128, 32, 64), (32, 256, 16, 32), (16, 256, 16, 32),
+                                     (64, 64, 64, 128), (128, 64, 64, 128), (64, 64, 14, 100)],
+                         ids=["s2-21", "s2-2b", "s3-2b-b6", "s3-2b", "k64-rowpair", "k64-rowpair-2chunks",
+                              "k64-rowpair-partial"])
 def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
     """k_wgrad3x3_halo for the stage-2/3 layers whose channel count is the
     feature height: K = 32 (branch21 128 -> 32) and the 16 / 32-channel
-    chunks (branch2b 32 -> 128 / 256, 16 -> 256), at 32 clips and the
-    production split count, against float64."""
+    chunks (branch2b 32 -> 128 / 256, 16 -> 256), and the K = 64 layers'
+    two-rows-per-step variant (k_wgrad3x3_halo<64, false, 64, 2>: 64 x 128
+    stage-2 shapes, two 64-channel chunks, and a partial last column segment),
+    at 32 clips and the production split count, against float64."""
     ops, call, lib, ptr, stream = env
     N = 32
     x, w, b, g = _data(N, H, W, C, K, 307, cuda)
