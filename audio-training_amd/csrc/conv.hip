@@ -2636,7 +2636,6 @@ __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
                 float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
   constexpr int SEGW = 64, HW = SEGW + 2, HR = NR + 2;
-  static_assert(NR == 1 || !UNP, "row pairs: plain dY only");
   // CW-channel chunks (C = 16 / 32 layers: the stage-2/3 branch2b): the 8 waves
   // are WC = CW / 16 channel blocks x WK = 8 / WC slices of K; a wave's nine
   // blocks are the nine taps of its channel block (CW = 64: 2 K halves x 4
@@ -2675,13 +2674,13 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       const int idx = tid + 512 * i;
       const int px = idx / DGR, cg = idx - px * DGR;
       if constexpr (UNP) {
-        const int w = w0 + px;
+        const int ro = px / SEGW, w = w0 + px - ro * SEGW, hh = h + ro;
         const bool okd = idx < DG && w < g.Q;
-        const long long e = (((long long)n * (g.P >> 1) + (h >> 1)) * (g.Q >> 1) + (w >> 1)) * g.K + cg * 8;
+        const long long e = (((long long)n * (g.P >> 1) + (hh >> 1)) * (g.Q >> 1) + (w >> 1)) * g.K + cg * 8;
         rd[i] = *reinterpret_cast<const u32x4*>(okd ? dY + e : zp);
         rda[i] = *reinterpret_cast<const uint2*>(okd ? amax + e : reinterpret_cast<const uint8_t*>(zp));
         if (i == 0) dpos = 0;
-        dpos |= (unsigned)(((h & 1) << 1) | (w & 1)) << (2 * i);
+        dpos |= (unsigned)(((hh & 1) << 1) | (w & 1)) << (2 * i);
       } else {
         const int ro = px / SEGW, pw = px - ro * SEGW;  // row of the group, pixel of the segment
         rd[i] = *reinterpret_cast<const u32x4*>(idx < DG && w0 + pw < g.Q
@@ -3429,7 +3428,9 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   const int cw = g.C % 64 == 0 ? 64 : g.C;  // 16 / 32-channel layers: one chunk of C
   // K = 64 (plain dY): two output rows per step (ACFE_WG64_NR=1: one)
   static const int nr64 = getenv("ACFE_WG64_NR") ? atoi(getenv("ACFE_WG64_NR")) : 2;
-  const int nr = (g.K == 64 && !amax && cw == 64 && g.P % 2 == 0 && nr64 == 2) ? 2 : 1;
+  static const int nru = getenv("ACFE_WGU_NR") ? atoi(getenv("ACFE_WGU_NR")) : 2;
+  // (the K = 128 pooled-gradient variant spills at two rows: 138 VGPRs)
+  const int nr = (cw == 64 && g.P % 2 == 0 && g.K == 64 && ((!amax && nr64 == 2) || (amax && nru == 2))) ? 2 : 1;
   const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * ((g.Q + 63) / 64));
   int sp = 256 / nchunk;
   if (sp > splits) sp = (int)splits;
@@ -3451,7 +3452,10 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   } else if (g.K == 128) {
     if (amax) WH(128, true); else WH(128, false);
   } else if (g.K == 64) {
-    if (amax) WH(64, true);
+    if (amax && nr == 2)
+      hipLaunchKernelGGL((k_wgrad3x3_halo<64, true, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
+                         (const uint16_t*)dy, ws, nchunk, nseg, per, amax);
+    else if (amax) WH(64, true);
     else if (nr == 2)
       hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
                          (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);

@@ -120,12 +120,14 @@ def test_conv_fwd_pool_production(env, cuda):
     torch.testing.assert_close(st1.sum(0)[:, :K].cpu(), _sums(y1), rtol=1e-6, atol=1e-6)
 
 
-def test_conv_unpool_backward_production(env, cuda):
-    """acfe_conv2d_dgrad_unpool / acfe_conv2d_wgrad_unpool at the T1 shape
-    from a pooled gradient and argmax bytes: dX and dW against the float64
-    gradients of the exact convolution of the expanded (unpooled) gradient."""
+@pytest.mark.parametrize("N,H,W,C,K", [(8, 128, 256, 128, 128), (16, 64, 128, 128, 64)], ids=["s1b0", "s2b0"])
+def test_conv_unpool_backward_production(env, cuda, N, H, W, C, K):
+    """acfe_conv2d_dgrad_unpool / acfe_conv2d_wgrad_unpool at the T1 stage-1
+    shape and the stage-2 branch21 (128 -> 64 @ 64x128; its weight gradient on
+    the two-rows-per-step halo kernel) from a pooled gradient and argmax bytes:
+    dX and dW against the float64 gradients of the exact convolution of the
+    expanded (unpooled) gradient."""
     ops, call, lib, ptr, stream = env
-    N, H, W, C, K = 8, 128, 256, 128, 128
     x, w, b, g = _data(N, H, W, C, K, 102, cuda)
     P, Q = H // 2, W // 2
     gp = (torch.randn((N, P, Q, K), generator=g) * 0.5).to(BF)
