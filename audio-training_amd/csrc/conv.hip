@@ -3430,7 +3430,10 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   static const int nr64 = getenv("ACFE_WG64_NR") ? atoi(getenv("ACFE_WG64_NR")) : 2;
   static const int nru = getenv("ACFE_WGU_NR") ? atoi(getenv("ACFE_WGU_NR")) : 2;
   // (the K = 128 pooled-gradient variant spills at two rows: 138 VGPRs)
-  const int nr = (cw == 64 && g.P % 2 == 0 && g.K == 64 && ((!amax && nr64 == 2) || (amax && nru == 2))) ? 2 : 1;
+  static const int nr32 = getenv("ACFE_WG32_NR") ? atoi(getenv("ACFE_WG32_NR")) : 2;
+  const int nr = (cw == 64 && g.P % 2 == 0 &&
+                  ((g.K == 64 && ((!amax && nr64 == 2) || (amax && nru == 2))) || (g.K == 32 && !amax && nr32 == 2)))
+                     ? 2 : 1;
   const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * ((g.Q + 63) / 64));
   int sp = 256 / nchunk;
   if (sp > splits) sp = (int)splits;
@@ -3460,8 +3463,11 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
       hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
                          (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);
     else WH(64, false);
+  } else if (nr == 2) {  // the stage-2 branch21 (128 -> 32): 36 MFMAs per wave per two-row step
+    hipLaunchKernelGGL((k_wgrad3x3_halo<32, false, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
+                       (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);
   } else {
-    WH(32, false);  // the stage-2 branch21 (128 -> 32): 18 MFMAs per wave per segment
+    WH(32, false);  // (18 MFMAs per wave per segment)
   }
 #undef WHC
 #undef WH

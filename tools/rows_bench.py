@@ -34,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--iters", type=int, default=7)
-    ap.add_argument("--only", default="", help="comma list of pool,unpool,wunpool,add,drop64,wg64,wu64")
+    ap.add_argument("--only", default="", help="comma list of pool,unpool,wunpool,add,drop64,wg64,wu64,wg32")
     a = ap.parse_args()
     from acfe._lib import call, lib
     from acfe._torch import ptr, stream
@@ -89,7 +89,7 @@ def main():
         torch.cuda.empty_cache()
     # 64 x 128 layers: conv2b 128->64 + add, and 64->64 conv21 (+dropout, BN sums)
     H, W = 64, 128
-    for C, K, kind in ((128, 64, "add"), (64, 64, "add"), (64, 64, "drop64"), (64, 64, "wg64"), (128, 64, "wu64")):
+    for C, K, kind in ((128, 64, "add"), (64, 64, "add"), (64, 64, "drop64"), (64, 64, "wg64"), (128, 64, "wu64"), (128, 32, "wg32")):
         if only and kind not in only:
             continue
         flops = 2.0 * N * H * W * K * 9 * C
@@ -114,11 +114,15 @@ def main():
                    lambda: call("acfe_conv2d_wgrad_unpool", ptr(x), N, H, W, C, ptr(gp), ptr(amr), K, 1, 1, ptr(dw),
                                 0.0, 1, ptr(ws), stream()), [dw])
             del ws, dw, gp, amr
-        elif kind == "wg64":  # the 64 -> 64 weight gradient (k_wgrad3x3_halo<64, false>)
+        elif kind == "wg64" or kind == "wg32":  # 64 -> 64 @ 64x128, 128 -> 32 @ 32x64 (stage-2 branch21)
+            if kind == "wg32":
+                H, W = 32, 64
+                flops = 2.0 * N * H * W * K * 9 * C
+                x = (torch.randn((N, H, W, C), generator=g) * 0.5).to(bf).to(dev)
             ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=dev)
             dw = torch.empty((K, 3, 3, C), device=dev)
             dy = (torch.randn((N, H, W, K), generator=g) * 0.5).to(bf).to(dev)
-            report(f"wgrad 3x3 {C}->{K} @64x128", flops,
+            report(f"wgrad 3x3 {C}->{K} @{H}x{W}", flops,
                    lambda: call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy), K, 3, 3, 1, 1, 1, H, W, ptr(dw), 0.0, 1,
                                 ptr(ws), stream()), [dw])
             del ws, dw, dy
