@@ -3568,7 +3568,7 @@ static bool rows128_xres() {
 static int rows64_xres() {
   static const int v = [] {
     const char* e = getenv("ACFE_ROWS64_XRES");
-    const int t = e ? atoi(e) : 6;  // (8 rows: fwd_add 128->64 0.89 vs 0.92 ms, dropout 0.53 vs 0.56, r02ay -- but the BN-prologue kernels stay at 6 rows and the prologue/unfused bit-identity tests compare per-tile statistics slabs)
+    const int t = e ? atoi(e) : 8;  // 8 rows (BN-prologue kernels too, so prologue and plain paths tile alike): r02ay fwd_add 128->64 0.89 vs 0.92 ms, dropout 0.53 vs 0.56
     return t == 6 || t == 8 ? t : 0;
   }();
   return v;
@@ -3606,7 +3606,10 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
   }
   if constexpr (KB == 64 && PM != 2) {
     // BatchNormalization prologue (acfe_conv2d_bn_prologue_supported): 6 chunk-resident rows
-    if (g.pro_sc) return launch_rows_tr<KB, PM, 6, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+    if (g.pro_sc) {
+      if (rows64_xres() == 8) return launch_rows_tr<KB, PM, 8, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+      return launch_rows_tr<KB, PM, 6, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+    }
   }
   if constexpr (KB == 64) {
     const int xr = rows64_xres();
