@@ -24,6 +24,10 @@ SIGNATURES: dict[str, list] = {
     "acfe_version": [],
     "acfe_last_error": [],
     "acfe_crc32c": [P, C.c_size_t, C.c_uint32],
+    "acfe_tfr_open": [C.c_char_p, I32, P],
+    "acfe_tfr_next": [P, I32, P, P],
+    "acfe_tfr_close": [P],
+    "acfe_example_audio": [P, C.c_uint64, C.c_char_p, P, I64, P, I32, P],
     "acfe_mel_filterbank": [I32, I32, F64, F64, I32, F64, P],
     "acfe_plan_create": [I32, I32, I32, I32, F64, F64, F64, P, P],
     "acfe_plan_destroy": [P],
@@ -31,6 +35,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_normalize_stats": [P, I64, I32, I32, P, P],
     "acfe_normalize_apply": [P, I64, I32, I32, P, P, P],
     "acfe_mixup": [P, P, P, P, P, I32, I32, P, P],
+    "acfe_gather_rows": [P, I64, I64, P, I32, I32, P, I64, P],
     "acfe_mel_fwd": [P, P, I64, I32, I32, P, I32, I32, P, I32, P],
     "acfe_mel_from_spec": [P, P, I64, I32, I32, I32, I32, P, I32, P],
     "acfe_pcen_partials": [I32, I32],
@@ -113,6 +118,7 @@ PAD_END, PAD_CENTER_CONSTANT, PAD_CENTER_REFLECT = 0, 1, 2
 LAYOUT_BTM, LAYOUT_BMT = 0, 1
 DTYPE_F32, DTYPE_BF16 = 0, 1
 E_INVAL = -1000
+E_IO, E_CORRUPT = -1002, -1003
 
 
 class AcfeError(RuntimeError):

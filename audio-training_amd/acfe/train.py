@@ -158,7 +158,10 @@ class Trainer:
             arena_ptrs = {p.data_ptr() for p in self.arena.params}
             log = [e for e in log if e[0].data_ptr() in arena_ptrs]
             if log and len({d for _, d, _ in log}) == 1:
-                self.packer = ops.WeightPacker(log, self.device)
+                try:
+                    self.packer = ops.WeightPacker(log, self.device)
+                except ValueError:  # beyond the batch kernel's 256 packings: keep per-call packing
+                    self.pack_once = False
         self.opt.step(grad_scale=scale)
         return loss, z
 

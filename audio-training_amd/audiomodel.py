@@ -181,15 +181,19 @@ def train_model(args):
             trainer.holder.load_state_dict(sd)
     files, rshard = shard_files(tfdataset._files(td / "train"), rank, world)
     load_raw = bool(args.load_raw)
-    train_ds = tfdataset.AudioDataset(files, labels, batch_size=args.batch_size, shuffle=args.shuffle,
-                                      augment=args.augment and load_raw, device=dev, drop_remainder=world > 1,
-                                      seed=args.seed, record_shard=rshard, load_raw=load_raw)
+    # tfdataset.get_dataset (audiomodel.py:1607-1621): this rank's share of the
+    # shards; epoch_size = the examples one epoch of this rank yields
+    train_ds, _, epoch_size, _, _ = tfdataset.get_dataset(
+        td / "train", labels, files=files, record_shard=rshard, batch_size=args.batch_size, shuffle=args.shuffle,
+        augment=args.augment and load_raw, device=dev, drop_remainder=world > 1, seed=args.seed, load_raw=load_raw)
+    logging.info("rank %d: %d training examples, %d batches per epoch", rank, epoch_size, len(train_ds))
     val_dir = td / "validation"
     val_ds = None
     if val_dir.exists() and tfdataset._files(val_dir):
         vfiles, vshard = shard_files(tfdataset._files(val_dir), rank, world)
-        val_ds = tfdataset.AudioDataset(vfiles, labels, batch_size=args.batch_size, shuffle=False, device=dev,
-                                        record_shard=vshard, load_raw=load_raw)
+        val_ds, _, _, _, _ = tfdataset.get_dataset(val_dir, labels, files=vfiles, record_shard=vshard,
+                                                   batch_size=args.batch_size, shuffle=False, device=dev,
+                                                   load_raw=load_raw)
     history = {"loss": [], "val_loss": [], "val_accuracy": [], "clips_per_s": []}
     out_dir = Path(args.checkpoint_dir) / args.name
     best = float("inf")

@@ -264,6 +264,43 @@ ACFE_API int acfe_mixup(const float* x1, const float* s1, const float* x2, const
   return launch_rc("acfe_mixup");
 }
 
+// Batch assembly from the loader's device-resident clip pool (tfdataset
+// AudioDataset): out[i][0:n) = pool[idx[i] * pool_stride + 0:n), 16-B vectors
+// when both strides and n are multiples of 4 floats.
+__global__ void k_gather_rows4(const float4* __restrict__ pool, int64_t ps4, const int* __restrict__ idx, int n4,
+                               float4* __restrict__ out, int64_t os4) {
+  const int b = blockIdx.y;
+  const float4* src = pool + (int64_t)idx[b] * ps4;
+  float4* dst = out + (int64_t)b * os4;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) dst[i] = src[i];
+}
+__global__ void k_gather_rows1(const float* __restrict__ pool, int64_t ps, const int* __restrict__ idx, int n,
+                               float* __restrict__ out, int64_t os) {
+  const int b = blockIdx.y;
+  const float* src = pool + (int64_t)idx[b] * ps;
+  float* dst = out + (int64_t)b * os;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) dst[i] = src[i];
+}
+
+ACFE_API int acfe_gather_rows(const float* pool, int64_t pool_stride, int64_t pool_rows, const int* idx_dev,
+                              int batch, int n, float* out, int64_t out_stride, void* stream) {
+  if (!pool || !idx_dev || !out || batch < 0 || batch > 65535 || n <= 0 || pool_rows <= 0 ||
+      pool_stride < n || out_stride < n)
+    return ACFE_E_INVAL;
+  if (batch == 0) return ACFE_OK;
+  const bool v4 = (pool_stride % 4 == 0) && (out_stride % 4 == 0) && (n % 4 == 0) &&
+                  ((uintptr_t)pool % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (v4) {
+    hipLaunchKernelGGL(k_gather_rows4, dim3(cdiv(n / 4, 256 * 8), batch), dim3(256), 0, strm(stream),
+                       reinterpret_cast<const float4*>(pool), pool_stride / 4, idx_dev, n / 4,
+                       reinterpret_cast<float4*>(out), out_stride / 4);
+  } else {
+    hipLaunchKernelGGL(k_gather_rows1, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, strm(stream), pool,
+                       pool_stride, idx_dev, n, out, out_stride);
+  }
+  return launch_rc("acfe_gather_rows");
+}
+
 // ------------------------------------------------------------ FFT helpers
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }

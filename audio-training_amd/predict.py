@@ -93,6 +93,7 @@ def track_windows(frames, sr, tracks, segment_length=3, stride=1, fmin=100, fmax
         start, end = 0, segment_length
         sr_end, sr_start = int(t.end * sr), int(sr * t.start)
         if pad_short_tracks:
+            end = min(end, t.length)  # predict_utils.py:75-77
             track_frames = frames[sr_start:sr_end]
         else:  # centre short tracks in one window
             missing = sample_size - (sr_end - sr_start)

@@ -2,20 +2,44 @@
 
 get_dataset(dir, labels, global_epoch=None, **args) keeps the reference
 signature and return tuple (dataset, remapped, epoch_size, labels,
-extra_label_map).  The dataset reads the GZIP TFRecord shards of `dir`
-(audio/raw [144000] f32, audio/class/text, ...; tfdataset.py:1005-1060) with a
-pool of reader threads (zlib releases the GIL), assembles batches in pinned
-host memory and hands out DEVICE tensors: x [B, 144000] fp32 raw audio (the
-normalize / mix_up / STFT / mel work happens on the GPU, acfe.train.FrontEnd)
-and y [B, len(labels)] one-hot.  With augment=True each item is a pair of
-batches for mix_up (tfdataset.py:473-481).
+extra_label_map).  The dataset hands out DEVICE batches: x [B, 144000] fp32 raw
+audio (normalize / mix_up / STFT / mel run on the GPU, acfe.train.FrontEnd), or
+[B, 2049, 513] stored magnitude spectrograms (load_raw=False), and y
+[B, len(labels)] one-hot; with augment=True each item is a pair of batches for
+mix_up (tfdataset.py:473-481).
+
+Pipeline (every record is inflated and parsed ONCE):
+
+  reader threads   native shard reader (tfrecord.ShardReader: libdeflate
+                   inflate, hardware CRC-32C) + acfe_example_audio, which
+                   copies the record's floats straight into a slot of a
+                   pinned staging chunk (no per-clip Python copies; ctypes
+                   drops the GIL inside both calls)
+  mover thread     one host->device copy per full chunk (64 clips) on a side
+                   stream into a frame of the device-resident clip pool
+  consumer         the pool is the shuffle buffer (tfdataset.py:835-838,
+                   4096 examples): a batch is B slots drawn uniformly from the
+                   resident clips and gathered on the device
+                   (acfe_gather_rows); each example is a primary exactly once
+                   per epoch (one pass, as the reference's dataset)
+
+mix_up partners.  The reference zips a second, independently shuffled full
+pass over the same records (tfdataset.py:473-480), i.e. it decodes every
+record twice to pair each example with a random other example.  Here the
+partner batch is B clips drawn uniformly from the same resident pool (the
+primaries of the current batch included, as an independent pass may also
+return them) and gathered on the device: the same distribution of pairs
+(uniform over the dataset, up to the shuffle-buffer locality both pipelines
+have), without the second decode.
 """
 from __future__ import annotations
 
+import ctypes
 import logging
 import queue
 import random
 import threading
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 import numpy as np
@@ -27,13 +51,102 @@ N_SAMPLES = 48000 * 3
 HOP_LENGTH, NFFT, SR, BREAK_FREQ, FMIN, FMAX = 281, 4096, 48000, 1000, 100, 11000  # tfdataset.py:42-56
 N_MELS = 160
 DIMENSIONS = (160, 513, 1)
+SPEC_SHAPE = (2049, 513)
+SHUFFLE_BUFFER = 4096          # ds.shuffle(4096) per dataset, tfdataset.py:835-838
+CHUNK_BYTES = 64 << 20         # pinned staging chunk (64 raw clips)
+POOL_BYTES = 6 << 30           # cap of the device-resident shuffle pool
+_POLL = 0.1                    # seconds between stop-flag checks of blocked threads
+_TEXT_CAP = 256
+
+
+def _lib():
+    from acfe._lib import lib
+
+    return lib
+
+
+class _Stop(Exception):
+    pass
+
+
+class _Staging:
+    """Pinned host chunks of `per` slots that reader threads fill concurrently.
+    claim() hands out (chunk, slot) positions of the chunk being filled;
+    commit() records the slot's label (-1 = filtered out after the copy); a
+    chunk whose positions are all handed out and committed goes to `full`."""
+
+    def __init__(self, buf, stop):
+        nchunks, per = buf.shape[0], buf.shape[1]
+        self.per, self.stop = per, stop
+        self.buf = buf
+        self.free: queue.Queue = queue.Queue()
+        for c in range(nchunks):
+            self.free.put(c)
+        self.full: queue.Queue = queue.Queue()
+        self.lock = threading.Lock()
+        self.cur = None
+        self.pos = 0
+        self.pending = [0] * nchunks
+        self.sealed = [False] * nchunks
+        self.count = [0] * nchunks
+        self.labels = np.full((nchunks, per), -1, np.int32)
+
+    def claim(self):
+        while True:
+            with self.lock:
+                if self.cur is not None:
+                    c, p = self.cur, self.pos
+                    self.pos += 1
+                    self.pending[c] += 1
+                    if self.pos == self.per:
+                        self._seal(c, self.per)
+                    return c, p
+            try:  # wait for a free chunk without holding the lock
+                c = self.free.get(timeout=_POLL)
+            except queue.Empty:
+                if self.stop.is_set():
+                    raise _Stop
+                continue
+            with self.lock:
+                if self.cur is None:
+                    self.cur, self.pos = c, 0
+                    self.labels[c].fill(-1)
+                    self.sealed[c] = False
+                else:  # another thread opened one meanwhile
+                    self.free.put(c)
+
+    def _seal(self, c, n):  # lock held
+        self.cur = None
+        self.sealed[c] = True
+        self.count[c] = n
+        if self.pending[c] == 0:
+            self.full.put(c)
+
+    def commit(self, c, p, label):
+        with self.lock:
+            self.labels[c, p] = label
+            self.pending[c] -= 1
+            if self.sealed[c] and self.pending[c] == 0:
+                self.full.put(c)
+
+    def flush(self):
+        """All readers are done: seal the partially filled chunk."""
+        with self.lock:
+            if self.cur is not None:
+                c, n = self.cur, self.pos
+                if n == 0:
+                    self.cur = None
+                    self.free.put(c)
+                else:
+                    self._seal(c, n)
 
 
 class AudioDataset:
     """Iterable over device batches; one pass = one epoch."""
 
     def __init__(self, files, labels, batch_size=32, shuffle=True, augment=False, device=None, threads=8,
-                 drop_remainder=False, seed=0, label_map=None, record_shard=None, load_raw=True):
+                 drop_remainder=False, seed=0, label_map=None, record_shard=None, load_raw=True,
+                 shuffle_buffer=SHUFFLE_BUFFER, epoch_size=None):
         """record_shard=(rank, world): keep only the records whose (file index
         + record index) % world == rank -- data-parallel sharding when there
         are fewer shard files than ranks (otherwise ranks take whole files).
@@ -45,103 +158,311 @@ class AudioDataset:
         self.load_raw = load_raw
         if not load_raw:
             augment = False
-        self.batch_size, self.shuffle, self.augment = batch_size, shuffle, augment
-        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.threads, self.drop_remainder, self.seed = threads, drop_remainder, seed
+        self.batch_size, self.shuffle, self.augment = int(batch_size), shuffle, augment
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.threads, self.drop_remainder, self.seed = max(1, int(threads)), drop_remainder, seed
         self.label_index = {l: i for i, l in enumerate(self.labels)}
         self.label_map = label_map or {}
         self.epoch = 0
+        self.key = b"audio/raw" if load_raw else b"audio/spectogram"
+        self.shape = (N_SAMPLES,) if load_raw else SPEC_SHAPE
+        self.nfloats = int(np.prod(self.shape))
+        clip_bytes = 4 * self.nfloats
+        self.per_chunk = max(1, min(64, CHUNK_BYTES // clip_bytes))
+        buf = max(shuffle_buffer if shuffle else 0, self.batch_size)
+        buf = min(buf, max(self.batch_size, POOL_BYTES // clip_bytes))
+        self.buffer = buf
+        self.frames = -(-(buf + self.batch_size) // self.per_chunk) + 2
+        self._epoch_size = epoch_size
+        self._pool = None
+        self._stage_buf = None
+        self.error = None
 
-    def _examples(self, files):
-        q: queue.Queue = queue.Queue(maxsize=4 * self.batch_size)
-        DONE = object()
-        idx = iter(range(len(files)))
-        lock = threading.Lock()
-        stable = {f: i for i, f in enumerate(self.files)}
+    # ---------------------------------------------------------------- counting
+    def _label_of(self, text: str):
+        lab = self.label_map.get(text, text)
+        return self.label_index.get(lab)
+
+    def _keep(self, i, r):
         shard = self.record_shard
+        return shard is None or (i + r) % shard[1] == shard[0]
 
-        def worker():
-            while True:
-                with lock:
-                    i = next(idx, None)
-                if i is None:
-                    q.put(DONE)
-                    return
-                for r, rec in enumerate(tfr.read_records(files[i], ignore_errors=True)):  # tfdataset.py:226
-                    if shard is not None and (stable.get(files[i], i) + r) % shard[1] != shard[0]:
-                        continue
-                    ex = tfr.parse_audio_example(rec, load_raw=self.load_raw)
-                    x = ex["raw"] if self.load_raw else ex["spectrogram"]
-                    if not np.all(np.isfinite(x)):  # NaN/Inf filter, tfdataset.py:297
-                        continue
-                    lab = self.label_map.get(ex["text"], ex["text"])
-                    if lab not in self.label_index:
-                        continue
-                    q.put((x, self.label_index[lab]))
+    def _count_file(self, i, path):
+        lib = _lib()
+        text = ctypes.create_string_buffer(_TEXT_CAP)
+        cnt = ctypes.c_int64()
+        scratch = np.empty(self.nfloats, np.float32)  # the NaN / Inf filter needs the values
+        n = 0
+        try:
+            with tfr.ShardReader(path) as rd:
+                r = 0
+                while True:
+                    try:
+                        rec = rd.next()
+                    except IOError:
+                        break
+                    if rec is None:
+                        break
+                    if self._keep(i, r):
+                        fl = lib.acfe_example_audio(rec[0], rec[1], self.key, scratch.ctypes.data, self.nfloats,
+                                                    text, _TEXT_CAP, ctypes.byref(cnt))
+                        if fl >= 0 and fl & 2 and self._label_of(text.value.decode(errors="replace")) is not None:
+                            n += 1
+                    r += 1
+        except IOError as e:
+            logging.warning("skipping unreadable shard %s: %s", path, e)
+        return n
 
-        ts = [threading.Thread(target=worker, daemon=True) for _ in range(min(self.threads, max(1, len(files))))]
-        for t in ts:
-            t.start()
-        live = len(ts)
-        while live:
-            item = q.get()
-            if item is DONE:
-                live -= 1
-                continue
-            yield item
-
-    def _batches(self):
-        files = list(self.files)
-        rng = random.Random(self.seed + self.epoch)
-        if self.shuffle:
-            rng.shuffle(files)
-        buf = []
-        pool = []
-        for ex in self._examples(files):
-            pool.append(ex)
-            if self.shuffle and len(pool) < 4 * self.batch_size:  # shuffle buffer, tfdataset.py:835-890
-                continue
-            j = rng.randrange(len(pool)) if self.shuffle else 0
-            buf.append(pool.pop(j))
-            if len(buf) == self.batch_size:
-                yield buf
-                buf = []
-        while pool:
-            buf.append(pool.pop(rng.randrange(len(pool)) if self.shuffle else 0))
-            if len(buf) == self.batch_size:
-                yield buf
-                buf = []
-        if buf and not self.drop_remainder:
-            yield buf
-
-    def _to_device(self, items):
-        b = len(items)
-        pin = torch.device(self.device).type == "cuda"
-        x = torch.empty((b,) + tuple(items[0][0].shape), dtype=torch.float32, pin_memory=pin)
-        y = torch.zeros((b, len(self.labels)), dtype=torch.float32, pin_memory=pin)
-        for i, (raw, lab) in enumerate(items):
-            x[i] = torch.from_numpy(raw)
-            y[i, lab] = 1.0
-        return x.to(self.device, non_blocking=True), y.to(self.device, non_blocking=True)
-
-    def __iter__(self):
-        it = self._batches()
-        self.epoch += 1
-        if not self.augment:
-            for items in it:
-                yield self._to_device(items)
-            return
-        # second independent pass over the data for mix_up (tfdataset.py:473-480)
-        other = AudioDataset(self.files, self.labels, self.batch_size, True, False, self.device, self.threads,
-                             self.drop_remainder, self.seed + 7919 * self.epoch, self.label_map, self.record_shard,
-                             self.load_raw)
-        for a, b in zip(it, other._batches()):
-            if len(a) != len(b):
-                break
-            yield self._to_device(a), self._to_device(b)
+    def count(self) -> int:
+        """Examples one epoch yields (the reference's epoch_size, computed by
+        its get_distribution pass over the dataset, tfdataset.py:853-857):
+        records of this rank's share whose label is kept and whose float
+        feature has the expected size and is finite (the filters of
+        read_tfrecord / filter_nan_samples, tfdataset.py:297)."""
+        if self._epoch_size is None:
+            stable = {f: i for i, f in enumerate(self.files)}
+            with ThreadPoolExecutor(min(self.threads, max(1, len(self.files)))) as ex:
+                self._epoch_size = sum(ex.map(lambda f: self._count_file(stable[f], f), self.files))
+        return self._epoch_size
 
     def __len__(self):
-        return -1
+        n = self.count()
+        b = self.batch_size
+        return n // b if self.drop_remainder else -(-n // b)
+
+    # ---------------------------------------------------------------- readers
+    def _reader(self, files, stage: _Staging, stop, stable):
+        lib = _lib()
+        text = ctypes.create_string_buffer(_TEXT_CAP)
+        cnt = ctypes.c_int64()
+        row = stage.buf[0, 0].numel()
+        base = stage.buf.data_ptr()
+        while not stop.is_set():
+            try:
+                path = files.get_nowait()
+            except queue.Empty:
+                return
+            i = stable.get(path, 0)
+            try:
+                with tfr.ShardReader(path) as rd:
+                    r = -1
+                    while not stop.is_set():
+                        r += 1
+                        try:
+                            rec = rd.next()
+                        except IOError:  # corrupt record: the rest of the file is dropped (tfdataset.py:226)
+                            logging.warning("corrupt record %d in %s: rest of the file skipped", r, path)
+                            break
+                        if rec is None:
+                            break
+                        if not self._keep(i, r):
+                            continue
+                        fl = lib.acfe_example_audio(rec[0], rec[1], self.key, None, self.nfloats, text, _TEXT_CAP,
+                                                    ctypes.byref(cnt))
+                        if fl < 0 or not fl & 1 or cnt.value != self.nfloats:
+                            continue
+                        lab = self._label_of(text.value.decode(errors="replace"))
+                        if lab is None:
+                            continue
+                        c, p = stage.claim()
+                        dst = base + ((c * stage.per + p) * row) * 4
+                        fl = lib.acfe_example_audio(rec[0], rec[1], self.key, dst, self.nfloats, None, 0,
+                                                    ctypes.byref(cnt))
+                        # NaN / Inf filter (tfdataset.py:297): the slot stays empty
+                        stage.commit(c, p, lab if fl >= 0 and fl & 2 else -1)
+            except _Stop:
+                return
+            except Exception as e:  # noqa: BLE001 -- an unreadable shard ends that file, not the epoch
+                logging.warning("skipping shard %s: %s", path, e)
+
+    # ---------------------------------------------------------------- pool
+    def _ensure_pool(self):
+        if self._pool is None:
+            rows = self.frames * self.per_chunk
+            self._pool = torch.empty((rows, self.nfloats), dtype=torch.float32, device=self.device)
+        return self._pool
+
+    def _mover(self, stage: _Staging, ready: queue.Queue, free_frames: queue.Queue, stop, readers_done):
+        """Full pinned chunks -> device pool frames (one copy per chunk)."""
+        try:
+            cuda = self.device.type == "cuda"
+            cs = torch.cuda.Stream(self.device) if cuda else None
+            pool = self._pool
+            while True:
+                try:
+                    c = stage.full.get(timeout=_POLL)
+                except queue.Empty:
+                    if stop.is_set():
+                        return
+                    if readers_done.is_set() and stage.full.empty():
+                        with stage.lock:
+                            idle = stage.cur is None and not any(stage.pending)
+                        if idle:
+                            ready.put(None)
+                            return
+                    continue
+                n = stage.count[c]
+                labels = stage.labels[c, :n].copy()
+                while True:
+                    try:
+                        f, ev = free_frames.get(timeout=_POLL)
+                        break
+                    except queue.Empty:
+                        if stop.is_set():
+                            return
+                lo = f * self.per_chunk
+                if cuda:
+                    with torch.cuda.stream(cs):
+                        if ev is not None:
+                            cs.wait_event(ev)  # the gathers that read this frame last are done
+                        pool[lo:lo + n].copy_(stage.buf[c, :n], non_blocking=True)
+                        done = torch.cuda.Event()
+                        done.record(cs)
+                    done.synchronize()
+                else:
+                    pool[lo:lo + n].copy_(stage.buf[c, :n])
+                stage.free.put(c)
+                ready.put((f, labels))
+        except Exception as e:  # noqa: BLE001
+            self.error = e
+            logging.exception("loader mover thread failed")
+            ready.put(None)
+
+    def _stream(self, augment):
+        """Generator of (x1 idx, x2 idx or None, labels) batches for one epoch."""
+        files = list(self.files)
+        rng = random.Random(self.seed + 1000003 * self.epoch)
+        if self.shuffle:
+            rng.shuffle(files)  # load_dataset shuffles the file names (tfdataset.py:195-197)
+        stable = {f: i for i, f in enumerate(self.files)}
+        stop, readers_done = threading.Event(), threading.Event()
+        if self._stage_buf is None:  # pinned once per dataset, reused every epoch
+            self._stage_buf = torch.empty((max(4, self.threads // 2), self.per_chunk, self.nfloats),
+                                          dtype=torch.float32, pin_memory=self.device.type == "cuda")
+        stage = _Staging(self._stage_buf, stop)
+        self.error = None
+        pool = self._ensure_pool()
+        fq: queue.Queue = queue.Queue()
+        for f in files:
+            fq.put(f)
+        free_frames: queue.Queue = queue.Queue()
+        for f in range(self.frames):
+            free_frames.put((f, None))
+        ready: queue.Queue = queue.Queue()
+        nthreads = min(self.threads, max(1, len(files)))
+        readers = [threading.Thread(target=self._reader, args=(fq, stage, stop, stable), daemon=True)
+                   for _ in range(nthreads)]
+        for t in readers:
+            t.start()
+
+        def watch():
+            for t in readers:
+                t.join()
+            stage.flush()
+            readers_done.set()
+
+        watcher = threading.Thread(target=watch, daemon=True)
+        watcher.start()
+        mover = threading.Thread(target=self._mover, args=(stage, ready, free_frames, stop, readers_done),
+                                 daemon=True)
+        mover.start()
+        per = self.per_chunk
+        live: list[int] = []                   # pool rows not yet used as a primary this epoch
+        left = [0] * self.frames               # unconsumed valid rows per frame
+        lab = np.full(self.frames * per, -1, np.int32)
+        target = self.buffer if self.shuffle else self.batch_size
+        done = False
+        try:
+            while True:
+                while not done and len(live) < target:
+                    item = ready.get()
+                    if item is None:
+                        done = True
+                        break
+                    f, labels = item
+                    rows = [f * per + j for j in range(len(labels)) if labels[j] >= 0]
+                    lab[f * per:f * per + len(labels)] = labels
+                    left[f] = len(rows)
+                    if not rows:
+                        free_frames.put((f, None))
+                        continue
+                    live.extend(rows)
+                if self.error is not None:
+                    raise RuntimeError("TFRecord loader failed") from self.error
+                if len(live) < self.batch_size:  # the stream has ended (the fill loop stops only then)
+                    if not live or self.drop_remainder:
+                        return
+                b = min(self.batch_size, len(live))
+                if self.shuffle:
+                    pick = []
+                    for _ in range(b):  # uniform draw without replacement (swap-remove)
+                        j = rng.randrange(len(live))
+                        live[j], live[-1] = live[-1], live[j]
+                        pick.append(live.pop())
+                else:
+                    pick, live = live[:b], live[b:]
+                partner = None
+                if augment:
+                    resident = live + pick
+                    partner = [resident[rng.randrange(len(resident))] for _ in range(b)]
+                drained = set()
+                for r in pick:
+                    f = r // per
+                    left[f] -= 1
+                    if left[f] == 0:
+                        drained.add(f)
+                yield pick, partner, lab, drained, free_frames
+        finally:
+            stop.set()
+            for t in readers + [watcher, mover]:
+                t.join(timeout=5)
+
+    def _labels(self, rows, lab):
+        """One-hot labels, copied to the device asynchronously from pinned
+        memory (a pageable source would make the copy wait for the queue)."""
+        cuda = self.device.type == "cuda"
+        y = torch.zeros((len(rows), len(self.labels)), dtype=torch.float32, pin_memory=cuda)
+        y[torch.arange(len(rows)), torch.from_numpy(lab[np.asarray(rows)].astype(np.int64))] = 1.0
+        return y.to(self.device, non_blocking=True)
+
+    def _gather(self, rows):
+        pool = self._pool
+        b = len(rows)
+        idx = np.asarray(rows, np.int32)
+        assert idx.min() >= 0 and idx.max() < pool.shape[0]
+        if self.device.type != "cuda":
+            return pool.index_select(0, torch.from_numpy(idx.astype(np.int64))).reshape((b,) + self.shape)
+        from acfe._lib import call
+        from acfe._torch import stream
+
+        idx_dev = torch.from_numpy(idx).pin_memory().to(self.device, non_blocking=True)
+        out = torch.empty((b,) + self.shape, dtype=torch.float32, device=self.device)
+        call("acfe_gather_rows", pool.data_ptr(), self.nfloats, pool.shape[0], idx_dev.data_ptr(), b, self.nfloats,
+             out.data_ptr(), self.nfloats, stream())
+        return out
+
+    def __iter__(self):
+        augment = self.augment
+        self.epoch += 1
+        n = 0
+        for pick, partner, lab, drained, free_frames in self._stream(augment):
+            x1 = self._gather(pick)
+            y1 = self._labels(pick, lab)
+            if augment:
+                x2 = self._gather(partner)
+                y2 = self._labels(partner, lab)
+            # frames whose every row has now been used as a primary go back to
+            # the mover once the gathers above have run (stream-ordered event)
+            for f in drained:
+                ev = None
+                if self.device.type == "cuda":
+                    ev = torch.cuda.Event()
+                    ev.record()
+                free_frames.put((f, ev))
+            n += len(pick)
+            yield ((x1, y1), (x2, y2)) if augment else (x1, y1)
+        if self._epoch_size is None and self.record_shard is None:
+            self._epoch_size = n
 
 
 def _files(dir):
@@ -151,11 +472,27 @@ def _files(dir):
 
 
 def count_examples(dir) -> int:
-    return sum(1 for f in _files(dir) for _ in tfr.read_records(f, ignore_errors=True))
+    n = 0
+    for f in _files(dir):
+        with tfr.ShardReader(f) as rd:
+            while True:
+                try:
+                    if rd.next() is None:
+                        break
+                except IOError:
+                    break
+                n += 1
+    return n
 
 
 def get_dataset(dir, labels, global_epoch=None, **args):
-    """tfdataset.get_dataset (tfdataset.py:429-506) -> (dataset, remapped, epoch_size, labels, extra_label_map)."""
+    """tfdataset.get_dataset (tfdataset.py:429-506) -> (dataset, remapped,
+    epoch_size, labels, extra_label_map).  epoch_size is the number of
+    examples one epoch yields (the reference counts them with a full pass,
+    get_distribution, :853-857; here a header-only pass of the native reader,
+    or args["epoch_size"] when the caller already knows it).  Extra keys
+    accepted here: device, threads, seed, label_map, record_shard, files,
+    drop_remainder, shuffle_buffer."""
     global N_MELS, FMIN, FMAX, NFFT, BREAK_FREQ
     if args.get("n_mels"):
         N_MELS = args["n_mels"]
@@ -165,15 +502,18 @@ def get_dataset(dir, labels, global_epoch=None, **args):
         NFFT = args["n_fft"]
     if args.get("break_freq") is not None:
         BREAK_FREQ = args["break_freq"]
-    files = _files(dir)
+    files = args.get("files") or _files(dir)
     if not files:
         raise FileNotFoundError(f"no *.tfrecord under {dir}")
     labels = list(labels)
     remapped = {l: [l] for l in labels}
-    epoch_size = args.get("epoch_size") or None
-    ds = AudioDataset(files, labels, batch_size=args.get("batch_size", 32), shuffle=args.get("shuffle", True),
-                      augment=args.get("augment", False), device=args.get("device"),
+    load_raw = args.get("load_raw", True)
+    ds = AudioDataset(files, labels, batch_size=args.get("batch_size") or 32, shuffle=args.get("shuffle", True),
+                      augment=args.get("augment", False) and load_raw, device=args.get("device"),
                       threads=args.get("threads", 8), seed=args.get("seed", 0),
-                      label_map=args.get("label_map"), load_raw=args.get("load_raw", True))
-    logging.info("dataset %s: %d shards, %d labels", dir, len(files), len(labels))
+                      drop_remainder=args.get("drop_remainder", False), label_map=args.get("label_map"),
+                      record_shard=args.get("record_shard"), load_raw=load_raw,
+                      shuffle_buffer=args.get("shuffle_buffer", SHUFFLE_BUFFER), epoch_size=args.get("epoch_size"))
+    epoch_size = ds.count()
+    logging.info("dataset %s: %d shards, %d labels, %d examples", dir, len(files), len(labels), epoch_size)
     return ds, remapped, epoch_size, labels, {}

@@ -11,9 +11,8 @@ fields, packed floats/int64s); CRC-32C comes from libacfe (host C code).
 """
 from __future__ import annotations
 
+import ctypes
 import gzip
-import zlib
-import io
 import struct
 from typing import Iterable, Iterator
 
@@ -194,78 +193,71 @@ class TFRecordWriter:
         self.close()
 
 
-class _InflateReader:
-    """Sequential reader over a GZIP file inflated in 8 MiB chunks by one
-    zlib object (gzip.GzipFile inflates 8 KiB per call, each call taking the
-    GIL: with several reader threads the loader ran slower than with one)."""
+class ShardReader:
+    """One TFRecord shard through the native reader (acfe_tfr_* in libacfe:
+    whole-file inflate with libdeflate, hardware CRC-32C); records are
+    zero-copy (pointer, length) views valid until close().  ctypes releases
+    the GIL inside every call, so reader threads inflate and parse in
+    parallel."""
 
-    CHUNK = 8 << 20
+    def __init__(self, path, compression: str | None = "GZIP"):
+        from acfe._lib import lib
 
-    def __init__(self, path):
-        self.f = open(path, "rb")
-        self.z = zlib.decompressobj(wbits=47)  # gzip or zlib header, multi-member via restart below
-        self.buf = bytearray()
-        self.pos = 0
-        self.eof = False
+        self._lib = lib
+        self._h = ctypes.c_void_p()
+        rc = lib.acfe_tfr_open(str(path).encode(), 1 if compression == "GZIP" else 0, ctypes.byref(self._h))
+        if rc < 0:
+            self._h = None
+            raise IOError(f"cannot open TFRecord shard {path} (rc={rc})")
+        self._ptr = ctypes.c_void_p()
+        self._len = ctypes.c_uint64()
 
-    def _fill(self, need):
-        while len(self.buf) - self.pos < need and not self.eof:
-            chunk = self.f.read(self.CHUNK)
-            if self.pos:
-                del self.buf[:self.pos]
-                self.pos = 0
-            if not chunk:
-                self.buf += self.z.flush()
-                self.eof = True
-                break
-            out = self.z.decompress(chunk)
-            while self.z.eof and self.z.unused_data:  # concatenated gzip members
-                rest = self.z.unused_data
-                self.buf += out
-                self.z = zlib.decompressobj(wbits=47)
-                out = self.z.decompress(rest)
-            self.buf += out
+    def next(self, check_crc=True):
+        """(address, length) of the next record, None at a clean end; IOError on
+        a truncated / CRC-failing record (nothing after it is readable)."""
+        rc = self._lib.acfe_tfr_next(self._h, int(check_crc), ctypes.byref(self._ptr), ctypes.byref(self._len))
+        if rc == 1:
+            return self._ptr.value, self._len.value
+        if rc == 0:
+            return None
+        raise IOError("corrupt or truncated TFRecord")
 
-    def read(self, n):
-        self._fill(n)
-        b = bytes(self.buf[self.pos:self.pos + n])
-        self.pos += len(b)
-        return b
+    def close(self):
+        if self._h is not None:
+            self._lib.acfe_tfr_close(self._h)
+            self._h = None
 
     def __enter__(self):
         return self
 
     def __exit__(self, *a):
-        self.f.close()
+        self.close()
+
+    def __del__(self):
+        self.close()
 
 
 def read_records(path, compression: str | None = "GZIP", check_crc=True, ignore_errors=False) -> Iterator[bytes]:
     """tf.data.TFRecordDataset(path, compression_type="GZIP") record stream.
     ignore_errors mirrors tf.data.experimental.ignore_errors() (tfdataset.py:226):
-    a corrupt record ends the file instead of raising."""
-    opener = _InflateReader if compression == "GZIP" else (lambda p: open(p, "rb"))
-    with opener(path) as f:
+    an unreadable file or a corrupt record ends the file instead of raising."""
+    try:
+        r = ShardReader(path, compression)
+    except IOError:
+        if ignore_errors:
+            return
+        raise
+    with r:
         while True:
-            head = f.read(12)
-            if not head:
-                return
             try:
-                if len(head) < 12:
-                    raise IOError("truncated record header")
-                ln = struct.unpack("<Q", head[:8])[0]
-                if check_crc and struct.unpack("<I", head[8:])[0] != masked_crc(head[:8]):
-                    raise IOError("corrupt record length")
-                data = f.read(ln)
-                tail = f.read(4)
-                if len(data) < ln or len(tail) < 4:
-                    raise IOError("truncated record")
-                if check_crc and struct.unpack("<I", tail)[0] != masked_crc(data):
-                    raise IOError("corrupt record data")
-            except (IOError, OSError, EOFError, gzip.BadGzipFile, zlib.error):
+                rec = r.next(check_crc)
+            except IOError:
                 if ignore_errors:
                     return
                 raise
-            yield data
+            if rec is None:
+                return
+            yield ctypes.string_at(rec[0], rec[1])
 
 
 def write_records(path, records: Iterable[bytes], compression="GZIP") -> int:

@@ -69,6 +69,33 @@ const char* acfe_last_error(void);
  * (tfdataset.py:212-214).  No GPU involved. */
 uint32_t acfe_crc32c(const void* data, size_t n, uint32_t crc);
 
+/* ---- Native TFRecord reader (host code; replaces tf.data.TFRecordDataset(
+ * filenames, compression_type="GZIP") + ignore_errors(), tfdataset.py:212-226,
+ * and the parse of read_tfrecord, tfdataset.py:1005-1060).  Reentrant; one
+ * reader per thread.  Python calls these through ctypes, which releases the
+ * GIL for the call, so reader threads inflate and parse in parallel. */
+#define ACFE_E_IO (-1002)       /* file cannot be opened / read            */
+#define ACFE_E_CORRUPT (-1003)  /* framing, CRC or protobuf error          */
+typedef struct acfe_tfr_s* acfe_tfr_t;
+/* Open a shard (compression 1 = GZIP, 0 = none): the file is read and
+ * inflated whole into host memory owned by the reader. */
+int acfe_tfr_open(const char* path, int compression, acfe_tfr_t* reader);
+/* Next record: 1 and (*data_host, *len) pointing into the reader's buffer
+ * (valid until close); 0 at a clean end; ACFE_E_CORRUPT on a truncated or
+ * CRC-failing record (nothing after it is readable, as tf.data's
+ * ignore_errors() ends the file there). */
+int acfe_tfr_next(acfe_tfr_t reader, int check_crc, const uint8_t** data_host, uint64_t* len);
+int acfe_tfr_close(acfe_tfr_t reader);
+/* Fields of one tf.train.Example: the float_list of `float_key`
+ * ("audio/raw" [144000] or "audio/spectogram" [2049*513]) -> *count floats,
+ * copied to out_host when out_host != NULL and *count == n_out; the first
+ * value of "audio/class/text" -> text_host (NUL-terminated, truncated to
+ * text_cap).  Returns flags: 1 = float key present, 2 = copied and all
+ * finite (the NaN/Inf filter of tfdataset.py:297), 4 = text present; or
+ * ACFE_E_CORRUPT for a malformed message. */
+int acfe_example_audio(const uint8_t* rec, uint64_t len, const char* float_key, float* out_host,
+                       int64_t n_out, char* text_host, int text_cap, int64_t* count);
+
 /* custommel.mel_f restated in C (float64 arithmetic, float32 result) into a
  * caller-owned HOST array out_host[n_mels][1 + n_fft/2]. */
 int acfe_mel_filterbank(int sr, int n_mels, double fmin, double fmax, int n_fft,
@@ -97,6 +124,12 @@ int acfe_normalize_apply(const float* x, int64_t clip_stride, int batch, int n,
  * stats1/stats2 may be NULL (inputs already normalised). */
 int acfe_mixup(const float* x1, const float* stats1, const float* x2, const float* stats2,
                const float* lam, int batch, int n, float* y, void* stream);
+/* Batch assembly from a device-resident clip pool (the loader's shuffle
+ * buffer, tfdataset.py:835-838): out[i][0..n) = pool[idx_dev[i]][0..n) for
+ * i < batch; idx_dev (device int32) must hold row numbers < pool_rows (the
+ * caller checks them on the host before the launch). */
+int acfe_gather_rows(const float* pool, int64_t pool_stride, int64_t pool_rows, const int* idx_dev, int batch,
+                     int n, float* out, int64_t out_stride, void* stream);
 
 /* Fused framing -> periodic Hann -> n_fft real FFT (LDS radix-8/4 Stockham)
  * -> |X|^power (power 1 or 2) -> banded mel, for every frame of every clip.

@@ -136,3 +136,22 @@ def test_track_windows_follow_load_samples():
     w = predict.track_windows(tiny, SR, [it.Signal(0.1, 0.5, 1000, 3000, 1)], rng=np.random.RandomState(0))[0]
     nz = np.flatnonzero(w[0])
     assert w.shape == (1, n) and np.array_equal(w[0][nz[0]:nz[0] + SR], tiny)
+
+
+def test_track_windows_pad_short_tracks():
+    """pad_short_tracks=True (predict_utils.py:75-77): a short track is NOT
+    re-centred; its own samples are zero padded at a random offset into one
+    window, and a track longer than one window still gets one window per
+    stride while end <= its length."""
+    rng = np.random.default_rng(4)
+    frames = rng.standard_normal(SR * 12).astype(np.float32)
+    short = it.Signal(4.0, 5.0, 1000, 3000, 1)
+    long_ = it.Signal(1.0, 5.5, 1000, 3000, 1)
+    w = predict.track_windows(frames, SR, [short, long_], pad_short_tracks=True, rng=np.random.RandomState(1))
+    n = 3 * SR
+    assert w[0].shape == (1, n)
+    nz = np.flatnonzero(w[0][0])
+    assert np.array_equal(w[0][0][nz[0]:nz[0] + SR], frames[4 * SR:5 * SR])
+    assert w[1].shape == (2, n)  # windows at +0 and +1 s; +2 s would end past 4.5 s
+    for k in range(2):
+        assert np.array_equal(w[1][k], frames[(1 + k) * SR:(4 + k) * SR])
