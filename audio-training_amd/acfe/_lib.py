@@ -50,6 +50,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_fwd_dropout": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P, F32,
                                 C.c_uint64, P],
     "acfe_conv2d_dgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P],
+    "acfe_conv2d_dgrad_workspace": [I32] * 13,
     "acfe_conv2d_wgrad_workspace": [I32, I32, I32, I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_wgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, I32, P, P],
     "acfe_stem_blocks": [I32, I32, I32],
@@ -111,7 +112,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_loss": [P, P, I32, I32, I32, F32, P, P, P, P],
     "acfe_adam_step": [P, P, P, P, I64, F32, F32, F32, F32, F32, P],
 }
-_RESTYPES = {"acfe_last_error": C.c_char_p, "acfe_conv2d_wgrad_workspace": I64, "acfe_crc32c": C.c_uint32,
+_RESTYPES = {"acfe_last_error": C.c_char_p, "acfe_conv2d_wgrad_workspace": I64, "acfe_conv2d_dgrad_workspace": I64, "acfe_crc32c": C.c_uint32,
              "acfe_c1bn_workspace": I64}
 
 PAD_END, PAD_CENTER_CONSTANT, PAD_CENTER_REFLECT = 0, 1, 2

@@ -227,8 +227,9 @@ def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=No
         wf = pack_weights(w, x.dtype, True)
         dx = _empty(x.shape, x.dtype, x.device)
         ws = None
-        if stride > 1:
-            ws = _empty((N * ((P - 1) * stride + 1) * ((Q - 1) * stride + 1) * K,), x.dtype, x.device)
+        if stride > 1:  # sub-pixel phases: packed sub-kernels + one phase image
+            nb = lib.acfe_conv2d_dgrad_workspace(N, P, Q, K, C, R, S, stride, pt, pl, H, W, dt)
+            ws = _empty((max(nb, 1),), torch.uint8, x.device)
         with _Timed(w, "dgrad"):
             call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
                  ptr(ws), s)

@@ -2299,24 +2299,6 @@ __global__ void __launch_bounds__(256) k_pack_w_batch(const PackDesc* __restrict
   }
 }
 
-// ------------------------------------------------------------------ zero insertion (strided dgrad)
-template <typename T>
-__global__ void k_zero_insert(const T* __restrict__ dy, int N, int P, int Q, int K, int st, int Hu, int Wu,
-                              T* __restrict__ out) {
-  const long long total = (long long)N * Hu * Wu * K;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int k = (int)(i % K);
-    long long t = i / K;
-    const int w = (int)(t % Wu);
-    t /= Wu;
-    const int h = (int)(t % Hu);
-    const int n = (int)(t / Hu);
-    T v = (T)0;
-    if (h % st == 0 && w % st == 0 && h / st < P && w / st < Q)
-      v = dy[(((long long)n * P + h / st) * Q + w / st) * K + k];
-    out[i] = v;
-  }
-}
 
 // ------------------------------------------------------------------ wgrad
 // Block: 256 threads; output tile BMW (k rows) x 128 (rsc cols); reduction over
@@ -3048,47 +3030,22 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   return g;
 }
 
-// Debug / A-B switch read once per process (e.g. ACFE_CONV_NO_PIPE=1 selects the
-// 2-stage k_conv_fwd_g path instead of k_conv_fwd_p).
-static bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && v[0] && v[0] != '0';
-}
-
 static int pick_bn(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
-static int rows64_tr();
-static bool rows128_xres();
-static int rows64_xres();
 
-// waves per k_conv3x3_narrow workgroup (ACFE_NARROW_WAVES: 4 or 8)
-static int narrow_waves() {
-  const char* e = getenv("ACFE_NARROW_WAVES");
-  const int v = e ? atoi(e) : 0;
-  return v == 4 || v == 8 ? v : 8;
-}
 
+// k_conv3x3_narrow with 8 waves per workgroup (4 waves measured slower, r02v)
 template <int KB, int SW>
 static void launch_narrow(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
-                          double* stats, int tiles_h, int tiles_w, long long nt, int grid_m, int gp, int nw,
-                          hipStream_t s) {
+                          double* stats, int tiles_h, int tiles_w, long long nt, int grid_m, int gp, hipStream_t s) {
   const uint16_t *xx = (const uint16_t*)x, *ww = (const uint16_t*)wp;
   uint16_t* yy = (uint16_t*)y;
-  if (nw == 8) {
-    if (g.drop.on)
-      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, true, 8>), dim3(gp), dim3(512), 0, s, g, xx, ww, bias, yy, stats,
-                         tiles_h, tiles_w, (int)nt, grid_m);
-    else
-      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, false, 8>), dim3(gp), dim3(512), 0, s, g, xx, ww, bias, yy, stats,
-                         tiles_h, tiles_w, (int)nt, grid_m);
-  } else {
-    if (g.drop.on)
-      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, true, 4>), dim3(gp), dim3(256), 0, s, g, xx, ww, bias, yy, stats,
-                         tiles_h, tiles_w, (int)nt, grid_m);
-    else
-      hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, false, 4>), dim3(gp), dim3(256), 0, s, g, xx, ww, bias, yy, stats,
-                         tiles_h, tiles_w, (int)nt, grid_m);
-  }
+  if (g.drop.on)
+    hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, true, 8>), dim3(gp), dim3(512), 0, s, g, xx, ww, bias, yy, stats,
+                       tiles_h, tiles_w, (int)nt, grid_m);
+  else
+    hipLaunchKernelGGL((k_conv3x3_narrow<KB, SW, false, 8>), dim3(gp), dim3(512), 0, s, g, xx, ww, bias, yy, stats,
+                       tiles_h, tiles_w, (int)nt, grid_m);
 }
 
 template <typename T, int BN, int WM, int WN>
@@ -3097,18 +3054,11 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
   const int tiles_m = (int)((g.M + 127) / 128);
   dim3 grid(grid_m, g.Kp / BN);
   if constexpr (sizeof(T) == 2 && BN >= 64) {
-    static const bool no_pipe = getenv_flag("ACFE_CONV_NO_PIPE");
-    static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS");
-    if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && !no_rows && (!g.drop.on || g.idx32) &&
+    if (g.R == 3 && g.S == 3 && g.st == 1 && g.C % 64 == 0 && g.K == BN && (!g.drop.on || g.idx32) &&
         ((uintptr_t)y & 15) == 0) {  // (16-B epilogue stores)
-      // 6 output rows per tile halves the weight traffic per pixel, but at K = 128
-      // its register staging spills (measured 1.4x slower): 3 rows there
-      static const int rows_tr = getenv("ACFE_CONV_ROWS_TR") ? atoi(getenv("ACFE_CONV_ROWS_TR")) : 0;
-      const int xr64 = BN == 64 && rows_tr == 0 ? rows64_xres() : 0;
-      const bool xres = (BN == 128 && rows_tr == 0 && rows128_xres()) || xr64 != 0;
-      const int tr = rows_tr == 3 || rows_tr == 6 ? rows_tr
-                     : BN == 64 ? (xr64 ? xr64 : rows64_tr())
-                                : (xres ? 4 : 6);
+      // chunk-resident halo rows: 4-row tiles at K = 128, 8 at K = 64 (r02z-ba:
+      // the 6-row per-step staging, 3-row and 5-row tiles all measured slower)
+      constexpr int tr = BN == 128 ? 4 : 8;
       const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + 63) / 64;  // partial last column tile
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
@@ -3117,40 +3067,12 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
         if (gp >= 64) gp &= ~7;
         // each workgroup writes statistics slab row blockIdx.x: never more
         // workgroups than the caller's slab rows (narrow images have more
-        // 6 x 64 tiles than 128-pixel slab rows)
+        // tiles than 128-pixel slab rows)
         if (stats && gp > grid_m) gp = grid_m;
 #define ROWS(TR_, PM_, ...)                                                                                   \
   hipLaunchKernelGGL((k_conv3x3_rows<BN, TR_, PM_, ##__VA_ARGS__>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x, \
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m, nullptr)
-        bool done = false;
-        if constexpr (BN == 128) {
-          if (xres) {
-            if (g.drop.on) ROWS(4, 4, true); else ROWS(4, 0, true);
-            done = true;
-          }
-        } else {
-          if (xres) {
-            if (tr == 8) {
-              if (g.drop.on) ROWS(8, 4, true); else ROWS(8, 0, true);
-            } else {
-              if (g.drop.on) ROWS(6, 4, true); else ROWS(6, 0, true);
-            }
-            done = true;
-          }
-        }
-        if constexpr (BN == 64) {
-          if (tr == 5) {
-            if (g.drop.on) ROWS(5, 4); else ROWS(5, 0);
-            done = true;
-          }
-        }
-        if (!done) {
-          if (tr == 3) {
-            if (g.drop.on) ROWS(3, 4); else ROWS(3, 0);
-          } else {
-            if (g.drop.on) ROWS(6, 4); else ROWS(6, 0);
-          }
-        }
+        if (g.drop.on) ROWS(tr, 4, true); else ROWS(tr, 0, true);
 #undef ROWS
         return launch_rc("acfe_conv2d_fwd");
       }
@@ -3160,7 +3082,7 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
     const long long img = (long long)g.H * g.W * g.C * 2;
     const long long span = ((256 + (long long)g.P * g.Q - 1) / ((long long)g.P * g.Q) + 1) * img;
     if (g.C % 64 == 0 && g.K % BN == 0 && g.R * g.S <= 64 && g.R < 32 && g.M < (1ll << 31) &&
-        span < (1ll << 31) && !no_pipe) {
+        span < (1ll << 31)) {
       // persistent: one 512-thread workgroup per CU (256 CUs), a multiple of 8
       const int ny = g.Kp / BN, tiles = (int)((g.M + 255) / 256);
       int gp = 256 / ny;
@@ -3191,9 +3113,8 @@ static int launch_1x1(const ConvGeom& g, const void* x, const void* wp, const fl
 template <typename T>
 static int launch_fwd(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                       double* stats, int grid_m, hipStream_t s) {
-  static const bool no_1x1 = getenv_flag("ACFE_CONV_NO_1X1");
   if (sizeof(T) == 2 && g.R == 1 && g.S == 1 && g.st == 1 && g.pt == 0 && g.pl == 0 && g.C % 8 == 0 &&
-      g.K % 4 == 0 && g.ldy == g.K && !no_1x1 && ((g.C <= 32 && g.K <= 128) || (g.K <= 32 && g.C <= 128))) {
+      g.K % 4 == 0 && g.ldy == g.K && ((g.C <= 32 && g.K <= 128) || (g.K <= 32 && g.C <= 128))) {
     const int ncs = (g.C + 31) / 32, nkb = (g.K + 15) / 16;
     if (nkb >= 4 && g.K != nkb * 16) goto general;  // WIDE tile stores whole 16-channel blocks
     // dispatch on (reduction steps, 16-channel output blocks)
@@ -3204,11 +3125,10 @@ static int launch_fwd(const ConvGeom& g, const void* x, const void* wp, const fl
   }
 general:
   if constexpr (sizeof(T) == 2) {
-    static const bool no_narrow = getenv_flag("ACFE_CONV_NO_NARROW");
     if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W &&
         g.C % 64 == 0 && (g.K == 32 || g.K == 16) && g.C * g.K <= 4096 && g.ldy == g.K &&
-        g.M * g.K < (1ll << 32) && !no_narrow) {
-      static const int nw = narrow_waves();
+        g.M * g.K < (1ll << 32)) {
+      constexpr int nw = 8;
       // tiles of nw * 32 pixels: segw columns x tr rows
       const int segw = g.Q <= 32 ? 32 : 64, tr = nw * 32 / segw;
       const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + segw - 1) / segw;
@@ -3219,11 +3139,11 @@ general:
         if (gp >= 64) gp &= ~7;
         if (stats && gp > grid_m) gp = grid_m;  // one statistics slab row per workgroup
         if (g.K == 32) {
-          if (segw == 64) launch_narrow<32, 64>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
-          else launch_narrow<32, 32>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
+          if (segw == 64) launch_narrow<32, 64>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, s);
+          else launch_narrow<32, 32>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, s);
         } else {
-          if (segw == 64) launch_narrow<16, 64>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
-          else launch_narrow<16, 32>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, nw, s);
+          if (segw == 64) launch_narrow<16, 64>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, s);
+          else launch_narrow<16, 32>(g, x, wp, bias, y, stats, tiles_h, tiles_w, nt, grid_m, gp, s);
         }
         return launch_rc("acfe_conv2d_fwd(narrow)");
       }
@@ -3328,8 +3248,105 @@ ACFE_API int acfe_conv2d_fwd_dropout(const void* x, int N, int H, int W, int C, 
 }
 
 // dX = conv^T(dY, W).  wflip = acfe_conv2d_pack_weights(..., flip=1).
-// workspace: for stride > 1, device buffer of N*Hu*Wu*K elements of dtype with
-// Hu = (P-1)*stride + 1, Wu = (Q-1)*stride + 1 (NULL allowed for stride 1).
+//
+// stride 1: a stride-1 conv of dY with the flipped weights.
+// stride > 1: sub-pixel (phase) decomposition instead of zero insertion.  The
+// rows of dX with h = a (mod st) receive contributions only from the filter
+// rows r = (a + pad_top) (mod st); for each of the st x st phases (a, b) the
+// phase image dX[:, a::st, b::st, :] is a stride-1 conv of dY itself with the
+// (Ra x Sb)-tap sub-kernel of those rows / columns -- every MFMA multiplies a
+// real dY value (zero insertion spent 4x / 9x the MACs on inserted zeros at
+// stride 2 / 3 and wrote an st^2-times larger upsampled copy of dY) -- written
+// to a phase buffer and scattered into dX; phases without taps are zero.
+//   For phase row a: r0 = (a + pt) % st, Ra = ceil((R - r0) / st) taps r0 + st j,
+//   da = (a + pt - r0) / st; output row i of the phase reads dY row
+//   i + da - j, i.e. the sub-kernel flipped (t = Ra-1-j) is a stride-1 conv
+//   with offset c = da - (Ra - 1): pad_top = max(0, -c), and max(0, c) extra
+//   leading output rows that the scatter skips.
+namespace {
+struct PhaseAxis {
+  int n;    // phase rows (or columns) of dX: ceil((H - a) / st)
+  int r0;   // first filter row of the phase
+  int taps; // filter rows of the phase (0: no contribution)
+  int pad;  // top pad of the phase conv
+  int off;  // leading output rows skipped by the scatter
+};
+PhaseAxis phase_axis(int H, int R, int st, int pt, int a) {
+  PhaseAxis x{};
+  x.n = H > a ? (H - a + st - 1) / st : 0;
+  x.r0 = (a + pt) % st;
+  x.taps = x.r0 < R ? (R - x.r0 + st - 1) / st : 0;
+  const int da = (a + pt - x.r0) / st;
+  const int c = da - (x.taps - 1);
+  x.pad = c < 0 ? -c : 0;
+  x.off = c > 0 ? c : 0;
+  return x;
+}
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+}  // namespace
+
+// phase sub-kernel, packed for the forward conv of dY (K inputs -> C outputs):
+// out[c][(t*Sb + u)*K + k] = wflip[c][((R-1-r)*S + (S-1-s))*K + k] with
+// r = r0 + st*(Ra-1-t), s = s0 + st*(Sb-1-u); rows padded to rows_p, columns
+// zero-padded to cols_p
+template <typename T>
+__global__ void k_pack_phase(const T* __restrict__ wflip, int ld_flip, int K, int R, int S, int st, int r0, int ra,
+                             int s0, int sb, int rows_p, int cols_p, T* __restrict__ out) {
+  const long long total = (long long)rows_p * cols_p;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int row = (int)(i / cols_p), col = (int)(i - (long long)row * cols_p);
+    T v = (T)0;
+    if (col < ra * sb * K) {
+      const int k = col % K, tu = col / K, t = tu / sb, u = tu % sb;
+      const int r = r0 + st * (ra - 1 - t), sx = s0 + st * (sb - 1 - u);
+      v = wflip[(long long)row * ld_flip + ((R - 1 - r) * S + (S - 1 - sx)) * K + k];
+    }
+    out[i] = v;
+  }
+}
+
+// dX[n][a + st i][b + st j][:] = ph[n][off_r + i][off_c + j][:] (ph == NULL: zeros)
+template <typename T>
+__global__ void k_phase_scatter(const T* __restrict__ ph, int N, int PH, int PW, int C, int off_r, int off_c, int a,
+                                int b, int st, int Ha, int Wa, int H, int W, T* __restrict__ dx) {
+  constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
+  const int cv = C / V;
+  const long long total = (long long)N * Ha * Wa * cv;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int c = (int)(e % cv);
+    long long t = e / cv;
+    const int j = (int)(t % Wa);
+    t /= Wa;
+    const int i = (int)(t % Ha);
+    const int n = (int)(t / Ha);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (ph) v = *reinterpret_cast<const uint4*>(ph + (((long long)n * PH + off_r + i) * PW + off_c + j) * C + c * V);
+    *reinterpret_cast<uint4*>(dx + (((long long)n * H + a + st * i) * W + b + st * j) * C + c * V) = v;
+  }
+}
+
+ACFE_API long long acfe_conv2d_dgrad_workspace(int N, int P, int Q, int K, int C, int R, int S, int stride,
+                                               int pad_top, int pad_left, int H, int W, int dtype) {
+  if (N < 0 || P <= 0 || Q <= 0 || K <= 0 || C <= 0 || R <= 0 || S <= 0 || stride <= 0 || H <= 0 || W <= 0 ||
+      (dtype != 0 && dtype != 1))
+    return ACFE_E_INVAL;
+  if (stride == 1) return 0;
+  const size_t es = dtype == ACFE_DTYPE_BF16 ? 2 : 4;
+  const int BK = dtype == ACFE_DTYPE_BF16 ? 64 : 32;
+  const int rows_p = (C + pick_bn(C) - 1) / pick_bn(C) * pick_bn(C);
+  size_t wbytes = 0, tmax = 0;
+  for (int a = 0; a < stride; ++a)
+    for (int b = 0; b < stride; ++b) {
+      const PhaseAxis ra = phase_axis(H, R, stride, pad_top, a), cb = phase_axis(W, S, stride, pad_left, b);
+      if (!ra.n || !cb.n || !ra.taps || !cb.taps) continue;
+      const int cols_p = (ra.taps * cb.taps * K + BK - 1) / BK * BK;
+      wbytes += align256((size_t)rows_p * cols_p * es);
+      const size_t tb = (size_t)N * (ra.n + ra.off) * (cb.n + cb.off) * C * es;
+      if (tb > tmax) tmax = tb;
+    }
+  return (long long)(wbytes + align256(tmax));
+}
+
 ACFE_API int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R,
                                int S, int stride, int pad_top, int pad_left, int H, int W, void* dx,
                                int dtype, void* workspace, void* stream) {
@@ -3337,29 +3354,69 @@ ACFE_API int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const
       (dtype != 0 && dtype != 1))
     return ACFE_E_INVAL;
   if (N == 0) return ACFE_OK;
-  const void* src = dy;
-  int Hs = P, Ws = Q;
-  if (stride > 1) {
-    if (!workspace) return ACFE_E_INVAL;
-    const int Hu = (P - 1) * stride + 1, Wu = (Q - 1) * stride + 1;
-    const long long total = (long long)N * Hu * Wu * K;
-    int grid = cdiv(total, 256);
-    if (grid > 8192) grid = 8192;
-    if (dtype == ACFE_DTYPE_BF16)
-      hipLaunchKernelGGL(k_zero_insert<uint16_t>, dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)dy, N, P,
-                         Q, K, stride, Hu, Wu, (uint16_t*)workspace);
-    else
-      hipLaunchKernelGGL(k_zero_insert<float>, dim3(grid), dim3(256), 0, strm(stream), (const float*)dy, N, P, Q, K,
-                         stride, Hu, Wu, (float*)workspace);
-    int rc = launch_rc("acfe_conv2d_dgrad(zero_insert)");
+  if (stride == 1)  // stride-1 conv of dY with flipped weights: input channels K, output C
+    return acfe_conv2d_fwd(dy, N, P, Q, K, wflip, C, R, S, 1, R - 1 - pad_top, S - 1 - pad_left, H, W,
+                           nullptr, dx, dtype, nullptr, stream);
+  const size_t es = dtype == ACFE_DTYPE_BF16 ? 2 : 4;
+  if (!workspace || (C * es) % 16 != 0 || ((uintptr_t)dx & 15)) return ACFE_E_INVAL;
+  const int BK = dtype == ACFE_DTYPE_BF16 ? 64 : 32;
+  const int rows_p = (C + pick_bn(C) - 1) / pick_bn(C) * pick_bn(C);
+  int ld_flip, rp_full;
+  {
+    int rc = acfe_conv2d_packed_shape(K, R, S, C, dtype, 1, &rp_full, &ld_flip);
     if (rc) return rc;
-    src = workspace;
-    Hs = Hu;
-    Ws = Wu;
   }
-  // stride-1 conv of (upsampled) dY with flipped weights: input channels K, output C
-  return acfe_conv2d_fwd(src, N, Hs, Ws, K, wflip, C, R, S, 1, R - 1 - pad_top, S - 1 - pad_left, H, W,
-                         nullptr, dx, dtype, nullptr, stream);
+  // weights of every phase first (one region each), then the phase image buffer
+  size_t wbytes = 0;
+  for (int a = 0; a < stride; ++a)
+    for (int b = 0; b < stride; ++b) {
+      const PhaseAxis ra = phase_axis(H, R, stride, pad_top, a), cb = phase_axis(W, S, stride, pad_left, b);
+      if (!ra.n || !cb.n || !ra.taps || !cb.taps) continue;
+      wbytes += align256((size_t)rows_p * ((ra.taps * cb.taps * K + BK - 1) / BK * BK) * es);
+    }
+  unsigned char* wsb = static_cast<unsigned char*>(workspace);
+  void* tmp = wsb + wbytes;
+  hipStream_t s = strm(stream);
+  size_t wo = 0;
+  for (int a = 0; a < stride; ++a)
+    for (int b = 0; b < stride; ++b) {
+      const PhaseAxis ra = phase_axis(H, R, stride, pad_top, a), cb = phase_axis(W, S, stride, pad_left, b);
+      if (!ra.n || !cb.n) continue;
+      const bool taps = ra.taps && cb.taps;
+      const int PH = ra.n + ra.off, PW = cb.n + cb.off;
+      if (taps) {
+        const int cols_p = (ra.taps * cb.taps * K + BK - 1) / BK * BK;
+        void* wph = wsb + wo;
+        wo += align256((size_t)rows_p * cols_p * es);
+        const long long tot = (long long)rows_p * cols_p;
+        int grid = cdiv(tot, 256);
+        if (grid > 2048) grid = 2048;
+        if (dtype == ACFE_DTYPE_BF16)
+          hipLaunchKernelGGL(k_pack_phase<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)wflip, ld_flip,
+                             K, R, S, stride, ra.r0, ra.taps, cb.r0, cb.taps, rows_p, cols_p, (uint16_t*)wph);
+        else
+          hipLaunchKernelGGL(k_pack_phase<float>, dim3(grid), dim3(256), 0, s, (const float*)wflip, ld_flip, K, R,
+                             S, stride, ra.r0, ra.taps, cb.r0, cb.taps, rows_p, cols_p, (float*)wph);
+        int rc = launch_rc("acfe_conv2d_dgrad(pack_phase)");
+        if (rc) return rc;
+        rc = acfe_conv2d_fwd(dy, N, P, Q, K, wph, C, ra.taps, cb.taps, 1, ra.pad, cb.pad, PH, PW, nullptr, tmp,
+                             dtype, nullptr, stream);
+        if (rc) return rc;
+      }
+      const long long tot = (long long)N * ra.n * cb.n * (C * (long long)es / 16);
+      int grid = cdiv(tot, 256);
+      if (grid > 8192) grid = 8192;
+      if (dtype == ACFE_DTYPE_BF16)
+        hipLaunchKernelGGL(k_phase_scatter<uint16_t>, dim3(grid), dim3(256), 0, s,
+                           taps ? (const uint16_t*)tmp : nullptr, N, PH, PW, C, ra.off, cb.off, a, b, stride, ra.n,
+                           cb.n, H, W, (uint16_t*)dx);
+      else
+        hipLaunchKernelGGL(k_phase_scatter<float>, dim3(grid), dim3(256), 0, s, taps ? (const float*)tmp : nullptr,
+                           N, PH, PW, C, ra.off, cb.off, a, b, stride, ra.n, cb.n, H, W, (float*)dx);
+      const int rc = launch_rc("acfe_conv2d_dgrad(phase_scatter)");
+      if (rc) return rc;
+    }
+  return ACFE_OK;
 }
 
 // Split-K plan of the wgrad: `splits` pixel chunks of `chunk` rows, splits a
@@ -3379,14 +3436,10 @@ static void wgrad_combine(const float* ws, int nsplit, long long n, float beta, 
 static void wgrad_plan(long long M, int kd, int K, long long* splits_o, long long* chunk_o) {
   const int bmw = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const long long tiles = (long long)((kd + 127) / 128) * ((K + bmw - 1) / bmw);
-  // target workgroup count of the split-K grid (ACFE_WGRAD_WGS overrides, for A/B):
-  // 4096 measured 1.1 ms/step faster than 1024 once the combine ran split-parallel
-  // (k_wgrad_reduce_g), the halo kernels gaining most from the finer pixel ranges
-  static const long long target = [] {
-    const char* e = getenv("ACFE_WGRAD_WGS");
-    const long long v = e ? atoll(e) : 0;
-    return v >= 256 && v <= 16384 ? v : 4096LL;
-  }();
+  // target workgroup count of the split-K grid: 4096 measured 1.1 ms/step
+  // faster than 1024 once the combine ran split-parallel (k_wgrad_reduce_g),
+  // the halo kernels gaining most from the finer pixel ranges (r01r)
+  constexpr long long target = 4096;
   long long splits = (target + tiles - 1) / tiles;
   long long chunk = (M + splits - 1) / splits;
   chunk = (chunk + 63) / 64 * 64;
@@ -3426,14 +3479,10 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
 static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
                              long long splits, hipStream_t s, int* used) {
   const int cw = g.C % 64 == 0 ? 64 : g.C;  // 16 / 32-channel layers: one chunk of C
-  // K = 64 (plain dY): two output rows per step (ACFE_WG64_NR=1: one)
-  static const int nr64 = getenv("ACFE_WG64_NR") ? atoi(getenv("ACFE_WG64_NR")) : 2;
-  static const int nru = getenv("ACFE_WGU_NR") ? atoi(getenv("ACFE_WGU_NR")) : 2;
-  // (the K = 128 pooled-gradient variant spills at two rows: 138 VGPRs)
-  static const int nr32 = getenv("ACFE_WG32_NR") ? atoi(getenv("ACFE_WG32_NR")) : 2;
-  const int nr = (cw == 64 && g.P % 2 == 0 &&
-                  ((g.K == 64 && ((!amax && nr64 == 2) || (amax && nru == 2))) || (g.K == 32 && !amax && nr32 == 2)))
-                     ? 2 : 1;
+  // two output rows per step for the K = 64 (plain or pooled dY) and K = 32
+  // layers (r02au-aw: 72 instead of 36 MFMAs per wave per barrier); the K =
+  // 128 pooled-gradient variant spills at two rows (138 VGPRs) and keeps one
+  const int nr = (cw == 64 && g.P % 2 == 0 && (g.K == 64 || (g.K == 32 && !amax))) ? 2 : 1;
   const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * ((g.Q + 63) / 64));
   int sp = 256 / nchunk;
   if (sp > splits) sp = (int)splits;
@@ -3509,19 +3558,17 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   ConvGeom g = make_geom(N, H, W, C, K, R, S, stride, pad_top, pad_left, P, Q, 64, 128);
   g.ldy = K;
   int rc;
-  static const bool no_halo_w = getenv_flag("ACFE_WGRAD_NO_HALO");
-  static const bool halo32 = !getenv_flag("ACFE_WGRAD_NO_HALO32");
   if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 &&
-      ((C % 64 == 0 && (K == 64 || K == 128 || (K == 32 && halo32))) ||
-       (halo32 && ((C == 32 && (K == 128 || K == 256)) || (C == 16 && K == 256)))) &&
-      (long long)N * P * ((Q + 63) / 64) < (1ll << 31) && !no_halo_w) {
+      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32)) ||
+       ((C == 32 && (K == 128 || K == 256)) || (C == 16 && K == 256))) &&
+      (long long)N * P * ((Q + 63) / 64) < (1ll << 31)) {
     // halo-staged kernel; its split count stays within the planned workspace
     int used = 0;
     rc = wgrad_halo_launch(g, x, dy, nullptr, workspace, splits, strm(stream), &used);
     if (rc) return rc;
     splits = used;
   } else if (dtype == ACFE_DTYPE_BF16 && S == 10 && stride == 1 && C % 64 == 0 && K == 128 &&
-             (long long)N * P * ((Q + 31) / 32) < (1ll << 31) && !no_halo_w) {
+             (long long)N * P * ((Q + 31) / 32) < (1ll << 31)) {
     int used = 0;
     rc = wgrad_row_halo_launch(g, x, dy, workspace, splits, strm(stream), &used);
     if (rc) return rc;
@@ -3551,37 +3598,11 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
 // output is never written; the backward reads the pooled gradient + argmax
 // bytes and expands them in its input staging (dgrad: k_conv3x3_rows<C, 6, 2>,
 // wgrad: k_wgrad3x3_halo<K, true>).
-// K = 128 rows kernels: 4-row tiles with chunk-resident halo rows
-// (ACFE_ROWS_XRES=0: the 6-row per-step staging; r02z: fwd_pool 4.97 -> 4.89 ms,
-// dgrad_unpool 5.19 -> 4.75 ms)
-static bool rows128_xres() {
-  static const bool v = [] {
-    const char* e = getenv("ACFE_ROWS_XRES");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
-}
-// K = 64 rows kernels with chunk-resident halo rows: the tile rows (6, 8) or 0
-// (off: the per-step staging with a double-buffered image), ACFE_ROWS64_XRES;
-// r02z on the 64x128 layers: 6 rows fwd_add 128->64 1.037 -> 0.968 ms, 64->64
-// 0.717 -> 0.658 ms, fwd_dropout 0.614 -> 0.544 ms (8 rows: 1.003 / 0.678 / 0.525)
-static int rows64_xres() {
-  static const int v = [] {
-    const char* e = getenv("ACFE_ROWS64_XRES");
-    const int t = e ? atoi(e) : 8;  // 8 rows (BN-prologue kernels too, so prologue and plain paths tile alike): r02ay fwd_add 128->64 0.89 vs 0.92 ms, dropout 0.53 vs 0.56
-    return t == 6 || t == 8 ? t : 0;
-  }();
-  return v;
-}
-static int rows64_tr() {  // output rows per tile of the K = 64 rows kernels (ACFE_ROWS64_TR: 5 or 6)
-  static const int v = [] {
-    const char* e = getenv("ACFE_ROWS64_TR");
-    const int t = e ? atoi(e) : 0;
-    return t == 5 || t == 6 ? t : 6;  // 5 rows (conflict-free 160-B pitch) measured within 2 % of 6 (r02aa)
-  }();
-  return v;
-}
-
+// Rows-kernel tiles: K = 128 4-row tiles with chunk-resident halo rows (r02z:
+// fwd_pool 4.97 -> 4.89 ms, dgrad_unpool 5.19 -> 4.75 ms against the 6-row
+// per-step staging); K = 64 8 chunk-resident rows, the BN-prologue kernels too,
+// so prologue and plain paths tile alike (r02ay/ba: fwd_add 128->64 0.89 vs
+// 0.92 ms at 6 rows, dropout 0.53 vs 0.56; the per-step staging 1.04 / 0.61).
 template <int KB, int PM, int TR, bool XR = false, bool PR = false>
 static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                           double* stats, int srows, uint8_t* amax, hipStream_t s, const char* what) {
@@ -3600,31 +3621,20 @@ static int launch_rows_tr(const ConvGeom& g, const void* x, const void* wp, cons
 template <int KB, int PM>
 static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                        int srows, uint8_t* amax, hipStream_t s, const char* what) {
-  // pooling (PM 1 / 2) needs row pairs: 6 rows (or 4 chunk-resident rows)
   if constexpr (KB == 128) {
-    if (rows128_xres()) return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
-  }
-  if constexpr (KB == 64 && PM != 2) {
-    // BatchNormalization prologue (acfe_conv2d_bn_prologue_supported): 6 chunk-resident rows
-    if (g.pro_sc) {
-      if (rows64_xres() == 8) return launch_rows_tr<KB, PM, 8, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
-      return launch_rows_tr<KB, PM, 6, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+    return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
+  } else {
+    static_assert(KB == 64, "rows kernels: K in {64, 128}");
+    if constexpr (PM != 2) {
+      // BatchNormalization prologue (acfe_conv2d_bn_prologue_supported)
+      if (g.pro_sc) return launch_rows_tr<KB, PM, 8, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
     }
+    return launch_rows_tr<KB, PM, 8, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
   }
-  if constexpr (KB == 64) {
-    const int xr = rows64_xres();
-    if (xr == 6) return launch_rows_tr<KB, PM, 6, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
-    if (xr == 8) return launch_rows_tr<KB, PM, 8, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
-  }
-  if constexpr (KB == 64 && PM != 1 && PM != 2) {
-    if (rows64_tr() == 5) return launch_rows_tr<KB, PM, 5>(g, x, wp, bias, y, stats, srows, amax, s, what);
-  }
-  return launch_rows_tr<KB, PM, 6>(g, x, wp, bias, y, stats, srows, amax, s, what);
 }
 
 ACFE_API int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {
-  static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS") || getenv_flag("ACFE_CONV_NO_POOL");
-  return !no_rows && dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
+  return dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
          (K == 64 || K == 128) && W >= 2 && W % 2 == 0 && H >= 2 && H % 2 == 0 &&
          (long long)N * ((H + 5) / 6) * ((W + 63) / 64) < (1ll << 31) &&
          (long long)N * H * ((W + 63) / 64) < (1ll << 31) &&
@@ -3713,8 +3723,7 @@ ACFE_API int acfe_conv2d_wgrad_unpool(const void* x, int N, int H, int W, int C,
 // (slab rows = acfe_conv2d_stats_rows(N*H*W, K), nullable); the conv output
 // itself is never stored.  Shapes: acfe_conv2d_rows_supported.
 ACFE_API int acfe_conv2d_rows_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {
-  static const bool no_rows = getenv_flag("ACFE_CONV_NO_ROWS") || getenv_flag("ACFE_CONV_NO_ADD");
-  return !no_rows && dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
+  return dtype == ACFE_DTYPE_BF16 && N > 0 && R == 3 && S == 3 && C > 0 && C % 64 == 0 &&
          (K == 64 || K == 128) && W > 0 && H > 0 && (long long)N * ((H + 5) / 6) * ((W + 63) / 64) < (1ll << 31);
 }
 
@@ -4326,10 +4335,6 @@ k_stem_wgrad_mfma(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
   }
 }
 
-static bool stem_mfma_on() {
-  static const bool off = getenv("ACFE_STEM_VALU") && getenv("ACFE_STEM_VALU")[0] == '1';
-  return !off;
-}
 
 ACFE_API int acfe_stem_blocks(int N, int H, int W) {
   const long long t = (long long)N * ((H + STEM_TH - 1) / STEM_TH) * ((W + STEM_TW - 1) / STEM_TW);
@@ -4354,7 +4359,7 @@ ACFE_API int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int 
   hipLaunchKernelGGL((k_stem_fwd<TI, TO, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x, N, H, W, \
                      pad_top, pad_left, weff, bias, (TO*)y, stats_partial, th, tw)
 #define SF(TI, TO) if (R == 5) SF1(TI, TO, 5); else SF1(TI, TO, 3)
-  if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16 && stem_mfma_on()) {
+  if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16) {
     if (R == 5)
       hipLaunchKernelGGL((k_stem_fwd_mfma<5, 5>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, N, H, W,
                          pad_top, pad_left, weff, bias, (uint16_t*)y, stats_partial, th, tw);
@@ -4379,7 +4384,7 @@ ACFE_API int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, 
   hipLaunchKernelGGL((k_stem_dgrad<TG, TO, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TG*)dy, N, H, \
                      W, pad_top, pad_left, weff, (TO*)dx, th, tw)
 #define SD(TG, TO) if (R == 5) SD1(TG, TO, 5); else SD1(TG, TO, 3)
-  if (dy_dtype == ACFE_DTYPE_BF16 && dx_dtype == ACFE_DTYPE_BF16 && stem_mfma_on()) {
+  if (dy_dtype == ACFE_DTYPE_BF16 && dx_dtype == ACFE_DTYPE_BF16) {
     const int g2 = acfe_stem_blocks(N, H, W);
     if (R == 5)
       hipLaunchKernelGGL((k_stem_dgrad_mfma<5, 5>), dim3(g2), dim3(256), 0, strm(stream), (const uint16_t*)dy, N, H,
@@ -4406,7 +4411,7 @@ ACFE_API int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_
   hipLaunchKernelGGL((k_stem_wgrad<TI, TG, RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const TI*)x,        \
                      (const TG*)dy, N, H, W, pad_top, pad_left, workspace, th, tw)
 #define SW(TI, TG) if (R == 5) SW1(TI, TG, 5); else SW1(TI, TG, 3)
-  if (x_dtype == ACFE_DTYPE_BF16 && dy_dtype == ACFE_DTYPE_BF16 && stem_mfma_on()) {
+  if (x_dtype == ACFE_DTYPE_BF16 && dy_dtype == ACFE_DTYPE_BF16) {
     if (R == 5)
       hipLaunchKernelGGL((k_stem_wgrad_mfma<5, 5>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x,
                          (const uint16_t*)dy, N, H, W, pad_top, pad_left, workspace, th, tw);

@@ -98,7 +98,7 @@ ACFE_API int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmi
     band[3 * m + 1] = e - s + 1;
     band[3 * m + 2] = (int)vals.size();
     for (int k = s; k <= e; ++k) vals.push_back(w_host[(size_t)m * nb + k]);
-    while (vals.size() & 7) vals.push_back(0.f);  // k_mel_w reads whole 8-tap groups
+    while (vals.size() & 7) vals.push_back(0.f);  // k_mel_w2 reads whole 8-tap groups
     kmin = s < kmin ? s : kmin;
     kmax = e > kmax ? e : kmax;
   }
@@ -543,209 +543,22 @@ __device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
   }
 }
 
-template <int NC, int R, int NS>
-__device__ __forceinline__ void stockham_pass_w(float2* buf, const float2 (*bw)[4], int lane) {
-  constexpr int NB = NC / R, PER = NB / 64;
-  static_assert(NB % 64 == 0 && NB % 8 == 0 && NS % 8 == 0, "pass shape");
-  float2 v[PER][R];
-#pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    const int j = lane + 64 * p, jm = j & (NS - 1);
-    const float2* src = buf + padx(j);
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[p][r] = src[r * (NB + NB / 8)];
-    float2 w[R];
-    twiddle_pows<R>(bw[p], w);
-#pragma unroll
-    for (int r = 1; r < R; ++r) v[p][r] = cmul(v[p][r], w[r]);
-  }
-#pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    const int j = lane + 64 * p, jm = j & (NS - 1);
-    dft<R>(v[p]);
-    float2* dst = buf + padx((j / NS) * NS * R + jm);
-#pragma unroll
-    for (int r = 0; r < R; ++r) dst[r * (NS + NS / 8)] = v[p][r];
-  }
-  __syncthreads();  // one-wave workgroup: orders the lanes' LDS exchange
-}
-
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_mel_w(const float* __restrict__ raw, int64_t cs, int n,
-                                              const float* __restrict__ stats, int pad_mode, int power,
-                                              int n_frames, int fpw, int hop, const float2* __restrict__ tw,
-                                              const float2* __restrict__ rtw, const float* __restrict__ win,
-                                              const int* __restrict__ band, const float* __restrict__ vals,
-                                              int n_mels, int kmin, int kmax, float* __restrict__ out,
-                                              int layout) {
-  constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16;
-  // [NC + NC/8] padded points; the nk (+8 zero) power bins reuse the front of
-  // that buffer once the FFT has been read (nk <= 1024: 18 KB per wave, so 8
-  // waves fit a CU's LDS), else they follow it
-  extern __shared__ float2 wbuf[];
-  const int nk = kmax - kmin + 1;
-  const bool alias = nk <= 1024;
-  float* pw = alias ? reinterpret_cast<float*>(wbuf) : reinterpret_cast<float*>(wbuf + NC + NC / 8);
-  const int lane = threadIdx.x;
-  const int b = blockIdx.y;
-  const float* xb = raw + (int64_t)b * cs;
-  const bool do_norm = stats != nullptr;
-  const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
-  const int f0 = blockIdx.x * fpw;
-  // the lane's base twiddles of passes 2 and 3 (W^{t}, W^{2t}, W^{4t}, W^{8t}
-  // with t = jm * NC / (NS R)) stay in 32 VGPRs for all of its frames
-  float2 bw2[2][4], bw3[4][4];
-  {
-    const int t = (lane & 15) * 8;  // pass 2: jm = j & 15 is the same for both butterflies
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bw2[0][q] = bw2[1][q] = tw[(t << q) & (NC - 1)];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) bw3[p][q] = tw[((lane + 64 * p) << q) & (NC - 1)];
-      bw3[p][3] = make_float2(1.f, 0.f);
-    }
-  }
-  for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
-    // the per-lane window loads are frame-invariant: an opaque zero offset
-    // keeps the compiler from hoisting their 64 VGPRs out of the frame loop
-    int zo;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
-    const float* winf = win + zo;
-    // and the powers of the base twiddles are recomputed per frame rather than
-    // hoisted (116 VGPRs): the empty asm makes the bases opaque each iteration
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      asm volatile("" : "+v"(bw2[0][q].x), "+v"(bw2[0][q].y));
-      bw2[1][q] = bw2[0][q];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(bw3[p][q].x), "+v"(bw3[p][q].y));
-    }
-    const int start = (pad_mode == ACFE_PAD_END) ? f * hop : f * hop - L / 2;
-    const bool inb = start >= 0 && start + L <= n;
-    // pass 1 (NS = 1, radix 16) from memory: z[j + r*NB0] = x[2(j + r NB0)] + i x[2(j + r NB0) + 1]
-    __syncthreads();  // the previous frame's readers of wbuf / pw are done
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int j = lane + 64 * p;
-      // uniform branch outside the unrolled loads: all 32 sample loads of an
-      // interior frame are issued back to back
-      float xa[16], xc[16], wa[16], wc[16];
-      const float* ws = winf + 2 * j;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) wa[r] = ws[2 * r * NB0], wc[r] = ws[2 * r * NB0 + 1];
-      if (inb) {
-        const float* xs = xb + start + 2 * j;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) xa[r] = xs[2 * r * NB0], xc[r] = xs[2 * r * NB0 + 1];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int nn = 2 * (j + r * NB0);
-          xa[r] = fetch(xb, n, start + nn, pad_mode, false, 0.f, 1.f);
-          xc[r] = fetch(xb, n, start + nn + 1, pad_mode, false, 0.f, 1.f);
-        }
-      }
-      float2 v[16];
-      if (do_norm) {
-        // zero padding is applied after normalisation (fetch returns 0 outside)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int nn = 2 * (j + r * NB0);
-          const bool ia = inb || in_sig(start + nn, n, pad_mode), ic = inb || in_sig(start + nn + 1, n, pad_mode);
-          v[r] = make_float2(ia ? norm1(xa[r], mn, rng) * wa[r] : 0.f, ic ? norm1(xc[r], mn, rng) * wc[r] : 0.f);
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = make_float2(xa[r] * wa[r], xc[r] * wc[r]);
-      }
-      dft<16>(v);
-      float2* dst = wbuf + j * 18;  // padx(16 j + r) = 18 j + r + r / 8
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dst[r + (r >> 3)] = v[r];
-    }
-    __syncthreads();
-    stockham_pass_w<NC, 16, 16>(wbuf, bw2, lane);
-    stockham_pass_w<NC, 8, 256>(wbuf, bw3, lane);
-    // real-FFT post-processing + power for bins [kmin, kmax], up to 16 bins
-    // per lane per round with their rtw loads issued together
-    for (int i0 = lane; i0 < nk; i0 += 1024) {
-      float2 rt[16];
-      float pv[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) rt[u] = i0 + 64 * u < nk ? rtw[kmin + i0 + 64 * u] : make_float2(0.f, 0.f);
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = i0 + 64 * u;
-        pv[u] = 0.f;
-        if (i < nk) {
-          const int k = kmin + i;
-          const float2 zk = wbuf[padx(k & (NC - 1))];
-          const float2 zm = wbuf[padx((NC - k) & (NC - 1))];
-          const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-          const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
-          const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
-          const float2 X = cadd(E, cmul(rt[u], O));
-          pv[u] = X.x * X.x + X.y * X.y;
-        }
-      }
-      if (alias) __syncthreads();  // every lane's FFT reads precede the aliased writes (one round)
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (i0 + 64 * u < nk) pw[i0 + 64 * u] = pv[u];
-    }
-    if (lane < 8) pw[nk + lane] = 0.f;  // the mel loop's padded 8-tap groups read up to nk + 7
-    if (power != 2) {
-      for (int k = lane; k < nk; k += 64) pw[k] = sqrtf(pw[k]);
-    }
-    __syncthreads();
-    // banded mel over balanced band pairs (m, n_mels-1-m): a short low band and
-    // a long high band per lane, their taps in whole 8-tap groups (the plan pads
-    // each band's taps with zeros, pw has 8 zero floats past nk)
-    for (int q = lane; q < (n_mels + 1) / 2; q += 64) {
-      const int m0 = q, m1 = n_mels - 1 - q;
-      const bool h1 = m1 != m0;
-      const int s0 = band[3 * m0], pl0 = (band[3 * m0 + 1] + 7) & ~7, off0 = band[3 * m0 + 2];
-      const int s1 = band[3 * m1], pl1 = h1 ? (band[3 * m1 + 1] + 7) & ~7 : 0, off1 = band[3 * m1 + 2];
-      const float4* v0 = reinterpret_cast<const float4*>(vals + off0);
-      const float4* v1 = reinterpret_cast<const float4*>(vals + off1);
-      const float* p0 = pw + (s0 - kmin);
-      const float* p1 = pw + (s1 - kmin);
-      float acc0 = 0.f, acc1 = 0.f;
-      const int lmax = pl0 > pl1 ? pl0 : pl1;
-      for (int i0 = 0; i0 < lmax; i0 += 8) {
-        if (i0 < pl0) {
-          const float4 a = v0[i0 / 4], c = v0[i0 / 4 + 1];
-          acc0 += a.x * p0[i0] + a.y * p0[i0 + 1] + a.z * p0[i0 + 2] + a.w * p0[i0 + 3] + c.x * p0[i0 + 4] +
-                  c.y * p0[i0 + 5] + c.z * p0[i0 + 6] + c.w * p0[i0 + 7];
-        }
-        if (i0 < pl1) {
-          const float4 a = v1[i0 / 4], c = v1[i0 / 4 + 1];
-          acc1 += a.x * p1[i0] + a.y * p1[i0 + 1] + a.z * p1[i0 + 2] + a.w * p1[i0 + 3] + c.x * p1[i0 + 4] +
-                  c.y * p1[i0 + 5] + c.z * p1[i0 + 6] + c.w * p1[i0 + 7];
-        }
-      }
-      const size_t rowo = layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels : 0;
-      out[layout == ACFE_LAYOUT_BTM ? rowo + m0 : ((size_t)b * n_mels + m0) * n_frames + f] = acc0;
-      if (h1) out[layout == ACFE_LAYOUT_BTM ? rowo + m1 : ((size_t)b * n_mels + m1) * n_frames + f] = acc1;
-    }
-  }
-}
-
-// Two waves per frame (128 threads): the same radix-16/16/8 Stockham passes,
-// twiddles, post-processing and band sums as k_mel_w -- every value is
-// computed by the same operations in the same order, so the output is
-// bit-identical -- with each lane holding half the butterflies, so a wave
-// needs <= 128 VGPRs and the 18 KB frame buffer is shared by two waves:
-// 16 waves per CU (k_mel_w: 8, limited by LDS and 206+ VGPRs; its waves sat
-// waiting 41 % of their time, rocprofv3 SQ counters r02n).
+// n_fft = 4096: two waves per frame (128 threads).  2048-point complex FFT of
+// the even/odd sample pairs (the 4096-point real FFT) as radix-16/16/8
+// Stockham passes in an 18 KB LDS frame buffer, base twiddles held in VGPRs
+// (their powers recomputed per frame), real-FFT post-processing + |X|^power on
+// bins kmin..kmax, then the banded mel sums.  Each lane holds half of a
+// one-wave design's butterflies, so a wave needs <= 168 VGPRs: 12 waves per CU
+// (the one-wave-per-frame kernel it replaced ran 8, limited by LDS and 206
+// VGPRs; its waves sat waiting 41 % of their time, rocprofv3 SQ counters r02n).
 #ifndef ACFE_MEL_W2_WPE
 #define ACFE_MEL_W2_WPE 3
 #endif
-// k_mel_w2's LDS index: one float2 of padding per 16 points (k_mel_w pads one
-// per 8): pass-1 rows (stride 17), pass-2/3 stores (16-lane groups of
-// consecutive points) are bank-conflict free; the 32-lane reads keep one
-// colliding lane pair either way (k_mel_w: 50 % of its LDS cycles were
-// conflicts, SQ counters r02n)
+// k_mel_w2's LDS index: one float2 of padding per 16 points: pass-1 rows
+// (stride 17), pass-2/3 stores (16-lane groups of consecutive points) are
+// bank-conflict free; the 32-lane reads keep one colliding lane pair (the
+// one-wave kernel's pad-per-8 layout had 50 % of its LDS cycles in conflicts,
+// SQ counters r02n)
 __device__ __forceinline__ int padx16(int i) { return i + (i >> 4); }
 
 template <int NC, int R, int NS, int NT>
@@ -909,14 +722,6 @@ k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
   }
 }
 
-static bool mel_wave_path() {
-  static const int v = [] {
-    const char* e = getenv("ACFE_MEL_BLOCK");
-    return (e && atoi(e)) ? 0 : 1;
-  }();
-  return v != 0;
-}
-
 ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch, int n,
                           const float* stats, int pad_mode, int power, float* out, int layout,
                           void* stream) {
@@ -927,27 +732,13 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   if (pad_mode == ACFE_PAD_CENTER_REFLECT && n <= p->n_fft / 2) return ACFE_E_INVAL;
   if (batch == 0) return ACFE_OK;
   const int T = acfe_plan_num_frames(p, n, pad_mode);
-  if (p->n_fft == 4096 && mel_wave_path()) {
-    static const int fpw_env = [] {
-      const char* e = getenv("ACFE_MEL_FPW");
-      const int v = e ? atoi(e) : 0;
-      return v > 0 && v <= 64 ? v : 4;
-    }();
-    const int fpw = fpw_env;
+  if (p->n_fft == 4096) {
+    constexpr int fpw = 4;  // frames per workgroup (2: 1.51 ms, 8: equal, r01n/r02y)
     const int nk = p->kmax - p->kmin + 1;
-    const size_t shm = sizeof(float2) * (2048 + 2048 / 8) + (nk <= 1024 ? 0 : sizeof(float) * (nk + 8));
     const size_t shm2 = sizeof(float2) * (2048 + 2048 / 16) + (nk <= 1024 ? 0 : sizeof(float) * (nk + 8));
-    // ACFE_MEL_W1=1: the one-wave-per-frame kernel (read per call: the A/B test flips it)
-    const char* w1 = getenv("ACFE_MEL_W1");
-    const bool one_wave = w1 && atoi(w1);
-    if (one_wave)
-      hipLaunchKernelGGL(k_mel_w, dim3(cdiv(T, fpw), batch), dim3(64), shm, strm(stream), raw, cs, n, stats,
-                         pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
-                         p->n_mels, p->kmin, p->kmax, out, layout);
-    else
-      hipLaunchKernelGGL(k_mel_w2, dim3(cdiv(T, fpw), batch), dim3(128), shm2, strm(stream), raw, cs, n, stats,
-                         pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
-                         p->n_mels, p->kmin, p->kmax, out, layout);
+    hipLaunchKernelGGL(k_mel_w2, dim3(cdiv(T, fpw), batch), dim3(128), shm2, strm(stream), raw, cs, n, stats,
+                       pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
+                       p->n_mels, p->kmin, p->kmax, out, layout);
     return launch_rc("acfe_mel_fwd");
   }
   const int fpb = 4;

@@ -211,8 +211,12 @@ int acfe_conv2d_fwd_dropout(const void* x, int N, int H, int W, int C, const voi
                             int stride, int pad_top, int pad_left, int P, int Q, const float* bias, void* y,
                             int dtype, double* stats_partial, float drop_rate, unsigned long long seed,
                             void* stream);
-/* dX of the convolution above (wflip = flip=1 packing).  workspace: for
- * stride > 1, N*((P-1)*stride+1)*((Q-1)*stride+1)*K elements of dtype. */
+/* dX of the convolution above (wflip = flip=1 packing).  stride > 1 runs the
+ * st x st sub-pixel phases as stride-1 convs of dY with the phase sub-kernels
+ * (no zero insertion) and needs `workspace` of acfe_conv2d_dgrad_workspace
+ * bytes (C * sizeof(dtype) a multiple of 16, dx 16-B aligned). */
+long long acfe_conv2d_dgrad_workspace(int N, int P, int Q, int K, int C, int R, int S, int stride, int pad_top,
+                                      int pad_left, int H, int W, int dtype);
 int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R, int S,
                       int stride, int pad_top, int pad_left, int H, int W, void* dx, int dtype,
                       void* workspace, void* stream);

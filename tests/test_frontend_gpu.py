@@ -95,23 +95,23 @@ def test_mel_streaming_windows(fe, cuda):
 
 @pytest.mark.parametrize("n_mels,pad_mode,norm,power", [(128, "end", True, 2), (160, "constant", True, 2),
                                                         (128, "reflect", False, 1), (40, "end", True, 2)])
-def test_mel_two_wave_kernel_bit_identical(fe, cuda, monkeypatch, n_mels, pad_mode, norm, power):
-    """k_mel_w2 (two waves per frame, the default) runs the same radix
-    passes, twiddles and band sums in the same order as k_mel_w
-    (ACFE_MEL_W1=1); the compiler's multiply-add contraction may differ
-    between the two kernels, so they agree to fp32 rounding (<= 1e-6 of the
-    per-clip maximum; both are checked against the float64 oracle above),
-    including the padded boundary frames, the un-normalised input, power 1
-    and a plan whose bins do not fill a thread round (40 mels up to 1.5 kHz)."""
+def test_mel_kernel_modes(fe, cuda, n_mels, pad_mode, norm, power):
+    """k_mel_w2 across its modes against the float64 oracle: normalise-on-load
+    (stats) or raw input, the three framings (padded boundary frames), power 1
+    and 2, and a plan whose bins do not fill a thread round (40 mels up to
+    1.5 kHz)."""
     raw = synth_clips(3, seed=17)
-    plan = _plan(fe, n_mels=n_mels, fmax=11000 if n_mels != 40 else 1500)
+    fmax = 11000 if n_mels != 40 else 1500
+    plan = _plan(fe, n_mels=n_mels, fmax=fmax)
     x = torch.from_numpy(raw).to(cuda)
     st = fe.normalize_stats(x) if norm else None
-    outs = []
-    for w1 in ("1", "0"):
-        monkeypatch.setenv("ACFE_MEL_W1", w1)
-        outs.append(plan.mel(x, st, pad_mode=pad_mode, power=power, layout="btm").cpu().numpy())
-    _rel_close(outs[1], outs[0], 1e-6)
+    out = plan.mel(x, st, pad_mode=pad_mode, power=power, layout="btm").cpu().numpy()
+    src = of.normalize(raw) if norm else raw.astype(np.float64)
+    if pad_mode == "end":
+        ref = of.raw_to_mel(src, plan.weights, 4096, 281, power=power)
+    else:
+        ref = of.get_spect(src, plan.weights, 4096, 281, power, pad_mode)
+    _rel_close(out, ref.transpose(0, 2, 1), 2e-5)
 
 
 def test_mel_short_and_empty(fe, cuda):

@@ -50,6 +50,12 @@ CONV_CASES = [
     (2, 16, 33, 64, 128, 1, 1, 2, "valid"),
     (2, 22, 31, 128, 256, 3, 3, 3, "same"),
     (2, 22, 31, 128, 256, 1, 1, 3, "valid"),
+    # strided dgrad by sub-pixel phases: even sizes (pad_top 0), "valid" 3x3,
+    # stride 3 with every phase offset, a phase with more taps than rows
+    (2, 16, 34, 64, 128, 3, 3, 2, "same"),
+    (2, 21, 29, 64, 64, 3, 3, 2, "valid"),
+    (2, 23, 35, 64, 128, 3, 3, 3, "same"),
+    (2, 3, 5, 64, 64, 3, 3, 2, "same"),
     (1, 300, 5, 16, 64, 3, 3, 1, "same"),
     # halo-staged 3x3 wgrad (Q % 64 == 0, C % 64 == 0, K in {64, 128}): 1-3 channel chunks
     (2, 10, 64, 128, 128, 3, 3, 1, "same"),

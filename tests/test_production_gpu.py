@@ -206,6 +206,41 @@ def test_conv_rows_dgrad_wgrad_production(env, cuda):
     assert ((d - dw_exact).abs().max() / dw_exact.abs().max()).item() < 5e-4
 
 
+@pytest.mark.parametrize("H,W,C,K,R,st", [(128, 513, 64, 128, 3, 2), (64, 257, 128, 256, 3, 3),
+                                          (128, 513, 64, 128, 1, 2), (64, 257, 128, 256, 1, 3)],
+                         ids=["s2b0_conv2a", "s3b0_conv2a", "s2b0_shortcut", "s3b0_shortcut"])
+def test_strided_dgrad_wr_resnet_production(env, cuda, H, W, C, K, R, st):
+    """wr_resnet's strided layers (resnet/wr_resnet.py:22, stage-2/3 block-0
+    conv2a 3x3 and the 1x1 shortcuts at strides 2 and 3, TF "same" / "valid"
+    padding) at the T1/I input 128 x 513: the sub-pixel phase dgrad against
+    the float64 transposed convolution of the same bf16 operands, every
+    element within one bf16 ulp + 1e-4."""
+    ops, call, lib, ptr, stream = env
+    N = 2
+    g = torch.Generator(device="cpu").manual_seed(7 + st + R)
+    w = (torch.randn((K, R, R, C), generator=g) * (1.0 / (R * C ** 0.5))).to(cuda)
+    if R == 3:
+        P, pt = ops.same_padding(H, 3, st)
+        Q, pl = ops.same_padding(W, 3, st)
+    else:
+        P, Q, pt, pl = ops.valid_out(H, 1, st), ops.valid_out(W, 1, st), 0, 0
+    dy = (torch.randn((N, P, Q, K), generator=g) * 0.5).to(BF).to(cuda)
+    wf = ops.pack_weights(w, BF, True)
+    dx = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+    nb = lib.acfe_conv2d_dgrad_workspace(N, P, Q, K, C, R, R, st, pt, pl, H, W, 1)
+    ws = torch.empty((nb,), dtype=torch.uint8, device=cuda)
+    call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, R, st, pt, pl, H, W, ptr(dx), 1, ptr(ws), stream())
+    torch.cuda.synchronize()
+    wd = w.cpu().to(BF).to(F64).permute(0, 3, 1, 2)
+    gd = dy.cpu().to(F64).permute(0, 3, 1, 2)
+    # exact dX: the adjoint of the padded strided conv, cropped to H x W
+    xr = torch.zeros((N, C, H, W), dtype=F64, requires_grad=True)
+    xp = F.pad(xr, (pl, max(0, (Q - 1) * st + R - W - pl), pt, max(0, (P - 1) * st + R - H - pt)))
+    (F.conv2d(xp, wd, stride=st) * gd).sum().backward()
+    assert torch.isfinite(dx.float()).all()
+    _within_ulp(dx, xr.grad.permute(0, 2, 3, 1), what="strided dgrad")
+
+
 def test_bird_t1_shape_eval_parity(cuda):
     """wr_resnet_bird at the T1 input (128 mels x 513 frames, 50 classes), bf16,
     eval-mode BN, 2 clips, against the bf16-storage float64 oracle

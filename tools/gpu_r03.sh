@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-3 GPU session driver: each step has its own time limit; the first
+# failing step ends the script.  usage: tools/gpu_r03.sh TAG STEP...
+#   steps: new (new parity tests), tests (all -m gpu), smoke, bench, prof, e2e, wrn, infer
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=$1; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+step() { # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 $t "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -6 $O/$name.log
+  [ $rc -eq 0 ] || exit $rc
+}
+PYT="python -u -m pytest -x -v -s --timeout 240 --timeout-method thread"
+for s in "$@"; do
+  case $s in
+    new) step new 900 $PYT -m gpu tests/test_dp_gpu.py tests/test_e2e_gpu.py \
+           "tests/test_model_gpu.py::test_model_bf16_train_well_conditioned" ;;
+    tests) step tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+            python bench.py --no-cpu-baseline --steps 10 --warmup 3 ;;
+    e2e) step e2e 900 python bench.py --workload e2e --clips ${CLIPS:-8192} --steps 40 --warmup 4 --no-cpu-baseline ;;
+    wrn) step wrn 600 python bench.py --model wrn --classes 2 --no-cpu-baseline ;;
+    wrnprof) step wrnprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wprof -o run -- \
+            python bench.py --model wrn --classes 2 --no-cpu-baseline --steps 10 --warmup 3 ;;
+    infer) step infer 600 python bench.py --workload infer --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done
