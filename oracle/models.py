@@ -75,6 +75,28 @@ def logmeanexp(x, axis, sharpness=5.0):
     return (torch.logsumexp(x * sharpness, dim=axis) - math.log(x.shape[axis])) / sharpness
 
 
+def bird_block(X, p, pre, stride, relu_out, training=True, state=None, storage=None):
+    """wr_resnet_bird.basic_block (:103-179) on NCHW X; `pre` = "blocks.{i}."."""
+    S = storage
+    sc = X
+    Y = X
+    if stride > 1:
+        Y = bn(Y, p, pre + "bn2a0", training, relu=True, state=state, storage=S)
+        Y = conv(Y, p[pre + "conv2a0.weight"], p[pre + "conv2a0.bias"], storage=S)
+    Y = bn(Y, p, pre + "bn2a", training, relu=True, state=state, storage=S)
+    Y = conv(Y, p[pre + "conv21.weight"], p[pre + "conv21.bias"], storage=S)
+    if stride > 1:
+        Y = F.max_pool2d(Y, stride, stride)
+    Y = bn(Y, p, pre + "bn2b", training, relu=True, state=state, storage=S)
+    Y = conv(Y, p[pre + "conv2b.weight"], p[pre + "conv2b.bias"], storage=S)
+    if pre + "shortcut.weight" in p:
+        sc = conv(_q(avgpool_same(sc, stride), S), p[pre + "shortcut.weight"], p[pre + "shortcut.bias"], storage=S)
+    X = Y + sc
+    if relu_out:
+        X = F.relu(X)
+    return _q(X, S)
+
+
 def wr_resnet_bird(x_nchw, p, training=True, state=None, depth=22, k=4, storage=None):
     """wr_resnet_bird.WRResNet forward (:7-80) -> logits.  p: name -> tensor."""
     n = int((depth - 4) / 6)
@@ -85,26 +107,7 @@ def wr_resnet_bird(x_nchw, p, training=True, state=None, depth=22, k=4, storage=
     bi = 0
     for stage in range(1, 4):
         for d in range(n):
-            pre = f"blocks.{bi}."
-            stride = 2 if d == 0 else 1
-            sc = X
-            Y = X
-            if stride > 1:
-                Y = bn(Y, p, pre + "bn2a0", training, relu=True, state=state, storage=S)
-                Y = conv(Y, p[pre + "conv2a0.weight"], p[pre + "conv2a0.bias"], storage=S)
-            Y = bn(Y, p, pre + "bn2a", training, relu=True, state=state, storage=S)
-            Y = conv(Y, p[pre + "conv21.weight"], p[pre + "conv21.bias"], storage=S)
-            if stride > 1:
-                Y = F.max_pool2d(Y, stride, stride)
-            Y = bn(Y, p, pre + "bn2b", training, relu=True, state=state, storage=S)
-            Y = conv(Y, p[pre + "conv2b.weight"], p[pre + "conv2b.bias"], storage=S)
-            if pre + "shortcut.weight" in p:
-                sc = conv(_q(avgpool_same(sc, stride), S), p[pre + "shortcut.weight"], p[pre + "shortcut.bias"],
-                          storage=S)
-            X = Y + sc
-            if stage + d > 1:
-                X = F.relu(X)
-            X = _q(X, S)
+            X = bird_block(X, p, f"blocks.{bi}.", 2 if d == 0 else 1, stage + d > 1, training, state, S)
             bi += 1
     X = bn(X, p, "final_bn", training, relu=True, state=state, storage=S)
     X = conv(X, p["head_conv1.weight"], p["head_conv1.bias"], storage=S)
@@ -118,6 +121,19 @@ def wr_resnet_bird(x_nchw, p, training=True, state=None, depth=22, k=4, storage=
     return X @ p["prediction.kernel"] + p["prediction.bias"]
 
 
+def wrn_block(X, p, pre, stride, training=True, state=None, storage=None):
+    """wr_resnet.basic_block (:46-90) on NCHW X; `pre` = "blocks.{i}."."""
+    S = storage
+    Y = bn(X, p, pre + "bn2a", training, relu=True, state=state, storage=S)
+    Y = conv(Y, p[pre + "conv2a.weight"], p[pre + "conv2a.bias"], stride, storage=S)
+    Y = bn(Y, p, pre + "bn2b", training, relu=True, state=state, storage=S)
+    Y = conv(Y, p[pre + "conv2b.weight"], p[pre + "conv2b.bias"], storage=S)
+    sc = X
+    if pre + "shortcut.weight" in p:
+        sc = conv(X, p[pre + "shortcut.weight"], p[pre + "shortcut.bias"], stride, "valid", storage=S)
+    return _q(F.relu(Y + sc), S)
+
+
 def wr_resnet(x_nchw, p, training=True, state=None, depth=22, k=4, storage=None):
     """wr_resnet.WRResNet forward (:5-33) -> logits."""
     n = int((depth - 4) / 6)
@@ -126,16 +142,7 @@ def wr_resnet(x_nchw, p, training=True, state=None, depth=22, k=4, storage=None)
     bi = 0
     for stage in range(1, 4):
         for d in range(n):
-            pre = f"blocks.{bi}."
-            stride = stage if d == 0 else 1
-            Y = bn(X, p, pre + "bn2a", training, relu=True, state=state, storage=S)
-            Y = conv(Y, p[pre + "conv2a.weight"], p[pre + "conv2a.bias"], stride, storage=S)
-            Y = bn(Y, p, pre + "bn2b", training, relu=True, state=state, storage=S)
-            Y = conv(Y, p[pre + "conv2b.weight"], p[pre + "conv2b.bias"], storage=S)
-            sc = X
-            if pre + "shortcut.weight" in p:
-                sc = conv(X, p[pre + "shortcut.weight"], p[pre + "shortcut.bias"], stride, "valid", storage=S)
-            X = _q(F.relu(Y + sc), S)
+            X = wrn_block(X, p, f"blocks.{bi}.", stage if d == 0 else 1, training, state, S)
             bi += 1
     X = bn(X, p, "final_bn", training, relu=True, state=state, storage=S)
     X = X.mean((2, 3))

@@ -19,12 +19,14 @@ The wr_resnet case is config I's composed fp32 path (front end + PCEN +
 wr_resnet forward at 128 x 513), here with its backward as well.
 
 Tolerances (fp32 compute, eval-mode BN, dropout 0; oracle in float64):
-  PCEN features   max |dev - ref| <= 1e-4 on the [-1, 1] output
-  logits          rel-L2 <= 1e-4
-  loss            |dev - ref| <= 1e-4 * max(1, |ref|)
-  gradient arena  rel-L2 <= 1e-3 (model + PCEN parameters together)
-  PCEN gradients  rel-L2 <= 1e-2 (four scalars summed over 3 x 128 x 513
+  PCEN features   max |dev - ref| <= 2e-5 on the [-1, 1] output
+  logits          rel-L2 <= 2e-5
+  loss            |dev - ref| <= 2e-5 * max(1, |ref|)
+  gradient arena  rel-L2 <= 2e-4 (model + PCEN parameters together)
+  PCEN gradients  rel-L2 <= 1e-3 (four scalars summed over 3 x 128 x 513
                   elements through the batch-global min/max)
+Measured on MI355X (r03a): features 1.2e-6; logits 2.3e-6 (wr_resnet) /
+3.1e-7 (wr_resnet_bird); arena 1.1e-5 / 3.0e-5; PCEN gradients 1.7e-6 / 6.1e-5.
 """
 import numpy as np
 import pytest
@@ -108,8 +110,8 @@ def test_raw_clips_to_logits_and_gradients(cuda, kind):
     ep = rel(fe.pcen.params.grad, gp_ref)
     print(f"{kind}: features {ef:.2e} logits {ez:.2e} loss {abs(loss.item() - l_ref.item()):.2e} "
           f"arena {eg:.2e} pcen-grad {ep:.2e}")
-    assert ef <= 1e-4, ef
-    assert ez <= 1e-4, (ez, z, z_ref)
-    assert abs(loss.item() - l_ref.item()) <= 1e-4 * max(1.0, abs(l_ref.item()))
-    assert eg <= 1e-3, eg
-    assert ep <= 1e-2, (ep, fe.pcen.params.grad, gp_ref)
+    assert ef <= 2e-5, ef
+    assert ez <= 2e-5, (ez, z, z_ref)
+    assert abs(loss.item() - l_ref.item()) <= 2e-5 * max(1.0, abs(l_ref.item()))
+    assert eg <= 2e-4, eg
+    assert ep <= 1e-3, (ep, fe.pcen.params.grad, gp_ref)

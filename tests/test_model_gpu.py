@@ -161,41 +161,74 @@ def test_model_step_parity(cuda, kind, prec, training):
         assert rel(m.state_dict()[k], v) < (1e-4 if dtype == torch.float32 else 3e-2), k
 
 
-@pytest.mark.parametrize("kind", ["bird", "wrn"])
-def test_model_bf16_train_well_conditioned(cuda, kind):
-    """bf16 training-mode step on a batch large enough for BatchNormalization's
-    batch statistics to be well conditioned (N = 16 at 128 x 64; VERDICT r02
-    next #1): against the oracle with the same bf16 storage points (float64
-    arithmetic), rel-L2(logits) <= 2e-2, |loss| <= 2e-2 relative,
-    rel-L2(gradient arena) <= 5e-2, and the moving statistics <= 2e-2."""
-    from acfe import ops
+BLOCK_CASES = [("bird", 0, 8, 128, 128), ("bird", 1, 8, 128, 128), ("bird", 3, 8, 128, 128),
+               ("wrn", 0, 4, 64, 64), ("wrn", 3, 4, 64, 64)]
 
-    H, W, classes, N = 128, 64, 10, 16
-    m = _build(kind, (H, W, 3), classes, torch.bfloat16, cuda)
+
+@pytest.mark.parametrize("kind,bi,N,H,W", BLOCK_CASES,
+                         ids=["bird-s1b0", "bird-s1b1", "bird-s2b0", "wrn-s1b0", "wrn-s2b0"])
+def test_block_bf16_train_fixed_bounds(cuda, kind, bi, N, H, W):
+    """bf16 training-mode residual blocks with FIXED bounds (VERDICT r02 next
+    #1, the well-conditioned bf16 training case).
+
+    A whole-model bf16 training step at init is not well conditioned at any
+    batch size: the loss gradient reaching the pooled head is nearly uniform
+    over pixels, so every training-mode BatchNormalization backward cancels it
+    (dy - mean(dy) - x_hat mean(dy x_hat)) and what is left is bf16 rounding
+    noise -- two bf16-storage oracles (fp32 vs fp64 accumulation) differ by
+    63 % in their gradients at N = 16, 128 x 64 (test_model_step_parity keeps
+    that case with spread-relative bounds).  Here each block runs in training
+    mode on a random bf16 input with a random per-pixel upstream gradient,
+    which keeps the BN backward well conditioned (the two oracles agree to
+    1e-4 .. 1e-2), and the device is held to fixed bounds against the
+    float64-accumulating oracle with the same bf16 storage points:
+    rel-L2 output <= 1e-2, input gradient <= 2e-2, parameter arena <= 2e-2
+    (5e-2 for the stride-2 stage-2 block, whose two oracles differ by 1.4e-2),
+    BN moving statistics <= 1e-2.  The device's fused nodes all run: BN
+    prologues, conv epilogue statistics, pooled epilogue, residual links,
+    1x1+BN node, phase dgrad (wrn stride 2)."""
+    m = _build(kind, (H, W, 3), 10, torch.bfloat16, cuda)
     m.train(True)
-    x = _input(N, H, W, seed=7).to(torch.bfloat16).double()
-    tgt = torch.zeros(N, classes, dtype=torch.float64)
-    tgt[torch.arange(N), (torch.arange(N) * 7) % classes] = 1
-    fwd = om.wr_resnet_bird if kind == "bird" else om.wr_resnet
-    p = {k: v.detach().double().cpu().clone() for k, v in m.state_dict().items()}
+    blk = m.blocks[bi]
+    pre = f"blocks.{bi}."
+    if kind == "bird":
+        h, w, c = H, W // 2, 16
+    else:
+        h, w, c = H, W, 16
+    for j in range(bi):
+        b = m.blocks[j]
+        h, w, c = -(-h // b.stride), -(-w // b.stride), b.out_channels
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((N, c, h, w), generator=g, dtype=torch.float64).to(torch.bfloat16).double()
+    # oracle (float64 arithmetic, bf16 storage points)
+    p = {k: v.detach().double().cpu().clone() for k, v in m.state_dict().items() if k.startswith(pre)}
     prm = {k: v.requires_grad_(True) for k, v in p.items() if "moving" not in k}
     st = {k: v for k, v in p.items() if "moving" in k}
-    z_ref = fwd(x[:, None].repeat(1, 3, 1, 1), prm, True, st, storage="bf16")
-    l_ref = om.keras_loss(z_ref, tgt, "cce")
-    l_ref.backward()
-    z = m(x.to(torch.bfloat16).to(cuda))
-    loss, dz = ops.loss_and_grad(z, tgt.float().to(cuda), "cce")
-    z.backward(dz)
-    names = [n for n, _ in m.named_parameters()]
-    g_dev = torch.cat([q.grad.reshape(-1).double().cpu() for q in m.parameters()])
-    g_ref = torch.cat([prm[n].grad.reshape(-1) for n in names])
-    ez, eg = rel(z, z_ref), rel(g_dev, g_ref)
-    print(f"{kind} bf16 train N={N}: logits {ez:.3e} arena {eg:.3e} loss {loss.item():.5f} vs {l_ref.item():.5f}")
-    assert ez <= 2e-2, ez
-    assert abs(loss.item() - l_ref.item()) <= 2e-2 * max(1.0, abs(l_ref.item()))
-    assert eg <= 5e-2, eg
+    xr = x.clone().requires_grad_(True)
+    if kind == "bird":
+        z_ref = om.bird_block(xr, prm, pre, blk.stride, blk.relu_out, True, st, storage="bf16")
+    else:
+        z_ref = om.wrn_block(xr, prm, pre, blk.stride, True, st, storage="bf16")
+    dz = torch.randn(z_ref.shape, generator=torch.Generator().manual_seed(12), dtype=torch.float64)
+    dz = dz.to(torch.bfloat16).double()
+    (z_ref * dz).sum().backward()
+    # device (NHWC)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda).requires_grad_(True)
+    z, _ = blk(xd)
+    z.backward(dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda))
+    names = [n for n, _ in blk.named_parameters()]
+    g_dev = torch.cat([q.grad.reshape(-1).double().cpu() for q in blk.parameters()])
+    g_ref = torch.cat([prm[pre + n].grad.reshape(-1) for n in names])
+    ez = rel(z.permute(0, 3, 1, 2), z_ref)
+    ex = rel(xd.grad.permute(0, 3, 1, 2), xr.grad)
+    eg = rel(g_dev, g_ref)
+    print(f"{kind} block {bi} bf16 train: out {ez:.2e} dx {ex:.2e} arena {eg:.2e}")
+    assert ez <= 1e-2, ez
+    assert ex <= 2e-2, ex
+    assert eg <= (5e-2 if (kind, bi) == ("bird", 3) else 2e-2), eg
+    sd = blk.state_dict()
     for k, v in st.items():
-        assert rel(m.state_dict()[k], v) < 2e-2, k
+        assert rel(sd[k[len(pre):]], v) <= 1e-2, k
 
 
 def test_bird_shapes_reference_config(cuda):
