@@ -35,7 +35,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_normalize_stats": [P, I64, I32, I32, P, P],
     "acfe_normalize_apply": [P, I64, I32, I32, P, P, P],
     "acfe_mixup": [P, P, P, P, P, I32, I32, P, P],
-    "acfe_gather_rows": [P, I64, I64, P, I32, I32, P, I64, P],
+    "acfe_copy_rows": [P, I64, I64, P, P, I64, I64, P, I32, I32, P],
     "acfe_mel_fwd": [P, P, I64, I32, I32, P, I32, I32, P, I32, P],
     "acfe_mel_from_spec": [P, P, I64, I32, I32, I32, I32, P, I32, P],
     "acfe_pcen_partials": [I32, I32],

@@ -264,41 +264,37 @@ ACFE_API int acfe_mixup(const float* x1, const float* s1, const float* x2, const
   return launch_rc("acfe_mixup");
 }
 
-// Batch assembly from the loader's device-resident clip pool (tfdataset
-// AudioDataset): out[i][0:n) = pool[idx[i] * pool_stride + 0:n), 16-B vectors
-// when both strides and n are multiples of 4 floats.
-__global__ void k_gather_rows4(const float4* __restrict__ pool, int64_t ps4, const int* __restrict__ idx, int n4,
-                               float4* __restrict__ out, int64_t os4) {
+// Row copies of the loader's device-resident clip pool (tfdataset
+// AudioDataset): dst[dst_idx[i]][0:n) = src[src_idx[i]][0:n) for i < count
+// (a NULL index list is the identity): chunk -> free pool slots (scatter) and
+// pool slots -> batch (gather); 16-B vectors when strides, n and both bases
+// allow.
+template <typename V>
+__global__ void k_copy_rows(const V* __restrict__ src, int64_t ss, const int* __restrict__ si, V* __restrict__ dst,
+                            int64_t ds, const int* __restrict__ di, int n) {
   const int b = blockIdx.y;
-  const float4* src = pool + (int64_t)idx[b] * ps4;
-  float4* dst = out + (int64_t)b * os4;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) dst[i] = src[i];
-}
-__global__ void k_gather_rows1(const float* __restrict__ pool, int64_t ps, const int* __restrict__ idx, int n,
-                               float* __restrict__ out, int64_t os) {
-  const int b = blockIdx.y;
-  const float* src = pool + (int64_t)idx[b] * ps;
-  float* dst = out + (int64_t)b * os;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) dst[i] = src[i];
+  const V* s = src + (int64_t)(si ? si[b] : b) * ss;
+  V* d = dst + (int64_t)(di ? di[b] : b) * ds;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) d[i] = s[i];
 }
 
-ACFE_API int acfe_gather_rows(const float* pool, int64_t pool_stride, int64_t pool_rows, const int* idx_dev,
-                              int batch, int n, float* out, int64_t out_stride, void* stream) {
-  if (!pool || !idx_dev || !out || batch < 0 || batch > 65535 || n <= 0 || pool_rows <= 0 ||
-      pool_stride < n || out_stride < n)
+ACFE_API int acfe_copy_rows(const float* src, int64_t src_stride, int64_t src_rows, const int* src_idx,
+                            float* dst, int64_t dst_stride, int64_t dst_rows, const int* dst_idx, int count, int n,
+                            void* stream) {
+  if (!src || !dst || count < 0 || count > 65535 || n <= 0 || src_stride < n || dst_stride < n ||
+      (!src_idx && count > src_rows) || (!dst_idx && count > dst_rows))
     return ACFE_E_INVAL;
-  if (batch == 0) return ACFE_OK;
-  const bool v4 = (pool_stride % 4 == 0) && (out_stride % 4 == 0) && (n % 4 == 0) &&
-                  ((uintptr_t)pool % 16 == 0) && ((uintptr_t)out % 16 == 0);
-  if (v4) {
-    hipLaunchKernelGGL(k_gather_rows4, dim3(cdiv(n / 4, 256 * 8), batch), dim3(256), 0, strm(stream),
-                       reinterpret_cast<const float4*>(pool), pool_stride / 4, idx_dev, n / 4,
-                       reinterpret_cast<float4*>(out), out_stride / 4);
-  } else {
-    hipLaunchKernelGGL(k_gather_rows1, dim3(cdiv(n, 256 * 8), batch), dim3(256), 0, strm(stream), pool,
-                       pool_stride, idx_dev, n, out, out_stride);
-  }
-  return launch_rc("acfe_gather_rows");
+  if (count == 0) return ACFE_OK;
+  const bool v4 = src_stride % 4 == 0 && dst_stride % 4 == 0 && n % 4 == 0 && ((uintptr_t)src & 15) == 0 &&
+                  ((uintptr_t)dst & 15) == 0;
+  if (v4)
+    hipLaunchKernelGGL(k_copy_rows<float4>, dim3(cdiv(n / 4, 256 * 8), count), dim3(256), 0, strm(stream),
+                       reinterpret_cast<const float4*>(src), src_stride / 4, src_idx, reinterpret_cast<float4*>(dst),
+                       dst_stride / 4, dst_idx, n / 4);
+  else
+    hipLaunchKernelGGL(k_copy_rows<float>, dim3(cdiv(n, 256 * 8), count), dim3(256), 0, strm(stream), src,
+                       src_stride, src_idx, dst, dst_stride, dst_idx, n);
+  return launch_rc("acfe_copy_rows");
 }
 
 // ------------------------------------------------------------ FFT helpers

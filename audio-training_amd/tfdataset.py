@@ -16,12 +16,14 @@ Pipeline (every record is inflated and parsed ONCE):
                    pinned staging chunk (no per-clip Python copies; ctypes
                    drops the GIL inside both calls)
   mover thread     one host->device copy per full chunk (64 clips) on a side
-                   stream into a frame of the device-resident clip pool
+                   stream, its clips scattered into free slots of the
+                   device-resident clip pool (acfe_copy_rows)
   consumer         the pool is the shuffle buffer (tfdataset.py:835-838,
                    4096 examples): a batch is B slots drawn uniformly from the
-                   resident clips and gathered on the device
-                   (acfe_gather_rows); each example is a primary exactly once
-                   per epoch (one pass, as the reference's dataset)
+                   resident clips and gathered on the device (acfe_copy_rows),
+                   their slots refilled as the next chunks arrive; each
+                   example is a primary exactly once per epoch (one pass, as
+                   the reference's dataset)
 
 mix_up partners.  The reference zips a second, independently shuffled full
 pass over the same records (tfdataset.py:473-480), i.e. it decodes every
@@ -172,9 +174,10 @@ class AudioDataset:
         buf = max(shuffle_buffer if shuffle else 0, self.batch_size)
         buf = min(buf, max(self.batch_size, POOL_BYTES // clip_bytes))
         self.buffer = buf
-        self.frames = -(-(buf + self.batch_size) // self.per_chunk) + 2
+        self.pool_rows = buf + 2 * self.per_chunk
         self._epoch_size = epoch_size
         self._pool = None
+        self._dstage = None
         self._stage_buf = None
         self.error = None
 
@@ -278,12 +281,35 @@ class AudioDataset:
     # ---------------------------------------------------------------- pool
     def _ensure_pool(self):
         if self._pool is None:
-            rows = self.frames * self.per_chunk
-            self._pool = torch.empty((rows, self.nfloats), dtype=torch.float32, device=self.device)
+            self._pool = torch.empty((self.pool_rows, self.nfloats), dtype=torch.float32, device=self.device)
+            if self.device.type == "cuda":  # one chunk on the device: pinned -> here -> scattered into free slots
+                self._dstage = torch.empty((self.per_chunk, self.nfloats), dtype=torch.float32, device=self.device)
         return self._pool
 
-    def _mover(self, stage: _Staging, ready: queue.Queue, free_frames: queue.Queue, stop, readers_done):
-        """Full pinned chunks -> device pool frames (one copy per chunk)."""
+    def _copy_rows(self, src, src_idx, dst, dst_idx, n):
+        """dst[dst_idx[i]] = src[src_idx[i]] on the device (acfe_copy_rows; the
+        index lists are host ints, copied to the device on the current stream)."""
+        from acfe._lib import call
+        from acfe._torch import stream
+
+        def dev_idx(ix, rows):
+            if ix is None:
+                return None
+            a = np.asarray(ix, np.int32)
+            assert a.min() >= 0 and a.max() < rows
+            return torch.from_numpy(a).pin_memory().to(self.device, non_blocking=True)
+
+        si, di = dev_idx(src_idx, src.shape[0]), dev_idx(dst_idx, dst.shape[0])
+        call("acfe_copy_rows", src.data_ptr(), self.nfloats, src.shape[0], None if si is None else si.data_ptr(),
+             dst.data_ptr(), self.nfloats, dst.shape[0], None if di is None else di.data_ptr(), n, self.nfloats,
+             stream())
+        return si, di  # (kept alive by the caller until the launch's stream has passed them)
+
+    def _mover(self, stage: _Staging, ready: queue.Queue, slots: "_SlotPool", stop, readers_done):
+        """Full pinned chunks -> the device pool: one host->device copy per
+        chunk into a device staging chunk, then its valid rows are scattered
+        into free pool slots (acfe_copy_rows) once the batch gathers that last
+        read those slots have run (event of their release)."""
         try:
             cuda = self.device.type == "cuda"
             cs = torch.cuda.Stream(self.device) if cuda else None
@@ -302,34 +328,39 @@ class AudioDataset:
                             return
                     continue
                 n = stage.count[c]
-                labels = stage.labels[c, :n].copy()
-                while True:
-                    try:
-                        f, ev = free_frames.get(timeout=_POLL)
-                        break
-                    except queue.Empty:
-                        if stop.is_set():
-                            return
-                lo = f * self.per_chunk
+                labels = stage.labels[c, :n]
+                valid = [j for j in range(n) if labels[j] >= 0]
+                if not valid:
+                    stage.free.put(c)
+                    continue
+                got = slots.acquire(len(valid), stop)
+                if got is None:
+                    return
+                dst, ev = got
                 if cuda:
                     with torch.cuda.stream(cs):
                         if ev is not None:
-                            cs.wait_event(ev)  # the gathers that read this frame last are done
-                        pool[lo:lo + n].copy_(stage.buf[c, :n], non_blocking=True)
+                            cs.wait_event(ev)
+                        self._dstage[:n].copy_(stage.buf[c, :n], non_blocking=True)
+                        keep = self._copy_rows(self._dstage, valid, pool, dst, len(valid))
                         done = torch.cuda.Event()
                         done.record(cs)
                     done.synchronize()
+                    del keep
                 else:
-                    pool[lo:lo + n].copy_(stage.buf[c, :n])
+                    pool.index_copy_(0, torch.tensor(dst, dtype=torch.int64),
+                                     stage.buf[c, torch.tensor(valid, dtype=torch.int64)])
+                out_labels = labels[valid].copy()
                 stage.free.put(c)
-                ready.put((f, labels))
+                ready.put((dst, out_labels))
         except Exception as e:  # noqa: BLE001
             self.error = e
             logging.exception("loader mover thread failed")
             ready.put(None)
 
     def _stream(self, augment):
-        """Generator of (x1 idx, x2 idx or None, labels) batches for one epoch."""
+        """Generator of (primary slots, partner slots or None, slot labels,
+        slot pool) per batch of one epoch."""
         files = list(self.files)
         rng = random.Random(self.seed + 1000003 * self.epoch)
         if self.shuffle:
@@ -341,13 +372,11 @@ class AudioDataset:
                                           dtype=torch.float32, pin_memory=self.device.type == "cuda")
         stage = _Staging(self._stage_buf, stop)
         self.error = None
-        pool = self._ensure_pool()
+        self._ensure_pool()
         fq: queue.Queue = queue.Queue()
         for f in files:
             fq.put(f)
-        free_frames: queue.Queue = queue.Queue()
-        for f in range(self.frames):
-            free_frames.put((f, None))
+        slots = _SlotPool(self.pool_rows)
         ready: queue.Queue = queue.Queue()
         nthreads = min(self.threads, max(1, len(files)))
         readers = [threading.Thread(target=self._reader, args=(fq, stage, stop, stable), daemon=True)
@@ -363,13 +392,13 @@ class AudioDataset:
 
         watcher = threading.Thread(target=watch, daemon=True)
         watcher.start()
-        mover = threading.Thread(target=self._mover, args=(stage, ready, free_frames, stop, readers_done),
-                                 daemon=True)
+        mover = threading.Thread(target=self._mover, args=(stage, ready, slots, stop, readers_done), daemon=True)
         mover.start()
-        per = self.per_chunk
-        live: list[int] = []                   # pool rows not yet used as a primary this epoch
-        left = [0] * self.frames               # unconsumed valid rows per frame
-        lab = np.full(self.frames * per, -1, np.int32)
+        live: list[int] = []                   # resident slots not yet used as a primary this epoch
+        lab = np.full(self.pool_rows, -1, np.int32)
+        # the shuffle buffer: batches are drawn once `target` clips are resident
+        # (or the epoch's records are exhausted); the pool holds target + 2
+        # chunks, so the mover always finds free slots while the buffer refills
         target = self.buffer if self.shuffle else self.batch_size
         done = False
         try:
@@ -379,14 +408,9 @@ class AudioDataset:
                     if item is None:
                         done = True
                         break
-                    f, labels = item
-                    rows = [f * per + j for j in range(len(labels)) if labels[j] >= 0]
-                    lab[f * per:f * per + len(labels)] = labels
-                    left[f] = len(rows)
-                    if not rows:
-                        free_frames.put((f, None))
-                        continue
-                    live.extend(rows)
+                    dst, labels = item
+                    lab[dst] = labels
+                    live.extend(dst)
                 if self.error is not None:
                     raise RuntimeError("TFRecord loader failed") from self.error
                 if len(live) < self.batch_size:  # the stream has ended (the fill loop stops only then)
@@ -405,13 +429,7 @@ class AudioDataset:
                 if augment:
                     resident = live + pick
                     partner = [resident[rng.randrange(len(resident))] for _ in range(b)]
-                drained = set()
-                for r in pick:
-                    f = r // per
-                    left[f] -= 1
-                    if left[f] == 0:
-                        drained.add(f)
-                yield pick, partner, lab, drained, free_frames
+                yield pick, partner, lab, slots
         finally:
             stop.set()
             for t in readers + [watcher, mover]:
@@ -428,41 +446,61 @@ class AudioDataset:
     def _gather(self, rows):
         pool = self._pool
         b = len(rows)
-        idx = np.asarray(rows, np.int32)
-        assert idx.min() >= 0 and idx.max() < pool.shape[0]
         if self.device.type != "cuda":
-            return pool.index_select(0, torch.from_numpy(idx.astype(np.int64))).reshape((b,) + self.shape)
-        from acfe._lib import call
-        from acfe._torch import stream
-
-        idx_dev = torch.from_numpy(idx).pin_memory().to(self.device, non_blocking=True)
+            return pool.index_select(0, torch.tensor(rows, dtype=torch.int64)).reshape((b,) + self.shape)
         out = torch.empty((b,) + self.shape, dtype=torch.float32, device=self.device)
-        call("acfe_gather_rows", pool.data_ptr(), self.nfloats, pool.shape[0], idx_dev.data_ptr(), b, self.nfloats,
-             out.data_ptr(), self.nfloats, stream())
+        self._copy_rows(pool, rows, out.view(b, self.nfloats), None, b)
         return out
 
     def __iter__(self):
         augment = self.augment
         self.epoch += 1
         n = 0
-        for pick, partner, lab, drained, free_frames in self._stream(augment):
+        for pick, partner, lab, slots in self._stream(augment):
             x1 = self._gather(pick)
             y1 = self._labels(pick, lab)
             if augment:
                 x2 = self._gather(partner)
                 y2 = self._labels(partner, lab)
-            # frames whose every row has now been used as a primary go back to
-            # the mover once the gathers above have run (stream-ordered event)
-            for f in drained:
-                ev = None
-                if self.device.type == "cuda":
-                    ev = torch.cuda.Event()
-                    ev.record()
-                free_frames.put((f, ev))
+            # the primaries' slots are free for new clips once the gathers
+            # above have run (an event on the launch stream orders the refill)
+            ev = None
+            if self.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+            slots.release(pick, ev)
             n += len(pick)
             yield ((x1, y1), (x2, y2)) if augment else (x1, y1)
         if self._epoch_size is None and self.record_shard is None:
             self._epoch_size = n
+
+
+class _SlotPool:
+    """Free slots of the device clip pool.  release() returns a batch's
+    primary slots with the event recorded after the gathers that read them;
+    acquire(n) hands out n free slots and the newest such event (events of
+    one stream complete in order, so waiting for it covers every older one)."""
+
+    def __init__(self, rows):
+        self.free = list(range(rows - 1, -1, -1))
+        self.ev = None
+        self.cv = threading.Condition()
+
+    def release(self, rows, ev):
+        with self.cv:
+            self.free.extend(rows)
+            if ev is not None:
+                self.ev = ev
+            self.cv.notify_all()
+
+    def acquire(self, n, stop):
+        with self.cv:
+            while len(self.free) < n:
+                if stop.is_set():
+                    return None
+                self.cv.wait(timeout=_POLL)
+            out = [self.free.pop() for _ in range(n)]
+            return out, self.ev
 
 
 def _files(dir):

@@ -400,8 +400,11 @@ def run_e2e(a):
     jobs = [(os.path.join(tmp, f"{i:05d}.tfrecord"), i * per, min(per, a.clips - i * per), classes)
             for i in range(nsh) if a.clips - i * per > 0]
     t0 = time.perf_counter()
+    print(f"e2e: writing {a.clips} clips into {len(jobs)} GZIP shards", file=sys.stderr, flush=True)
     with ProcessPoolExecutor(min(16, len(jobs))) as ex:
-        list(ex.map(_write_shard, jobs))
+        for i, _ in enumerate(ex.map(_write_shard, jobs)):
+            print(f"e2e: shard {i + 1}/{len(jobs)} written ({time.perf_counter() - t0:.1f} s)", file=sys.stderr,
+                  flush=True)
     t_write = time.perf_counter() - t0
     import tfdataset
     from acfe.frontend import sample_mixup_lambda
@@ -429,14 +432,19 @@ def run_e2e(a):
         lam = sample_mixup_lambda(x1.shape[0], 0.5, 0.25, device=dev)
         return trainer.step(x1, mix_labels(y1, y2, lam), x2, lam)[0]
 
+    t1 = time.perf_counter()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    print(f"e2e: {a.warmup} warm-up steps in {time.perf_counter() - t1:.1f} s (shuffle buffer fill included)",
+          file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     n = 0
-    for _ in range(a.steps):
+    for i in range(a.steps):
         loss = step()
         n += 1
+        if (i + 1) % 10 == 0:
+            print(f"e2e: {i + 1} timed steps, {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     import shutil
@@ -447,7 +455,9 @@ def run_e2e(a):
            "ms_per_step": round(el / max(n, 1) * 1e3, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
            "data": f"synthetic clips written as {len(jobs)} GZIP TFRecord shards ({a.clips} clips, {t_write:.1f} s to "
-                   f"write, not timed), read by tfdataset.AudioDataset (16 reader threads, mix_up pairs)",
+                   f"write, not timed), read by tfdataset.AudioDataset: 16 native reader threads (libdeflate "
+                   f"inflate, each record decoded once), 4096-clip device shuffle pool, mix_up partners drawn "
+                   f"from the pool; host CPUs available to the process: {len(os.sched_getaffinity(0))}",
            "config": {"workload": "T1 end to end: TFRecord loader + training step",
                       "model": "wr_resnet_bird" if a.model == "bird" else "wr_resnet", "classes": classes,
                       "batch": a.batch}, "final_loss": round(float(loss.item()), 5)}

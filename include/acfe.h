@@ -124,12 +124,13 @@ int acfe_normalize_apply(const float* x, int64_t clip_stride, int batch, int n,
  * stats1/stats2 may be NULL (inputs already normalised). */
 int acfe_mixup(const float* x1, const float* stats1, const float* x2, const float* stats2,
                const float* lam, int batch, int n, float* y, void* stream);
-/* Batch assembly from a device-resident clip pool (the loader's shuffle
- * buffer, tfdataset.py:835-838): out[i][0..n) = pool[idx_dev[i]][0..n) for
- * i < batch; idx_dev (device int32) must hold row numbers < pool_rows (the
- * caller checks them on the host before the launch). */
-int acfe_gather_rows(const float* pool, int64_t pool_stride, int64_t pool_rows, const int* idx_dev, int batch,
-                     int n, float* out, int64_t out_stride, void* stream);
+/* Row copies of the loader's device-resident clip pool (the shuffle buffer,
+ * tfdataset.py:835-838): dst[dst_idx[i]][0..n) = src[src_idx[i]][0..n) for
+ * i < count; a NULL index list is the identity.  Index lists are device int32
+ * holding rows < src_rows / dst_rows (the caller checks them on the host
+ * before the launch). */
+int acfe_copy_rows(const float* src, int64_t src_stride, int64_t src_rows, const int* src_idx, float* dst,
+                   int64_t dst_stride, int64_t dst_rows, const int* dst_idx, int count, int n, void* stream);
 
 /* Fused framing -> periodic Hann -> n_fft real FFT (LDS radix-8/4 Stockham)
  * -> |X|^power (power 1 or 2) -> banded mel, for every frame of every clip.

@@ -82,6 +82,27 @@ def test_epoch_contract(shards, shuffle):
         assert sorted(seen) == keep and nb == len(ds)
 
 
+def test_pool_smaller_than_dataset_refills_slots(shards, monkeypatch):
+    """A shuffle pool far smaller than the epoch (4-clip chunks, 6-clip
+    buffer, 44 records): slots freed by each batch are refilled by the next
+    chunks, so the stream neither stalls nor repeats or loses an example."""
+    import tfdataset
+
+    monkeypatch.setattr(tfdataset, "CHUNK_BYTES", 4 * 4 * N)
+    d, keep = shards
+    ds = tfdataset.AudioDataset(tfdataset._files(d), ["bird", "noise"], batch_size=3, device="cpu", threads=3,
+                                shuffle_buffer=6, augment=True)
+    assert ds.per_chunk == 4 and ds.pool_rows == 6 + 8
+    t0 = time.perf_counter()
+    seen = []
+    for (x1, y1), (x2, y2) in ds:
+        for k, row in zip(_ids(x1), y1):
+            assert _label_ok(k, row)
+        seen += _ids(x1)
+    assert time.perf_counter() - t0 < 60
+    assert sorted(seen) == keep
+
+
 def test_mixup_pairs_and_drop_remainder(shards):
     import tfdataset
 
