@@ -820,10 +820,21 @@ constexpr int PCEN_TCH = 32;
 
 // 64 (b, m) rows per 256-thread workgroup: one wave runs the sequential EMA of
 // a 32-step chunk (a few dependent VALU ops per step, from LDS), then all four
-// waves evaluate the compression terms (the powf / logf bulk) of 8 steps each,
+// waves evaluate the compression terms (the pow / log bulk) of 8 steps each,
 // so 4 waves per SIMD instead of one hide the transcendental latency.
 constexpr int PCEN_RB = 64;
 ACFE_API int acfe_pcen_partials(int batch, int n_mels) { return cdiv((int64_t)batch * n_mels, PCEN_RB); }
+
+// a^b for a >= 0 from the hardware base-2 log / exp (v_log_f32, v_exp_f32,
+// ~1 ulp each): OCML's correctly-rounded powf is ~280 VALU instructions and
+// made the PCEN kernels compute-bound (33.6 M elements x 2 powf per batch of
+// 512 clips).  a = 0 gives 0 for b > 0; a < 0 gives NaN, as powf does for a
+// non-integer b.  The forward and the backward's recomputation use the same
+// function, so y (and the min / max tie test on it) stay bit-identical.
+__device__ __forceinline__ float pow_hw(float a, float b) {
+  return __builtin_amdgcn_exp2f(__fmul_rn(b, __builtin_amdgcn_logf(a)));
+}
+__device__ __forceinline__ float ln_hw(float a) { return __fmul_rn(__builtin_amdgcn_logf(a), 0.693147180559945309f); }
 
 struct PcenP {
   float g, b, r, w, inv_r, bpow;
@@ -835,7 +846,7 @@ __device__ __forceinline__ PcenP pcen_params(const float* __restrict__ prm) {
   p.r = fmaxf(prm[2], 1.0f);
   p.w = fminf(fmaxf(prm[3], 0.0f), 1.0f);
   p.inv_r = 1.0f / p.r;
-  p.bpow = powf(p.b, p.inv_r);
+  p.bpow = pow_hw(p.b, p.inv_r);  // so that x = 0 gives y = 0 exactly
   return p;
 }
 
@@ -892,7 +903,7 @@ __global__ void __launch_bounds__(256) k_pcen_fwd(const float* __restrict__ mel,
         if (tt < tn) {
           const float x = xs[tt][r], at = as[tt][r];
           const float v =
-              __fsub_rn(powf(__fadd_rn(__fdiv_rn(x, powf(__fadd_rn(eps, at), P.g)), P.b), P.inv_r), P.bpow);
+              __fsub_rn(pow_hw(__fadd_rn(__fdiv_rn(x, pow_hw(__fadd_rn(eps, at), P.g)), P.b), P.inv_r), P.bpow);
           tile[r][tt] = v;
           lmin = fminf(lmin, v);
           lmax = fmaxf(lmax, v);
@@ -1064,16 +1075,16 @@ __global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel,
         if (tt >= tn) continue;
         const float x = xs[tt][r], at = as[tt][r], dat = das[tt][r];
         const float s = __fadd_rn(eps, at);
-        const float sg = powf(s, P.g);
+        const float sg = pow_hw(s, P.g);
         const float q = __fdiv_rn(x, sg);
         const float u = __fadd_rn(q, P.b);
-        const float ur = powf(u, P.inv_r);
+        const float ur = pow_hw(u, P.inv_r);
         const float y = __fsub_rn(ur, P.bpow);
-        const float dydu = P.inv_r * ur / u;
-        const float d_g = dydu * (-q * logf(s));
+        const float dydu = P.inv_r * ur * __builtin_amdgcn_rcpf(u);  // (gradient terms: v_rcp_f32, ~1 ulp)
+        const float d_g = dydu * (-q * ln_hw(s));
         const float d_b = dydu - P.inv_r * P.bpow / P.b;
-        const float d_r = -(P.inv_r * P.inv_r) * (ur * logf(u) - P.bpow * lnb);
-        const float d_w = dydu * (-P.g * q / s) * dat;
+        const float d_r = -(P.inv_r * P.inv_r) * (ur * ln_hw(u) - P.bpow * lnb);
+        const float d_w = dydu * (-P.g * q * __builtin_amdgcn_rcpf(s)) * dat;
         const float d = tile[r][tt];
         acc[0] += d * d_g; acc[1] += d * d_b; acc[2] += d * d_r; acc[3] += d * d_w;
         if (y == mx) { acc[4] += d_g; acc[5] += d_b; acc[6] += d_r; acc[7] += d_w; }

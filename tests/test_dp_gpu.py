@@ -67,6 +67,24 @@ def rank_results(tmp_path_factory):
     return [torch.load(f"{out}.{r}.pt", weights_only=True) for r in range(world)]
 
 
+@pytest.fixture(scope="module")
+def rccl_result(rank_results, tmp_path_factory):
+    """A one-rank RCCL group (this box has one GPU) in a fresh child process,
+    started after the gloo pair has exited and before this process touches
+    the GPU."""
+    out = tmp_path_factory.mktemp("rccl") / "res"
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), ACFE_DP_TEST="rccl1")
+    p = subprocess.Popen([sys.executable, "-u", str(WORKER), str(out)], env=env)
+    try:
+        rc = p.wait(timeout=240)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        rc = p.wait()
+    assert rc == 0, rc
+    return torch.load(f"{out}.rccl.pt", weights_only=True)
+
+
 def _half_grads(tr, dev, world):
     from acfe import ops
 
@@ -83,6 +101,19 @@ def _half_grads(tr, dev, world):
         grads.append(tr.arena.grad.detach().clone())
         losses.append(float(loss))
     return grads, losses
+
+
+def test_rccl_bucket_allreduce_executes(rccl_result, cuda):
+    """RCCL ran the bucketed all-reduce of a real HIP backward (one rank: the
+    summed gradient equals the local one, which this process recomputes)."""
+    import dp_case
+
+    assert rccl_result["backend"] == "nccl"
+    assert [b for b, _ in rccl_result["launch_log"]] == list(range(len(rccl_result["launch_log"])))
+    assert len(rccl_result["launch_log"]) >= 3
+    tr = dp_case.make_trainer(cuda)
+    g, _ = _half_grads(tr, cuda, 1)
+    assert torch.equal(rccl_result["grad"], g[0].cpu())
 
 
 def test_dp_step_matches_single_process(rank_results, cuda):
