@@ -40,8 +40,8 @@ class Conv2D(nn.Module):
                                                   _seed(name, seed)))
         self.bias = nn.Parameter(torch.zeros(filters)) if use_bias else None
 
-    def forward(self, x, want_stats=False):
-        y, st = ops.conv2d(x, self.weight, self.bias, self.strides, self.padding, want_stats)
+    def forward(self, x, want_stats=False, link=None):
+        y, st = ops.conv2d(x, self.weight, self.bias, self.strides, self.padding, want_stats, link=link)
         return (y, st) if want_stats else y
 
 

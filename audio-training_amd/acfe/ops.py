@@ -258,11 +258,12 @@ def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=No
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pt, pl, P, Q, want_stats):
+    def forward(ctx, x, w, b, stride, pt, pl, P, Q, want_stats, link=None):
         ctx.bias = b
         y, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pt, pl, P, Q, b is not None)
+        ctx.link = link
         ctx.mark_non_differentiable(stats)
         return y, stats
 
@@ -270,9 +271,13 @@ class _Conv2dFn(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         x, w = ctx.saved_tensors
         stride, pt, pl, P, Q, has_b = ctx.conf
-        dx, dw, db = _conv_bwd(x, w, dy, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+        need_dx = ctx.needs_input_grad[0] or ctx.link is not None
+        dx, dw, db = _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, ctx.needs_input_grad[1],
                                has_b and ctx.needs_input_grad[2], bias=ctx.bias)
-        return dx, dw, db, None, None, None, None, None, None
+        if ctx.link is not None:  # the BN reading x adds this gradient in its own backward
+            ctx.link.grad = dx
+            dx = None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def _sums_ok(t: torch.Tensor) -> bool:
@@ -317,8 +322,13 @@ def channel_sum(x: torch.Tensor, C: int, into: torch.Tensor | None = None) -> to
     return out
 
 
-def conv2d(x, w, b=None, stride=1, padding="same", want_stats=False):
-    """Keras Conv2D on NHWC x with KRSC weights. Returns (y, stats_partial)."""
+def conv2d(x, w, b=None, stride=1, padding="same", want_stats=False, link=None):
+    """Keras Conv2D on NHWC x with KRSC weights. Returns (y, stats_partial).
+    link: a ResidualLink of the BatchNormalization that also reads x (a
+    residual block's conv shortcut): the backward hands dX to that BN, which
+    adds it inside its own backward (with the ReLU mask of x when x is a ReLU
+    output) instead of autograd accumulating it and a separate ReLU pass;
+    the conv must then be created after the BN (its backward runs first)."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
     if padding == "same":
@@ -328,7 +338,9 @@ def conv2d(x, w, b=None, stride=1, padding="same", want_stats=False):
         P, Q, pt, pl = valid_out(H, R, stride), valid_out(W, S, stride), 0, 0
     else:
         raise ValueError(padding)
-    return _Conv2dFn.apply(x, w, b, stride, pt, pl, P, Q, want_stats)
+    if link is not None and not (x.is_contiguous() and (P, Q) != (0, 0)):
+        link = None
+    return _Conv2dFn.apply(x, w, b, stride, pt, pl, P, Q, want_stats, link)
 
 
 # ------------------------------------------------------------------ stem (folded C=1)

@@ -41,15 +41,20 @@ class BasicBlock(nn.Module):
         the shape, else conv2d -> add).  A conv shortcut's gradient reaches x
         through autograd's accumulation; the gradient-tensor tags the fused
         nodes rely on are version-checked (ops._tag)."""
-        link = ops.ResidualLink.make() if self.shortcut is None else None
+        # the gradient of x from the shortcut (the Add's, or the 1x1 conv
+        # shortcut's dX) is summed inside bn2a's backward (ResidualLink), with
+        # the ReLU mask of x when x is the previous block's ReLU output
+        link = ops.ResidualLink.make()
         # BN outputs come back pending: the 3x3 convs apply them in their input
         # staging where ops.bn_prologue_ok covers the shape
         defer = ops.FUSE and ops.PROLOGUE
         y = self.bn2a(x, relu=True, stats=x_stats, link=link, defer=defer)
         y = conv_dropout_bn(self.conv2a, self.bn2b, y, self.dropout, defer=defer)
-        sc = x if self.shortcut is None else self.shortcut(x)
+        # (created after bn2a: its backward runs first and delivers the link)
+        sc = x if self.shortcut is None else self.shortcut(x, link=link)
         want = self.training and ops.FUSE
-        z, st = ops.conv_add(y, self.conv2b.weight, self.conv2b.bias, sc, relu=True, want_stats=want, link=link,
+        z, st = ops.conv_add(y, self.conv2b.weight, self.conv2b.bias, sc, relu=True, want_stats=want,
+                             link=link if self.shortcut is None else None,
                              stride=self.conv2b.strides, padding=self.conv2b.padding)
         return z, (st if want else None)
 

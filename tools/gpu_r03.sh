@@ -21,6 +21,7 @@ for s in "$@"; do
     new) step new 900 $PYT -m gpu tests/test_dp_gpu.py tests/test_ops_gpu.py tests/test_frontend_gpu.py \
            tests/test_production_gpu.py::test_strided_dgrad_wr_resnet_production tests/test_e2e_gpu.py \
            "tests/test_model_gpu.py::test_block_bf16_train_fixed_bounds" ;;
+    model) step model 900 $PYT -m gpu tests/test_model_gpu.py tests/test_e2e_gpu.py tests/test_dp_gpu.py tests/test_frontend_gpu.py ;;
     blk) step blk 600 $PYT -m gpu "tests/test_model_gpu.py::test_block_bf16_train_fixed_bounds" ;;
     tests) step tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
