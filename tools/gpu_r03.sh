@@ -24,6 +24,7 @@ for s in "$@"; do
     model) step model 900 $PYT -m gpu tests/test_model_gpu.py tests/test_e2e_gpu.py tests/test_dp_gpu.py tests/test_frontend_gpu.py ;;
     sqmel) step sqmel 400 bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w2' ;;
     sq64) step sq64 400 bash tools/pmc_sq.sh ${TAG}_r64 'k_conv3x3_rows<64, 8, [034], true, true>|k_wgrad3x3_halo<64, false' ;;
+    bnb) step bnb 300 bash -c "python tools/bn_bench.py --C 64 && python tools/bn_bench.py --C 128" ;;
     blk) step blk 600 $PYT -m gpu "tests/test_model_gpu.py::test_block_bf16_train_fixed_bounds" ;;
     tests) step tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
