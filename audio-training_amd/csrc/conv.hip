@@ -2092,6 +2092,164 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   }
 }
 
+// ------------------------------------------------------------------ 3x3 stride 1, 16 input channels
+// wr_resnet's stage-1 block-0 conv2a (resnet/wr_resnet.py:22: 3x3 16 -> 64 at
+// 128 x 513, 1.2 GFLOP per clip).  With C = 16 the generic im2col GEMM
+// gathers 32-byte pixel granules per tap and ran at ~130 TFLOP/s (r03e
+// profile: 4.76 ms per 512 clips).  Here the MFMA k dimension is tap-major:
+// k-step q covers taps 2q and 2q + 1 (16 channels each; the fifth step's
+// second half is the zero padding of the packed weights), so the nine taps are
+// five k-steps of v_mfma_f32_16x16x32_bf16 (90 % useful).  The packed weight
+// matrix (64 x 160 bf16) sits in VGPRs as A fragments for the workgroup's
+// lifetime; each 8-row x 64-pixel tile stages its 10 x 66-pixel, 16-channel
+// input halo in LDS once (48-B pixel pitch) and every lane reads its im2col B
+// fragment (8 channels of one tap) straight from it; the next tile's halo is
+// prefetched into registers during the MFMAs.  Epilogue of k_conv3x3_narrow:
+// bias, bf16 rounding, the pair-hash Dropout, BN sums.  Persistent, XCD-aware.
+template <bool DROP>
+__global__ void __launch_bounds__(512, 1)
+k_conv3x3_c16(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
+              int tiles_w, int ntiles, int srows) {
+  constexpr int KB = 64, TR = 8, SEGW = 64, HWX = SEGW + 2, XR = TR + 2, XRB = 48;
+  constexpr int FM = 4, FN = 4, NQ = 5;  // per wave: one tile row = 4 x 16 pixels x 64 channels
+  constexpr int XG = XR * HWX * 2;       // 16-B granules of the halo (two per pixel)
+  constexpr int XPT = (XG + 511) / 512;
+  __shared__ __attribute__((aligned(16))) unsigned char xs[XR * HWX * XRB];
+  __shared__ double sstat[2 * KB];
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // the wave's tile row
+  const int tpi = tiles_h * tiles_w;
+  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
+  for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
+  // A fragments: lane (l16, lg) of channel fragment fn holds W[fn * 16 + l16][q * 32 + lg * 8 .. + 7]
+  uint4 wa[NQ][FN];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn)
+      wa[q][fn] = *reinterpret_cast<const uint4*>(Wp + (long long)(fn * 16 + l16) * g.Kdp + q * 32 + lg * 8);
+  f4 bq[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn)
+    bq[fn] = bias ? *reinterpret_cast<const f4*>(bias + fn * 16 + lg * 4) : f4{0.f, 0.f, 0.f, 0.f};
+  // B fragment offsets (tile-invariant): k-step q -> tap min(2q + lg / 2, 8), channel half lg & 1
+  int boff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int t = min(2 * q + (lg >> 1), 8), r = t / 3, sx = t - 3 * r;
+    boff[q] = ((wid + r) * HWX + l16 + sx) * XRB + (lg & 1) * 16;
+  }
+  const TileWalk walk(ntiles);
+  u32x4 rx[XPT];
+  auto gload = [&](int tm) __attribute__((always_inline)) {
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    const int h0 = hb * TR - g.pt, w0 = wb * SEGW - g.pl;
+    const uint16_t* img = X + (long long)n * g.H * g.W * 16;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i, px = idx >> 1;
+      const int xrow = px / HWX, xpix = px - xrow * HWX;
+      const int hin = h0 + xrow, win = w0 + xpix;
+      const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
+      rx[i] = *reinterpret_cast<const u32x4*>(ok ? img + ((long long)hin * g.W + win) * 16 + (idx & 1) * 8 : zp);
+    }
+  };
+  int tm = walk.tm;
+  if (tm < walk.end) gload(tm);
+  for (; tm < walk.end; tm += walk.step) {
+    __syncthreads();  // every wave is done reading the previous tile's halo
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + 512 * i;
+      if (idx < XG) *reinterpret_cast<u32x4*>(xs + (idx >> 1) * XRB + (idx & 1) * 16) = rx[i];
+    }
+    __syncthreads();
+    if (tm + walk.step < walk.end) gload(tm + walk.step);
+    f4 acc[FM][FN];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      uint4 xb[FM];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) xb[fm] = *reinterpret_cast<const uint4*>(xs + boff[q] + fm * 16 * XRB);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], wa[q][fn], xb[fm], uint16_t());
+    }
+    // epilogue (k_conv3x3_narrow's): pixel (row wid, column fm * 16 + l16), channels fn * 16 + lg * 4 + j
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    const int h = hb * TR + wid;
+    float s1[FN][4], s2[FN][4];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s1[fn][j] = s2[fn][j] = 0.f;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int w = wb * SEGW + fm * 16 + l16;
+      const bool inb = h < g.P && w < g.Q;
+      const unsigned pix = ((unsigned)n * g.P + h) * g.Q + w;  // < 2^32: launch checks M * K < 2^32
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int c = fn * 16 + lg * 4;
+        float r[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = bf2f(f2bf(acc[fm][fn][j] + bq[fn][j]));
+        if constexpr (DROP) {
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const uint32_t hh = drop_pair_hash32(g.drop, pix * (unsigned)g.K + c + 2 * pr);
+            r[2 * pr] = (hh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(r[2 * pr] * g.drop.scl)) : 0.f;
+            r[2 * pr + 1] = (hh >> 16) >= g.drop.thr ? bf2f(f2bf(r[2 * pr + 1] * g.drop.scl)) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float f = inb ? r[j] : 0.f;
+          s1[fn][j] += f;
+          s2[fn][j] += f * f;
+        }
+        uint2 v;
+        v.x = (__float_as_uint(r[0]) >> 16) | (__float_as_uint(r[1]) & 0xffff0000u);
+        v.y = (__float_as_uint(r[2]) >> 16) | (__float_as_uint(r[3]) & 0xffff0000u);
+        uint2* dst = inb ? reinterpret_cast<uint2*>(Y + (size_t)pix * g.ldy + c) : &g_store_sink[lane];
+        *dst = v;
+      }
+    }
+    if (stats) {
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) {
+            s1[fn][j] += __shfl_xor(s1[fn][j], off, 64);
+            s2[fn][j] += __shfl_xor(s2[fn][j], off, 64);
+          }
+          if (l16 == 0) {
+            const int c = fn * 16 + lg * 4 + j;
+            atomicAdd(&sstat[c], (double)s1[fn][j]);
+            atomicAdd(&sstat[KB + c], (double)s2[fn][j]);
+          }
+        }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    for (int c = tid; c < g.Kp; c += 512) {
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = c < KB ? sstat[c] : 0.0;
+      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = c < KB ? sstat[KB + c] : 0.0;
+    }
+    for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
+      for (int c = tid; c < 2 * g.Kp; c += 512) stats[((long long)rr * 2 + (c / g.Kp)) * g.Kp + (c % g.Kp)] = 0.0;
+  }
+}
+
 // ------------------------------------------------------------------ 1x1 conv, register-resident weights
 // 1x1 stride-1 convolutions with few input or few output channels (C or K <= 32:
 // the 16->128 stage-1 entry conv, the 16->64 shortcut, and their dgrads
@@ -3125,6 +3283,25 @@ static int launch_fwd(const ConvGeom& g, const void* x, const void* wp, const fl
   }
 general:
   if constexpr (sizeof(T) == 2) {
+    if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W && g.C == 16 &&
+        g.K == 64 && g.Kp == 64 && g.Kdp >= 160 && g.ldy == g.K && g.M * g.K < (1ll << 32) &&
+        ((uintptr_t)x & 15) == 0 && ((uintptr_t)wp & 15) == 0 && ((uintptr_t)y & 7) == 0) {
+      const int tiles_h = (g.P + 7) / 8, tiles_w = (g.Q + 63) / 64;
+      const long long nt = (long long)g.N * tiles_h * tiles_w;
+      if (nt < (1ll << 31)) {
+        int gp = 256;
+        if (gp > nt) gp = (int)nt;
+        if (gp >= 64) gp &= ~7;
+        if (stats && gp > grid_m) gp = grid_m;  // one statistics slab row per workgroup
+        if (g.drop.on)
+          hipLaunchKernelGGL(k_conv3x3_c16<true>, dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
+        else
+          hipLaunchKernelGGL(k_conv3x3_c16<false>, dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,
+                             (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m);
+        return launch_rc("acfe_conv2d_fwd(c16)");
+      }
+    }
     if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W &&
         g.C % 64 == 0 && (g.K == 32 || g.K == 16) && g.C * g.K <= 4096 && g.ldy == g.K &&
         g.M * g.K < (1ll << 32)) {

@@ -52,10 +52,11 @@ def _dropout(env, t, rate, seed):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32], ids=["bf16", "f32"])
-@pytest.mark.parametrize("K", [128, 64, 32])
-def test_conv_fwd_dropout(env, cuda, dtype, K):
+@pytest.mark.parametrize("K,C", [(128, 64), (64, 64), (32, 64), (64, 16)], ids=["128", "64", "32", "64c16"])
+def test_conv_fwd_dropout(env, cuda, dtype, K, C):
+    """(C = 16, K = 64 bf16: k_conv3x3_c16, the tap-major 16-channel kernel)"""
     ops, call, lib, ptr, stream = env
-    N, H, W, C, R = 2, 12, 40, 64, 3
+    N, H, W, R = 2, 12, 40, 3
     g = torch.Generator(device="cpu").manual_seed(1)
     x = torch.randn((N, H, W, C), generator=g).to(dtype).to(cuda)
     w = (torch.randn((K, R, R, C), generator=g) * 0.05).to(cuda)

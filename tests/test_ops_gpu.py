@@ -57,6 +57,8 @@ CONV_CASES = [
     (2, 23, 35, 64, 128, 3, 3, 3, "same"),
     (2, 3, 5, 64, 64, 3, 3, 2, "same"),
     (1, 300, 5, 16, 64, 3, 3, 1, "same"),
+    # 16 input channels, 64 outputs (k_conv3x3_c16): ragged row / column tiles
+    (2, 20, 70, 16, 64, 3, 3, 1, "same"),
     # halo-staged 3x3 wgrad (Q % 64 == 0, C % 64 == 0, K in {64, 128}): 1-3 channel chunks
     (2, 10, 64, 128, 128, 3, 3, 1, "same"),
     (2, 9, 128, 64, 64, 3, 3, 1, "same"),
@@ -118,6 +120,7 @@ BIG_CASES = [
     (2, 128, 300, 16, 128, 1, 1),
     (1, 128, 600, 128, 64, 1, 1),
     (1, 64, 520, 128, 256, 3, 3),
+    (2, 128, 513, 16, 64, 3, 3),  # wr_resnet's 16 -> 64 conv at the T1 input (k_conv3x3_c16, many tiles per CU)
 ]
 
 

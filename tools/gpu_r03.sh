@@ -25,6 +25,9 @@ for s in "$@"; do
     sqmel) step sqmel 400 bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w2' ;;
     sq64) step sq64 400 bash tools/pmc_sq.sh ${TAG}_r64 'k_conv3x3_rows<64, 8, [034], true, true>|k_wgrad3x3_halo<64, false' ;;
     bnb) step bnb 300 bash -c "python tools/bn_bench.py --C 64 && python tools/bn_bench.py --C 128" ;;
+    bnab) step bnab 400 bash -c 'for r in 1 2; do for L in base bnold; do if [ $L = base ]; then E=""; else E=$PWD/abtest/$L.so; fi; echo "== $L"; ACFE_LIB=$E python tools/bn_bench.py --C 64 || exit 1; ACFE_LIB=$E python tools/bn_bench.py --C 128 || exit 1; done; done' ;;
+    c16) step c16 600 $PYT -m gpu tests/test_ops_gpu.py tests/test_fused_gpu.py -k "16 or c16 or 513" ;;
+    wrn) step wrn 600 python bench.py --model wrn --classes 2 --no-cpu-baseline ;;
     blk) step blk 600 $PYT -m gpu "tests/test_model_gpu.py::test_block_bf16_train_fixed_bounds" ;;
     tests) step tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -32,7 +35,6 @@ for s in "$@"; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
             python bench.py --no-cpu-baseline --steps 10 --warmup 3 ;;
     e2e) step e2e 900 python bench.py --workload e2e --clips ${CLIPS:-8192} --steps 40 --warmup 4 --no-cpu-baseline ;;
-    wrn) step wrn 600 python bench.py --model wrn --classes 2 --no-cpu-baseline ;;
     wrnprof) step wrnprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wprof -o run -- \
             python bench.py --model wrn --classes 2 --no-cpu-baseline --steps 10 --warmup 3 ;;
     infer) step infer 600 python bench.py --workload infer --no-cpu-baseline ;;
