@@ -447,7 +447,10 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce8(const TG* __restrict__ d
         a[j] = b[j] = 0.f, da[j] = db[j] = 0.0;
       }
       int cnt = 0;
-      auto acc = [&](const float* g, const float* xv) __attribute__((always_inline)) {
+      for (long long r = r0 + rs; r < r1; r += rpp) {
+        float g[8], xv[8];
+        ld8(dy + r * C + cv * 8, g);
+        ld8(x + r * C + cv * 8, xv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float gj = (relu && !(xv[j] * sc[j] + sh[j] > 0.f)) ? 0.f : g[j];
@@ -459,24 +462,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce8(const TG* __restrict__ d
           for (int j = 0; j < 8; ++j) da[j] += a[j], db[j] += b[j], a[j] = b[j] = 0.f;
           cnt = 0;
         }
-      };
-      long long r = r0 + rs;
-      // two rows' loads in flight per iteration (4 workgroups per CU: the
-      // statistics-slab grid is capped at 1024 blocks); same accumulation order
-      for (; r + rpp < r1; r += 2 * rpp) {
-        float g0[8], x0[8], g1[8], x1[8];
-        ld8(dy + r * C + cv * 8, g0);
-        ld8(x + r * C + cv * 8, x0);
-        ld8(dy + (r + rpp) * C + cv * 8, g1);
-        ld8(x + (r + rpp) * C + cv * 8, x1);
-        acc(g0, x0);
-        acc(g1, x1);
-      }
-      if (r < r1) {
-        float g0[8], x0[8];
-        ld8(dy + r * C + cv * 8, g0);
-        ld8(x + r * C + cv * 8, x0);
-        acc(g0, x0);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -594,71 +579,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
 #pragma unroll
   for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
   const unsigned v0 = blockIdx.x * 256 + threadIdx.x;
-  const unsigned stride = gridDim.x * 256;
-  if (256 % CV == 0 && !pa.g) {
-    // C / 8 divides the block size (every layer of both models): a thread's 8
-    // channels are the same in every grid-stride iteration, so its BN
-    // constants live in registers (no per-element LDS reads or channel
-    // modulo), and two iterations are issued together (twice the loads in
-    // flight per wave -- the statistics-slab launch has only 4 workgroups per
-    // CU).  Same arithmetic as the general loop below: bit-identical output.
-    const int c0 = (int)(v0 % CV) * 8;
-    float rsc[8], rsh[8], ra[8], rb[8], rc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      rsc[j] = sm[c0 + j];
-      rsh[j] = sm[C + c0 + j];
-      ra[j] = sm[2 * C + c0 + j];
-      rb[j] = sm[3 * C + c0 + j];
-      rc[j] = sm[4 * C + c0 + j];
-    }
-    auto finish = [&](unsigned v, float* g, float* xv, float* o) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float gj = ((relu & 1) && !(xv[j] * rsc[j] + rsh[j] > 0.f)) ? 0.f : g[j];
-        const float r = ra[j] * gj + rb[j] * xv[j] + rc[j];
-        o[j] = add ? o[j] + r : r;
-        if ((relu & 2) && !(xv[j] > 0.f)) o[j] = 0.f;
-      }
-      if (drop.on) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = drop_apply<TO>(drop, (uint64_t)v * 8 + j, rnd(o[j], TO()));
-      }
-      st8(dx + (size_t)v * 8, o);
-      if (sum_part) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float r = rnd(o[j], TO());
-          sa[j] += r;
-          sb[j] += (double)r * r;
-        }
-      }
-    };
-    unsigned v = v0;
-    for (; v + stride < nvec; v += 2 * stride) {
-      float g0[8], x0[8], o0[8], g1[8], x1[8], o1[8];
-      ld8(dy + (size_t)v * 8, g0);
-      ld8(x + (size_t)v * 8, x0);
-      ld8(dy + (size_t)(v + stride) * 8, g1);
-      ld8(x + (size_t)(v + stride) * 8, x1);
-      if (add) {
-        ld8(add + (size_t)v * 8, o0);
-        ld8(add + (size_t)(v + stride) * 8, o1);
-      }
-      finish(v, g0, x0, o0);
-      finish(v + stride, g1, x1, o1);
-    }
-    if (v < nvec) {
-      float g0[8], x0[8], o0[8];
-      ld8(dy + (size_t)v * 8, g0);
-      ld8(x + (size_t)v * 8, x0);
-      if (add) ld8(add + (size_t)v * 8, o0);
-      finish(v, g0, x0, o0);
-    }
-    if (sum_part) stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, sum_part);
-    return;
-  }
-  for (unsigned v = v0; v < nvec; v += stride) {
+  for (unsigned v = v0; v < nvec; v += gridDim.x * 256) {
     const int c0 = (int)(v % CV) * 8;
     float g[8], xv[8], o[8];
     ld8(dy + (size_t)v * 8, g);
