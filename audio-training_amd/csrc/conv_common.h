@@ -1,0 +1,103 @@
+// Definitions shared by the convolution translation units (conv.hip,
+// pool1w.hip): vector types, the launch geometry, the XCD-aware tile walk and
+// the LDS-DMA / wait helpers.
+#pragma once
+#include "common.h"
+
+#include <type_traits>
+
+namespace acfe {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+// Native 16-byte vector for register staging (HIP's uint4 struct-with-union
+// defeats SROA: arrays of it were demoted to scratch).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t T16;
+
+struct ConvGeom {
+  int N, H, W, C;    // input
+  int K, P, Q;       // output
+  int R, S, st, pt, pl;
+  int Kd, Kdp, Kp;   // R*S*C, padded to BK, K padded to BN
+  int ldy;           // output row stride (elements)
+  long long M;       // N*P*Q
+  Drop drop;         // optional Dropout of the output (flat index m*K + k), fused in the epilogue
+  int dbg;           // diagnostics (ACFE_CONV_DBG=8: loop-segment cycle stamps), 0 in production
+  const uint16_t* res;  // k_conv3x3_rows PM 3: residual added in the epilogue (same layout as Y)
+  int res_relu;         // PM 3: ReLU after the residual add
+  int idx32;            // M * K < 2^32: output element (dropout) indices fit 32 bits
+  // k_conv3x3_rows PRO: BatchNormalization (+ReLU) of the input applied while
+  // staging it, x' = (ReLU)(x * pro_sc[c] + pro_sh[c]) (acfe_bn_apply's
+  // arithmetic); x' is also stored to pro_out (nullable) for the backward
+  const float* pro_sc;
+  const float* pro_sh;
+  int pro_relu;
+  uint16_t* pro_out;
+};
+
+// XCD-aware walk over the M tiles of a persistent grid.  Workgroups are
+// dispatched round-robin over the 8 XCDs (linear id % 8), each with its own
+// L2; neighbouring M tiles share im2col input rows (a 3x3 conv reads every
+// input row from 3 output rows), so each XCD takes one contiguous eighth of the
+// tiles and its G/8 resident workgroups sweep that range side by side.
+// Falls back to the plain stride when the grid is not a multiple of 8.
+struct TileWalk {
+  int tm, end, step;
+  __device__ TileWalk(int tiles_m) {
+    const int G = gridDim.x;
+    if (G >= 8 && (G & 7) == 0) {
+      const int xcd = blockIdx.x & 7, chunk = (tiles_m + 7) >> 3;
+      tm = xcd * chunk + (blockIdx.x >> 3);
+      end = min((xcd + 1) * chunk, tiles_m);
+      step = G >> 3;
+    } else {
+      tm = blockIdx.x;
+      end = tiles_m;
+      step = G;
+    }
+  }
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// 16-B buffer_load ... lds: LDS byte address (wave-uniform) in M0, descriptor
+// in SGPRs, per-lane voffset; an out-of-range voffset lands zeros in LDS.
+typedef int i4 __attribute__((ext_vector_type(4)));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void bldsx4(unsigned voff, i4 desc, unsigned m0v) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(desc),
+               "s"(m0v)
+               : "memory", "m0");
+}
+// the same with a wave-uniform byte offset in soffset
+__device__ __forceinline__ void bldsx4s(unsigned voff, i4 desc, unsigned soff, unsigned m0v) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(desc),
+               "s"(soff), "s"(m0v)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// acfe_conv2d_fwd_pool at K = C = 128 on the one-wave-per-SIMD kernel
+// (pool1w.hip); returns ACFE_E_INVAL when the shape is not its case
+int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+                  int srows, uint8_t* amax, hipStream_t s, const char* what);
+
+}  // namespace acfe

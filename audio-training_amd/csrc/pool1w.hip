@@ -1,0 +1,513 @@
+// k_conv3x3_pool1w: the pooled 3x3 convolution of acfe_conv2d_fwd_pool at
+// K = C = 128 with one wave per SIMD (built with -fno-slp-vectorize: packed
+// f32 VALU beside MFMAs costs more issue time than the two scalar ops).
+#include "conv_common.h"
+
+using namespace acfe;
+
+// ------------------------------------------------------------------ pooled 3x3 conv, one wave per SIMD
+// k_conv3x3_pool1w<NCH, DROP>: acfe_conv2d_fwd_pool at K = 128, C = 64 NCH
+// (NCH even: the dominant T1 layer, stage-1 block-0 branch21 128 -> 128 @
+// 128 x 256 -> MaxPool2D(2) -> Dropout -> BN, resnet/wr_resnet_bird.py:136-147).
+// Same tile, LDS images, weight pieces and pooled epilogue arithmetic as
+// k_conv3x3_rows<128, 4, 1, true> (4 rows x 64 px x 128 channels, chunk-resident
+// halo rows, pixels x weights MFMA order), but four waves, one per SIMD, each
+// owning a 16-column strip of the four rows and ALL 128 channels (8 weight
+// fragments per 4 pixel fragments: 0.375 instead of 0.5 ds_read_b128 per MFMA;
+// 128 accumulators per lane in the accumulator file).  The pooled epilogue of
+// tile i - 1 runs beside the MFMAs of tile i: at the first MFMA group of a tile
+// each accumulator is read out, biased and rounded to bf16 (the value a
+// separate conv would have stored) into 64 packed registers just before its
+// first MFMA of the new tile overwrites it (C = 0), and the max / argmax /
+// dropout / BN sums / stores of those values run in four parts between the
+// MFMA groups of steps 1..4, the statistics shuffles in steps 3 and 5 -- the
+// 8-wave kernel stopped its MFMAs for the whole epilogue (16 % of every step,
+// DESIGN §4.1).  Every step is one straight block: no branches (the last
+// tile's loads are clamped; out-of-image and phantom stores go to a sink), and
+// the MFMA groups are fenced by sched_barrier with the next group's fragments
+// read during the current one.
+#ifndef P1W_WPG
+#define P1W_WPG 4  // weight pieces per MFMA group (groups 0..2)
+#endif
+#ifndef P1W_NOEPI
+#define P1W_NOEPI 0  // (timing experiments only: no epilogue parts)
+#endif
+#ifdef ACFE_P1W_STAMPS
+// diagnostic build (make stamps): per-wave s_memtime totals of the step
+// segments, read back by acfe_debug_pool1w_stamps (tools/pool1w_stamps.py)
+__device__ unsigned long long g_p1w_stamps[4096 * 8];
+#endif
+#ifndef P1W_GLRS
+#define P1W_GLRS 1  // filter-row step that requests the next chunk's halo rows
+#endif
+#ifndef P1W_NODMA
+#define P1W_NODMA 0  // (timing experiments only: no weight pieces)
+#endif
+#ifndef P1W_NOGLOAD
+#define P1W_NOGLOAD 0  // (timing experiments only: no halo-row loads)
+#endif
+#ifndef P1W_NORESTAGE
+#define P1W_NORESTAGE 0  // (timing experiments only: no chunk restage)
+#endif
+template <int NCH, bool DROP>
+__global__ void __launch_bounds__(256, 1)
+k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+                 const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
+                 int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
+  static_assert(NCH % 2 == 0, "even step count per tile: weight buffer parity is static");
+  constexpr int KB = 128, TR = 4, FM = 4, FN = 4, NH = 2, NF = NH * FN, SEGW = 64, HWX = SEGW + 2, XRB = 160;
+  constexpr int NT = 256, NS = 3 * NCH;                          // threads, steps per tile
+  constexpr int XROWS = TR + 2, XBYTES = XROWS * HWX * XRB;      // 63 360 B
+  constexpr int WBYTES = 3 * KB * 128, WBASE = XBYTES;           // 2 x 49 152 B
+  constexpr int XG = XROWS * HWX * 8, XPT = (XG + NT - 1) / NT;  // 16-B input granules
+  constexpr int WPW = 3 * KB * 8 / 64 / (NT / 64);               // 12 weight pieces per wave per step
+  constexpr int SMEM = XBYTES + 2 * WBYTES;
+  static_assert(SMEM <= 163840, "LDS");
+  static_assert(XPT * NT - XG <= 2 * XROWS * HWX, "spare granules fit the pixel pads");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4;
+  const int wp = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tpi = tiles_h * tiles_w;
+  const TileWalk walk(ntiles);
+  const int ntl = walk.tm < walk.end ? (walk.end - walk.tm + walk.step - 1) / walk.step : 0;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
+#ifdef ACFE_P1W_STAMPS
+  unsigned long long stv[6] = {0, 0, 0, 0, 0, 0}, stl = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int i) __attribute__((always_inline)) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    stv[i] += t - stl;
+    stl = t;
+  };
+#else
+  auto stamp = [](int) __attribute__((always_inline)) {};
+#endif
+
+  // bias of the lane's channels h * 64 + 4 l16 + [0, 4)
+  f4 bch[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+    bch[h] = bias ? *reinterpret_cast<const f4*>(bias + h * 64 + 4 * l16) : f4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- weight pieces (k_conv3x3_rows' SWP layout: LDS rows [kk][s][phys(k)]
+  // of 64 B, phys(k) = k ^ ((k >> 2) & 3), granule slot ^ ((l16 >> 2) & 2) on
+  // the reading side).  A piece is 16 rows (1 KB) of one (kk, s): wave wp
+  // loads row blocks kb = 2 wp, 2 wp + 1 of all six (kk, s), so its source
+  // offsets are one VGPR (the lane's row and swizzled granule; the swizzle
+  // term (kb >> 1) & 1 = wp & 1 is per wave) plus a uniform soffset formed
+  // per piece.
+  const int l4 = lane >> 2;
+  const unsigned vwl = (unsigned)((l4 ^ ((l4 >> 2) & 3)) * g.Kdp * 2) +
+                       ((((unsigned)lane & 3u) ^ ((wp & 1) ? 2u : 0u)) << 4);
+  const int sob = __builtin_amdgcn_readfirstlane(2 * wp * 16 * g.Kdp * 2);  // row block 2 wp
+  unsigned wlo = 0, whi = 0, wlb = 0;
+  auto wprep = [&](int st, int wb) __attribute__((always_inline)) {
+    const int cc = st / 3, r = st - cc * 3;
+    const unsigned long long base = (unsigned long long)(uintptr_t)Wp + ((unsigned)(r * 3 * g.C + cc * 64) * 2u);
+    wlo = (unsigned)base;
+    whi = (unsigned)(base >> 32);
+    wlb = lds0 + WBASE + wb * WBYTES + 2 * wp * 1024;
+  };
+  // piece j = 2 (kk * 3 + s) + b: row block 2 wp + b of (kk, s)
+  auto wpiece = [&](int j) __attribute__((always_inline)) {
+    const int ks = j >> 1, b = j & 1, kk = ks / 3, s_ = ks - kk * 3;
+    const i4 dw = {__builtin_amdgcn_readfirstlane((int)wlo), __builtin_amdgcn_readfirstlane((int)whi),
+                   (int)0x80000000u, 0x00020000};
+    int sb_ = sob;
+    asm volatile("" : "+s"(sb_));  // formed here, not hoisted into a dozen live registers
+    const unsigned so = (unsigned)(sb_ + s_ * g.C * 2 + kk * 64 + b * 16 * g.Kdp * 2);
+    const unsigned lb = (unsigned)__builtin_amdgcn_readfirstlane((int)(wlb + (ks * 128 + b * 16) * 64));
+    if (!P1W_NODMA) bldsx4s(vwl, dw, so, lb);
+  };
+
+  // ---- input halo rows of a 64-channel chunk, register-staged (granule i of
+  // this thread: halo pixel (tid >> 3) + 32 i, channel slot tid & 7)
+  // (granule offsets are recomputed per chunk: nothing per granule stays live)
+  const int gr = tid & 7, CB = g.C * 2;
+  u32x4 rx[XPT];
+  int sh0 = 0, sw0 = 0;  // staged tile: input row / column of halo pixel (0, 0)
+  __amdgpu_buffer_rsrc_t xrs;
+  auto stage_tile = [&](int tl) __attribute__((always_inline)) {
+    const int tm = walk.tm + tl * walk.step;
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    sh0 = hb * TR - g.pt;
+    sw0 = wb * SEGW - g.pl;
+    xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long long)n * g.H * g.W * g.C), (short)0,
+                                            g.H * g.W * CB, 0x00020000);
+  };
+  auto gload = [&](int cc) __attribute__((always_inline)) {
+    if (P1W_NOGLOAD) return;
+    int t0 = tid;
+    asm volatile("" : "+v"(t0));  // keep the per-granule arithmetic here (not hoisted and spilled)
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const unsigned idx = (unsigned)t0 + NT * i;
+      const unsigned xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
+      const unsigned hin = (unsigned)sh0 + xrow, win = (unsigned)sw0 + xpix;
+      const bool ok = idx < (unsigned)XG && win < (unsigned)g.W && hin < (unsigned)g.H;
+      const unsigned off = (hin * (unsigned)g.W + win) * (unsigned)CB + (idx & 7u) * 16u + (unsigned)cc * 128u;
+      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? off : 0x80000000u, 0, 0);
+    }
+  };
+  // LDS slot of granule i; the last round's threads past the image write
+  // their (zero) granule into the never-read 32-B pads of pixels 0..79, so
+  // the restage is one branch-free block
+  auto sslot = [&](int i) __attribute__((always_inline)) {
+    const int idx = tid + NT * i, e = idx - XG;
+    return idx < XG ? (idx >> 3) * XRB + gr * 16 : (e >> 1) * XRB + 128 + (e & 1) * 16;
+  };
+  auto sstore = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) *reinterpret_cast<u32x4*>(smem + sslot(i)) = rx[i];
+  };
+
+  // ---- fragment offsets: A rows 4 q' + j = window q' of fragment fm (row pair
+  // fm / 2, pooled column wp * 8 + (fm & 1) * 4 + (q' ^ (q' >> 1))), pixel j
+  int xoff[FM];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int qq = l16 >> 2, j = l16 & 3;
+    const int a = wp * 8 + (fm & 1) * 4 + (qq ^ (qq >> 1));
+    xoff[fm] = (((fm >> 1) * 2 + (j >> 1)) * HWX + 2 * a + (j & 1)) * XRB + q * 16;
+  }
+  int wrb[NH][FN];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int k = h * 64 + FN * l16 + fn;
+      wrb[h][fn] = (k ^ ((k >> 2) & 3)) * 64 + ((q ^ ((l16 >> 2) & 2)) << 4);
+    }
+
+  f4 acc[FM][NF];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // the previous tile's conv outputs, biased and rounded to bf16, packed
+  // (pixels j = 0, 1 | 2, 3 of window q of fragment fm, channel n)
+  u32x2 prev[FM][NF];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) prev[i][j] = u32x2{0u, 0u};
+  auto pack1 = [&](int fm, int n) __attribute__((always_inline)) {
+    const float b = bch[n / FN][n % FN];
+    const b2v lo = __builtin_convertvector((f2v){acc[fm][n][0] + b, acc[fm][n][1] + b}, b2v);
+    const b2v hi = __builtin_convertvector((f2v){acc[fm][n][2] + b, acc[fm][n][3] + b}, b2v);
+    prev[fm][n] = u32x2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
+  };
+
+  // pooled output and argmax bytes (< 2^31 bytes each, checked by the launcher)
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)Y, (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)amax, (short)0, 0x7FFFFFFF, 0x00020000);
+  // ---- pooled epilogue of `prev`, in parts: part (h, fm2) = channel half h,
+  // fragment pair fm2 (pooled row fm2 / 2 of the tile)
+  const int P2 = g.P >> 1, Q2 = g.Q >> 1;
+  const bool odd = (lane & 1) != 0;
+  float sb[FN], sq[FN];  // BN sums of the half in progress
+  double dstat[NH][2];
+#pragma unroll
+  for (int k = 0; k < FN; ++k) sb[k] = sq[k] = 0.f;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) dstat[h][0] = dstat[h][1] = 0.0;
+  // part (h, fm2) in units: unit (hf, pr) pools channels 2 pr, 2 pr + 1 of
+  // fragment fm2 + hf (their dropout pair hash, max / first-maximum argmax,
+  // BN sums) into eyv / eav; the store unit exchanges fragment halves between
+  // lane pairs and writes 16 B pooled + 8 B argmax per lane
+  unsigned eyv[2][2], eav[2];
+  auto tile_of = [&](int tm, int& n, int& hb, int& wb) __attribute__((always_inline)) {
+    n = tm / tpi;
+    const int rem = tm - n * tpi;
+    hb = rem / tiles_w;
+    wb = rem - hb * tiles_w;
+  };
+  auto epi_unit = [&](int h, int fm2, int hf, int pr, int tm, bool live) __attribute__((always_inline)) {
+    int n, hb, wb;
+    tile_of(tm, n, hb, wb);
+    const int cf = h * 64 + FN * l16;
+    const int hp2 = hb * (TR / 2) + (fm2 >> 1);
+    const int fm = fm2 + hf;
+    const int wq = wb * (SEGW / 2) + wp * 8 + hf * 4 + (q ^ (q >> 1));
+    const bool inb = live && hp2 < P2 && wq < Q2;
+    unsigned keep = 3u;
+    if constexpr (DROP) {
+      const unsigned pp = ((unsigned)n * P2 + hp2) * Q2 + wq;
+      const uint32_t hh = drop_pair_hash32(g.drop, pp * (unsigned)KB + cf + 2 * pr);
+      keep = ((hh & 0xFFFFu) >= g.drop.thr ? 1u : 0u) | ((hh >> 16) >= g.drop.thr ? 2u : 0u);
+    }
+    float mv[2];
+    unsigned avb = 0u;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int fn = 2 * pr + e;
+      const u32x2 pv = prev[fm][h * FN + fn];
+      const float a[4] = {__uint_as_float(pv[0] << 16), __uint_as_float(pv[0] & 0xffff0000u),
+                          __uint_as_float(pv[1] << 16), __uint_as_float(pv[1] & 0xffff0000u)};
+      float m = a[0];
+      unsigned am = 0;
+      if (a[1] > m) m = a[1], am = 1;
+      if (a[2] > m) m = a[2], am = 2;
+      if (a[3] > m) m = a[3], am = 3;
+      if constexpr (DROP) m = ((keep >> e) & 1u) ? bf2f(f2bf(m * g.drop.scl)) : 0.f;
+      mv[e] = m;
+      avb |= am << (8 * fn);
+      const float f = inb ? m : 0.f;
+      sb[fn] += f;
+      sq[fn] += f * f;
+    }
+    eav[hf] = pr == 0 ? avb : (eav[hf] | avb);
+    eyv[hf][pr] = (__float_as_uint(mv[0]) >> 16) | (__float_as_uint(mv[1]) & 0xffff0000u);
+  };
+  auto epi_store = [&](int h, int fm2, int tm, bool live) __attribute__((always_inline)) {
+    int n, hb, wb;
+    tile_of(tm, n, hb, wb);
+    const int hp2 = hb * (TR / 2) + (fm2 >> 1);
+    // even lane: fragment fm2 (own | partner's channels), odd lane: fm2 + 1
+    unsigned ys[2], yo[2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      ys[pr] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(odd ? eyv[0][pr] : eyv[1][pr]), 0xB1, 0xF, 0xF, false);
+      yo[pr] = odd ? eyv[1][pr] : eyv[0][pr];
+    }
+    const unsigned as = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(odd ? eav[0] : eav[1]), 0xB1, 0xF, 0xF, false);
+    const unsigned ao = odd ? eav[1] : eav[0];
+    const int wq = wb * (SEGW / 2) + wp * 8 + (odd ? 4 : 0) + (q ^ (q >> 1));
+    const bool inb = live && hp2 < P2 && wq < Q2;
+    const unsigned c0 = h * 64 + FN * (l16 & ~1);
+    // buffer stores into the pooled output: an out-of-range offset (outside
+    // the image, or the phantom epilogue before the first tile) is dropped
+    // by the hardware -- no branch, no sink
+    const unsigned pix = ((unsigned)n * P2 + hp2) * Q2 + wq;  // (output bytes < 2^31: launcher)
+    __builtin_amdgcn_raw_buffer_store_b128(odd ? u32x4{ys[0], ys[1], yo[0], yo[1]} : u32x4{yo[0], yo[1], ys[0], ys[1]},
+                                           yr, inb ? (pix * (unsigned)g.ldy + c0) * 2u : 0x80000000u, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(odd ? u32x2{as, ao} : u32x2{ao, as}, ar,
+                                          inb ? pix * (unsigned)KB + c0 : 0x80000000u, 0, 0);
+  };
+  auto epi_part = [&](int h, int fm2, int tm, bool live) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) epi_unit(h, fm2, u >> 1, u & 1, tm, live);
+    epi_store(h, fm2, tm, live);
+  };
+  // statistics of half h of a finished tile: sums over the four window groups,
+  // lane group q keeps values 2 q + k of [sb[0..4), sq[0..4)]
+  auto epi_stats = [&](int h) __attribute__((always_inline)) {
+    // (lane-group butterflies by v_permlane16_swap / v_permlane32_swap: with
+    // both operands x, the two results hold x of the partner rows, so their
+    // sum is the sum over lanes l, l ^ 16 (then l ^ 32))
+    auto bfly = [](float& v, auto swp) __attribute__((always_inline)) {
+      const auto r = swp(__float_as_uint(v));
+      v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    };
+    auto s16 = [](unsigned x) { return __builtin_amdgcn_permlane16_swap(x, x, false, false); };
+    auto s32 = [](unsigned x) { return __builtin_amdgcn_permlane32_swap(x, x, false, false); };
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      bfly(sb[fn], s16);
+      bfly(sq[fn], s16);
+      bfly(sb[fn], s32);
+      bfly(sq[fn], s32);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float v = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int idx = qq * 2 + k, fn = idx % FN;
+        v = q == qq ? (idx < FN ? sb[fn] : sq[fn]) : v;
+      }
+      dstat[h][k] += (double)v;
+    }
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) sb[fn] = sq[fn] = 0.f;
+  };
+
+  // ---- one tile: NS steps (chunk cc = cst / 3, filter row rs = cst % 3),
+  // with the previous tile's epilogue (tile ptm; `live` false before the
+  // first tile: every store to the sink, no statistics)
+  auto run_tile = [&](int tl, int ptm, bool live) __attribute__((always_inline)) {
+    static_for<0, NS>([&](auto I) __attribute__((always_inline)) {
+      constexpr int cst = decltype(I)::value, cc = cst / 3, rs = cst % 3;
+      // the next chunk's halo rows (the next tile's first chunk after the last
+      // one; clamped to this tile at the end of the walk: loaded, never used)
+      // next step's weights (weights depend on the step only, not the tile)
+      wprep((cst + 1) % NS, (cst + 1) & 1);
+      // vector-memory ops issued after this step's last weight piece, left in
+      // flight by its closing wait: the halo-row loads (rs == 1, needed one
+      // step later) and the epilogue part's two stores
+      constexpr int NLATE = (rs == P1W_GLRS ? XPT : 0) + (cst <= 3 && !P1W_NOEPI ? 2 : 0);
+      const unsigned char* Xl = smem + rs * (HWX * XRB);
+      // (this buffer's base as an opaque per-step value: the eight fragment
+      // row addresses are formed once per step, the group offsets are
+      // immediates -- hoisted, the 2 x 6 x 8 address registers spilled)
+      unsigned wofs = WBASE + (cst & 1) * WBYTES;
+      asm volatile("" : "+v"(wofs));
+      const unsigned char* Wl = smem + wofs;
+      // MFMA group grp = (tap s, channel half kk); its fragments are read
+      // during the previous group
+      auto frags = [&](int grp, uint4 (&wf)[NH][FN], uint4 (&xf)[FM]) __attribute__((always_inline)) {
+        const int s = grp >> 1, kk = grp & 1;
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn)
+            wf[h][fn] = *reinterpret_cast<const uint4*>(Wl + (kk * 3 + s) * KB * 64 + wrb[h][fn]);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) xf[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + s * XRB + kk * 64);
+      };
+      uint4 wfa[NH][FN], xfa[FM], wfb[NH][FN], xfb[FM];
+      frags(0, wfa, xfa);
+      static_for<0, 6>([&](auto G) __attribute__((always_inline)) {
+        constexpr int grp = decltype(G)::value;
+        auto body = [&](uint4 (&wf)[NH][FN], uint4 (&xf)[FM], uint4 (&wn)[NH][FN], uint4 (&xn)[FM])
+                        __attribute__((always_inline)) {
+          constexpr int gs = (grp + 1) >> 1, gk = (grp + 1) & 1;  // next group's tap / channel half
+          if constexpr (grp + 1 < 6) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+              xn[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + gs * XRB + gk * 64);
+          }
+          // next step's weight pieces: WPG per group over the first 12 / WPG
+          // groups, then the next chunk's halo rows (rs == 1): the end-of-step
+          // wait counts only what was issued after the last piece
+#pragma unroll
+          for (int j = 0; j < WPW; ++j)
+            if (j / P1W_WPG == grp) wpiece(j);
+          if constexpr (rs == P1W_GLRS && grp == (WPW - 1) / P1W_WPG) {
+            if constexpr (cc + 1 == NCH) stage_tile(tl + 1 < ntl ? tl + 1 : tl);
+            gload(cc + 1 == NCH ? 0 : cc + 1);
+          }
+          // weight fragment n feeds its four MFMAs, then its register takes the
+          // next group's fragment n (one fragment set plus the pixel fragments
+          // of two groups live, not two full sets)
+#pragma unroll
+          for (int n = 0; n < NF; ++n) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) {
+              // a tile's first MFMA of an accumulator takes C = 0; its last one
+              // is followed by the packing of the finished value
+              const f4 cin = (cst == 0 && grp == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[fm][n];
+              acc[fm][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf8, xf[fm]), __builtin_bit_cast(bf8, wf[n / FN][n % FN]), cin, 0, 0, 0);
+              if constexpr (cst == NS - 1 && grp == 5) pack1(fm, n);
+            }
+            if constexpr (grp + 1 < 6)
+              wn[n / FN][n % FN] = *reinterpret_cast<const uint4*>(Wl + (gk * 3 + gs) * KB * 64 + wrb[n / FN][n % FN]);
+          }
+          // the previous tile's epilogue: part (h, fm2) in steps 0..3 (done
+          // before the next chunk's rows are staged in registers at step 2),
+          // the statistics of half 0 in step 2, of half 1 in step 4
+          // part p = cst (h = p >> 1, fm2 = 2 (p & 1)) over groups 0..4 of
+          // steps 0..3, the statistics of half h in group 5 of steps 1 / 3
+          if constexpr (cst <= 3 && !P1W_NOEPI) {
+            if constexpr (grp < 4) epi_unit(cst >> 1, (cst & 1) * 2, grp >> 1, grp & 1, ptm, live);
+            if constexpr (grp == 4) epi_store(cst >> 1, (cst & 1) * 2, ptm, live);
+            if constexpr (grp == 5 && (cst & 1)) epi_stats(cst >> 1);
+          }
+        };
+        if constexpr ((grp & 1) == 0) body(wfa, xfa, wfb, xfb);
+        else body(wfb, xfb, wfa, xfa);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      stamp(0);
+      if constexpr (rs == 2 && !P1W_NORESTAGE) {
+        __syncthreads();  // every wave has finished reading the chunk's rows
+        stamp(3);
+        sstore();
+        stamp(4);
+        wait_vmcnt<NLATE>();  // next step's weight pieces landed
+        __syncthreads();
+        stamp(5);
+      } else {
+        wait_vmcnt<NLATE>();
+        stamp(1);
+        __syncthreads();
+        stamp(2);
+      }
+    });
+  };
+
+  if (ntl > 0) {
+    stage_tile(0);
+    gload(0);
+    wprep(0, 0);
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) wpiece(j);
+    sstore();
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  for (int tl = 0; tl < ntl; ++tl) {
+    const int tm = walk.tm + tl * walk.step;
+    run_tile(tl, tl > 0 ? tm - walk.step : tm, tl > 0);
+  }
+  // the last tile's epilogue (packed by its last step)
+  if (ntl > 0) {
+    const int tm = walk.tm + (ntl - 1) * walk.step;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      epi_part(p >> 1, (p & 1) * 2, tm, true);
+      if (p & 1) epi_stats(p >> 1);
+    }
+  }
+#ifdef ACFE_P1W_STAMPS
+  if (lane == 0 && blockIdx.x * 4 + wp < 4096)
+    for (int i = 0; i < 6; ++i) g_p1w_stamps[(blockIdx.x * 4 + wp) * 8 + i] = stv[i];
+#endif
+  wait_vmcnt<0>();
+  __syncthreads();
+  if (stats) {
+    // fixed-order sum of the four waves' partials (same slots in the same lanes)
+    double* red = reinterpret_cast<double*>(smem);
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) red[((wp * 64 + lane) * NH + h) * 2 + k] = dstat[h][k];
+    __syncthreads();
+    if (wp < NH) {
+      const int h = wp;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += red[((w * 64 + lane) * NH + h) * 2 + k];
+        const int idx = q * 2 + k;
+        stats[((long long)blockIdx.x * 2 + idx / FN) * g.Kp + h * 64 + FN * l16 + idx % FN] = v;
+      }
+    }
+    for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
+      for (int c = tid; c < 2 * KB; c += NT) stats[((long long)rr * 2 + (c / KB)) * g.Kp + (c % KB)] = 0.0;
+  }
+}
+
+namespace acfe {
+
+int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+                  int srows, uint8_t* amax, hipStream_t s, const char* what) {
+  if (g.K != 128 || g.C != 128 || (long long)g.N * (g.P / 2) * (g.Q / 2) * g.ldy * 2 >= (1ll << 31))
+    return ACFE_E_INVAL;
+  if ((uintptr_t)y & 15) return ACFE_E_INVAL;
+  const int tiles_h = (g.P + 3) / 4, tiles_w = (g.Q + 63) / 64;
+  const long long nt = (long long)g.N * tiles_h * tiles_w;
+  int gp = 256;
+  if (gp > nt) gp = (int)nt;
+  if (gp >= 64) gp &= ~7;
+  if (stats && gp > srows) gp = srows;
+  if (g.drop.on)
+    hipLaunchKernelGGL((k_conv3x3_pool1w<2, true>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,
+                       (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
+  else
+    hipLaunchKernelGGL((k_conv3x3_pool1w<2, false>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,
+                       (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
+  return launch_rc(what);
+}
+
+}  // namespace acfe
+
+#ifdef ACFE_P1W_STAMPS
+ACFE_API int acfe_debug_pool1w_stamps(unsigned long long* host, int n) {
+  if (n > 4096 * 8) n = 4096 * 8;
+  return hip_rc(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_p1w_stamps), sizeof(unsigned long long) * n), "stamps");
+}
+#endif

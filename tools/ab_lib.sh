@@ -11,7 +11,8 @@ case $1 in
     out=$ROOT/abtest/$name; mkdir -p $out
     cd $ROOT/audio-training_amd/csrc
     for f in *.hip; do
-      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $flags -c $f -o $out/${f%.hip}.o &
+      extra=""; [ $f = pool1w.hip ] && extra=-fno-slp-vectorize
+      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $flags $extra -c $f -o $out/${f%.hip}.o &
     done
     wait
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $ROOT/abtest/$name.so $out/*.o
