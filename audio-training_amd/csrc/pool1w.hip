@@ -126,29 +126,47 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   // (granule offsets are recomputed per chunk: nothing per granule stays live)
   const int gr = tid & 7, CB = g.C * 2;
   u32x4 rx[XPT];
-  int sh0 = 0, sw0 = 0;  // staged tile: input row / column of halo pixel (0, 0)
   __amdgpu_buffer_rsrc_t xrs;
+  // Granule i of this thread: halo row xrow_i, pixel xpix_i (tile
+  // independent).  rel[i] = its byte offset from the tile's halo origin,
+  // computed once; per tile, stage_tile forms the halo origin's offset and a
+  // 13-bit mask of the granules whose column lies inside the image; rows
+  // outside the image need no mask (their offsets fall outside the image's
+  // buffer range, which loads zeros)
+  int rel[XPT];
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int idx = tid + NT * i;
+    const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
+    rel[i] = (xrow * g.W + xpix) * CB + gr * 16;
+  }
+  int tbase = 0;       // byte offset of halo pixel (0, 0) (may be negative)
+  unsigned cmask = 0;  // granules whose column is inside the image
   auto stage_tile = [&](int tl) __attribute__((always_inline)) {
     const int tm = walk.tm + tl * walk.step;
     const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
-    sh0 = hb * TR - g.pt;
-    sw0 = wb * SEGW - g.pl;
+    const int sh0 = hb * TR - g.pt, sw0 = wb * SEGW - g.pl;
+    tbase = (sh0 * g.W + sw0) * CB;
     xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long long)n * g.H * g.W * g.C), (short)0,
                                             g.H * g.W * CB, 0x00020000);
-  };
-  auto gload = [&](int cc) __attribute__((always_inline)) {
-    if (P1W_NOGLOAD) return;
     int t0 = tid;
-    asm volatile("" : "+v"(t0));  // keep the per-granule arithmetic here (not hoisted and spilled)
+    asm volatile("" : "+v"(t0));  // (per tile, not hoisted)
+    cmask = 0;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const unsigned idx = (unsigned)t0 + NT * i;
-      const unsigned xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
-      const unsigned hin = (unsigned)sh0 + xrow, win = (unsigned)sw0 + xpix;
-      const bool ok = idx < (unsigned)XG && win < (unsigned)g.W && hin < (unsigned)g.H;
-      const unsigned off = (hin * (unsigned)g.W + win) * (unsigned)CB + (idx & 7u) * 16u + (unsigned)cc * 128u;
-      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? off : 0x80000000u, 0, 0);
+      const unsigned xpix = (idx % (HWX * 8)) >> 3;
+      const bool ok = idx < (unsigned)XG && (unsigned)(sw0 + (int)xpix) < (unsigned)g.W;
+      cmask |= (ok ? 1u : 0u) << i;
     }
+  };
+  auto gload = [&](int cc) __attribute__((always_inline)) {
+    if (P1W_NOGLOAD) return;
+    const int b0 = tbase + cc * 128;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i)
+      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ((cmask >> i) & 1u) ? (unsigned)(b0 + rel[i]) : 0x80000000u,
+                                                    0, 0);
   };
   // LDS slot of granule i; the last round's threads past the image write
   // their (zero) granule into the never-read 32-B pads of pixels 0..79, so

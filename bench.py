@@ -266,7 +266,7 @@ def main():
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
     traffic = None
-    pmc = next((q for q in (ROOT / "profiles" / f"pmc_dominant_{t}.json" for t in ("r02b", "r02", "r01l"))
+    pmc = next((q for q in (ROOT / "profiles" / f"pmc_dominant_{t}.json" for t in ("r03", "r02b", "r02", "r01l"))
                 if q.exists()), None)
     if pmc is not None and a.batch == 512 and a.model == "bird":  # measured on this launch's shape
         try:
@@ -274,7 +274,7 @@ def main():
         except Exception:
             traffic = None
     counters = None
-    sq = next((q for q in (ROOT / "profiles" / f"sq_dominant_{t}.json" for t in ("r02b", "r02")) if q.exists()),
+    sq = next((q for q in (ROOT / "profiles" / f"sq_dominant_{t}.json" for t in ("r03", "r02b", "r02")) if q.exists()),
               ROOT / "profiles" / "sq_dominant_r02.json")
     if sq.exists():  # SQ counters of the same kernel (tools/pmc_sq.sh, separate rocprofv3 --pmc passes)
         try:
@@ -308,7 +308,7 @@ def main():
             "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
         },
         "roofline": {
-            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_rows<128,4,1,true>: 4 rows x 64 px x 128 ch per workgroup, chunk-resident halo rows, 2x2 max-pool + dropout + BN sums in the epilogue, lanes own whole 2x2 windows)",
+            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_pool1w<2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)",
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,

@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNEL = "k_conv3x3_rows"
+KERNEL = os.environ.get("KNAME", "k_conv3x3_pool1w")
 
 
 def per_dispatch(d):
@@ -46,8 +46,8 @@ def main():
     B, H, W, C, K = 512, 128, 256, 128, 128
     if pool:  # input + pooled output + 1-byte argmax per pooled output (weights negligible)
         algo = B * H * W * C * 2 + B * (H // 2) * (W // 2) * K * 3 + K * 9 * C * 2
-        kern = (os.environ.get("KLABEL", "k_conv3x3_rows<128, 4, 1, true") +
-                "> (s1b0 conv21 3x3 128->128 @128x256 + 2x2 max-pool/dropout/BN-sums epilogue, batch 512)")
+        kern = (os.environ.get("KLABEL", "k_conv3x3_pool1w<2, true>") +
+                " (s1b0 conv21 3x3 128->128 @128x256 + 2x2 max-pool/dropout/BN-sums epilogue, batch 512)")
         src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes inside bench.py (tools/pmc_pool.sh)"
     else:
         algo = (B * H * W * C + B * H * W * K) * 2 + K * 9 * C * 2
