@@ -40,6 +40,15 @@ __device__ unsigned long long g_p1w_stamps[4096 * 8];
 #ifndef P1W_GLRS
 #define P1W_GLRS 1  // filter-row step that requests the next chunk's halo rows
 #endif
+#ifndef P1W_GLSPREAD
+#define P1W_GLSPREAD 1  // halo loads spread over the groups after the last weight piece (p1w_j: 4.27 -> 4.22 ms)
+#endif
+#ifndef P1W_SGB
+#define P1W_SGB 0  // sched_group_barrier issue pattern (VALU per MFMA), 0 = scheduler's choice
+#endif
+#ifndef P1W_NOHASH
+#define P1W_NOHASH 0  // (timing experiments only: no dropout hash)
+#endif
 #ifndef P1W_NODMA
 #define P1W_NODMA 0  // (timing experiments only: no weight pieces)
 #endif
@@ -160,11 +169,11 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
       cmask |= (ok ? 1u : 0u) << i;
     }
   };
-  auto gload = [&](int cc) __attribute__((always_inline)) {
+  auto gload = [&](int cc, int i0 = 0, int i1 = XPT) __attribute__((always_inline)) {
     if (P1W_NOGLOAD) return;
     const int b0 = tbase + cc * 128;
 #pragma unroll
-    for (int i = 0; i < XPT; ++i)
+    for (int i = i0; i < i1; ++i)
       rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ((cmask >> i) & 1u) ? (unsigned)(b0 + rel[i]) : 0x80000000u,
                                                     0, 0);
   };
@@ -203,6 +212,7 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+#define ACCE(fm, n, j) acc[fm][n][j]
   // the previous tile's conv outputs, biased and rounded to bf16, packed
   // (pixels j = 0, 1 | 2, 3 of window q of fragment fm, channel n)
   u32x2 prev[FM][NF];
@@ -212,8 +222,8 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
     for (int j = 0; j < NF; ++j) prev[i][j] = u32x2{0u, 0u};
   auto pack1 = [&](int fm, int n) __attribute__((always_inline)) {
     const float b = bch[n / FN][n % FN];
-    const b2v lo = __builtin_convertvector((f2v){acc[fm][n][0] + b, acc[fm][n][1] + b}, b2v);
-    const b2v hi = __builtin_convertvector((f2v){acc[fm][n][2] + b, acc[fm][n][3] + b}, b2v);
+    const b2v lo = __builtin_convertvector((f2v){ACCE(fm, n, 0) + b, ACCE(fm, n, 1) + b}, b2v);
+    const b2v hi = __builtin_convertvector((f2v){ACCE(fm, n, 2) + b, ACCE(fm, n, 3) + b}, b2v);
     prev[fm][n] = u32x2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
   };
 
@@ -250,7 +260,7 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
     const int wq = wb * (SEGW / 2) + wp * 8 + hf * 4 + (q ^ (q >> 1));
     const bool inb = live && hp2 < P2 && wq < Q2;
     unsigned keep = 3u;
-    if constexpr (DROP) {
+    if constexpr (DROP && !P1W_NOHASH) {
       const unsigned pp = ((unsigned)n * P2 + hp2) * Q2 + wq;
       const uint32_t hh = drop_pair_hash32(g.drop, pp * (unsigned)KB + cf + 2 * pr);
       keep = ((hh & 0xFFFFu) >= g.drop.thr ? 1u : 0u) | ((hh >> 16) >= g.drop.thr ? 2u : 0u);
@@ -392,9 +402,12 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
 #pragma unroll
           for (int j = 0; j < WPW; ++j)
             if (j / P1W_WPG == grp) wpiece(j);
-          if constexpr (rs == P1W_GLRS && grp == (WPW - 1) / P1W_WPG) {
-            if constexpr (cc + 1 == NCH) stage_tile(tl + 1 < ntl ? tl + 1 : tl);
-            gload(cc + 1 == NCH ? 0 : cc + 1);
+          constexpr int G0 = (WPW - 1) / P1W_WPG;  // group of the last weight piece
+          constexpr int NGL = P1W_GLSPREAD ? 6 - G0 : 1;  // groups carrying the halo loads
+          if constexpr (rs == P1W_GLRS && grp >= G0 && grp < G0 + NGL) {
+            if constexpr (cc + 1 == NCH && grp == G0) stage_tile(tl + 1 < ntl ? tl + 1 : tl);
+            constexpr int per = (XPT + NGL - 1) / NGL;
+            gload(cc + 1 == NCH ? 0 : cc + 1, (grp - G0) * per, (grp - G0 + 1) * per < XPT ? (grp - G0 + 1) * per : XPT);
           }
           // weight fragment n feeds its four MFMAs, then its register takes the
           // next group's fragment n (one fragment set plus the pixel fragments
@@ -426,6 +439,17 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
         };
         if constexpr ((grp & 1) == 0) body(wfa, xfa, wfb, xfb);
         else body(wfb, xfb, wfa, xfa);
+        if constexpr (P1W_SGB > 0) {
+          // issue pattern per MFMA: the MFMA, a fragment read while any are
+          // left, then up to P1W_SGB VALU and one SALU
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (i < 12) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, P1W_SGB, 0);
+            __builtin_amdgcn_sched_group_barrier(0x004, 1, 0);
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       });
       stamp(0);
