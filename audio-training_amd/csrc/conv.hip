@@ -48,18 +48,6 @@ __device__ __forceinline__ void mma(f4& acc, const uint4& a, const uint4& b, flo
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
 }
-// 2x2 max-pool backward on the fly: 8 bf16 of the pooled gradient and their 8
-// argmax bytes -> the values that land on tap `pos` ((row & 1) * 2 + (col & 1)) of
-// the window, zeros elsewhere (acfe_maxpool2d_bwd_argmax's scatter, gathered).
-__device__ __forceinline__ u32x4 unpool_mask(uint2 a, unsigned pos) {
-  u32x4 m;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const unsigned w = d < 2 ? a.x : a.y, sh = (d & 1) * 16;
-    m[d] = (((w >> sh) & 0xffu) == pos ? 0xFFFFu : 0u) | (((w >> (sh + 8)) & 0xffu) == pos ? 0xFFFF0000u : 0u);
-  }
-  return m;
-}
 __device__ __forceinline__ uint16_t cvt_out(float v, uint16_t) { return f2bf(v); }
 __device__ __forceinline__ float cvt_out(float v, float) { return v; }
 __device__ __forceinline__ float to_f(uint16_t v) { return bf2f(v); }
@@ -3731,6 +3719,10 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
     if constexpr (PM == 1 && ACFE_POOL1W) {
       // one wave per SIMD, the previous tile's epilogue beside this tile's MFMAs
       const int rc = launch_pool1w(g, x, wp, bias, y, stats, srows, amax, s, what);
+      if (rc != ACFE_E_INVAL) return rc;
+    }
+    if constexpr (PM == 2 && ACFE_POOL1W) {
+      const int rc = launch_unpool1w(g, x, wp, y, amax, s, what);
       if (rc != ACFE_E_INVAL) return rc;
     }
     return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);

@@ -87,6 +87,19 @@ __device__ __forceinline__ void bldsx4s(unsigned voff, i4 desc, unsigned soff, u
 }
 #pragma clang diagnostic pop
 
+// 2x2 max-pool backward on the fly: 8 bf16 of the pooled gradient and their 8
+// argmax bytes -> the values that land on tap `pos` ((row & 1) * 2 + (col & 1)) of
+// the window, zeros elsewhere (acfe_maxpool2d_bwd_argmax's scatter, gathered).
+__device__ __forceinline__ u32x4 unpool_mask(uint2 a, unsigned pos) {
+  u32x4 m;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const unsigned w = d < 2 ? a.x : a.y, sh = (d & 1) * 16;
+    m[d] = (((w >> sh) & 0xffu) == pos ? 0xFFFFu : 0u) | (((w >> (sh + 8)) & 0xffu) == pos ? 0xFFFF0000u : 0u);
+  }
+  return m;
+}
+
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
@@ -99,5 +112,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 // (pool1w.hip); returns ACFE_E_INVAL when the shape is not its case
 int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                   int srows, uint8_t* amax, hipStream_t s, const char* what);
+// acfe_conv2d_dgrad_unpool at K = C = 128 on the same kernel (PM 2)
+int launch_unpool1w(const ConvGeom& g, const void* dyp, const void* wflip, void* dx, uint8_t* amax, hipStream_t s,
+                    const char* what);
 
 }  // namespace acfe

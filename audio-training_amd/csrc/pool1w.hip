@@ -1,75 +1,62 @@
-// k_conv3x3_pool1w: the pooled 3x3 convolution of acfe_conv2d_fwd_pool at
-// K = C = 128 with one wave per SIMD (built with -fno-slp-vectorize: packed
-// f32 VALU beside MFMAs costs more issue time than the two scalar ops).
+// k_conv3x3_1w: the two dominant convolutions of the T1 step -- the pooled
+// forward of acfe_conv2d_fwd_pool and the unpooling dgrad of
+// acfe_conv2d_dgrad_unpool at K = C = 128 -- with one wave per SIMD (built
+// with -fno-slp-vectorize: packed f32 VALU beside MFMAs costs more issue time
+// than the two scalar ops).
 #include "conv_common.h"
 
 using namespace acfe;
 
-// ------------------------------------------------------------------ pooled 3x3 conv, one wave per SIMD
-// k_conv3x3_pool1w<NCH, DROP>: acfe_conv2d_fwd_pool at K = 128, C = 64 NCH
-// (NCH even: the dominant T1 layer, stage-1 block-0 branch21 128 -> 128 @
-// 128 x 256 -> MaxPool2D(2) -> Dropout -> BN, resnet/wr_resnet_bird.py:136-147).
-// Same tile, LDS images, weight pieces and pooled epilogue arithmetic as
-// k_conv3x3_rows<128, 4, 1, true> (4 rows x 64 px x 128 channels, chunk-resident
-// halo rows, pixels x weights MFMA order), but four waves, one per SIMD, each
-// owning a 16-column strip of the four rows and ALL 128 channels (8 weight
-// fragments per 4 pixel fragments: 0.375 instead of 0.5 ds_read_b128 per MFMA;
-// 128 accumulators per lane in the accumulator file).  The pooled epilogue of
-// tile i - 1 runs beside the MFMAs of tile i: at the first MFMA group of a tile
-// each accumulator is read out, biased and rounded to bf16 (the value a
-// separate conv would have stored) into 64 packed registers just before its
-// first MFMA of the new tile overwrites it (C = 0), and the max / argmax /
-// dropout / BN sums / stores of those values run in four parts between the
-// MFMA groups of steps 1..4, the statistics shuffles in steps 3 and 5 -- the
-// 8-wave kernel stopped its MFMAs for the whole epilogue (16 % of every step,
-// DESIGN §4.1).  Every step is one straight block: no branches (the last
-// tile's loads are clamped; out-of-image and phantom stores go to a sink), and
-// the MFMA groups are fenced by sched_barrier with the next group's fragments
-// read during the current one.
-#ifndef P1W_WPG
-#define P1W_WPG 4  // weight pieces per MFMA group (groups 0..2)
-#endif
-#ifndef P1W_NOEPI
-#define P1W_NOEPI 0  // (timing experiments only: no epilogue parts)
-#endif
+// ------------------------------------------------------------------ 3x3 conv, one wave per SIMD
+// k_conv3x3_1w<PM, NCH, DROP>, K = 128 output channels, C = 64 NCH input
+// channels (NCH even).  PM 1: acfe_conv2d_fwd_pool (stage-1 block-0 branch21
+// 128 -> 128 @ 128 x 256 -> MaxPool2D(2) -> Dropout -> BN,
+// resnet/wr_resnet_bird.py:136-147); PM 2: its dgrad from the pooled gradient
+// and the argmax bytes (the 2x2 max-pool backward expanded while staging).
+//
+// Same tile, LDS images and weight pieces as k_conv3x3_rows<128, 4, PM, true>
+// (4 rows x 64 px x 128 channels, chunk-resident halo rows: a step is one
+// 64-channel chunk x one filter row), but four waves, one per SIMD, each
+// owning a quarter of the tile's pixels and ALL 128 channels: 8 weight
+// fragments per 4 pixel fragments (0.375 instead of 0.5 ds_read_b128 per
+// MFMA) and 128 accumulators per lane in the accumulator file.
+//  * The epilogue of tile i - 1 runs beside the MFMAs of tile i: each
+//    accumulator's last MFMA of a tile is followed by its packing (biased,
+//    rounded to bf16: the value a separate conv would have stored) into 64
+//    packed registers, the tile's first MFMA of it takes C = 0, and the
+//    epilogue of the packed values (PM 1: max / first-maximum argmax / dropout
+//    / BN sums / stores; PM 2: 16-B channel-run stores) runs in units between
+//    the MFMA groups of steps 0..3.  The 8-wave kernel stopped its MFMAs for
+//    the whole epilogue (16 % of every step).
+//  * Every step is one straight block (no branches: the last tile's loads are
+//    clamped, out-of-image and phantom stores are buffer stores at an
+//    out-of-range offset), its MFMA groups fenced by sched_barrier with the
+//    next group's fragments read during the current one, the next step's
+//    weight pieces (LDS-DMA) in groups 0..2 and the next chunk's halo loads
+//    after them, so the step's closing vmcnt wait leaves the halo loads and
+//    epilogue stores in flight.
+//  * MFMA operand order: PM 1 pixels x weights (a lane's four accumulators
+//    are one 2x2 window of one channel), PM 2 weights x pixels (a lane holds
+//    16 consecutive channels of a pixel per channel half: 16-B stores).
 #ifdef ACFE_P1W_STAMPS
 // diagnostic build (make stamps): per-wave s_memtime totals of the step
 // segments, read back by acfe_debug_pool1w_stamps (tools/pool1w_stamps.py)
 __device__ unsigned long long g_p1w_stamps[4096 * 8];
 #endif
-#ifndef P1W_GLRS
-#define P1W_GLRS 1  // filter-row step that requests the next chunk's halo rows
-#endif
-#ifndef P1W_GLSPREAD
-#define P1W_GLSPREAD 1  // halo loads spread over the groups after the last weight piece (p1w_j: 4.27 -> 4.22 ms)
-#endif
-#ifndef P1W_SGB
-#define P1W_SGB 0  // sched_group_barrier issue pattern (VALU per MFMA), 0 = scheduler's choice
-#endif
-#ifndef P1W_NOHASH
-#define P1W_NOHASH 0  // (timing experiments only: no dropout hash)
-#endif
-#ifndef P1W_NODMA
-#define P1W_NODMA 0  // (timing experiments only: no weight pieces)
-#endif
-#ifndef P1W_NOGLOAD
-#define P1W_NOGLOAD 0  // (timing experiments only: no halo-row loads)
-#endif
-#ifndef P1W_NORESTAGE
-#define P1W_NORESTAGE 0  // (timing experiments only: no chunk restage)
-#endif
-template <int NCH, bool DROP>
+template <int PM, int NCH, bool DROP>
 __global__ void __launch_bounds__(256, 1)
-k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
-                 const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
-                 int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
+k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+             const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
+             int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
   static_assert(NCH % 2 == 0, "even step count per tile: weight buffer parity is static");
+  static_assert(PM == 1 || (PM == 2 && !DROP), "modes");
   constexpr int KB = 128, TR = 4, FM = 4, FN = 4, NH = 2, NF = NH * FN, SEGW = 64, HWX = SEGW + 2, XRB = 160;
   constexpr int NT = 256, NS = 3 * NCH;                          // threads, steps per tile
   constexpr int XROWS = TR + 2, XBYTES = XROWS * HWX * XRB;      // 63 360 B
   constexpr int WBYTES = 3 * KB * 128, WBASE = XBYTES;           // 2 x 49 152 B
   constexpr int XG = XROWS * HWX * 8, XPT = (XG + NT - 1) / NT;  // 16-B input granules
   constexpr int WPW = 3 * KB * 8 / 64 / (NT / 64);               // 12 weight pieces per wave per step
+  constexpr int WPG = 4;                                         // pieces per MFMA group (groups 0..2)
   constexpr int SMEM = XBYTES + 2 * WBYTES;
   static_assert(SMEM <= 163840, "LDS");
   static_assert(XPT * NT - XG <= 2 * XROWS * HWX, "spare granules fit the pixel pads");
@@ -92,90 +79,152 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
 #else
   auto stamp = [](int) __attribute__((always_inline)) {};
 #endif
+  auto tile_of = [&](int tm, int& n, int& hb, int& wb) __attribute__((always_inline)) {
+    n = tm / tpi;
+    const int rem = tm - n * tpi;
+    hb = rem / tiles_w;
+    wb = rem - hb * tiles_w;
+  };
 
-  // bias of the lane's channels h * 64 + 4 l16 + [0, 4)
+  // bias of the lane's channels h * 64 + 4 l16 + [0, 4) (PM 1)
   f4 bch[NH];
 #pragma unroll
   for (int h = 0; h < NH; ++h)
-    bch[h] = bias ? *reinterpret_cast<const f4*>(bias + h * 64 + 4 * l16) : f4{0.f, 0.f, 0.f, 0.f};
+    bch[h] = (PM == 1 && bias) ? *reinterpret_cast<const f4*>(bias + h * 64 + 4 * l16) : f4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- weight pieces (k_conv3x3_rows' SWP layout: LDS rows [kk][s][phys(k)]
-  // of 64 B, phys(k) = k ^ ((k >> 2) & 3), granule slot ^ ((l16 >> 2) & 2) on
-  // the reading side).  A piece is 16 rows (1 KB) of one (kk, s): wave wp
-  // loads row blocks kb = 2 wp, 2 wp + 1 of all six (kk, s), so its source
-  // offsets are one VGPR (the lane's row and swizzled granule; the swizzle
-  // term (kb >> 1) & 1 = wp & 1 is per wave) plus a uniform soffset formed
-  // per piece.
-  const int l4 = lane >> 2;
-  const unsigned vwl = (unsigned)((l4 ^ ((l4 >> 2) & 3)) * g.Kdp * 2) +
-                       ((((unsigned)lane & 3u) ^ ((wp & 1) ? 2u : 0u)) << 4);
-  const int sob = __builtin_amdgcn_readfirstlane(2 * wp * 16 * g.Kdp * 2);  // row block 2 wp
+  // ---- weight pieces (LDS-DMA, 1 KB each, 48 per step).  The lane part of a
+  // piece's source offset is one of two VGPRs per wave, the rest a uniform
+  // soffset formed per piece; LDS destination in M0.
+  //  PM 1 (k_conv3x3_rows' SWP layout): LDS rows [kk][s][phys(k)] of 64 B,
+  //   phys(k) = k ^ ((k >> 2) & 3), granule slot ^ ((l16 >> 2) & 2) on the
+  //   reading side; piece (kk, s, b) = 16 rows of row block 2 wp + b, whose
+  //   swizzle term (kb >> 1) & 1 = wp & 1.
+  //  PM 2 (CPERM layout): LDS rows [s][k] of 128 B, slot sigma holds granule
+  //   sigma ^ sw(k), sw(k) = ((k >> 4) & 3) << 1 | ((k >> 1) & 1); piece (s, b)
+  //   = 8 rows 32 wp + 8 b .., whose (k >> 4) & 3 = (2 wp + (b >> 1)) & 3.
+  unsigned vw[2];
+  int sob;
+  if constexpr (PM == 1) {
+    const int l4 = lane >> 2;
+    vw[0] = vw[1] = (unsigned)((l4 ^ ((l4 >> 2) & 3)) * g.Kdp * 2) +
+                    ((((unsigned)lane & 3u) ^ ((wp & 1) ? 2u : 0u)) << 4);
+    sob = __builtin_amdgcn_readfirstlane(2 * wp * 16 * g.Kdp * 2);  // row block 2 wp
+  } else {
+    const int l8 = lane >> 3;
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      const unsigned sw = ((unsigned)((2 * wp + bb) & 3) << 1) | ((unsigned)(lane >> 4) & 1u);
+      vw[bb] = (unsigned)(l8 * g.Kdp * 2) + ((((unsigned)lane & 7u) ^ sw) << 4);
+    }
+    sob = __builtin_amdgcn_readfirstlane(32 * wp * g.Kdp * 2);  // row 32 wp
+  }
   unsigned wlo = 0, whi = 0, wlb = 0;
   auto wprep = [&](int st, int wb) __attribute__((always_inline)) {
     const int cc = st / 3, r = st - cc * 3;
     const unsigned long long base = (unsigned long long)(uintptr_t)Wp + ((unsigned)(r * 3 * g.C + cc * 64) * 2u);
     wlo = (unsigned)base;
     whi = (unsigned)(base >> 32);
-    wlb = lds0 + WBASE + wb * WBYTES + 2 * wp * 1024;
+    wlb = lds0 + WBASE + wb * WBYTES;
   };
-  // piece j = 2 (kk * 3 + s) + b: row block 2 wp + b of (kk, s)
   auto wpiece = [&](int j) __attribute__((always_inline)) {
-    const int ks = j >> 1, b = j & 1, kk = ks / 3, s_ = ks - kk * 3;
     const i4 dw = {__builtin_amdgcn_readfirstlane((int)wlo), __builtin_amdgcn_readfirstlane((int)whi),
                    (int)0x80000000u, 0x00020000};
     int sb_ = sob;
     asm volatile("" : "+s"(sb_));  // formed here, not hoisted into a dozen live registers
-    const unsigned so = (unsigned)(sb_ + s_ * g.C * 2 + kk * 64 + b * 16 * g.Kdp * 2);
-    const unsigned lb = (unsigned)__builtin_amdgcn_readfirstlane((int)(wlb + (ks * 128 + b * 16) * 64));
-    if (!P1W_NODMA) bldsx4s(vwl, dw, so, lb);
+    unsigned so, lb, vo;
+    if constexpr (PM == 1) {  // j = 2 (kk * 3 + s) + b
+      const int ks = j >> 1, b = j & 1, kk = ks / 3, s_ = ks - kk * 3;
+      so = (unsigned)(sb_ + s_ * g.C * 2 + kk * 64 + b * 16 * g.Kdp * 2);
+      lb = wlb + (ks * 128 + 2 * wp * 16 + b * 16) * 64;
+      vo = vw[0];
+    } else {  // j = 4 s + b: rows 32 wp + 8 b .. of tap s
+      const int s_ = j >> 2, b = j & 3;
+      so = (unsigned)(sb_ + s_ * g.C * 2 + b * 8 * g.Kdp * 2);
+      lb = wlb + (s_ * 128 + 32 * wp + 8 * b) * 128;
+      vo = vw[b >> 1];
+    }
+    bldsx4s(vo, dw, so, (unsigned)__builtin_amdgcn_readfirstlane((int)lb));
   };
 
-  // ---- input halo rows of a 64-channel chunk, register-staged (granule i of
-  // this thread: halo pixel (tid >> 3) + 32 i, channel slot tid & 7)
-  // (granule offsets are recomputed per chunk: nothing per granule stays live)
+  // ---- input halo rows of a 64-channel chunk, register-staged: granule i of
+  // this thread = halo pixel (tid >> 3) + 32 i (row xrow_i, pixel xpix_i: tile
+  // independent), channel slot gr = tid & 7
   const int gr = tid & 7, CB = g.C * 2;
   u32x4 rx[XPT];
-  __amdgpu_buffer_rsrc_t xrs;
-  // Granule i of this thread: halo row xrow_i, pixel xpix_i (tile
-  // independent).  rel[i] = its byte offset from the tile's halo origin,
-  // computed once; per tile, stage_tile forms the halo origin's offset and a
-  // 13-bit mask of the granules whose column lies inside the image; rows
-  // outside the image need no mask (their offsets fall outside the image's
-  // buffer range, which loads zeros)
+  uint2 ra[PM == 2 ? XPT : 1];  // PM 2: the granules' argmax bytes
+  __amdgpu_buffer_rsrc_t xrs, ars;
+  // PM 1: rel[i] = byte offset of granule i from the tile's halo origin
+  // (computed once); per tile the origin's offset (may be negative) and a
+  // mask of the granules whose column lies inside the image (rows outside the
+  // image fall outside the image's buffer range, which loads zeros).
+  // PM 2: per tile, gel[i] = element offset of granule i's pooled-gradient
+  // granule in the image, a validity mask and the 2-bit window tap of each
+  // granule (unpool mask applied at the LDS store).
   int rel[XPT];
+  int tbase = 0;
+  unsigned cmask = 0, pos0 = 0, pos1 = 0;
+  if constexpr (PM == 1) {
 #pragma unroll
-  for (int i = 0; i < XPT; ++i) {
-    const int idx = tid + NT * i;
-    const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
-    rel[i] = (xrow * g.W + xpix) * CB + gr * 16;
+    for (int i = 0; i < XPT; ++i) {
+      const int idx = tid + NT * i;
+      const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
+      rel[i] = (xrow * g.W + xpix) * CB + gr * 16;
+    }
   }
-  int tbase = 0;       // byte offset of halo pixel (0, 0) (may be negative)
-  unsigned cmask = 0;  // granules whose column is inside the image
   auto stage_tile = [&](int tl) __attribute__((always_inline)) {
     const int tm = walk.tm + tl * walk.step;
-    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    int n, hb, wb;
+    tile_of(tm, n, hb, wb);
     const int sh0 = hb * TR - g.pt, sw0 = wb * SEGW - g.pl;
-    tbase = (sh0 * g.W + sw0) * CB;
-    xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long long)n * g.H * g.W * g.C), (short)0,
-                                            g.H * g.W * CB, 0x00020000);
     int t0 = tid;
     asm volatile("" : "+v"(t0));  // (per tile, not hoisted)
     cmask = 0;
+    if constexpr (PM == 1) {
+      tbase = (sh0 * g.W + sw0) * CB;
+      xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long long)n * g.H * g.W * g.C), (short)0,
+                                              g.H * g.W * CB, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const unsigned idx = (unsigned)t0 + NT * i;
-      const unsigned xpix = (idx % (HWX * 8)) >> 3;
-      const bool ok = idx < (unsigned)XG && (unsigned)(sw0 + (int)xpix) < (unsigned)g.W;
-      cmask |= (ok ? 1u : 0u) << i;
+      for (int i = 0; i < XPT; ++i) {
+        const unsigned idx = (unsigned)t0 + NT * i;
+        const unsigned xpix = (idx % (HWX * 8)) >> 3;
+        const bool ok = idx < (unsigned)XG && (unsigned)(sw0 + (int)xpix) < (unsigned)g.W;
+        cmask |= (ok ? 1u : 0u) << i;
+      }
+    } else {
+      // X = pooled gradient [N][H/2][W/2][C], amax its argmax bytes
+      const long long img = (long long)n * (g.H >> 1) * (g.W >> 1) * g.C;
+      const int nb = (g.H >> 1) * (g.W >> 1) * g.C;
+      xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + img), (short)0, nb * 2, 0x00020000);
+      ars = __builtin_amdgcn_make_buffer_rsrc((void*)(amax + img), (short)0, nb, 0x00020000);
+      pos0 = pos1 = 0;
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int idx = t0 + NT * i;
+        const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
+        const int hin = sh0 + xrow, win = sw0 + xpix;
+        const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
+        rel[i] = ((hin >> 1) * (g.W >> 1) + (win >> 1)) * g.C + gr * 8;
+        cmask |= (ok ? 1u : 0u) << i;
+        const unsigned p = ((unsigned)(hin & 1) << 1) | ((unsigned)win & 1u);
+        if (i < 8) pos0 |= p << (4 * i);
+        else pos1 |= p << (4 * (i - 8));
+      }
     }
   };
-  auto gload = [&](int cc, int i0 = 0, int i1 = XPT) __attribute__((always_inline)) {
-    if (P1W_NOGLOAD) return;
-    const int b0 = tbase + cc * 128;
+  auto gload = [&](int cc, int i0, int i1) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = i0; i < i1; ++i)
-      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ((cmask >> i) & 1u) ? (unsigned)(b0 + rel[i]) : 0x80000000u,
-                                                    0, 0);
+    for (int i = i0; i < i1; ++i) {
+      const bool ok = (cmask >> i) & 1u;
+      if constexpr (PM == 1) {
+        rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? (unsigned)(tbase + cc * 128 + rel[i]) : 0x80000000u,
+                                                      0, 0);
+      } else {
+        const unsigned e = (unsigned)(rel[i] + cc * 64);
+        rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? e * 2u : 0x80000000u, 0, 0);
+        const auto a8 = __builtin_amdgcn_raw_buffer_load_b64(ars, ok ? e : 0x80000000u, 0, 0);
+        ra[i] = uint2{a8[0], a8[1]};
+      }
+    }
   };
   // LDS slot of granule i; the last round's threads past the image write
   // their (zero) granule into the never-read 32-B pads of pixels 0..79, so
@@ -186,35 +235,57 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   };
   auto sstore = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) *reinterpret_cast<u32x4*>(smem + sslot(i)) = rx[i];
+    for (int i = 0; i < XPT; ++i) {
+      u32x4 v = rx[i];
+      if constexpr (PM == 2) v &= unpool_mask(ra[i], ((i < 8 ? pos0 >> (4 * i) : pos1 >> (4 * (i - 8)))) & 3u);
+      *reinterpret_cast<u32x4*>(smem + sslot(i)) = v;
+    }
   };
 
-  // ---- fragment offsets: A rows 4 q' + j = window q' of fragment fm (row pair
-  // fm / 2, pooled column wp * 8 + (fm & 1) * 4 + (q' ^ (q' >> 1))), pixel j
+  // ---- fragment offsets
   int xoff[FM];
+  int wrb[2][NH][FN];  // [kk] (PM 1: both equal)
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm) {
-    const int qq = l16 >> 2, j = l16 & 3;
-    const int a = wp * 8 + (fm & 1) * 4 + (qq ^ (qq >> 1));
-    xoff[fm] = (((fm >> 1) * 2 + (j >> 1)) * HWX + 2 * a + (j & 1)) * XRB + q * 16;
+    if constexpr (PM == 1) {
+      // A rows 4 q' + j = window q' of fragment fm (row pair fm / 2, pooled
+      // column wp * 8 + (fm & 1) * 4 + (q' ^ (q' >> 1))), pixel j
+      const int qq = l16 >> 2, j = l16 & 3;
+      const int a = wp * 8 + (fm & 1) * 4 + (qq ^ (qq >> 1));
+      xoff[fm] = (((fm >> 1) * 2 + (j >> 1)) * HWX + 2 * a + (j & 1)) * XRB + q * 16;
+    } else {
+      // B columns = pixels wp * 64 + fm * 16 + l16 (tile row wp)
+      xoff[fm] = (wp * HWX + fm * 16 + l16) * XRB + q * 16;
+    }
   }
-  int wrb[NH][FN];
 #pragma unroll
   for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      const int k = h * 64 + FN * l16 + fn;
-      wrb[h][fn] = (k ^ ((k >> 2) & 3)) * 64 + ((q ^ ((l16 >> 2) & 2)) << 4);
+      if constexpr (PM == 1) {
+        const int k = h * 64 + FN * l16 + fn;
+        wrb[0][h][fn] = wrb[1][h][fn] = (k ^ ((k >> 2) & 3)) * 64 + ((q ^ ((l16 >> 2) & 2)) << 4);
+      } else {
+        // A row m = l16 = channel h * 64 + 16 (m >> 2) + 4 fn + (m & 3)
+        const int k = h * 64 + 16 * (l16 >> 2) + 4 * fn + (l16 & 3);
+        const int sw = (((k >> 4) & 3) << 1) | ((k >> 1) & 1);
+        wrb[0][h][fn] = k * 128 + ((q ^ sw) << 4);
+        wrb[1][h][fn] = k * 128 + (((q + 4) ^ sw) << 4);
+      }
     }
+  // weight fragment of group (s, kk) relative to the buffer base
+  auto wfrag_off = [&](int s, int kk, int h, int fn) __attribute__((always_inline)) {
+    return PM == 1 ? (kk * 3 + s) * KB * 64 + wrb[0][h][fn] : s * KB * 128 + wrb[kk][h][fn];
+  };
 
   f4 acc[FM][NF];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-#define ACCE(fm, n, j) acc[fm][n][j]
-  // the previous tile's conv outputs, biased and rounded to bf16, packed
-  // (pixels j = 0, 1 | 2, 3 of window q of fragment fm, channel n)
+  // the previous tile's conv outputs, biased and rounded to bf16, packed:
+  // PM 1 pixels j = 0, 1 | 2, 3 of window q of fragment fm, channel n;
+  // PM 2 channels 4 fn + 0, 1 | 2, 3 of its 16-channel run, pixel l16 of fm
   u32x2 prev[FM][NF];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -222,16 +293,19 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
     for (int j = 0; j < NF; ++j) prev[i][j] = u32x2{0u, 0u};
   auto pack1 = [&](int fm, int n) __attribute__((always_inline)) {
     const float b = bch[n / FN][n % FN];
-    const b2v lo = __builtin_convertvector((f2v){ACCE(fm, n, 0) + b, ACCE(fm, n, 1) + b}, b2v);
-    const b2v hi = __builtin_convertvector((f2v){ACCE(fm, n, 2) + b, ACCE(fm, n, 3) + b}, b2v);
+    const b2v lo = __builtin_convertvector((f2v){acc[fm][n][0] + b, acc[fm][n][1] + b}, b2v);
+    const b2v hi = __builtin_convertvector((f2v){acc[fm][n][2] + b, acc[fm][n][3] + b}, b2v);
     prev[fm][n] = u32x2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
   };
 
-  // pooled output and argmax bytes (< 2^31 bytes each, checked by the launcher)
+  // ---- PM 1 epilogue: part (h, fm2) = channel half h, fragment pair fm2
+  // (pooled row fm2 / 2 of the tile), in units: unit (hf, pr) pools channels
+  // 2 pr, 2 pr + 1 of fragment fm2 + hf (their dropout pair hash, max /
+  // first-maximum argmax, BN sums) into eyv / eav; the store unit exchanges
+  // fragment halves between lane pairs and writes 16 B pooled + 8 B argmax
+  // per lane.  Pooled output and argmax bytes < 2^31 bytes (launcher).
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)Y, (short)0, 0x7FFFFFFF, 0x00020000);
   const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)amax, (short)0, 0x7FFFFFFF, 0x00020000);
-  // ---- pooled epilogue of `prev`, in parts: part (h, fm2) = channel half h,
-  // fragment pair fm2 (pooled row fm2 / 2 of the tile)
   const int P2 = g.P >> 1, Q2 = g.Q >> 1;
   const bool odd = (lane & 1) != 0;
   float sb[FN], sq[FN];  // BN sums of the half in progress
@@ -240,17 +314,7 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   for (int k = 0; k < FN; ++k) sb[k] = sq[k] = 0.f;
 #pragma unroll
   for (int h = 0; h < NH; ++h) dstat[h][0] = dstat[h][1] = 0.0;
-  // part (h, fm2) in units: unit (hf, pr) pools channels 2 pr, 2 pr + 1 of
-  // fragment fm2 + hf (their dropout pair hash, max / first-maximum argmax,
-  // BN sums) into eyv / eav; the store unit exchanges fragment halves between
-  // lane pairs and writes 16 B pooled + 8 B argmax per lane
   unsigned eyv[2][2], eav[2];
-  auto tile_of = [&](int tm, int& n, int& hb, int& wb) __attribute__((always_inline)) {
-    n = tm / tpi;
-    const int rem = tm - n * tpi;
-    hb = rem / tiles_w;
-    wb = rem - hb * tiles_w;
-  };
   auto epi_unit = [&](int h, int fm2, int hf, int pr, int tm, bool live) __attribute__((always_inline)) {
     int n, hb, wb;
     tile_of(tm, n, hb, wb);
@@ -260,7 +324,7 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
     const int wq = wb * (SEGW / 2) + wp * 8 + hf * 4 + (q ^ (q >> 1));
     const bool inb = live && hp2 < P2 && wq < Q2;
     unsigned keep = 3u;
-    if constexpr (DROP && !P1W_NOHASH) {
+    if constexpr (DROP) {
       const unsigned pp = ((unsigned)n * P2 + hp2) * Q2 + wq;
       const uint32_t hh = drop_pair_hash32(g.drop, pp * (unsigned)KB + cf + 2 * pr);
       keep = ((hh & 0xFFFFu) >= g.drop.thr ? 1u : 0u) | ((hh >> 16) >= g.drop.thr ? 2u : 0u);
@@ -304,19 +368,11 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
     const int wq = wb * (SEGW / 2) + wp * 8 + (odd ? 4 : 0) + (q ^ (q >> 1));
     const bool inb = live && hp2 < P2 && wq < Q2;
     const unsigned c0 = h * 64 + FN * (l16 & ~1);
-    // buffer stores into the pooled output: an out-of-range offset (outside
-    // the image, or the phantom epilogue before the first tile) is dropped
-    // by the hardware -- no branch, no sink
-    const unsigned pix = ((unsigned)n * P2 + hp2) * Q2 + wq;  // (output bytes < 2^31: launcher)
+    const unsigned pix = ((unsigned)n * P2 + hp2) * Q2 + wq;
     __builtin_amdgcn_raw_buffer_store_b128(odd ? u32x4{ys[0], ys[1], yo[0], yo[1]} : u32x4{yo[0], yo[1], ys[0], ys[1]},
                                            yr, inb ? (pix * (unsigned)g.ldy + c0) * 2u : 0x80000000u, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b64(odd ? u32x2{as, ao} : u32x2{ao, as}, ar,
                                           inb ? pix * (unsigned)KB + c0 : 0x80000000u, 0, 0);
-  };
-  auto epi_part = [&](int h, int fm2, int tm, bool live) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) epi_unit(h, fm2, u >> 1, u & 1, tm, live);
-    epi_store(h, fm2, tm, live);
   };
   // statistics of half h of a finished tile: sums over the four window groups,
   // lane group q keeps values 2 q + k of [sb[0..4), sq[0..4)]
@@ -350,42 +406,67 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) sb[fn] = sq[fn] = 0.f;
   };
+  // ---- PM 2 epilogue: unit (fm, h) stores the 16 consecutive channels
+  // h * 64 + 16 q .. of pixel (tile row wp, column fm * 16 + l16) as two 16-B
+  // stores into the image's dX (per-image buffer, < 2^31 bytes: launcher)
+  auto dx_unit = [&](int fm, int h, int tm, bool live) __attribute__((always_inline)) {
+    int n, hb, wb;
+    tile_of(tm, n, hb, wb);
+    const int hh = hb * TR + wp, ww = wb * SEGW + fm * 16 + l16;
+    const bool inb = live && hh < g.P && ww < g.Q;
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Y + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
+    const unsigned o = ((unsigned)(hh * g.Q + ww) * (unsigned)g.ldy + h * 64 + 16 * q) * 2u;
+    const u32x2 p0 = prev[fm][h * FN + 0], p1 = prev[fm][h * FN + 1], p2 = prev[fm][h * FN + 2],
+                p3 = prev[fm][h * FN + 3];
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{p0[0], p0[1], p1[0], p1[1]}, dr, inb ? o : 0x80000000u, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{p2[0], p2[1], p3[0], p3[1]}, dr, inb ? o + 16u : 0x80000000u, 0, 0);
+  };
+  // epilogue work in step cst (0..3), MFMA group grp; returns the number of
+  // vector-memory stores it issues (for the step's closing wait)
+  constexpr int EPI_STORES = PM == 1 ? 2 : 4;  // per step 0..3
+  auto epi_slot = [&](auto cstc, auto grpc, int ptm, bool live) __attribute__((always_inline)) {
+    constexpr int cst = decltype(cstc)::value, grp = decltype(grpc)::value;
+    if constexpr (PM == 1) {
+      // part p = cst (h = p >> 1, fm2 = 2 (p & 1)) over groups 0..4 of steps
+      // 0..3, the statistics of half h in group 5 of steps 1 / 3
+      if constexpr (grp < 4) epi_unit(cst >> 1, (cst & 1) * 2, grp >> 1, grp & 1, ptm, live);
+      if constexpr (grp == 4) epi_store(cst >> 1, (cst & 1) * 2, ptm, live);
+      if constexpr (grp == 5 && (cst & 1)) epi_stats(cst >> 1);
+    } else {
+      // units (fm = cst, h = 0 / 1) in groups 1 / 3
+      if constexpr (grp == 1 || grp == 3) dx_unit(cst, grp >> 1, ptm, live);
+    }
+  };
 
   // ---- one tile: NS steps (chunk cc = cst / 3, filter row rs = cst % 3),
   // with the previous tile's epilogue (tile ptm; `live` false before the
-  // first tile: every store to the sink, no statistics)
+  // first tile: every store dropped, no statistics)
   auto run_tile = [&](int tl, int ptm, bool live) __attribute__((always_inline)) {
     static_for<0, NS>([&](auto I) __attribute__((always_inline)) {
       constexpr int cst = decltype(I)::value, cc = cst / 3, rs = cst % 3;
-      // the next chunk's halo rows (the next tile's first chunk after the last
-      // one; clamped to this tile at the end of the walk: loaded, never used)
       // next step's weights (weights depend on the step only, not the tile)
       wprep((cst + 1) % NS, (cst + 1) & 1);
       // vector-memory ops issued after this step's last weight piece, left in
-      // flight by its closing wait: the halo-row loads (rs == 1, needed one
-      // step later) and the epilogue part's two stores
-      constexpr int NLATE = (rs == P1W_GLRS ? XPT : 0) + (cst <= 3 && !P1W_NOEPI ? 2 : 0);
+      // flight by its closing wait: the next chunk's halo loads (rs == 1,
+      // needed one step later) and the epilogue's stores
+      constexpr int NLATE = (rs == 1 ? XPT * (PM == 2 ? 2 : 1) : 0) + (cst <= 3 ? EPI_STORES : 0);
       const unsigned char* Xl = smem + rs * (HWX * XRB);
-      // (this buffer's base as an opaque per-step value: the eight fragment
-      // row addresses are formed once per step, the group offsets are
-      // immediates -- hoisted, the 2 x 6 x 8 address registers spilled)
+      // (this buffer's base as an opaque per-step value: the fragment row
+      // addresses are formed once per step, the group offsets are immediates
+      // -- hoisted, the 2 x 6 x 8 address registers spilled)
       unsigned wofs = WBASE + (cst & 1) * WBYTES;
       asm volatile("" : "+v"(wofs));
       const unsigned char* Wl = smem + wofs;
       // MFMA group grp = (tap s, channel half kk); its fragments are read
       // during the previous group
-      auto frags = [&](int grp, uint4 (&wf)[NH][FN], uint4 (&xf)[FM]) __attribute__((always_inline)) {
-        const int s = grp >> 1, kk = grp & 1;
-#pragma unroll
-        for (int h = 0; h < NH; ++h)
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn)
-            wf[h][fn] = *reinterpret_cast<const uint4*>(Wl + (kk * 3 + s) * KB * 64 + wrb[h][fn]);
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm) xf[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + s * XRB + kk * 64);
-      };
       uint4 wfa[NH][FN], xfa[FM], wfb[NH][FN], xfb[FM];
-      frags(0, wfa, xfa);
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) wfa[h][fn] = *reinterpret_cast<const uint4*>(Wl + wfrag_off(0, 0, h, fn));
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) xfa[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm]);
       static_for<0, 6>([&](auto G) __attribute__((always_inline)) {
         constexpr int grp = decltype(G)::value;
         auto body = [&](uint4 (&wf)[NH][FN], uint4 (&xf)[FM], uint4 (&wn)[NH][FN], uint4 (&xn)[FM])
@@ -396,22 +477,19 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
             for (int fm = 0; fm < FM; ++fm)
               xn[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + gs * XRB + gk * 64);
           }
-          // next step's weight pieces: WPG per group over the first 12 / WPG
-          // groups, then the next chunk's halo rows (rs == 1): the end-of-step
-          // wait counts only what was issued after the last piece
+          // next step's weight pieces (groups 0..2), then the next chunk's
+          // halo rows spread over groups 2..5 (the next tile's first chunk
+          // after the last one; clamped to this tile at the end of the walk)
 #pragma unroll
           for (int j = 0; j < WPW; ++j)
-            if (j / P1W_WPG == grp) wpiece(j);
-          constexpr int G0 = (WPW - 1) / P1W_WPG;  // group of the last weight piece
-          constexpr int NGL = P1W_GLSPREAD ? 6 - G0 : 1;  // groups carrying the halo loads
-          if constexpr (rs == P1W_GLRS && grp >= G0 && grp < G0 + NGL) {
+            if (j / WPG == grp) wpiece(j);
+          constexpr int G0 = (WPW - 1) / WPG, NGL = 6 - G0, per = (XPT + NGL - 1) / NGL;
+          if constexpr (rs == 1 && grp >= G0) {
             if constexpr (cc + 1 == NCH && grp == G0) stage_tile(tl + 1 < ntl ? tl + 1 : tl);
-            constexpr int per = (XPT + NGL - 1) / NGL;
             gload(cc + 1 == NCH ? 0 : cc + 1, (grp - G0) * per, (grp - G0 + 1) * per < XPT ? (grp - G0 + 1) * per : XPT);
           }
           // weight fragment n feeds its four MFMAs, then its register takes the
-          // next group's fragment n (one fragment set plus the pixel fragments
-          // of two groups live, not two full sets)
+          // next group's fragment n
 #pragma unroll
           for (int n = 0; n < NF; ++n) {
 #pragma unroll
@@ -419,41 +497,23 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
               // a tile's first MFMA of an accumulator takes C = 0; its last one
               // is followed by the packing of the finished value
               const f4 cin = (cst == 0 && grp == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[fm][n];
-              acc[fm][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  __builtin_bit_cast(bf8, xf[fm]), __builtin_bit_cast(bf8, wf[n / FN][n % FN]), cin, 0, 0, 0);
+              const bf8 xa = __builtin_bit_cast(bf8, xf[fm]), wa = __builtin_bit_cast(bf8, wf[n / FN][n % FN]);
+              if constexpr (PM == 1) acc[fm][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wa, cin, 0, 0, 0);
+              else acc[fm][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xa, cin, 0, 0, 0);
               if constexpr (cst == NS - 1 && grp == 5) pack1(fm, n);
             }
             if constexpr (grp + 1 < 6)
-              wn[n / FN][n % FN] = *reinterpret_cast<const uint4*>(Wl + (gk * 3 + gs) * KB * 64 + wrb[n / FN][n % FN]);
+              wn[n / FN][n % FN] = *reinterpret_cast<const uint4*>(Wl + wfrag_off(gs, gk, n / FN, n % FN));
           }
-          // the previous tile's epilogue: part (h, fm2) in steps 0..3 (done
-          // before the next chunk's rows are staged in registers at step 2),
-          // the statistics of half 0 in step 2, of half 1 in step 4
-          // part p = cst (h = p >> 1, fm2 = 2 (p & 1)) over groups 0..4 of
-          // steps 0..3, the statistics of half h in group 5 of steps 1 / 3
-          if constexpr (cst <= 3 && !P1W_NOEPI) {
-            if constexpr (grp < 4) epi_unit(cst >> 1, (cst & 1) * 2, grp >> 1, grp & 1, ptm, live);
-            if constexpr (grp == 4) epi_store(cst >> 1, (cst & 1) * 2, ptm, live);
-            if constexpr (grp == 5 && (cst & 1)) epi_stats(cst >> 1);
-          }
+          if constexpr (cst <= 3) epi_slot(std::integral_constant<int, cst>{}, std::integral_constant<int, grp>{}, ptm,
+                                           live);
         };
         if constexpr ((grp & 1) == 0) body(wfa, xfa, wfb, xfb);
         else body(wfb, xfb, wfa, xfa);
-        if constexpr (P1W_SGB > 0) {
-          // issue pattern per MFMA: the MFMA, a fragment read while any are
-          // left, then up to P1W_SGB VALU and one SALU
-#pragma unroll
-          for (int i = 0; i < 32; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            if (i < 12) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, P1W_SGB, 0);
-            __builtin_amdgcn_sched_group_barrier(0x004, 1, 0);
-          }
-        }
         __builtin_amdgcn_sched_barrier(0);
       });
       stamp(0);
-      if constexpr (rs == 2 && !P1W_NORESTAGE) {
+      if constexpr (rs == 2) {
         __syncthreads();  // every wave has finished reading the chunk's rows
         stamp(3);
         sstore();
@@ -472,7 +532,7 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
 
   if (ntl > 0) {
     stage_tile(0);
-    gload(0);
+    gload(0, 0, XPT);
     wprep(0, 0);
 #pragma unroll
     for (int j = 0; j < WPW; ++j) wpiece(j);
@@ -487,19 +547,28 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   // the last tile's epilogue (packed by its last step)
   if (ntl > 0) {
     const int tm = walk.tm + (ntl - 1) * walk.step;
+    if constexpr (PM == 1) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      epi_part(p >> 1, (p & 1) * 2, tm, true);
-      if (p & 1) epi_stats(p >> 1);
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) epi_unit(p >> 1, (p & 1) * 2, u >> 1, u & 1, tm, true);
+        epi_store(p >> 1, (p & 1) * 2, tm, true);
+        if (p & 1) epi_stats(p >> 1);
+      }
+    } else {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) dx_unit(fm, h, tm, true);
     }
   }
 #ifdef ACFE_P1W_STAMPS
-  if (lane == 0 && blockIdx.x * 4 + wp < 4096)
+  if (PM == 1 && lane == 0 && blockIdx.x * 4 + wp < 4096)
     for (int i = 0; i < 6; ++i) g_p1w_stamps[(blockIdx.x * 4 + wp) * 8 + i] = stv[i];
 #endif
   wait_vmcnt<0>();
   __syncthreads();
-  if (stats) {
+  if (PM == 1 && stats) {
     // fixed-order sum of the four waves' partials (same slots in the same lanes)
     double* red = reinterpret_cast<double*>(smem);
 #pragma unroll
@@ -525,23 +594,44 @@ k_conv3x3_pool1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
 
 namespace acfe {
 
+static void grid_1w(const ConvGeom& g, double* stats, int srows, int* tiles_h, int* tiles_w, long long* nt, int* gp) {
+  *tiles_h = (g.P + 3) / 4;
+  *tiles_w = (g.Q + 63) / 64;
+  *nt = (long long)g.N * *tiles_h * *tiles_w;
+  int n = 256;
+  if (n > *nt) n = (int)*nt;
+  if (n >= 64) n &= ~7;
+  if (stats && n > srows) n = srows;  // one statistics slab row per workgroup
+  *gp = n;
+}
+
 int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                   int srows, uint8_t* amax, hipStream_t s, const char* what) {
   if (g.K != 128 || g.C != 128 || (long long)g.N * (g.P / 2) * (g.Q / 2) * g.ldy * 2 >= (1ll << 31))
     return ACFE_E_INVAL;
   if ((uintptr_t)y & 15) return ACFE_E_INVAL;
-  const int tiles_h = (g.P + 3) / 4, tiles_w = (g.Q + 63) / 64;
-  const long long nt = (long long)g.N * tiles_h * tiles_w;
-  int gp = 256;
-  if (gp > nt) gp = (int)nt;
-  if (gp >= 64) gp &= ~7;
-  if (stats && gp > srows) gp = srows;
+  int th, tw, gp;
+  long long nt;
+  grid_1w(g, stats, srows, &th, &tw, &nt, &gp);
   if (g.drop.on)
-    hipLaunchKernelGGL((k_conv3x3_pool1w<2, true>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,
-                       (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
+    hipLaunchKernelGGL((k_conv3x3_1w<1, 2, true>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,
+                       (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows, amax);
   else
-    hipLaunchKernelGGL((k_conv3x3_pool1w<2, false>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,
-                       (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows, amax);
+    hipLaunchKernelGGL((k_conv3x3_1w<1, 2, false>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,
+                       (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows, amax);
+  return launch_rc(what);
+}
+
+int launch_unpool1w(const ConvGeom& g, const void* dyp, const void* wflip, void* dx, uint8_t* amax, hipStream_t s,
+                    const char* what) {
+  // dX of one image < 2^31 bytes (per-image buffer stores), 16-B channel runs
+  if (g.K != 128 || g.C != 128 || (long long)g.P * g.Q * g.ldy * 2 >= (1ll << 31) || ((uintptr_t)dx & 15))
+    return ACFE_E_INVAL;
+  int th, tw, gp;
+  long long nt;
+  grid_1w(g, nullptr, 0, &th, &tw, &nt, &gp);
+  hipLaunchKernelGGL((k_conv3x3_1w<2, 2, false>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)dyp,
+                     (const uint16_t*)wflip, nullptr, (uint16_t*)dx, nullptr, th, tw, (int)nt, 0, amax);
   return launch_rc(what);
 }
 

@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=$1; OLD=${2:-old}; ONLY=${3:-pool}
 O=gpurun_out/$TAG; mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu \
-  "tests/test_fused_gpu.py::test_conv_pool_kernels" tests/test_production_gpu.py -k "pool or partial" > $O/tests.log 2>&1
+  "tests/test_fused_gpu.py::test_conv_pool_kernels" tests/test_production_gpu.py -k "pool or partial or unpool" > $O/tests.log 2>&1
 rc=$?; tail -5 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for L in base $OLD; do
