@@ -308,7 +308,7 @@ def main():
             "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
         },
         "roofline": {
-            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_pool1w<2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)",
+            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_1w<1,2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)",
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,

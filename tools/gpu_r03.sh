@@ -22,8 +22,9 @@ for s in "$@"; do
            tests/test_production_gpu.py::test_strided_dgrad_wr_resnet_production tests/test_e2e_gpu.py \
            "tests/test_model_gpu.py::test_block_bf16_train_fixed_bounds" ;;
     model) step model 900 $PYT -m gpu tests/test_model_gpu.py tests/test_e2e_gpu.py tests/test_dp_gpu.py tests/test_frontend_gpu.py ;;
-    pmcp) step pmcp 400 bash tools/pmc_pool.sh r03 'k_conv3x3_pool1w' ;;
-    sqp) step sqp 400 bash -c "bash tools/pmc_sq.sh ${TAG}_p1w 'k_conv3x3_pool1w' && python tools/sq_json.py gpurun_out/pmc_${TAG}_p1w k_conv3x3_pool1w r03" ;;
+    pmcp) step pmcp 400 bash tools/pmc_pool.sh r03 'k_conv3x3_1w<1' ;;
+    sqp) step sqp 400 bash -c "bash tools/pmc_sq.sh ${TAG}_p1w 'k_conv3x3_1w' && python tools/sq_json.py gpurun_out/pmc_${TAG}_p1w 'k_conv3x3_1w<1' r03 && python tools/sq_summary.py gpurun_out/pmc_${TAG}_p1w 'k_conv3x3_1w<2'" ;;
+    sqmelr) step sqmelr 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w2' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w2" ;;
     stamps) step stamps 200 python tools/pool1w_stamps.py ;;
     sqmel) step sqmel 400 bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w2' ;;
     sq64) step sq64 400 bash tools/pmc_sq.sh ${TAG}_r64 'k_conv3x3_rows<64, 8, [034], true, true>|k_wgrad3x3_halo<64, false' ;;

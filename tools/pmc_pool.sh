@@ -1,13 +1,13 @@
 #!/bin/bash
 # HBM traffic (rocprofv3 --pmc, one counter group per pass, kernel-filtered) of
 # the bench's dominant kernel: the stage-1 block-0 3x3 128->128 conv forward with
-# the 2x2 max-pool epilogue (k_conv3x3_pool1w<2, true>: one wave per SIMD,
+# the 2x2 max-pool epilogue (k_conv3x3_1w<1, 2, true>: one wave per SIMD,
 # chunk-resident 4-row tiles), inside the T1 bench.  Then tools/pmc_traffic.py folds the passes into
 # profiles/pmc_dominant_<tag>.json.
 # usage: tools/pmc_pool.sh [tag] [kernel regex]
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-r02}
-RX=${2:-k_conv3x3_pool1w}
+RX=${2:-k_conv3x3_1w<1}
 O=gpurun_out/pmc_pool
 mkdir -p $O
 i=0

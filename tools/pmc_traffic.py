@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KERNEL = os.environ.get("KNAME", "k_conv3x3_pool1w")
+KERNEL = os.environ.get("KNAME", "k_conv3x3_1w<1")
 
 
 def per_dispatch(d):
@@ -46,7 +46,7 @@ def main():
     B, H, W, C, K = 512, 128, 256, 128, 128
     if pool:  # input + pooled output + 1-byte argmax per pooled output (weights negligible)
         algo = B * H * W * C * 2 + B * (H // 2) * (W // 2) * K * 3 + K * 9 * C * 2
-        kern = (os.environ.get("KLABEL", "k_conv3x3_pool1w<2, true>") +
+        kern = (os.environ.get("KLABEL", "k_conv3x3_1w<1, 2, true>") +
                 " (s1b0 conv21 3x3 128->128 @128x256 + 2x2 max-pool/dropout/BN-sums epilogue, batch 512)")
         src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes inside bench.py (tools/pmc_pool.sh)"
     else:
