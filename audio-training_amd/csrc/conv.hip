@@ -598,20 +598,6 @@ struct Stamps {
 __device__ uint2 g_store_sink[64];  // never read: target of masked-off epilogue stores
 __device__ u32x4 g_store_sink16[64];  // the same for 16-B stores
 
-// One step of a 16-lane butterfly reduce-scatter: lanes whose `BIT` is set keep
-// the upper half of v[0..CNT), the others the lower half, each adding the
-// partner's copy of the half it keeps (partner = DPP pattern CTRL).
-template <int CNT, int BIT, int CTRL, int NV>
-__device__ __forceinline__ void butterfly_step(float (&v)[NV], int lane) {
-  const bool up = (lane & BIT) != 0;
-#pragma unroll
-  for (int k = 0; k < CNT / 2; ++k) {
-    const float send = up ? v[k] : v[k + CNT / 2];
-    const float keep = up ? v[k + CNT / 2] : v[k];
-    const float got = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), CTRL, 0xF, 0xF, false));
-    v[k] = keep + got;
-  }
-}  // never read: target of masked-off epilogue stores
 
 template <int BN>
 __global__ void __launch_bounds__(512, 1)
@@ -3141,6 +3127,14 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
         // workgroups than the caller's slab rows (narrow images have more
         // tiles than 128-pixel slab rows)
         if (stats && gp > grid_m) gp = grid_m;
+#ifndef ACFE_POOL1W
+#define ACFE_POOL1W 1
+#endif
+        if constexpr (BN == 128 && ACFE_POOL1W) {
+          // one wave per SIMD (pool1w.hip), the previous tile's epilogue beside this tile's MFMAs
+          const int rc = launch_plain1w(g, x, wp, bias, y, stats, grid_m, s, "acfe_conv2d_fwd", 0);
+          if (rc != ACFE_E_INVAL) return rc;
+        }
 #define ROWS(TR_, PM_, ...)                                                                                   \
   hipLaunchKernelGGL((k_conv3x3_rows<BN, TR_, PM_, ##__VA_ARGS__>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x, \
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m, nullptr)
@@ -3723,6 +3717,10 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
     }
     if constexpr (PM == 2 && ACFE_POOL1W) {
       const int rc = launch_unpool1w(g, x, wp, y, amax, s, what);
+      if (rc != ACFE_E_INVAL) return rc;
+    }
+    if constexpr (PM == 3 && ACFE_POOL1W) {
+      const int rc = launch_plain1w(g, x, wp, bias, y, stats, srows, s, what, 3);
       if (rc != ACFE_E_INVAL) return rc;
     }
     return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);

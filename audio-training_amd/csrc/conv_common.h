@@ -100,6 +100,21 @@ __device__ __forceinline__ u32x4 unpool_mask(uint2 a, unsigned pos) {
   return m;
 }
 
+// One step of a 16-lane butterfly reduce-scatter: lanes whose `BIT` is set keep
+// the upper half of v[0..CNT), the others the lower half, each adding the
+// partner's copy of the half it keeps (partner = DPP pattern CTRL).
+template <int CNT, int BIT, int CTRL, int NV>
+__device__ __forceinline__ void butterfly_step(float (&v)[NV], int lane) {
+  const bool up = (lane & BIT) != 0;
+#pragma unroll
+  for (int k = 0; k < CNT / 2; ++k) {
+    const float send = up ? v[k] : v[k + CNT / 2];
+    const float keep = up ? v[k + CNT / 2] : v[k];
+    const float got = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), CTRL, 0xF, 0xF, false));
+    v[k] = keep + got;
+  }
+}
+
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
@@ -112,6 +127,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 // (pool1w.hip); returns ACFE_E_INVAL when the shape is not its case
 int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                   int srows, uint8_t* amax, hipStream_t s, const char* what);
+// 3x3 stride-1 forward / dgrad at K = C = 128 (plain, + dropout, + BN sums) on the same kernel (PM 0)
+// (pm 0: plain / dropout / BN sums; pm 3: + the residual g.res (+ReLU) of acfe_conv2d_fwd_add)
+int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+                   int srows, hipStream_t s, const char* what, int pm);
 // acfe_conv2d_dgrad_unpool at K = C = 128 on the same kernel (PM 2)
 int launch_unpool1w(const ConvGeom& g, const void* dyp, const void* wflip, void* dx, uint8_t* amax, hipStream_t s,
                     const char* what);

@@ -758,7 +758,7 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   if (batch == 0) return ACFE_OK;
   const int T = acfe_plan_num_frames(p, n, pad_mode);
   if (p->n_fft == 4096) {
-    constexpr int fpw = 4;  // frames per workgroup (2: 1.51 ms, 8: equal, r01n/r02y)
+    constexpr int fpw = 4;  // frames per workgroup (2: 1.51 ms, 8: equal, r01n/r02y; r03: 2 / 8 / 16 +3 / 0 / +2 %)
     const int nk = p->kmax - p->kmin + 1;
     const size_t shm2 = sizeof(float2) * (2048 + 2048 / 16) + (nk <= 1024 ? 0 : sizeof(float) * (nk + 8));
     hipLaunchKernelGGL(k_mel_w2, dim3(cdiv(T, fpw), batch), dim3(128), shm2, strm(stream), raw, cs, n, stats,

@@ -1,18 +1,22 @@
-// k_conv3x3_1w: the two dominant convolutions of the T1 step -- the pooled
-// forward of acfe_conv2d_fwd_pool and the unpooling dgrad of
-// acfe_conv2d_dgrad_unpool at K = C = 128 -- with one wave per SIMD (built
-// with -fno-slp-vectorize: packed f32 VALU beside MFMAs costs more issue time
-// than the two scalar ops).
+// k_conv3x3_1w: the 3x3 stride-1 convolutions at K = C = 128 -- the two
+// dominant ones of the T1 step (the pooled forward of acfe_conv2d_fwd_pool,
+// the unpooling dgrad of acfe_conv2d_dgrad_unpool) and the plain / dropout /
+// residual-add forwards and stride-1 dgrads (wr_resnet's 128-channel stages)
+// -- with one wave per SIMD (built with -fno-slp-vectorize: packed f32 VALU
+// beside MFMAs costs more issue time than the two scalar ops).
 #include "conv_common.h"
 
 using namespace acfe;
 
 // ------------------------------------------------------------------ 3x3 conv, one wave per SIMD
-// k_conv3x3_1w<PM, NCH, DROP>, K = 128 output channels, C = 64 NCH input
+// k_conv3x3_1w<PM, NCH, DROP, ST>, K = 128 output channels, C = 64 NCH input
 // channels (NCH even).  PM 1: acfe_conv2d_fwd_pool (stage-1 block-0 branch21
 // 128 -> 128 @ 128 x 256 -> MaxPool2D(2) -> Dropout -> BN,
 // resnet/wr_resnet_bird.py:136-147); PM 2: its dgrad from the pooled gradient
-// and the argmax bytes (the 2x2 max-pool backward expanded while staging).
+// and the argmax bytes (the 2x2 max-pool backward expanded while staging);
+// PM 0: acfe_conv2d_fwd / fwd_dropout / stride-1 dgrad (bias, optional pair-
+// hash Dropout, optional BN sums ST); PM 3: acfe_conv2d_fwd_add (+ the
+// residual, +ReLU, BN sums of the sum; resnet/wr_resnet.py:46-90).
 //
 // Same tile, LDS images and weight pieces as k_conv3x3_rows<128, 4, PM, true>
 // (4 rows x 64 px x 128 channels, chunk-resident halo rows: a step is one
@@ -36,20 +40,24 @@ using namespace acfe;
 //    after them, so the step's closing vmcnt wait leaves the halo loads and
 //    epilogue stores in flight.
 //  * MFMA operand order: PM 1 pixels x weights (a lane's four accumulators
-//    are one 2x2 window of one channel), PM 2 weights x pixels (a lane holds
-//    16 consecutive channels of a pixel per channel half: 16-B stores).
+//    are one 2x2 window of one channel), PM 0 / 2 / 3 weights x pixels (a
+//    lane holds 16 consecutive channels of a pixel per channel half: 16-B
+//    stores; the BN sums are reduced over the 16 pixel lanes by a DPP
+//    butterfly once per half and tile).
 #ifdef ACFE_P1W_STAMPS
 // diagnostic build (make stamps): per-wave s_memtime totals of the step
 // segments, read back by acfe_debug_pool1w_stamps (tools/pool1w_stamps.py)
 __device__ unsigned long long g_p1w_stamps[4096 * 8];
 #endif
-template <int PM, int NCH, bool DROP>
+template <int PM, int NCH, bool DROP, bool ST = true>
 __global__ void __launch_bounds__(256, 1)
 k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
              int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
   static_assert(NCH % 2 == 0, "even step count per tile: weight buffer parity is static");
-  static_assert(PM == 1 || (PM == 2 && !DROP), "modes");
+  static_assert(PM == 0 || PM == 1 || ((PM == 2 || PM == 3) && !DROP), "modes");
+  constexpr bool CPERM = PM != 1;     // weights x pixels operand order (PM 0 / 2 / 3)
+  constexpr bool DENSE = PM == 0 || PM == 3;  // full-resolution output with bias (PM 3: + residual)
   constexpr int KB = 128, TR = 4, FM = 4, FN = 4, NH = 2, NF = NH * FN, SEGW = 64, HWX = SEGW + 2, XRB = 160;
   constexpr int NT = 256, NS = 3 * NCH;                          // threads, steps per tile
   constexpr int XROWS = TR + 2, XBYTES = XROWS * HWX * XRB;      // 63 360 B
@@ -57,7 +65,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   constexpr int XG = XROWS * HWX * 8, XPT = (XG + NT - 1) / NT;  // 16-B input granules
   constexpr int WPW = 3 * KB * 8 / 64 / (NT / 64);               // 12 weight pieces per wave per step
   constexpr int WPG = 4;                                         // pieces per MFMA group (groups 0..2)
-  constexpr int SMEM = XBYTES + 2 * WBYTES;
+  constexpr int SMEM = XBYTES + 2 * WBYTES + (DENSE ? KB * 4 : 0);  // (PM 0 / 3: bias table)
   static_assert(SMEM <= 163840, "LDS");
   static_assert(XPT * NT - XG <= 2 * XROWS * HWX, "spare granules fit the pixel pads");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
@@ -86,11 +94,15 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     wb = rem - hb * tiles_w;
   };
 
-  // bias of the lane's channels h * 64 + 4 l16 + [0, 4) (PM 1)
+  // bias of the lane's channels h * 64 + 4 l16 + [0, 4) (PM 1); PM 0: a 128-entry
+  // LDS table (a lane's accumulators there are 4 channels each)
   f4 bch[NH];
 #pragma unroll
   for (int h = 0; h < NH; ++h)
     bch[h] = (PM == 1 && bias) ? *reinterpret_cast<const f4*>(bias + h * 64 + 4 * l16) : f4{0.f, 0.f, 0.f, 0.f};
+  float* btab = reinterpret_cast<float*>(smem + XBYTES + 2 * WBYTES);
+  if constexpr (DENSE)
+    if (tid < KB) btab[tid] = bias ? bias[tid] : 0.f;
 
   // ---- weight pieces (LDS-DMA, 1 KB each, 48 per step).  The lane part of a
   // piece's source offset is one of two VGPRs per wave, the rest a uniform
@@ -104,7 +116,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   //   = 8 rows 32 wp + 8 b .., whose (k >> 4) & 3 = (2 wp + (b >> 1)) & 3.
   unsigned vw[2];
   int sob;
-  if constexpr (PM == 1) {
+  if constexpr (!CPERM) {
     const int l4 = lane >> 2;
     vw[0] = vw[1] = (unsigned)((l4 ^ ((l4 >> 2) & 3)) * g.Kdp * 2) +
                     ((((unsigned)lane & 3u) ^ ((wp & 1) ? 2u : 0u)) << 4);
@@ -132,7 +144,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     int sb_ = sob;
     asm volatile("" : "+s"(sb_));  // formed here, not hoisted into a dozen live registers
     unsigned so, lb, vo;
-    if constexpr (PM == 1) {  // j = 2 (kk * 3 + s) + b
+    if constexpr (!CPERM) {  // j = 2 (kk * 3 + s) + b
       const int ks = j >> 1, b = j & 1, kk = ks / 3, s_ = ks - kk * 3;
       so = (unsigned)(sb_ + s_ * g.C * 2 + kk * 64 + b * 16 * g.Kdp * 2);
       lb = wlb + (ks * 128 + 2 * wp * 16 + b * 16) * 64;
@@ -163,7 +175,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   int rel[XPT];
   int tbase = 0;
   unsigned cmask = 0, pos0 = 0, pos1 = 0;
-  if constexpr (PM == 1) {
+  if constexpr (PM != 2) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + NT * i;
@@ -179,7 +191,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     int t0 = tid;
     asm volatile("" : "+v"(t0));  // (per tile, not hoisted)
     cmask = 0;
-    if constexpr (PM == 1) {
+    if constexpr (PM != 2) {
       tbase = (sh0 * g.W + sw0) * CB;
       xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (long long)n * g.H * g.W * g.C), (short)0,
                                               g.H * g.W * CB, 0x00020000);
@@ -215,7 +227,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
       const bool ok = (cmask >> i) & 1u;
-      if constexpr (PM == 1) {
+      if constexpr (PM != 2) {
         rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? (unsigned)(tbase + cc * 128 + rel[i]) : 0x80000000u,
                                                       0, 0);
       } else {
@@ -247,7 +259,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   int wrb[2][NH][FN];  // [kk] (PM 1: both equal)
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm) {
-    if constexpr (PM == 1) {
+    if constexpr (!CPERM) {
       // A rows 4 q' + j = window q' of fragment fm (row pair fm / 2, pooled
       // column wp * 8 + (fm & 1) * 4 + (q' ^ (q' >> 1))), pixel j
       const int qq = l16 >> 2, j = l16 & 3;
@@ -262,7 +274,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      if constexpr (PM == 1) {
+      if constexpr (!CPERM) {
         const int k = h * 64 + FN * l16 + fn;
         wrb[0][h][fn] = wrb[1][h][fn] = (k ^ ((k >> 2) & 3)) * 64 + ((q ^ ((l16 >> 2) & 2)) << 4);
       } else {
@@ -275,7 +287,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     }
   // weight fragment of group (s, kk) relative to the buffer base
   auto wfrag_off = [&](int s, int kk, int h, int fn) __attribute__((always_inline)) {
-    return PM == 1 ? (kk * 3 + s) * KB * 64 + wrb[0][h][fn] : s * KB * 128 + wrb[kk][h][fn];
+    return !CPERM ? (kk * 3 + s) * KB * 64 + wrb[0][h][fn] : s * KB * 128 + wrb[kk][h][fn];
   };
 
   f4 acc[FM][NF];
@@ -292,9 +304,15 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 #pragma unroll
     for (int j = 0; j < NF; ++j) prev[i][j] = u32x2{0u, 0u};
   auto pack1 = [&](int fm, int n) __attribute__((always_inline)) {
-    const float b = bch[n / FN][n % FN];
-    const b2v lo = __builtin_convertvector((f2v){acc[fm][n][0] + b, acc[fm][n][1] + b}, b2v);
-    const b2v hi = __builtin_convertvector((f2v){acc[fm][n][2] + b, acc[fm][n][3] + b}, b2v);
+    f4 b4;
+    if constexpr (DENSE) {  // channels h * 64 + 16 q + 4 fn + j
+      b4 = *reinterpret_cast<const f4*>(btab + (n / FN) * 64 + 16 * q + 4 * (n % FN));
+    } else {
+      const float b = bch[n / FN][n % FN];
+      b4 = f4{b, b, b, b};
+    }
+    const b2v lo = __builtin_convertvector((f2v){acc[fm][n][0] + b4[0], acc[fm][n][1] + b4[1]}, b2v);
+    const b2v hi = __builtin_convertvector((f2v){acc[fm][n][2] + b4[2], acc[fm][n][3] + b4[3]}, b2v);
     prev[fm][n] = u32x2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
   };
 
@@ -422,6 +440,90 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{p0[0], p0[1], p1[0], p1[1]}, dr, inb ? o : 0x80000000u, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{p2[0], p2[1], p3[0], p3[1]}, dr, inb ? o + 16u : 0x80000000u, 0, 0);
   };
+  // ---- PM 0 epilogue: unit (fm, h) = the 16 consecutive channels
+  // c0 = h * 64 + 16 q .. of pixel (tile row wp, column fm * 16 + l16):
+  // dropout (one pair hash per channel pair, acfe_dropout's mask), the BN sums
+  // of the stored values (ds[16] / dq[16] of the half in progress, reduced over
+  // the 16 pixel lanes by a DPP butterfly after its last unit), two 16-B stores
+  // into the image's output (per-image buffer, < 2^31 bytes: launcher)
+  float ds[16], dq[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ds[i] = dq[i] = 0.f;
+  // PM 3: the residual words of the step's two units, loaded in its group 0
+  u32x4 rres[2][2];
+  auto res_load = [&](int u, int fm, int h, int tm, bool live) __attribute__((always_inline)) {
+    int n, hb, wb;
+    tile_of(tm, n, hb, wb);
+    const int hh = hb * TR + wp, ww = wb * SEGW + fm * 16 + l16;
+    const bool inb = live && hh < g.P && ww < g.Q;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(g.res + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
+    const unsigned o = ((unsigned)(hh * g.Q + ww) * (unsigned)g.ldy + h * 64 + 16 * q) * 2u;
+    rres[u][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, inb ? o : 0x80000000u, 0, 0);
+    rres[u][1] = __builtin_amdgcn_raw_buffer_load_b128(rr, inb ? o + 16u : 0x80000000u, 0, 0);
+  };
+  auto dense_unit = [&](int fm, int h, int tm, bool live, int u = 0) __attribute__((always_inline)) {
+    int n, hb, wb;
+    tile_of(tm, n, hb, wb);
+    const int hh = hb * TR + wp, ww = wb * SEGW + fm * 16 + l16;
+    const bool inb = live && hh < g.P && ww < g.Q;
+    const int c0 = h * 64 + 16 * q;
+    unsigned w8[8];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) w8[2 * fn] = prev[fm][h * FN + fn][0], w8[2 * fn + 1] = prev[fm][h * FN + fn][1];
+    if constexpr (PM == 3) {
+      // z = (ReLU)(conv + residual), rounded to bf16 (ops.add's values)
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) {
+        const unsigned rw = rres[u][pr >> 2][pr & 3];
+        float lo = __uint_as_float(w8[pr] << 16) + __uint_as_float(rw << 16);
+        float hi = __uint_as_float(w8[pr] & 0xffff0000u) + __uint_as_float(rw & 0xffff0000u);
+        if (g.res_relu) lo = fmaxf(lo, 0.f), hi = fmaxf(hi, 0.f);
+        const b2v pk = __builtin_convertvector((f2v){lo, hi}, b2v);
+        w8[pr] = __builtin_bit_cast(unsigned, pk);
+      }
+    }
+    if constexpr (DROP || ST) {
+      const unsigned pix = ((unsigned)n * g.P + hh) * g.Q + ww;  // (M * K < 2^32: launcher)
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) {
+        float lo = __uint_as_float(w8[pr] << 16), hi = __uint_as_float(w8[pr] & 0xffff0000u);
+        if constexpr (DROP) {
+          const uint32_t hsh = drop_pair_hash32(g.drop, pix * (unsigned)KB + c0 + 2 * pr);
+          lo = (hsh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(lo * g.drop.scl)) : 0.f;
+          hi = (hsh >> 16) >= g.drop.thr ? bf2f(f2bf(hi * g.drop.scl)) : 0.f;
+          w8[pr] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+        }
+        if constexpr (ST) {
+          const float fl = inb ? lo : 0.f, fh = inb ? hi : 0.f;
+          ds[2 * pr] += fl;
+          dq[2 * pr] += fl * fl;
+          ds[2 * pr + 1] += fh;
+          dq[2 * pr + 1] += fh * fh;
+        }
+      }
+    }
+    const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Y + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
+    const unsigned o = ((unsigned)(hh * g.Q + ww) * (unsigned)g.ldy + c0) * 2u;
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{w8[0], w8[1], w8[2], w8[3]}, orr, inb ? o : 0x80000000u, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{w8[4], w8[5], w8[6], w8[7]}, orr, inb ? o + 16u : 0x80000000u, 0, 0);
+  };
+  // half h's sums: reduce-scatter over the 16 pixel lanes of each lane group
+  // (lane l16 keeps values b0 + k, k < 2, of [ds[0..16), dq[0..16)])
+  auto dense_stats = [&](int h) __attribute__((always_inline)) {
+    if constexpr (ST) {
+      float sv[32];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sv[i] = ds[i], sv[16 + i] = dq[i], ds[i] = dq[i] = 0.f;
+      butterfly_step<32, 8, 0x128>(sv, lane);
+      butterfly_step<16, 4, 0x141>(sv, lane);
+      butterfly_step<8, 2, 0x4E>(sv, lane);
+      butterfly_step<4, 1, 0xB1>(sv, lane);
+      dstat[h][0] += (double)sv[0];
+      dstat[h][1] += (double)sv[1];
+    }
+  };
   // epilogue work in step cst (0..3), MFMA group grp; returns the number of
   // vector-memory stores it issues (for the step's closing wait)
   constexpr int EPI_STORES = PM == 1 ? 2 : 4;  // per step 0..3
@@ -433,9 +535,20 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       if constexpr (grp < 4) epi_unit(cst >> 1, (cst & 1) * 2, grp >> 1, grp & 1, ptm, live);
       if constexpr (grp == 4) epi_store(cst >> 1, (cst & 1) * 2, ptm, live);
       if constexpr (grp == 5 && (cst & 1)) epi_stats(cst >> 1);
-    } else {
+    } else if constexpr (PM == 2) {
       // units (fm = cst, h = 0 / 1) in groups 1 / 3
       if constexpr (grp == 1 || grp == 3) dx_unit(cst, grp >> 1, ptm, live);
+    } else {
+      // units (fm, h) with h = cst >> 1, fm = 2 (cst & 1) + (grp == 3) in
+      // groups 1 / 3 (PM 3: their residual loads in group 0); half h's
+      // statistics in group 5 of steps 1 / 3
+      if constexpr (PM == 3 && grp == 0) {
+        res_load(0, 2 * (cst & 1), cst >> 1, ptm, live);
+        res_load(1, 2 * (cst & 1) + 1, cst >> 1, ptm, live);
+      }
+      if constexpr (grp == 1 || grp == 3)
+        dense_unit(2 * (cst & 1) + (grp == 3 ? 1 : 0), cst >> 1, ptm, live, grp == 3 ? 1 : 0);
+      if constexpr (grp == 5 && (cst & 1)) dense_stats(cst >> 1);
     }
   };
 
@@ -498,7 +611,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
               // is followed by the packing of the finished value
               const f4 cin = (cst == 0 && grp == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[fm][n];
               const bf8 xa = __builtin_bit_cast(bf8, xf[fm]), wa = __builtin_bit_cast(bf8, wf[n / FN][n % FN]);
-              if constexpr (PM == 1) acc[fm][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wa, cin, 0, 0, 0);
+              if constexpr (!CPERM) acc[fm][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wa, cin, 0, 0, 0);
               else acc[fm][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xa, cin, 0, 0, 0);
               if constexpr (cst == NS - 1 && grp == 5) pack1(fm, n);
             }
@@ -555,11 +668,21 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         epi_store(p >> 1, (p & 1) * 2, tm, true);
         if (p & 1) epi_stats(p >> 1);
       }
-    } else {
+    } else if constexpr (PM == 2) {
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int h = 0; h < NH; ++h) dx_unit(fm, h, tm, true);
+    } else {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          if constexpr (PM == 3) res_load(0, fm, h, tm, true);
+          dense_unit(fm, h, tm, true, 0);
+        }
+        dense_stats(h);
+      }
     }
   }
 #ifdef ACFE_P1W_STAMPS
@@ -568,7 +691,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 #endif
   wait_vmcnt<0>();
   __syncthreads();
-  if (PM == 1 && stats) {
+  if ((PM == 1 || (DENSE && ST)) && stats) {
     // fixed-order sum of the four waves' partials (same slots in the same lanes)
     double* red = reinterpret_cast<double*>(smem);
 #pragma unroll
@@ -583,8 +706,13 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         double v = 0.0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) v += red[((w * 64 + lane) * NH + h) * 2 + k];
-        const int idx = q * 2 + k;
-        stats[((long long)blockIdx.x * 2 + idx / FN) * g.Kp + h * 64 + FN * l16 + idx % FN] = v;
+        if constexpr (PM == 1) {
+          const int idx = q * 2 + k;
+          stats[((long long)blockIdx.x * 2 + idx / FN) * g.Kp + h * 64 + FN * l16 + idx % FN] = v;
+        } else {
+          const int idx = ((l16 >> 3) & 1) * 16 + ((l16 >> 2) & 1) * 8 + ((l16 >> 1) & 1) * 4 + (l16 & 1) * 2 + k;
+          stats[((long long)blockIdx.x * 2 + idx / 16) * g.Kp + h * 64 + 16 * q + idx % 16] = v;
+        }
       }
     }
     for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
@@ -619,6 +747,34 @@ int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float*
   else
     hipLaunchKernelGGL((k_conv3x3_1w<1, 2, false>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,
                        (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows, amax);
+  return launch_rc(what);
+}
+
+int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+                   int srows, hipStream_t s, const char* what, int pm) {
+  // 3x3 stride 1, K = C = 128, one image's output < 2^31 bytes, 32-bit
+  // dropout element indices, 16-B channel runs
+  if (g.K != 128 || g.C != 128 || g.R != 3 || g.S != 3 || g.st != 1 || g.ldy != 128 ||
+      (long long)g.P * g.Q * g.ldy * 2 >= (1ll << 31) || (g.drop.on && !g.idx32) || ((uintptr_t)y & 15))
+    return ACFE_E_INVAL;
+  int th, tw, gp;
+  long long nt;
+  grid_1w(g, stats, srows, &th, &tw, &nt, &gp);
+#define P1W_L(PM_, D, S_)                                                                                     \
+  hipLaunchKernelGGL((k_conv3x3_1w<PM_, 2, D, S_>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,        \
+                     (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows, nullptr)
+  if (pm == 3) {
+    if (!g.res || g.drop.on) return ACFE_E_INVAL;
+    if (stats) P1W_L(3, false, true);
+    else P1W_L(3, false, false);
+  } else if (g.drop.on) {
+    P1W_L(0, true, true);
+  } else if (stats) {
+    P1W_L(0, false, true);
+  } else {
+    P1W_L(0, false, false);
+  }
+#undef P1W_L
   return launch_rc(what);
 }
 

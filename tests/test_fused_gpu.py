@@ -52,9 +52,12 @@ def _dropout(env, t, rate, seed):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32], ids=["bf16", "f32"])
-@pytest.mark.parametrize("K,C", [(128, 64), (64, 64), (32, 64), (64, 16)], ids=["128", "64", "32", "64c16"])
+@pytest.mark.parametrize("K,C", [(128, 64), (64, 64), (32, 64), (64, 16), (128, 128)],
+                         ids=["128", "64", "32", "64c16", "128c128"])
 def test_conv_fwd_dropout(env, cuda, dtype, K, C):
-    """(C = 16, K = 64 bf16: k_conv3x3_c16, the tap-major 16-channel kernel)"""
+    """(C = 16, K = 64 bf16: k_conv3x3_c16, the tap-major 16-channel kernel;
+    K = C = 128 bf16: the one-wave k_conv3x3_1w<0> with the dropout and BN sums
+    between the next tile's MFMA groups, H = 12: a partial last row tile)"""
     ops, call, lib, ptr, stream = env
     N, H, W, R = 2, 12, 40, 3
     g = torch.Generator(device="cpu").manual_seed(1)
@@ -424,12 +427,13 @@ def test_pool_link(env, cuda):
 
 
 @pytest.mark.parametrize("relu", [False, True])
-@pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128), (32, 128), (16, 256), (32, 256)])
+@pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128), (32, 128), (16, 256), (32, 256), (128, 128)])
 def test_conv_add_node(env, cuda, relu, C, K):
     """(ReLU)(conv 3x3 + shortcut) with the Add in the conv epilogue
-    (acfe_conv2d_fwd_add: the rows kernel, or for the stage-2/3 conv2b shapes
-    C = 16 / 32, K = 128 / 256 the generic kernel with the Add in its row
-    stores) == conv2d -> add: z bit-exact, statistics to 1e-6, gradients of x,
+    (acfe_conv2d_fwd_add: the rows kernel -- K = C = 128: the one-wave
+    k_conv3x3_1w<3> --, or for the stage-2/3 conv2b shapes C = 16 / 32,
+    K = 128 / 256 the generic kernel with the Add in its row stores) ==
+    conv2d -> add: z bit-exact, statistics to 1e-6, gradients of x,
     w, b and the shortcut identical up to summation order."""
     ops = env[0]
     N, H, W = 2, 14, 128

@@ -287,14 +287,17 @@ def test_bird_t1_shape_eval_parity(cuda):
     assert ((g_dev - g_ref).norm() / g_ref.norm()).item() < 5e-2
 
 
-@pytest.mark.parametrize("W", [130, 513], ids=["W130", "W513"])
-def test_conv_rows_partial_column_tile(env, cuda, W):
+@pytest.mark.parametrize("W,H,C,K", [(130, 20, 64, 64), (513, 20, 64, 64), (130, 22, 128, 128), (513, 10, 128, 128)],
+                         ids=["W130", "W513", "W130k128", "W513k128"])
+def test_conv_rows_partial_column_tile(env, cuda, W, H, C, K):
     """wr_resnet's 513- / 257-wide stages run the rows / halo kernels with a
     partial last 64-pixel column tile (masked loads past Q, masked stores):
     fwd (+ BN sums), stride-1 dgrad and wgrad through the generic entry points
-    against float64, and the pooled forward at an even width."""
+    against float64, and the pooled forward at an even width.  K = C = 128:
+    the one-wave k_conv3x3_1w<0> (fwd with BN sums, dgrad without), H = 22 /
+    10: a partial last 4-row tile."""
     ops, call, lib, ptr, stream = env
-    N, H, C, K = 4, 20, 64, 64
+    N = 4
     x, w, b, g = _data(N, H, W, C, K, 107, cuda)
     assert lib.acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, 1)
     wp, wf = ops.pack_weights(w, BF, False), ops.pack_weights(w, BF, True)
