@@ -276,7 +276,7 @@ def main():
     counters = None
     sq = next((q for q in (ROOT / "profiles" / f"sq_dominant_{t}.json" for t in ("r03", "r02b", "r02")) if q.exists()),
               ROOT / "profiles" / "sq_dominant_r02.json")
-    if sq.exists():  # SQ counters of the same kernel (tools/pmc_sq.sh, separate rocprofv3 --pmc passes)
+    if sq.exists() and a.model == "bird":  # SQ counters of the same kernel (tools/pmc_sq.sh, separate --pmc passes)
         try:
             d = json.loads(sq.read_text())
             counters = {k: d[k] for k in ("mfma_busy_per_simd", "wave_time_waiting", "valu_insts_per_mfma",
@@ -308,7 +308,10 @@ def main():
             "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
         },
         "roofline": {
-            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} (k_conv3x3_1w<1,2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)",
+            "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} " + (
+                "(k_conv3x3_1w<1,2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)"
+                if a.model == "bird" else
+                "(k_conv3x3_rows<64,8,4,true,true>: bn2a + ReLU applied while staging the input rows, dropout + BN sums epilogue; 8 rows x 64 px x 64 ch per workgroup of 8 waves)"),
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-layer conv timing of one T1 training step (wr_resnet_bird, batch 512,
 bf16): HIP events around every conv's fwd / dgrad / wgrad (ops.watch_conv),
-with the layer's shape and achieved TFLOP/s.  usage: python tools/layer_profile.py"""
+with the layer's shape and achieved TFLOP/s.
+usage: python tools/layer_profile.py [batch] [wrn]   (wrn: wr_resnet, 2 classes)"""
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
@@ -11,14 +12,19 @@ import torch
 import bench
 from acfe import ops
 from acfe.train import FrontEnd, Trainer
-from resnet.wr_resnet_bird import WRResNet
 
 dev = torch.device("cuda", 0)
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
-model = WRResNet(input_shape=(128, 513, 3), classes=50, dtype=torch.bfloat16).to(dev)
+WRN = len(sys.argv) > 2 and sys.argv[2] == "wrn"
+if WRN:
+    from resnet.wr_resnet import WRResNet
+else:
+    from resnet.wr_resnet_bird import WRResNet
+NCLS = 2 if WRN else 50
+model = WRResNet(input_shape=(128, 513, 3), classes=NCLS, dtype=torch.bfloat16).to(dev)
 fe = FrontEnd(n_mels=128, dtype=torch.bfloat16, device=dev).to(dev)
 tr = Trainer(model, fe, lr=0.01, loss="cce", device=dev)
-x1, x2, lam, y = bench.make_batches(B, 50, dev, n_sets=1)[0]
+x1, x2, lam, y = bench.make_batches(B, NCLS, dev, n_sets=1)[0]
 for _ in range(2):
     tr.step(x1, y, x2, lam)
 torch.cuda.synchronize()
