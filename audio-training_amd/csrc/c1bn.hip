@@ -21,7 +21,11 @@
 //                        BN input-gradient coefficients dA = ca g + cb A + cc;
 //                        dW = ca o G + cb (W S + b s^T) + cc s^T,  db = ca sum g + cb sum A + M cc
 //   backward dx          dx = (W^T diag(ca)) g + (W^T diag(cb) W) x + W^T (cb b + cc)
-//                        (MFMA, reads dB and x, writes dx)
+//                        ca = scale is known before the sums, so the first term
+//                        P = (W^T diag(scale)) g (fp32, 64 B / pixel) is formed by
+//                        the backward-sums pass, which already holds g; the dx pass
+//                        then reads P and x (128 B / pixel) instead of dB and x
+//                        (288 B / pixel)
 //
 // A is the fp32 MFMA result of the bf16 weights and inputs (the unfused conv
 // rounds it to bf16 before the BN; the statistics and the ReLU mask here use
@@ -272,12 +276,12 @@ k_c1bn_apply(const uint16_t* __restrict__ X, const float* __restrict__ w, const 
 // block: the layout of mfma(xb, wa) (the recomputed conv output) and of the
 // MFMA A-operand over pixels.
 template <int NKB>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 registers: 2 waves / SIMD
 k_c1bn_bsum(const uint16_t* __restrict__ X, const float* __restrict__ w, const float* __restrict__ bias, long long M,
             int relu, const uint16_t* __restrict__ dY, const float* __restrict__ scale,
             const float* __restrict__ shift, float* __restrict__ slab, const float* __restrict__ xsc,
-            const float* __restrict__ xsh, int xrelu) {
-  constexpr int K = NKB * 16, LDB = K + 16, NOUT = K * 17;
+            const float* __restrict__ xsh, int xrelu, float* __restrict__ P) {
+  constexpr int K = NKB * 16, LDB = K + 16, NOUT = K * 17, NKS = NKB / 2;
   constexpr int TB = 32 * LDB, TXE = 32 * LDX, WE = TB + TXE;  // elements per wave
   constexpr int GPL = 32 * K / 8 / 64;                          // 16-B dB granules per lane per chunk
   constexpr int SMB = 4 * WE * 2 > 4 * NOUT * 4 ? 4 * WE * 2 : 4 * NOUT * 4;
@@ -295,6 +299,20 @@ k_c1bn_bsum(const uint16_t* __restrict__ X, const float* __restrict__ w, const f
     const int c = kb * 16 + l16;
     psc[kb] = scale[c];
     psh[kb] = shift[c] + scale[c] * (bias ? bias[c] : 0.f);
+  }
+  // (W o scale)^T as the A operand of P = (W^T diag(scale)) g: row = input
+  // channel l16, k-slot q*8+j <-> output channel ks*32 + (j>>2)*16 + q*4 + (j&3)
+  // (the k-slot order of 8-B dB row reads, as in k_c1bn_dx)
+  uint4 wt[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = ks * 32 + (j >> 2) * 16 + q * 4 + (j & 3);
+      v[j] = (float)((double)rbf(w[k * CIN + l16]) * (double)scale[k]);
+    }
+    wt[ks] = uint4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])};
   }
   f4 G[NKB], Gs[NKB];
 #pragma unroll
@@ -333,9 +351,30 @@ k_c1bn_bsum(const uint16_t* __restrict__ X, const float* __restrict__ w, const f
           if (!(fmaf(a0[r], psc[kb], psh[kb]) > 0.f)) g[r] = z;
           if (!(fmaf(a1[r], psc[kb], psh[kb]) > 0.f)) g[4 + r] = z;
         }
+        // masked g back into the tile for the P reads below (pixel rows 4q+r, 16+4q+r)
+        __bf16* tb = reinterpret_cast<__bf16*>(tB) + kb * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          tb[(4 * q + r) * LDB] = g[r];
+          tb[(16 + 4 * q + r) * LDB] = g[4 + r];
+        }
       }
       G[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, xt, G[kb], 0, 0, 0);
       Gs[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, ones, Gs[kb], 0, 0, 0);
+    }
+    // P = (W^T diag(scale)) g: lane = pixel l16 of block u, rows q*4+r = input channels
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const uint16_t* rowp = tB + (u * 16 + l16) * LDB + q * 4;
+      f4 ax = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const uint2 g0 = *reinterpret_cast<const uint2*>(rowp + ks * 32);
+        const uint2 g1 = *reinterpret_cast<const uint2*>(rowp + ks * 32 + 16);
+        ax = mfma16(wt[ks], uint4{g0.x, g0.y, g1.x, g1.y}, ax);
+      }
+      const long long px = px0 + u * 16 + l16;
+      if (px < M) *reinterpret_cast<f4*>(P + px * CIN + q * 4) = ax;
     }
   }
   __syncthreads();  // tiles dead; reuse smem for the cross-wave sum
@@ -410,28 +449,14 @@ k_c1bn_bfin(const float* __restrict__ tot, const float* __restrict__ gram, const
 }
 
 // ---------------------------------------------------------------- backward dx
-// dx = (W o ca)^T g + M2 x + c0 with g = dB masked by the forward ReLU.
-// Orientation mfma(wa, xb): lane (pixel l16) holds channels kb*16 + q*4 + r, the
-// layout of 8-byte dB loads; the dgrad MFMA's A-operand (W o ca)^T has its
-// k-slots permuted to that layout (slot q*8+j <-> channel ks*32 + (j>>2)*16 + q*4 + (j&3)).
-template <int NKB>
+// dx = P + M2 x + c0 (P from k_c1bn_bsum).  Orientation mfma(m2, xb): lane =
+// pixel l16, rows q*4 + r = input channels, the layout of P's 16-B row reads.
 __global__ void __launch_bounds__(256)
-k_c1bn_dx(const uint16_t* __restrict__ X, const float* __restrict__ w, const float* __restrict__ bias, long long M,
-          int relu, const uint16_t* __restrict__ dY, const float* __restrict__ scale, const float* __restrict__ shift,
-          const float* __restrict__ dxp, uint16_t* __restrict__ dX, const float* __restrict__ xsc,
-          const float* __restrict__ xsh, int xrelu) {
-  constexpr int K = NKB * 16, NKS = NKB / 2;
+k_c1bn_dx(const uint16_t* __restrict__ X, long long M, const float* __restrict__ P, const float* __restrict__ dxp,
+          int K, uint16_t* __restrict__ dX, const float* __restrict__ xsc, const float* __restrict__ xsh, int xrelu) {
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
-  uint4 wa[NKB], wt[NKS], m2 = {0u, 0u, 0u, 0u};
-  load_wa<NKB>(w, l16, q, wa);
   const XPro pro = make_xpro(xsc, xsh, xrelu, q);
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = dxp[(ks * 32 + (j >> 2) * 16 + q * 4 + (j & 3)) * CIN + l16];
-    wt[ks] = uint4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])};
-  }
+  uint4 m2 = {0u, 0u, 0u, 0u};
   if (q < 2) {
     const float* p = dxp + K * 16 + l16 * 16 + q * 8;  // M2[c = l16][c' = q*8 + j]
     m2 = uint4{pack2(p[0], p[1]), pack2(p[2], p[3]), pack2(p[4], p[5]), pack2(p[6], p[7])};
@@ -439,51 +464,25 @@ k_c1bn_dx(const uint16_t* __restrict__ X, const float* __restrict__ w, const flo
   float c0[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) c0[r] = dxp[K * 16 + 256 + q * 4 + r];
-  float psc[NKB * 4], psh[NKB * 4];
-#pragma unroll
-  for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = kb * 16 + q * 4 + r;
-      psc[kb * 4 + r] = scale[c];
-      psh[kb * 4 + r] = shift[c] + scale[c] * (bias ? bias[c] : 0.f);
-    }
-  const uint16_t* zp = reinterpret_cast<const uint16_t*>(c1_zero);
   const long long nblk = (M + 15) / 16;
   const long long wstride = (long long)gridDim.x * 4 * UNR;
   for (long long b0 = ((long long)blockIdx.x * 4 + wid) * UNR; b0 < nblk; b0 += wstride) {
     uint4 xb[UNR];
-    uint2 gy[UNR][NKB];
+    f4 pv[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const long long px = (b0 + u) * 16 + l16;
       xb[u] = load_x(X, px, M, q, pro);
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-        gy[u][kb] = *reinterpret_cast<const uint2*>(px < M ? dY + px * K + kb * 16 + q * 4 : zp);
+      pv[u] = px < M ? *reinterpret_cast<const f4*>(P + px * CIN + q * 4) : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const long long px = (b0 + u) * 16 + l16;
-      if (relu) {
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-          const f4 acc = mfma16(wa[kb], xb[u], f4{0.f, 0.f, 0.f, 0.f});
-          unsigned mk[2] = {0u, 0u};
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (fmaf(acc[r], psc[kb * 4 + r], psh[kb * 4 + r]) > 0.f) mk[r >> 1] |= (r & 1) ? 0xFFFF0000u : 0xFFFFu;
-          gy[u][kb].x &= mk[0];
-          gy[u][kb].y &= mk[1];
-        }
-      }
-      f4 ax = mfma16(m2, xb[u], f4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        ax = mfma16(wt[ks], uint4{gy[u][2 * ks].x, gy[u][2 * ks].y, gy[u][2 * ks + 1].x, gy[u][2 * ks + 1].y}, ax);
+      const f4 ax = mfma16(m2, xb[u], f4{0.f, 0.f, 0.f, 0.f});
       if (px < M)
         *reinterpret_cast<uint2*>(dX + px * CIN + q * 4) =
-            uint2{pack2(ax[0] + c0[0], ax[1] + c0[1]), pack2(ax[2] + c0[2], ax[3] + c0[3])};
+            uint2{pack2((pv[u][0] + ax[0]) + c0[0], (pv[u][1] + ax[1]) + c0[1]),
+                  pack2((pv[u][2] + ax[2]) + c0[2], (pv[u][3] + ax[3]) + c0[3])};
     }
   }
 }
@@ -514,12 +513,18 @@ k_c1bn_slab_sum(const float* __restrict__ slab, int nrows, int n, float* __restr
   }
 }
 
-constexpr int GRAM_GRID = 1024, APPLY_GRID = 4096, BSUM_GRID = 768, DX_GRID = 2048;
+// grids are whole multiples of the resident workgroups (bsum: 228 registers -> 2 per CU; apply: 160 -> 3 per CU)
+constexpr int GRAM_GRID = 1024, APPLY_GRID = 3072, BSUM_GRID = 512, DX_GRID = 2048;
 
 int c1_grid(long long M, int cap) {
   const long long steps = ((M + 15) / 16 + 4 * UNR - 1) / (4 * UNR);
   const long long g = steps < cap ? steps : cap;
   return (int)(g < 1 ? 1 : g);
+}
+
+// float offset of P [M][16] in the backward workspace (16-B aligned)
+long long p_offset(long long M, int K) {
+  return ((long long)c1_grid(M, BSUM_GRID) * K * 17 + K * 17 + K * 16 + 256 + 16 + 3) & ~3ll;
 }
 
 bool shape_ok(long long M, int C, int K, const void* x) {
@@ -534,7 +539,7 @@ ACFE_API int acfe_c1bn_supported(int C, int K) { return C == CIN && (K == 64 || 
 ACFE_API long long acfe_c1bn_workspace(long long M, int C, int K) {
   if (M <= 0 || C != CIN || K <= 0 || K > 128) return 0;
   const long long fwd = (long long)c1_grid(M, GRAM_GRID) * NGRAM;
-  const long long bwd = (long long)c1_grid(M, BSUM_GRID) * K * 17 + K * 17 + K * 16 + 256 + 16;
+  const long long bwd = p_offset(M, K) + M * CIN;  // slab, totals, dx constants, then P
   return fwd > bwd ? fwd : bwd;
 }
 
@@ -578,23 +583,20 @@ static int c1bn_bwd_impl(const void* dy, const void* x, long long M, int C, cons
   float* slab = workspace;
   float* tot = slab + (long long)gs * n;
   float* dxp = tot + n;
+  float* P = workspace + p_offset(M, K);
   hipStream_t s = strm(stream);
   if (K == 128)
     hipLaunchKernelGGL((k_c1bn_bsum<8>), dim3(gs), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, slab, xsc, xsh, xrelu);
+                       (const uint16_t*)dy, scale, shift, slab, xsc, xsh, xrelu, P);
   else
     hipLaunchKernelGGL((k_c1bn_bsum<4>), dim3(gs), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, slab, xsc, xsh, xrelu);
+                       (const uint16_t*)dy, scale, shift, slab, xsc, xsh, xrelu, P);
   hipLaunchKernelGGL(k_c1bn_slab_sum, dim3(cdiv(n, 16)), dim3(1024), 0, s, slab, gs, n, tot);
   hipLaunchKernelGGL(k_c1bn_bfin, dim3(1), dim3(128), 0, s, tot, gram, w, bias, scale, mean, invstd, M, count, K,
                      dgamma, dbeta, dw, db, dxp);
   const int gd = c1_grid(M, DX_GRID);
-  if (K == 128)
-    hipLaunchKernelGGL((k_c1bn_dx<8>), dim3(gd), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, dxp, (uint16_t*)dx, xsc, xsh, xrelu);
-  else
-    hipLaunchKernelGGL((k_c1bn_dx<4>), dim3(gd), dim3(256), 0, s, (const uint16_t*)x, w, bias, M, relu,
-                       (const uint16_t*)dy, scale, shift, dxp, (uint16_t*)dx, xsc, xsh, xrelu);
+  hipLaunchKernelGGL(k_c1bn_dx, dim3(gd), dim3(256), 0, s, (const uint16_t*)x, M, P, dxp, K, (uint16_t*)dx, xsc, xsh,
+                     xrelu);
   return launch_rc("acfe_c1bn_bwd");
 }
 
