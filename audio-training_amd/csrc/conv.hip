@@ -2705,9 +2705,13 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   unsigned dpos = 0;
   // part bit 0: the dY granules, bit 1: the input halo granules
   auto gload = [&](int sg, int part = 3) __attribute__((always_inline)) {
+    // segments walk down a 64-pixel column (row fastest): consecutive steps
+    // share NR + 1 of their NR + 2 halo rows (and, UNP, their pooled dY row),
+    // so the overlap is re-read from L2 one step later instead of a whole
+    // image row later (r03v: 9.8 GB of HBM reads per launch vs 5.9 GB algorithmic)
     const int PR = g.P / NR;  // row groups per image
     const int n = sg / (PR * QS), rem = sg - n * (PR * QS);
-    const int h = (rem / QS) * NR, w0 = (rem - (rem / QS) * QS) * SEGW;
+    const int h = (rem % PR) * NR, w0 = (rem / PR) * SEGW;
     const T16* dyrow = dY + (((long long)n * g.P + h) * g.Q + w0) * g.K;
 #pragma unroll
     for (int i = 0; i < ((part & 1) ? DPT : 0); ++i) {
