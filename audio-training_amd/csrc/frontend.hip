@@ -611,12 +611,20 @@ k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
   const bool alias = nk <= 1024;
   float* pw = alias ? reinterpret_cast<float*>(wbuf) : reinterpret_cast<float*>(wbuf + NC + NC / 16);
   const int tid = threadIdx.x;
-  const int b = blockIdx.y;
+  // XCD-aware work order: the hardware places workgroup L (x fastest) on XCD
+  // L % 8, so consecutive frame groups of a clip -- whose 4096-sample frames
+  // overlap by ~3.6 groups -- would land in eight different L2s and each
+  // fetch the clip's samples again.  Give every XCD a contiguous range of
+  // (clip, frame group) items instead (a bijection when the count is a
+  // multiple of 8; otherwise the plain order).
+  const int gx = gridDim.x, nwg = gx * gridDim.y, lin = blockIdx.x + gx * blockIdx.y;
+  const int item = nwg % 8 == 0 ? (lin % 8) * (nwg / 8) + lin / 8 : lin;
+  const int b = item / gx;
   const float* xb = raw + (int64_t)b * cs;
   const bool do_norm = stats != nullptr;
   const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
   const float rinv = __fdiv_rn(1.0f, rng);
-  const int f0 = blockIdx.x * fpw;
+  const int f0 = (item - b * gx) * fpw;
   // base twiddles: pass 2 (jm = j & 15), pass 3 (jm = j, two butterflies per lane)
   float2 bw2[1][4], bw3[2][4];
   {
