@@ -359,7 +359,9 @@ int acfe_conv2d_fwd_add_bn(const void* x, int N, int H, int W, int C, const void
  * gram = float[272] (sum x x^T, sum x; keep it for the backward; in eval mode
  * fill it with acfe_c1bn_stats too), then acfe_c1bn_apply writes y.
  * Backward: acfe_c1bn_bwd -> dx [M][16], dw [K][16], db [K], dgamma, dbeta
- * (nullable); count = M in training, 1e300 in eval. */
+ * (nullable); count = M in training, 1e300 in eval.  The workspace also holds
+ * the backward's fp32 [M][16] intermediate (W^T diag(scale)) g, so it grows
+ * with M (64 B per pixel). */
 int acfe_c1bn_supported(int C, int K);
 long long acfe_c1bn_workspace(long long M, int C, int K);
 int acfe_c1bn_stats(const void* x, long long M, int C, const float* w, int K, const float* bias, double* partial,
