@@ -14,6 +14,12 @@ Parity pinning:
   * `mel_f` / `mel_spec` are pinned bit-for-bit against golden vectors produced
     by the reference `custommel.py` itself (oracle/gen_golden.py ->
     tests/golden/mel_f_*.npz, mel_spec_p*.npz).
+  * The streaming path's index work -- identifytracks.merge_signals /
+    get_tracks_from_signals / Signal / get_end's chunk scan and
+    predict_utils.load_samples' window cutting -- is pinned bit-for-bit
+    against tests/golden/tracks_golden.npz, produced by the reference modules
+    themselves (oracle/gen_golden_tracks.py, stub librosa / cv2 / tensorflow
+    imports that those functions never call).
   * STFT (tf.signal.stft pad_end, librosa.stft center), PCEN, LME, Keras layer
     semantics and Adam live in third-party libraries (tensorflow, tfp,
     librosa, keras -- unpinned in requirements.txt:1-13) that are absent from
