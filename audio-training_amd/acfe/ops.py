@@ -339,6 +339,9 @@ def conv2d(x, w, b=None, stride=1, padding="same", want_stats=False, link=None):
     else:
         raise ValueError(padding)
     if link is not None and not (x.is_contiguous() and (P, Q) != (0, 0)):
+        # the conv cannot hand dX over: autograd accumulates it instead, and
+        # the linked BN must not wait for it (ResidualLink.declined)
+        link.declined = True
         link = None
     return _Conv2dFn.apply(x, w, b, stride, pt, pl, P, Q, want_stats, link)
 
@@ -406,6 +409,9 @@ class ResidualLink:
     def __init__(self):
         self.grad = None
         self.pool = None  # (pooled gradient, k) from an avg_pool_same(x, k, link=...) shortcut
+        # set by a consumer that could not take the link after all (ops.conv2d on a
+        # non-contiguous x): its gradient reaches x through autograd instead
+        self.declined = False
 
     @staticmethod
     def make():
@@ -591,7 +597,7 @@ class _BNFn(torch.autograd.Function):
         add = pool = None
         if link is not None:
             add, pool = link.take(), link.take_pool()
-            if add is None and pool is None:
+            if add is None and pool is None and not link.declined:
                 raise RuntimeError("ResidualLink: the shortcut gradient was not delivered before this BN's backward")
         dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool,
                                     params=ctx.gb)
@@ -1212,6 +1218,8 @@ def avg_pool_same(x, k, link=None):
     """AveragePooling2D(k, strides=k, "same"); with a ResidualLink the backward
     hands the pooled gradient to the BN that reads x (acfe_bn_bwd_apply_pool)."""
     ok = link is not None and x.dim() == 4 and x.shape[-1] % 8 == 0 and x.data_ptr() % 16 == 0
+    if link is not None and not ok:
+        link.declined = True  # autograd delivers this gradient instead (ResidualLink.declined)
     return _AvgPoolFn.apply(x, k, link if ok else None)
 
 

@@ -858,12 +858,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // PM 1 with the MFMA operands in pixels x weights order: each A row block
   // of four rows is one 2x2 window, so a lane's four accumulators are a whole
   // window of one channel and the pooling needs no cross-lane traffic
-  // (ACFE_POOL_LANEPAIR builds the weights x pixels lane-pair epilogue instead)
-#ifdef ACFE_POOL_LANEPAIR
-  constexpr bool SWP = false;
-#else
   constexpr bool SWP = PM == 1;
-#endif
   // CPERM (weights x pixels epilogues with the weight DMA): fragment fn, A row
   // m = output channel KB/2 wk + 4 FN (m >> 2) + 4 fn + (m & 3), so lane group
   // q = lane >> 4 holds 4 FN consecutive channels of its pixel across the FN
@@ -871,11 +866,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // 8-B ones); weight LDS rows keep 128 B with the granule swizzle
   // swzp(k) = ((k >> LQ) & 3) << 1 | ((k >> 1) & 1), which keeps the fragment
   // reads conflict-free under the permuted rows
-#ifdef ACFE_ROWS_NO_CPERM
-  constexpr bool CPERM = false;
-#else
   constexpr bool CPERM = !SWP && TR > 3;
-#endif
   constexpr int LQ = KB == 128 ? 4 : 3;  // log2(4 FN), FN = KB / 32
   constexpr int FN = KB / 32, FM = TR;                           // per wave: KB/2 channels x TR*16 pixels
   // 6-row tiles: weights by LDS-DMA into a double buffer (no staging VGPRs,
@@ -995,22 +986,11 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // scalar offset arithmetic); the 6-row K = 128 tiles, at the VGPR limit,
   // keep one VGPR and form the rest in soffset
   constexpr bool VOFF = !(KB == 128 && TR == 6) || CPERM;
-#ifdef ACFE_ROWS_NO_WILV
-  constexpr bool WILV = false;
-#else
-#ifndef ACFE_ROWS_WGRP
-#define ACFE_ROWS_WGRP 6  // r02ak same-box A/B: 6 -> fwd_pool 4.61 ms, 3 -> 4.73, 2 -> 4.61 (dgrad 4.52 / 4.57 / 4.62)
-#endif
-  constexpr int WGRP = ACFE_ROWS_WGRP;  // MFMA groups (of 6) that carry the next step's weight pieces
-#ifndef ACFE_ROWS_WILV64
-#define ACFE_ROWS_WILV64 0
-#endif
-  constexpr bool WILV = WDMA && (KB == 128 || ACFE_ROWS_WILV64);
-#ifndef ACFE_ROWS_GILV
-#define ACFE_ROWS_GILV 0  // r02aq same-box A/B: fwd_pool 4.81 ms with, 4.70 without; dgrad equal
-#endif
-  constexpr bool GILV = ACFE_ROWS_GILV && XRES && WILV;  // (input-row loads spread over the MFMA groups too)  // (K = 64: the iglp_opt(0) interleave is better without it)
-#endif
+  // MFMA groups (of 6) that carry the next step's weight pieces (r02ak same-box
+  // A/B: 6 -> fwd_pool 4.61 ms, 3 -> 4.73, 2 -> 4.61); K = 64: the iglp_opt(0)
+  // interleave is better without the pieces between the groups (r02ap)
+  constexpr int WGRP = 6;
+  constexpr bool WILV = WDMA && KB == 128;
   unsigned vwo[VOFF ? WPW : 1];
   unsigned vwl = 0;
   if constexpr (WDMA) {
@@ -1119,19 +1099,15 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       xm |= mm << (MB * i);
     }
   };
-  // part < 0: every granule; else the granules i with i % 3 == part (GILV:
-  // issued one part per MFMA group of the first three -- the step's closing
-  // wait needs them; part 0 first, it carries the tile setup)
-  auto gload = [&](int tl, int st, int part = -1) __attribute__((always_inline)) {
+  auto gload = [&](int tl, int st) __attribute__((always_inline)) {
     const int cc = st / 3, r = XRES ? 0 : st - cc * 3;
-    if (part <= 0 && tl != stl) {
+    if (tl != stl) {
       stage_tile(tl);
       stl = tl;
     }
     if constexpr (PM == 2) {
 #pragma unroll
       for (int i = 0; i < XPT; ++i) {
-        if (part >= 0 && i % 3 != part) continue;
         const int idx = tid + 512 * i;
         const int xrow = idx / (HWX * 8), xpix = (idx - xrow * (HWX * 8)) >> 3;
         const int hin = sh0 + xrow + r, win = sw0 + xpix;
@@ -1147,7 +1123,6 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       const int delta = r * g.W * CB + cc * 128;
 #pragma unroll
       for (int i = 0; i < XPT; ++i) {
-        if (part >= 0 && i % 3 != part) continue;
         const bool ok = (xm >> (MB * i + r)) & 1u;
         rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? xoffs[i] + delta : 0x80000000, 0, 0);
       }
@@ -1155,7 +1130,6 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     if constexpr (!WDMA) {
 #pragma unroll
       for (int i = 0; i < WPT; ++i) {
-        if (part > 0) continue;
         const int idx = tid + 512 * i;
         const int s = idx / (KB * 8), r2 = idx - s * (KB * 8), k = r2 >> 3, gw = r2 & 7;
         rw[i] = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + (r * 3 + s) * g.C + cc * 64 + gw * 8);
@@ -1647,7 +1621,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     const bool xnext = more && (!XRES || rs == 2);
     const bool xload = XRES && rs == 1 && t + 2 < L;  // this step requests the next chunk's rows
     if constexpr (XRES) {
-      if (xload && !GILV) gload(tl2, st2);
+      if (xload) gload(tl2, st2);
     } else {
       if (more) gload(tl1, st1);
     }
@@ -1669,10 +1643,7 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     // K = 64: let the scheduler interleave the fragment reads with the MFMAs
     // (fwd_add 128->64 1.084 -> 1.013 ms, dropout 64->64 0.649 -> 0.625 ms;
     // at K = 128 the same hint spills: fwd_pool 4.96 -> 5.35 ms, r02o)
-#ifndef ACFE_ROWS_IGLP64
-#define ACFE_ROWS_IGLP64 1
-#endif
-    if constexpr (KB == 64 && ACFE_ROWS_IGLP64) __builtin_amdgcn_iglp_opt(0);
+    if constexpr (KB == 64) __builtin_amdgcn_iglp_opt(0);
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
@@ -1684,10 +1655,6 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
           for (int j = 0; j < WPW; ++j)
             if ((j * WGRP) / WPW == s * 2 + kk && more) wpiece(j);
-        }
-        // GILV: the next chunk's input rows, one sixth per MFMA group
-        if constexpr (GILV) {
-          if (s * 2 + kk < 3 && xload) gload(tl2, st2, s * 2 + kk);
         }
         uint4 wf[FN], xf[FM];
 #pragma unroll
@@ -2786,11 +2753,8 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   int buf = 0;
   // WGI: the next segment's input-halo loads are issued after the first
   // 32-pixel half's MFMAs (their issue stalls then overlap MFMA work)
-#ifndef ACFE_WG_ILV
-#define ACFE_WG_ILV 1
-#endif
-  // (K = 64: no measurable difference, r02as: 0.518-0.522 vs 0.521-0.530 ms; ACFE_WG_ILV=2 turns it on)
-  constexpr bool WGI = ACFE_WG_ILV == 2 || (ACFE_WG_ILV != 0 && KB >= 128);
+  // (K = 64: no measurable difference, r02as: 0.518-0.522 vs 0.521-0.530 ms)
+  constexpr bool WGI = KB >= 128;
   for (int sg = sbeg; sg < send; ++sg) {
     const bool more = sg + 1 < send;
     if (more) gload(sg + 1, WGI ? 1 : 3);
@@ -3131,10 +3095,7 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
         // workgroups than the caller's slab rows (narrow images have more
         // tiles than 128-pixel slab rows)
         if (stats && gp > grid_m) gp = grid_m;
-#ifndef ACFE_POOL1W
-#define ACFE_POOL1W 1
-#endif
-        if constexpr (BN == 128 && ACFE_POOL1W) {
+        if constexpr (BN == 128) {
           // one wave per SIMD (pool1w.hip), the previous tile's epilogue beside this tile's MFMAs
           const int rc = launch_plain1w(g, x, wp, bias, y, stats, grid_m, s, "acfe_conv2d_fwd", 0);
           if (rc != ACFE_E_INVAL) return rc;
@@ -3711,19 +3672,16 @@ template <int KB, int PM>
 static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                        int srows, uint8_t* amax, hipStream_t s, const char* what) {
   if constexpr (KB == 128) {
-#ifndef ACFE_POOL1W
-#define ACFE_POOL1W 1
-#endif
-    if constexpr (PM == 1 && ACFE_POOL1W) {
+    if constexpr (PM == 1) {
       // one wave per SIMD, the previous tile's epilogue beside this tile's MFMAs
       const int rc = launch_pool1w(g, x, wp, bias, y, stats, srows, amax, s, what);
       if (rc != ACFE_E_INVAL) return rc;
     }
-    if constexpr (PM == 2 && ACFE_POOL1W) {
+    if constexpr (PM == 2) {
       const int rc = launch_unpool1w(g, x, wp, y, amax, s, what);
       if (rc != ACFE_E_INVAL) return rc;
     }
-    if constexpr (PM == 3 && ACFE_POOL1W) {
+    if constexpr (PM == 3) {
       const int rc = launch_plain1w(g, x, wp, bias, y, stats, srows, s, what, 3);
       if (rc != ACFE_E_INVAL) return rc;
     }

@@ -562,9 +562,6 @@ __device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
 // one-wave design's butterflies, so a wave needs <= 168 VGPRs: 12 waves per CU
 // (the one-wave-per-frame kernel it replaced ran 8, limited by LDS and 206
 // VGPRs; its waves sat waiting 41 % of their time, rocprofv3 SQ counters r02n).
-#ifndef ACFE_MEL_W2_WPE
-#define ACFE_MEL_W2_WPE 3
-#endif
 // k_mel_w2's LDS index: one float2 of padding per 16 points: pass-1 rows
 // (stride 17), pass-2/3 stores (16-lane groups of consecutive points) are
 // bank-conflict free; the 32-lane reads keep one colliding lane pair (the
@@ -600,7 +597,7 @@ __device__ __forceinline__ void stockham_pass_t(float2* buf, const float2 (*bw)[
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ACFE_MEL_W2_WPE)))
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3)))
 k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restrict__ stats, int pad_mode, int power,
          int n_frames, int fpw, int hop, const float2* __restrict__ tw, const float2* __restrict__ rtw,
          const float* __restrict__ win, const int* __restrict__ band, const float* __restrict__ vals, int n_mels,
@@ -683,12 +680,8 @@ k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
         for (int r = 0; r < 16; ++r) {
           const int nn = 2 * (j + r * NB0);
           const bool ia = inb || in_sig(start + nn, n, pad_mode), ic = inb || in_sig(start + nn + 1, n, pad_mode);
-#ifdef ACFE_MEL_NORM_DIV
-          v[r] = make_float2(ia ? norm1(xa[r], mn, rng) * wa[r] : 0.f, ic ? norm1(xc[r], mn, rng) * wc[r] : 0.f);
-#else
           v[r] = make_float2(ia ? norm1r(xa[r], mn, rng, rinv) * wa[r] : 0.f,
                              ic ? norm1r(xc[r], mn, rng, rinv) * wc[r] : 0.f);
-#endif
         }
       } else {
 #pragma unroll

@@ -115,18 +115,24 @@ struct Buf {
 };
 std::mutex g_buf_mu;
 std::vector<Buf> g_bufs;  // idle buffers, largest last
+size_t g_idle_bytes = 0;  // capacity held by g_bufs
+// idle inflate buffers kept for reuse: at most 64 and 1 GiB in total, so host
+// RAM does not stay at (peak reader concurrency) x 2 x (shard size) after a burst
+constexpr size_t kIdleCap = size_t(1) << 30;
 Buf take_buf() {
   std::lock_guard<std::mutex> g(g_buf_mu);
   if (g_bufs.empty()) return Buf();
   Buf b = g_bufs.back();
   g_bufs.pop_back();
+  g_idle_bytes -= b.cap;
   b.size = 0;
   return b;
 }
 void give_buf(Buf& b) {
   if (!b.p) return;
   std::lock_guard<std::mutex> g(g_buf_mu);
-  if (g_bufs.size() < 64) {
+  if (g_bufs.size() < 64 && g_idle_bytes + b.cap <= kIdleCap) {
+    g_idle_bytes += b.cap;
     g_bufs.push_back(b);
     std::sort(g_bufs.begin(), g_bufs.end(), [](const Buf& a, const Buf& c) { return a.cap < c.cap; });
   } else {

@@ -32,7 +32,10 @@ partner batch is B clips drawn uniformly from the same resident pool (the
 primaries of the current batch included, as an independent pass may also
 return them) and gathered on the device: the same distribution of pairs
 (uniform over the dataset, up to the shuffle-buffer locality both pipelines
-have), without the second decode.
+have), without the second decode.  In the epoch's tail, once the readers are
+done and the pool drains, the clips of the last buffer-full of primaries stay
+in the partner pool (nothing overwrites a released slot any more), so the last
+batches are not paired mostly with themselves.
 """
 from __future__ import annotations
 
@@ -179,6 +182,7 @@ class AudioDataset:
         self._pool = None
         self._dstage = None
         self._stage_buf = None
+        self._last_ev = None  # event after the newest gathers from the pool (orders the next epoch's refills)
         self.error = None
 
     # ---------------------------------------------------------------- counting
@@ -268,11 +272,15 @@ class AudioDataset:
                         if lab is None:
                             continue
                         c, p = stage.claim()
-                        dst = base + ((c * stage.per + p) * row) * 4
-                        fl = lib.acfe_example_audio(rec[0], rec[1], self.key, dst, self.nfloats, None, 0,
-                                                    ctypes.byref(cnt))
-                        # NaN / Inf filter (tfdataset.py:297): the slot stays empty
-                        stage.commit(c, p, lab if fl >= 0 and fl & 2 else -1)
+                        kept = -1  # NaN / Inf filter (tfdataset.py:297): the slot stays empty
+                        try:
+                            dst = base + ((c * stage.per + p) * row) * 4
+                            fl = lib.acfe_example_audio(rec[0], rec[1], self.key, dst, self.nfloats, None, 0,
+                                                        ctypes.byref(cnt))
+                            if fl >= 0 and fl & 2:
+                                kept = lab
+                        finally:  # a claimed slot is always committed, or its chunk never fills
+                            stage.commit(c, p, kept)
             except _Stop:
                 return
             except Exception as e:  # noqa: BLE001 -- an unreadable shard ends that file, not the epoch
@@ -376,7 +384,9 @@ class AudioDataset:
         fq: queue.Queue = queue.Queue()
         for f in files:
             fq.put(f)
-        slots = _SlotPool(self.pool_rows)
+        # the previous epoch's last gathers may still be queued on the compute
+        # stream: the first refill of this epoch waits for their event
+        slots = _SlotPool(self.pool_rows, self._last_ev)
         ready: queue.Queue = queue.Queue()
         nthreads = min(self.threads, max(1, len(files)))
         readers = [threading.Thread(target=self._reader, args=(fq, stage, stop, stable), daemon=True)
@@ -395,6 +405,7 @@ class AudioDataset:
         mover = threading.Thread(target=self._mover, args=(stage, ready, slots, stop, readers_done), daemon=True)
         mover.start()
         live: list[int] = []                   # resident slots not yet used as a primary this epoch
+        used: list[int] = []                   # slots already used as a primary (mix_up partners in the tail)
         lab = np.full(self.pool_rows, -1, np.int32)
         # the shuffle buffer: batches are drawn once `target` clips are resident
         # (or the epoch's records are exhausted); the pool holds target + 2
@@ -427,8 +438,17 @@ class AudioDataset:
                     pick, live = live[:b], live[b:]
                 partner = None
                 if augment:
-                    resident = live + pick
+                    # mix_up partners: any resident clip.  Once the readers are
+                    # done (nothing refills a released slot any more) the clips
+                    # of the last `target` primaries stay valid partners too,
+                    # so the tail batches do not shrink to pairing the batch
+                    # with itself (the reference draws partners from an
+                    # independent second pass, tfdataset.py:473-480)
+                    resident = live + pick + (used[-target:] if done else [])
                     partner = [resident[rng.randrange(len(resident))] for _ in range(b)]
+                used.extend(pick)
+                if len(used) > 2 * target:
+                    del used[:-target]
                 yield pick, partner, lab, slots
         finally:
             stop.set()
@@ -469,6 +489,8 @@ class AudioDataset:
                 ev = torch.cuda.Event()
                 ev.record()
             slots.release(pick, ev)
+            if ev is not None:
+                self._last_ev = ev
             n += len(pick)
             yield ((x1, y1), (x2, y2)) if augment else (x1, y1)
         if self._epoch_size is None and self.record_shard is None:
@@ -481,9 +503,9 @@ class _SlotPool:
     acquire(n) hands out n free slots and the newest such event (events of
     one stream complete in order, so waiting for it covers every older one)."""
 
-    def __init__(self, rows):
+    def __init__(self, rows, ev=None):
         self.free = list(range(rows - 1, -1, -1))
-        self.ev = None
+        self.ev = ev
         self.cv = threading.Condition()
 
     def release(self, rows, ev):
@@ -527,8 +549,9 @@ def get_dataset(dir, labels, global_epoch=None, **args):
     """tfdataset.get_dataset (tfdataset.py:429-506) -> (dataset, remapped,
     epoch_size, labels, extra_label_map).  epoch_size is the number of
     examples one epoch yields (the reference counts them with a full pass,
-    get_distribution, :853-857; here a header-only pass of the native reader,
-    or args["epoch_size"] when the caller already knows it).  Extra keys
+    get_distribution, :853-857; so does this: AudioDataset.count inflates every
+    shard and checks every record's label and float list -- a full decode
+    pass at startup -- unless args["epoch_size"] gives the number).  Extra keys
     accepted here: device, threads, seed, label_map, record_shard, files,
     drop_remainder, shuffle_buffer."""
     global N_MELS, FMIN, FMAX, NFFT, BREAK_FREQ

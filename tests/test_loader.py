@@ -179,3 +179,44 @@ def test_spectrogram_records(tmp_path):
     assert x.shape == (3, 2049, 513)
     for k in range(3):
         assert torch.equal(x[k], torch.from_numpy(specs[k]))
+
+
+def test_mixup_partners_in_the_epoch_tail(tmp_path):
+    """After the readers finish the pool drains; the last batches still draw
+    mix_up partners from the last buffer-full of clips, not only from the
+    batch's own primaries."""
+    import tfdataset
+
+    d = tmp_path / "train"
+    d.mkdir()
+    _write(d / "a.tfrecord", range(0, 40))
+    ds = tfdataset.AudioDataset(tfdataset._files(d), ["bird", "noise"], batch_size=4, augment=True, device="cpu",
+                                threads=1, shuffle_buffer=8, seed=3)
+    batches = [(_ids(x1), _ids(x2)) for (x1, _), (x2, _) in ds]
+    assert sorted(k for p, _ in batches for k in p) == list(range(40))
+    outside = sum(1 for p, q in batches[-2:] for k in q if k not in p)
+    assert outside > 0
+
+
+@pytest.mark.gpu
+def test_back_to_back_epochs_keep_gathered_clips(shards, cuda):
+    """A consumer that breaks an epoch and starts the next one at once: the new
+    epoch's first refills (side-stream copies into the pool) must wait for the
+    previous epoch's gathers still queued on the compute stream (the pool's
+    release event carries over epochs)."""
+    import tfdataset
+
+    d, keep = shards
+    ds = tfdataset.AudioDataset(tfdataset._files(d), ["bird", "noise"], batch_size=8, device=cuda, threads=3,
+                                shuffle_buffer=16)
+    for _ in range(3):
+        it = iter(ds)
+        torch.cuda._sleep(1_000_000_000)  # the gathers of the batch below queue behind ~0.5 s of spinning
+        x, y = next(it)
+        it.close()
+        it2 = iter(ds)
+        x2, y2 = next(it2)
+        it2.close()
+        for xb, yb in ((x, y), (x2, y2)):
+            for k, row in zip(_ids(xb.cpu()), yb.cpu()):
+                assert k in keep and _label_ok(k, row), k
