@@ -144,6 +144,43 @@ def cpu_baseline(batch=2, steps=2, model="bird", classes=50):
                       f"(fp32, {cores} threads) + Keras Adam; {dt:.1f} s"}
 
 
+def dominant_evidence(key: str, same_shape: bool):
+    """(traffic, counters) of the dominant kernel of workload `key` (t1, wrn,
+    t1_fp32, wrn_fp32, infer_fp32, stream_fp32, ...) from the committed PMC folds:
+    profiles/pmc_dominant_<key>_<round>.json (HBM bytes per launch, FETCH_SIZE x2
+    + WRITE_SIZE, tools/pmc_fold.py) and profiles/sq_dominant_<key>_<round>.json
+    (SQ counters, tools/sq_json.py), newest round first; T1 also falls back to
+    the earlier rounds' unsuffixed files.  Only used when this run has the
+    measured launch shape (same_shape)."""
+    if not same_shape:
+        return None, None
+    prof = ROOT / "profiles"
+
+    def newest(kind):
+        names = [f"{kind}_{key}_r{r:02d}.json" for r in range(9, 3, -1)]
+        if key == "t1":
+            names += [f"{kind}_r03.json", f"{kind}_r02b.json"]
+        return next((prof / n for n in names if (prof / n).exists()), None)
+
+    traffic = counters = None
+    pmc = newest("pmc_dominant")
+    if pmc is not None:
+        try:
+            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+        except ValueError:
+            traffic = None
+    sq = newest("sq_dominant")
+    if sq is not None:
+        try:
+            d = json.loads(sq.read_text())
+            counters = {k: d[k] for k in ("mfma_busy_per_simd", "wave_time_waiting", "valu_insts_per_mfma",
+                                          "lds_bank_conflict_share")}
+            counters["source"] = f"profiles/{sq.name}"
+        except (ValueError, KeyError):
+            counters = None
+    return traffic, counters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,25 +302,8 @@ def main():
     flops_launch = 2.0 * a.batch * H_t * W_t * K * R * S * C
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
-    traffic = None
-    pmc = next((q for q in (ROOT / "profiles" / f"pmc_dominant_{t}.json" for t in ("r03", "r02b", "r02", "r01l"))
-                if q.exists()), None)
-    if pmc is not None and a.batch == 512 and a.model == "bird":  # measured on this launch's shape
-        try:
-            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    counters = None
-    sq = next((q for q in (ROOT / "profiles" / f"sq_dominant_{t}.json" for t in ("r03", "r02b", "r02")) if q.exists()),
-              ROOT / "profiles" / "sq_dominant_r02.json")
-    if sq.exists() and a.model == "bird":  # SQ counters of the same kernel (tools/pmc_sq.sh, separate --pmc passes)
-        try:
-            d = json.loads(sq.read_text())
-            counters = {k: d[k] for k in ("mfma_busy_per_simd", "wave_time_waiting", "valu_insts_per_mfma",
-                                          "lds_bank_conflict_share")}
-            counters["source"] = f"profiles/{sq.name}"
-        except (ValueError, KeyError):
-            counters = None
+    key = ("t1" if a.model == "bird" else "wrn") + ("" if dtype == torch.bfloat16 else "_fp32")
+    traffic, counters = dominant_evidence(key, a.batch == 512)
     clips = world * a.batch * a.steps
     value = clips / elapsed
     out = {
@@ -543,6 +563,8 @@ def run_inference(a):
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
     value = units * a.steps / elapsed
+    key = ("stream" if stream else "infer") + ("_fp32" if dtype == torch.float32 else "_bf16")
+    traffic, counters = dominant_evidence(key, bs == (1024 if stream else 256))
     out = {
         "metric": ("windows/sec streaming inference (60-min 48 kHz recording, 3 s / 1.5 s windows)" if stream
                    else "clips/sec inference (3s@48kHz, front end + PCEN + wr_resnet fwd)"),
@@ -557,7 +579,8 @@ def run_inference(a):
                    "units_per_step": units, "batch": bs},
         "roofline": {"kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t}", "bound": "mfma",
                      "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                     "traffic": None, "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch},
+                     "traffic": traffic, "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
+                     "counters": counters},
         "mel_pipeline": {"avg_launch_ms": round(mel_ms, 4),
                          "GBps": round(avg_clips * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2)},
     }

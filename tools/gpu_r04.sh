@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-4 GPU session: GPU parity tests + smoke, then for each workload a bench
+# line and a rocprofv3 kernel-trace summary of the same command.  Every GPU step
+# has its own time limit; the first failing step ends the script.
+# usage: tools/gpu_r04.sh <tag> [workloads...]   (workloads: tests t1 wrn t1fp32 infer stream)
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=${1:-r04}; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+step() { # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 $t "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -c 400 $O/$name.log; echo
+  [ $rc -eq 0 ] || exit $rc
+}
+bp() { # name benchargs...  (bench line + rocprof of the same command)
+  local name=$1; shift
+  step ${name}_bench 600 python bench.py "$@"
+  step ${name}_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${name}_prof -o run -- \
+      python bench.py --no-cpu-baseline "$@"
+}
+for w in "$@"; do
+  case $w in
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+           step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    t1) bp t1 --steps 20 --warmup 5 ;;
+    wrn) bp wrn --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    t1fp32) bp t1fp32 --dtype fp32 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    infer) bp infer --workload infer --steps 5 --warmup 2 ;;
+    stream) bp stream --workload stream --dtype fp32 --steps 3 --warmup 1 ;;
+  esac
+done
+echo done
