@@ -524,9 +524,13 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       dstat[h][1] += (double)sv[1];
     }
   };
-  // epilogue work in step cst (0..3), MFMA group grp; returns the number of
-  // vector-memory stores it issues (for the step's closing wait)
-  constexpr int EPI_STORES = PM == 1 ? 2 : 4;  // per step 0..3
+  // epilogue work in step cst (0..3), MFMA group grp.  EPI_LATE: its vector-
+  // memory stores issued AFTER the step's last weight piece (group 2), which
+  // the step's closing wait may leave in flight: PM 1 the store unit of group
+  // 4, PM 0 / 2 / 3 the unit of group 3 (the group-1 unit's stores precede the
+  // group-2 pieces and must not be counted, or the wait would let the last
+  // pieces land after the barrier)
+  constexpr int EPI_LATE = 2;  // per step 0..3
   auto epi_slot = [&](auto cstc, auto grpc, int ptm, bool live) __attribute__((always_inline)) {
     constexpr int cst = decltype(cstc)::value, grp = decltype(grpc)::value;
     if constexpr (PM == 1) {
@@ -563,7 +567,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       // vector-memory ops issued after this step's last weight piece, left in
       // flight by its closing wait: the next chunk's halo loads (rs == 1,
       // needed one step later) and the epilogue's stores
-      constexpr int NLATE = (rs == 1 ? XPT * (PM == 2 ? 2 : 1) : 0) + (cst <= 3 ? EPI_STORES : 0);
+      constexpr int NLATE = (rs == 1 ? XPT * (PM == 2 ? 2 : 1) : 0) + (cst <= 3 ? EPI_LATE : 0);
       const unsigned char* Xl = smem + rs * (HWX * XRB);
       // (this buffer's base as an opaque per-step value: the fragment row
       // addresses are formed once per step, the group offsets are immediates

@@ -27,6 +27,10 @@ for w in "$@"; do
     tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
+    t1old) ACFE_CONV1W64=0 bp t1old --steps 20 --warmup 5 --no-cpu-baseline ;;
+    wrnold) ACFE_CONV1W64=0 bp wrnold --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    convtests) step convtests 600 python -u -m pytest tests/test_production_gpu.py tests/test_fused_gpu.py \
+                 tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     wrn) bp wrn --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     t1fp32) bp t1fp32 --dtype fp32 --steps 10 --warmup 3 --no-cpu-baseline ;;
     infer) bp infer --workload infer --steps 5 --warmup 2 ;;
