@@ -124,6 +124,14 @@ class WRResNet(nn.Module):
             m.keras_auto = True
 
     def forward(self, x):
+        y = self.head_maps(x)
+        y = ops.logmeanexp(y, axis=1, sharpness=5)  # [N, W, classes]
+        y = ops.logmeanexp(y, axis=2, sharpness=5)  # [N, W]   (class axis, as in the reference)
+        return self.prediction(y)
+
+    def head_maps(self, x):
+        """The per-pixel class maps [N, h, w, classes] of conv2d_head_3
+        (wr_resnet_bird.py:69-70), before the two logmeanexp poolings."""
         if x.dim() == 4:
             x = x[..., 0]
         y, st = self.conv1_1(x, want_stats=True)
@@ -139,10 +147,7 @@ class WRResNet(nn.Module):
         y, st = self.head_conv2(y, want_stats=True)
         y = self.head_bn2(y, stats=st)
         y = ops.dropout(y, self.dropout, self.training)
-        y = self.head_conv3(y)
-        y = ops.logmeanexp(y, axis=1, sharpness=5)  # [N, W, classes]
-        y = ops.logmeanexp(y, axis=2, sharpness=5)  # [N, W]   (class axis, as in the reference)
-        return self.prediction(y)
+        return self.head_conv3(y)
 
     def predict(self, x):
         return ops.sigmoid(self.forward(x))

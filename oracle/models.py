@@ -97,8 +97,10 @@ def bird_block(X, p, pre, stride, relu_out, training=True, state=None, storage=N
     return _q(X, S)
 
 
-def wr_resnet_bird(x_nchw, p, training=True, state=None, depth=22, k=4, storage=None):
-    """wr_resnet_bird.WRResNet forward (:7-80) -> logits.  p: name -> tensor."""
+def wr_resnet_bird(x_nchw, p, training=True, state=None, depth=22, k=4, storage=None, head_maps=False):
+    """wr_resnet_bird.WRResNet forward (:7-80) -> logits.  p: name -> tensor.
+    head_maps: return conv2d_head_3's output [N, classes, h, w] instead (before
+    the logmeanexp poolings, :69-74)."""
     n = int((depth - 4) / 6)
     S = storage
     X = conv(x_nchw, p["conv1_1.weight"], p["conv1_1.bias"], storage=S)
@@ -115,6 +117,8 @@ def wr_resnet_bird(x_nchw, p, training=True, state=None, depth=22, k=4, storage=
     X = conv(X, p["head_conv2.weight"], p["head_conv2.bias"], storage=S)
     X = bn(X, p, "head_bn2", training, state=state, storage=S)
     X = conv(X, p["head_conv3.weight"], p["head_conv3.bias"], storage=S)
+    if head_maps:
+        return X
     X = X.permute(0, 2, 3, 1)  # NHWC for the Keras axis numbering of logmeanexp
     X = logmeanexp(X, axis=1)   # [N, W, classes]
     X = logmeanexp(X, axis=2)   # [N, W]

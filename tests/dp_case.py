@@ -1,6 +1,7 @@
 """The data-parallel GPU case shared by tests/test_dp_gpu.py and its rank
 processes (tests/dp_gpu_worker.py): the HIP Trainer on wr_resnet_bird (bf16,
-dropout 0, eval-mode BatchNormalization, PCEN on) fed by mix_up pairs of
+dropout 0, eval-mode BatchNormalization -- or training mode with per-replica
+statistics --, PCEN on) fed by mix_up pairs of
 synthetic 64-frame clips; a global batch of 8 split evenly over the ranks."""
 import torch
 
@@ -12,7 +13,9 @@ N_SAMPLES = 64 * 281        # 64 frames (pad_end): model input 128 x 64
 CLASSES = 10
 
 
-def make_trainer(dev, bucket_bytes=BUCKET_BYTES):
+def make_trainer(dev, bucket_bytes=BUCKET_BYTES, training=False):
+    """training: BatchNormalization in training mode (per-replica batch
+    statistics, MirroredStrategy's non-synced BN) instead of eval mode."""
     from acfe.train import FrontEnd, Trainer
     from resnet.wr_resnet_bird import WRResNet
 
@@ -33,7 +36,7 @@ def make_trainer(dev, bucket_bytes=BUCKET_BYTES):
     m = m.to(dev)
     fe = FrontEnd(n_mels=128, dtype=torch.bfloat16, device=dev, pcen=True).to(dev)
     tr = Trainer(m, fe, lr=0.01, loss="cce", device=dev, bucket_bytes=bucket_bytes)
-    tr.train(False)  # eval-mode BN: no statistics coupling the clips of a batch
+    tr.train(training)  # eval-mode BN: no statistics coupling the clips of a batch
     return tr
 
 

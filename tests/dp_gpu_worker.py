@@ -57,7 +57,8 @@ def main(out_prefix):
     from acfe import ops
 
     ops.set_seed_rank(rank)
-    tr = dp_case.make_trainer(dev, bucket_bytes=dp_case.BUCKET_BYTES)
+    training = os.environ.get("ACFE_DP_BN") == "train"
+    tr = dp_case.make_trainer(dev, bucket_bytes=dp_case.BUCKET_BYTES, training=training)
     assert tr.buckets is not None and tr.world == world
     x1, x2, lam, y = dp_case.batch(dev, rank, world)
     print(f"rank {rank}: step 1", flush=True)

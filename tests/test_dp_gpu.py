@@ -5,8 +5,9 @@ Two ranks are started as fresh child processes (tests/dp_gpu_worker.py) BEFORE
 this process touches the GPU; both run on cuda:0 with the gloo backend (RCCL
 refuses two ranks on one device; the collective sequence, the bucket
 machinery and the Trainer are the production ones).  Each rank trains one step
-on its half of the global batch (eval-mode BN, dropout 0, per-replica PCEN
-min/max as MirroredStrategy would run it).  This process then recomputes, on
+on its half of the global batch (dropout 0, per-replica PCEN min/max as
+MirroredStrategy would run it; BatchNormalization in eval mode, and once more
+in training mode with per-replica batch statistics).  This process then recomputes, on
 one GPU without any collective, the arena gradient of each half and checks:
 
 * the all-reduced arena on every rank == g(half 0) + g(half 1) bit for bit
@@ -45,8 +46,7 @@ def _free_port():
     return p
 
 
-@pytest.fixture(scope="module")
-def rank_results(tmp_path_factory):
+def _run_ranks(tmp_path_factory, bn_mode):
     if torch.cuda.device_count() < 1:  # counting devices does not initialise HIP
         pytest.skip("no GPU")
     out = tmp_path_factory.mktemp("dp") / "res"
@@ -54,7 +54,7 @@ def rank_results(tmp_path_factory):
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), ACFE_DP_BN=bn_mode)
         procs.append(subprocess.Popen([sys.executable, "-u", str(WORKER), str(out)], env=env))
     rcs = []
     for p in procs:
@@ -65,6 +65,19 @@ def rank_results(tmp_path_factory):
             rcs.append(p.wait())
     assert rcs == [0] * world, rcs
     return [torch.load(f"{out}.{r}.pt", weights_only=True) for r in range(world)]
+
+
+@pytest.fixture(scope="module")
+def rank_results(tmp_path_factory):
+    return _run_ranks(tmp_path_factory, "eval")
+
+
+@pytest.fixture(scope="module")
+def rank_results_train(tmp_path_factory):
+    """The same two ranks with training-mode BatchNormalization: each replica
+    normalises with its own half-batch statistics (Keras MirroredStrategy's
+    default non-synced BN)."""
+    return _run_ranks(tmp_path_factory, "train")
 
 
 @pytest.fixture(scope="module")
@@ -86,6 +99,9 @@ def rccl_result(rank_results, tmp_path_factory):
 
 
 def _half_grads(tr, dev, world):
+    """Each rank's half-batch gradient recomputed in this process (in the
+    trainer's BN mode: training mode normalises each half with its own
+    statistics, as each replica does)."""
     from acfe import ops
 
     import dp_case
@@ -116,11 +132,13 @@ def test_rccl_bucket_allreduce_executes(rccl_result, cuda):
     assert torch.equal(rccl_result["grad"], g[0].cpu())
 
 
-def test_dp_step_matches_single_process(rank_results, cuda):
+@pytest.mark.parametrize("bn_mode", ["eval", "train"])
+def test_dp_step_matches_single_process(request, cuda, bn_mode):
     import dp_case
 
+    rank_results = request.getfixturevalue("rank_results" if bn_mode == "eval" else "rank_results_train")
     world = len(rank_results)
-    tr = dp_case.make_trainer(cuda)
+    tr = dp_case.make_trainer(cuda, training=bn_mode == "train")
     assert tr.buckets is None  # single process: no collective
     p0 = tr.arena.flat.detach().clone()
     grads, losses = _half_grads(tr, cuda, world)
