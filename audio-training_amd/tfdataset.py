@@ -25,6 +25,18 @@ Pipeline (every record is inflated and parsed ONCE):
                    example is a primary exactly once per epoch (one pass, as
                    the reference's dataset)
 
+cache=True (the reference's dataset.cache(), "Caching to mem",
+tfdataset.py:792-793, 832-834): the decoded clips are kept in HBM.  The first
+epoch streams as above into a pool sized for the whole epoch whose slots are
+never recycled; once it has run to its end, later epochs start no reader
+threads at all -- the same shuffle buffer is fed from the resident clips in
+their decode order, so an epoch costs device gathers only (288 GB of HBM hold
+~250 000 decoded 3 s clips; the default budget is half of the device's
+memory, beyond it the dataset streams every epoch).  The reference turns its
+cache off for mix_up training (tfdataset.py:469-470) because its partners come
+from a second, independently shuffled pipeline; here partners are drawn from
+the resident pool, so the cache applies to mix_up training as well.
+
 mix_up partners.  The reference zips a second, independently shuffled full
 pass over the same records (tfdataset.py:473-480), i.e. it decodes every
 record twice to pair each example with a random other example.  Here the
@@ -151,13 +163,16 @@ class AudioDataset:
 
     def __init__(self, files, labels, batch_size=32, shuffle=True, augment=False, device=None, threads=8,
                  drop_remainder=False, seed=0, label_map=None, record_shard=None, load_raw=True,
-                 shuffle_buffer=SHUFFLE_BUFFER, epoch_size=None):
+                 shuffle_buffer=SHUFFLE_BUFFER, epoch_size=None, cache=False, cache_bytes=None):
         """record_shard=(rank, world): keep only the records whose (file index
         + record index) % world == rank -- data-parallel sharding when there
         are fewer shard files than ranks (otherwise ranks take whole files).
         load_raw=False: batches of the stored magnitude spectrograms
         [B, 2049, 513] (audio/spectogram, tfdataset.py:1032-1034, 1081-1082);
-        there is no mix_up on that path (tfdataset.py:503-504)."""
+        there is no mix_up on that path (tfdataset.py:503-504).
+        cache: keep the decoded clips device-resident after the first full
+        epoch (module docstring); cache_bytes caps the device memory it may
+        take (default: half of the device's memory)."""
         self.files, self.labels = list(files), list(labels)
         self.record_shard = record_shard
         self.load_raw = load_raw
@@ -184,6 +199,9 @@ class AudioDataset:
         self._stage_buf = None
         self._last_ev = None  # event after the newest gathers from the pool (orders the next epoch's refills)
         self.error = None
+        self.cache = bool(cache)
+        self.cache_bytes = cache_bytes
+        self._cached = None  # (pool rows in decode order, slot labels) once a whole epoch is resident
 
     # ---------------------------------------------------------------- counting
     def _label_of(self, text: str):
@@ -287,6 +305,27 @@ class AudioDataset:
                 logging.warning("skipping shard %s: %s", path, e)
 
     # ---------------------------------------------------------------- pool
+    def _cache_plan(self) -> bool:
+        """Can the whole epoch be kept resident?  If so the pool is sized for it."""
+        if not self.cache:
+            return False
+        n = self.count()
+        budget = self.cache_bytes
+        if budget is None:
+            budget = (torch.cuda.get_device_properties(self.device).total_memory // 2 if self.device.type == "cuda"
+                      else 1 << 30)
+        need = (n + self.per_chunk) * 4 * self.nfloats
+        if need > budget:
+            logging.warning("dataset cache: %d clips need %.1f GB > budget %.1f GB; streaming every epoch", n,
+                            need / 1e9, budget / 1e9)
+            self.cache = False
+            return False
+        rows = max(self.pool_rows, n + self.per_chunk)
+        if self._pool is not None and self._pool.shape[0] < rows:
+            self._pool = None
+        self.pool_rows = rows
+        return True
+
     def _ensure_pool(self):
         if self._pool is None:
             self._pool = torch.empty((self.pool_rows, self.nfloats), dtype=torch.float32, device=self.device)
@@ -366,11 +405,62 @@ class AudioDataset:
             logging.exception("loader mover thread failed")
             ready.put(None)
 
+    def _draw(self, rng, live, used, target, done, augment):
+        """One batch from the shuffle buffer `live` (uniform draw without
+        replacement) and its mix_up partners -> (pick, partner)."""
+        b = min(self.batch_size, len(live))
+        if self.shuffle:
+            pick = []
+            for _ in range(b):  # uniform draw without replacement (swap-remove)
+                j = rng.randrange(len(live))
+                live[j], live[-1] = live[-1], live[j]
+                pick.append(live.pop())
+        else:
+            pick = live[:b]
+            del live[:b]
+        partner = None
+        if augment:
+            # mix_up partners: any resident clip.  Once the readers are done
+            # (nothing refills a released slot any more) the clips of the last
+            # `target` primaries stay valid partners too, so the tail batches
+            # do not shrink to pairing the batch with itself (the reference
+            # draws partners from an independent second pass, tfdataset.py:473-480)
+            resident = live + pick + (used[-target:] if done else [])
+            partner = [resident[rng.randrange(len(resident))] for _ in range(b)]
+        used.extend(pick)
+        if len(used) > 2 * target:
+            del used[:-target]
+        return pick, partner
+
+    def _stream_cached(self, augment, rng):
+        """An epoch over the device-resident clips: the shuffle buffer is fed
+        from the cache in decode order (no reader threads, no host copies)."""
+        order, lab = self._cached
+        slots = _SlotPool(0)  # nothing is ever refilled: releases are no-ops
+        slots.keep = True
+        target = self.buffer if self.shuffle else self.batch_size
+        live: list[int] = []
+        used: list[int] = []
+        pos = 0
+        while True:
+            while pos < len(order) and len(live) < target:
+                live.append(order[pos])
+                pos += 1
+            done = pos == len(order)
+            if len(live) < self.batch_size and (not live or self.drop_remainder):
+                return
+            pick, partner = self._draw(rng, live, used, target, done, augment)
+            yield pick, partner, lab, slots
+
     def _stream(self, augment):
         """Generator of (primary slots, partner slots or None, slot labels,
         slot pool) per batch of one epoch."""
-        files = list(self.files)
         rng = random.Random(self.seed + 1000003 * self.epoch)
+        if self._cached is not None:
+            yield from self._stream_cached(augment, rng)
+            return
+        caching = self._cache_plan()
+        files = list(self.files)
         if self.shuffle:
             rng.shuffle(files)  # load_dataset shuffles the file names (tfdataset.py:195-197)
         stable = {f: i for i, f in enumerate(self.files)}
@@ -387,6 +477,8 @@ class AudioDataset:
         # the previous epoch's last gathers may still be queued on the compute
         # stream: the first refill of this epoch waits for their event
         slots = _SlotPool(self.pool_rows, self._last_ev)
+        slots.keep = caching  # caching epoch: every clip keeps its slot
+        order: list[int] = []  # caching: slots in decode order
         ready: queue.Queue = queue.Queue()
         nthreads = min(self.threads, max(1, len(files)))
         readers = [threading.Thread(target=self._reader, args=(fq, stage, stop, stable), daemon=True)
@@ -422,34 +514,18 @@ class AudioDataset:
                     dst, labels = item
                     lab[dst] = labels
                     live.extend(dst)
+                    if caching:
+                        order.extend(dst)
                 if self.error is not None:
                     raise RuntimeError("TFRecord loader failed") from self.error
                 if len(live) < self.batch_size:  # the stream has ended (the fill loop stops only then)
                     if not live or self.drop_remainder:
-                        return
-                b = min(self.batch_size, len(live))
-                if self.shuffle:
-                    pick = []
-                    for _ in range(b):  # uniform draw without replacement (swap-remove)
-                        j = rng.randrange(len(live))
-                        live[j], live[-1] = live[-1], live[j]
-                        pick.append(live.pop())
-                else:
-                    pick, live = live[:b], live[b:]
-                partner = None
-                if augment:
-                    # mix_up partners: any resident clip.  Once the readers are
-                    # done (nothing refills a released slot any more) the clips
-                    # of the last `target` primaries stay valid partners too,
-                    # so the tail batches do not shrink to pairing the batch
-                    # with itself (the reference draws partners from an
-                    # independent second pass, tfdataset.py:473-480)
-                    resident = live + pick + (used[-target:] if done else [])
-                    partner = [resident[rng.randrange(len(resident))] for _ in range(b)]
-                used.extend(pick)
-                if len(used) > 2 * target:
-                    del used[:-target]
+                        break
+                pick, partner = self._draw(rng, live, used, target, done, augment)
                 yield pick, partner, lab, slots
+            if caching and done and self.error is None:
+                # the whole epoch went through: later epochs run from the device
+                self._cached = (order, lab.copy())
         finally:
             stop.set()
             for t in readers + [watcher, mover]:
@@ -506,11 +582,13 @@ class _SlotPool:
     def __init__(self, rows, ev=None):
         self.free = list(range(rows - 1, -1, -1))
         self.ev = ev
+        self.keep = False  # dataset cache: released slots keep their clips
         self.cv = threading.Condition()
 
     def release(self, rows, ev):
         with self.cv:
-            self.free.extend(rows)
+            if not self.keep:
+                self.free.extend(rows)
             if ev is not None:
                 self.ev = ev
             self.cv.notify_all()
@@ -553,7 +631,8 @@ def get_dataset(dir, labels, global_epoch=None, **args):
     shard and checks every record's label and float list -- a full decode
     pass at startup -- unless args["epoch_size"] gives the number).  Extra keys
     accepted here: device, threads, seed, label_map, record_shard, files,
-    drop_remainder, shuffle_buffer."""
+    drop_remainder, shuffle_buffer, cache_bytes; cache (the reference's
+    dataset.cache(), off unless asked for) keeps the decoded clips in HBM."""
     global N_MELS, FMIN, FMAX, NFFT, BREAK_FREQ
     if args.get("n_mels"):
         N_MELS = args["n_mels"]
@@ -574,7 +653,8 @@ def get_dataset(dir, labels, global_epoch=None, **args):
                       threads=args.get("threads", 8), seed=args.get("seed", 0),
                       drop_remainder=args.get("drop_remainder", False), label_map=args.get("label_map"),
                       record_shard=args.get("record_shard"), load_raw=load_raw,
-                      shuffle_buffer=args.get("shuffle_buffer", SHUFFLE_BUFFER), epoch_size=args.get("epoch_size"))
+                      shuffle_buffer=args.get("shuffle_buffer", SHUFFLE_BUFFER), epoch_size=args.get("epoch_size"),
+                      cache=args.get("cache", False), cache_bytes=args.get("cache_bytes"))
     epoch_size = ds.count()
     logging.info("dataset %s: %d shards, %d labels, %d examples", dir, len(files), len(labels), epoch_size)
     return ds, remapped, epoch_size, labels, {}

@@ -220,3 +220,68 @@ def test_back_to_back_epochs_keep_gathered_clips(shards, cuda):
         for xb, yb in ((x, y), (x2, y2)):
             for k, row in zip(_ids(xb.cpu()), yb.cpu()):
                 assert k in keep and _label_ok(k, row), k
+
+
+def test_dataset_cache_epochs(shards, monkeypatch):
+    """cache=True (the reference's dataset.cache(), tfdataset.py:792-793): the
+    first full epoch streams from the shards and keeps every clip resident;
+    later epochs start no reader threads, still yield every kept example
+    exactly once with its label, reshuffled, with mix_up partners from the
+    resident clips; an epoch broken off early caches nothing."""
+    import tfdataset
+
+    d, keep = shards
+    ds = tfdataset.AudioDataset(tfdataset._files(d), ["bird", "noise"], batch_size=8, device="cpu", threads=3,
+                                shuffle_buffer=16, augment=True, cache=True)
+    it = iter(ds)
+    next(it)
+    it.close()
+    assert ds._cached is None  # broken off: not cached
+    orders = []
+    for epoch in range(3):
+        if epoch == 2:  # cached epochs never touch the shards
+            monkeypatch.setattr(tfdataset.AudioDataset, "_reader", lambda *a, **k: (_ for _ in ()).throw(
+                AssertionError("reader started on a cached epoch")))
+        seen = []
+        for (x1, y1), (x2, y2) in ds:
+            for k, row in zip(_ids(x1), y1):
+                assert _label_ok(k, row), k
+            for k, row in zip(_ids(x2), y2):
+                assert k in keep and _label_ok(k, row), k
+            seen += _ids(x1)
+        assert sorted(seen) == keep
+        orders.append(seen)
+        assert ds._cached is not None
+    assert orders[1] != orders[2]  # reshuffled every epoch
+
+
+def test_dataset_cache_over_budget_streams(shards):
+    import tfdataset
+
+    d, keep = shards
+    ds = tfdataset.AudioDataset(tfdataset._files(d), ["bird", "noise"], batch_size=8, device="cpu", threads=3,
+                                shuffle_buffer=16, cache=True, cache_bytes=4 * N * 10)
+    for _ in range(2):
+        assert sorted(k for x, _ in ds for k in _ids(x)) == keep
+    assert ds._cached is None and not ds.cache
+
+
+@pytest.mark.gpu
+def test_dataset_cache_on_device(shards, cuda):
+    """The HBM-resident cache on the GPU: epochs 2-3 gather every kept clip
+    (with its label) from the device pool the first epoch filled."""
+    import tfdataset
+
+    d, keep = shards
+    ds = tfdataset.AudioDataset(tfdataset._files(d), ["bird", "noise"], batch_size=8, device=cuda, threads=3,
+                                shuffle_buffer=16, augment=True, cache=True)
+    for epoch in range(3):
+        seen = []
+        for (x1, y1), (x2, y2) in ds:
+            for k, row in zip(_ids(x1.cpu()), y1.cpu()):
+                assert _label_ok(k, row), k
+            for k, row in zip(_ids(x2.cpu()), y2.cpu()):
+                assert k in keep and _label_ok(k, row), k
+            seen += _ids(x1.cpu())
+        assert sorted(seen) == keep
+        assert ds._cached is not None

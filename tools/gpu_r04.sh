@@ -26,6 +26,13 @@ for w in "$@"; do
   case $w in
     tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
            step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    testsall) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/testsall.log 2>&1
+              rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
+              case $rc in 0|1) ;; *) exit $rc ;; esac ;;
+    melab) step mel_w3 300 python tools/mel_bench.py --iters 15
+           ACFE_MEL_W2=1 step mel_w2 300 python tools/mel_bench.py --iters 15
+           step mel_w3b 300 python tools/mel_bench.py --iters 15 ;;
+    dpold) ACFE_CONV1W64=0 step dpold 600 python -u -m pytest tests/test_dp_gpu.py -m gpu -v --timeout 240 --timeout-method thread ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
     t1old) ACFE_CONV1W64=0 bp t1old --steps 20 --warmup 5 --no-cpu-baseline ;;
     wrnold) ACFE_CONV1W64=0 bp wrnold --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
