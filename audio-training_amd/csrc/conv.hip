@@ -3060,13 +3060,6 @@ static int pick_bn(int K) { return K <= 32 ? 32 : (K <= 64 ? 64 : 128); }
 
 
 
-// ACFE_CONV1W64=0: the K = 64 3x3 layers stay on the 8-wave rows kernel
-// (same-box A/B of the one-wave kernel, conv1w64.hip)
-static bool use_conv1w64() {
-  static const bool on = !(getenv("ACFE_CONV1W64") && atoi(getenv("ACFE_CONV1W64")) == 0);
-  return on;
-}
-
 // k_conv3x3_narrow with 8 waves per workgroup (4 waves measured slower, r02v)
 template <int KB, int SW>
 static void launch_narrow(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
@@ -3105,10 +3098,6 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
         if constexpr (BN == 128) {
           // one wave per SIMD (pool1w.hip), the previous tile's epilogue beside this tile's MFMAs
           const int rc = launch_plain1w(g, x, wp, bias, y, stats, grid_m, s, "acfe_conv2d_fwd", 0);
-          if (rc != ACFE_E_INVAL) return rc;
-        } else if (use_conv1w64()) {
-          // K = 64: one wave per SIMD as well (conv1w64.hip)
-          const int rc = launch_conv1w64(g, x, wp, bias, y, stats, grid_m, s, "acfe_conv2d_fwd", 0);
           if (rc != ACFE_E_INVAL) return rc;
         }
 #define ROWS(TR_, PM_, ...)                                                                                   \
@@ -3699,14 +3688,6 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
     return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
   } else {
     static_assert(KB == 64, "rows kernels: K in {64, 128}");
-    if constexpr (PM == 0 || PM == 3 || PM == 4) {
-      // plain / dropout / residual-add forwards and stride-1 dgrads (with or
-      // without the BN prologue) on the one-wave K = 64 kernel (conv1w64.hip)
-      if (use_conv1w64()) {
-        const int rc = launch_conv1w64(g, x, wp, bias, y, stats, srows, s, what, PM == 3 ? 3 : 0);
-        if (rc != ACFE_E_INVAL) return rc;
-      }
-    }
     if constexpr (PM != 2) {
       // BatchNormalization prologue (acfe_conv2d_bn_prologue_supported)
       if (g.pro_sc) return launch_rows_tr<KB, PM, 8, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);

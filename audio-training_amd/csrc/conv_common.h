@@ -131,11 +131,6 @@ int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float*
 // (pm 0: plain / dropout / BN sums; pm 3: + the residual g.res (+ReLU) of acfe_conv2d_fwd_add)
 int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                    int srows, hipStream_t s, const char* what, int pm);
-// 3x3 stride-1 forward / dgrad at K = 64, C = 64 / 128 on the one-wave K = 64
-// kernel (conv1w64.hip): pm 0 plain / dropout / BN sums, pm 3 + residual; the
-// BatchNormalization prologue when g.pro_sc is set
-int launch_conv1w64(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
-                    int srows, hipStream_t s, const char* what, int pm);
 // acfe_conv2d_dgrad_unpool at K = C = 128 on the same kernel (PM 2)
 int launch_unpool1w(const ConvGeom& g, const void* dyp, const void* wflip, void* dx, uint8_t* amax, hipStream_t s,
                     const char* what);

@@ -98,7 +98,7 @@ ACFE_API int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmi
     band[3 * m + 1] = e - s + 1;
     band[3 * m + 2] = (int)vals.size();
     for (int k = s; k <= e; ++k) vals.push_back(w_host[(size_t)m * nb + k]);
-    while (vals.size() & 7) vals.push_back(0.f);  // k_mel_w2 reads whole 8-tap groups
+    while (vals.size() & 7) vals.push_back(0.f);  // k_mel_w3 reads whole 8-tap groups
     kmin = s < kmin ? s : kmin;
     kmax = e > kmax ? e : kmax;
   }
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(1024) k_norm_stats(const float* __restrict__ x
 // norm1 with the division as a multiply by rinv = RN(1 / rng) and one FMA
 // correction (Markstein): q = RN(t rinv), e = t - rng q (exact by FMA),
 // RN(q + e rinv) = RN(t / rng) -- the correctly rounded quotient without the
-// ~10-instruction division sequence (k_mel_w2 divides every sample of every
+// ~10-instruction division sequence (k_mel_w3 divides every sample of every
 // overlapping frame; exhaustive-style check of the identity: 20 000 random
 // float32 pairs incl. all-ones-mantissa divisors, exact rational arithmetic)
 __device__ __forceinline__ float norm1r(float v, float mn, float rng, float rinv) {
@@ -498,11 +498,8 @@ __global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int6
   }
 }
 
-// ---- wave-per-frame variant for n_fft = 4096 (NC = 2048 = 16 x 16 x 8).
-// One 64-lane workgroup owns its frames end to end: the three Stockham passes
-// (radix 16, 16, 8) keep every butterfly in VGPRs and exchange through the
-// wave's own LDS slice, so no workgroup of 4 waves waits at a barrier for its
-// slowest global load; 6-7 independent waves per CU hide each other's latency.
+// ---- n_fft = 4096 (NC = 2048 = 16 x 16 x 8): radix-16 / 16 / 8 Stockham
+// passes with every butterfly in VGPRs (k_mel_w3 below).
 template <>
 __device__ __forceinline__ void dft<16>(float2* v) {
   // X[k1 + 4 k2] = DFT4_{n2}( W16^{n2 k1} * DFT4_{n1}(x[4 n1 + n2])[k1] )
@@ -532,11 +529,8 @@ __device__ __forceinline__ void dft<16>(float2* v) {
   }
 }
 
-// In-place Stockham pass over the wave's NC points, span NS, radix R: all of a
-// lane's butterfly inputs are read before any output is written.  NB and NS
-// are multiples of 8, so every padded LDS address is the lane's base plus a
-// compile-time offset; the twiddles W^{r t} come from W^t, W^{2t}, W^{4t},
-// W^{8t} (at most two extra complex products each).
+// The twiddles W^{r t} of a radix-R butterfly from W^t, W^{2t}, W^{4t}, W^{8t}
+// (at most two extra complex products each).
 template <int R>
 __device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
   // bw = {W^t, W^2t, W^4t, W^8t}
@@ -554,66 +548,84 @@ __device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
   }
 }
 
-// n_fft = 4096: two waves per frame (128 threads).  2048-point complex FFT of
-// the even/odd sample pairs (the 4096-point real FFT) as radix-16/16/8
-// Stockham passes in an 18 KB LDS frame buffer, base twiddles held in VGPRs
-// (their powers recomputed per frame), real-FFT post-processing + |X|^power on
-// bins kmin..kmax, then the banded mel sums.  Each lane holds half of a
-// one-wave design's butterflies, so a wave needs <= 168 VGPRs: 12 waves per CU
-// (the one-wave-per-frame kernel it replaced ran 8, limited by LDS and 206
-// VGPRs; its waves sat waiting 41 % of their time, rocprofv3 SQ counters r02n).
-// k_mel_w2's LDS index: one float2 of padding per 16 points: pass-1 rows
-// (stride 17), pass-2/3 stores (16-lane groups of consecutive points) are
-// bank-conflict free; the 32-lane reads keep one colliding lane pair (the
-// one-wave kernel's pad-per-8 layout had 50 % of its LDS cycles in conflicts,
-// SQ counters r02n)
-__device__ __forceinline__ int padx16(int i) { return i + (i >> 4); }
+// ---- k_mel_w3 (n_fft = 4096): two waves (128 threads) per frame, 4 frames
+// per workgroup.  Frame + periodic Hann (computed, not loaded) + the 4096-point
+// real FFT as a 2048-point complex FFT of the even / odd sample pairs (radix
+// 16 / 16 / 8 Stockham passes through a 16 KB LDS frame buffer, base twiddles
+// held in VGPRs and their powers recomputed per frame) + real-FFT
+// post-processing and |X|^power of bins kmin..kmax + the banded mel sums (one
+// band per lane, zero-padded 8-tap groups).  r04 over the r02-r03 kernel
+// (k_mel_w2: padded LDS, pass-3 results stored and re-read by the
+// post-processing, 148 VGPRs): one LDS round trip fewer, no bank conflicts,
+// 128 VGPRs (4 waves per SIMD); T1 1.16 -> 0.91 ms per 512 clips.
+//  * LDS holds the 2048 points unpadded under the XOR swizzle msw(i): the low
+//    five bits (the float2's bank group in a 32-lane half-wave) are XORed with
+//    bits 5..8 (and bit 8 into bit 4), so the pass-1 rows (stride 16), the
+//    pass-2 / pass-3 reads (consecutive points per half-wave) and the pass-2
+//    stores (two 16-point runs 256 apart) all hit 32 distinct bank pairs.
+//  * Pass 3 (radix 8, span 256) gives lane t the butterflies j0 = t and
+//    j1 = 256 - t (j1 = 128 for t = 0), i.e. the complex bins j + 256 r that
+//    the real-FFT post-processing pairs as k <-> 2048 - k: the |X|^power of
+//    every bin is formed from the lane's own registers, with the post twiddle
+//    W_4096^k = W_4096^j W_16^r from one per-lane base, and written straight
+//    into the power vector (aliased onto the FFT buffer: 16 KB of LDS per
+//    workgroup).
+__device__ __forceinline__ int msw(int i) { return i ^ ((i >> 5) & 15) ^ (((i >> 8) & 1) << 4); }
 
-template <int NC, int R, int NS, int NT>
-__device__ __forceinline__ void stockham_pass_t(float2* buf, const float2 (*bw)[4], int tid) {
-  constexpr int NB = NC / R, PER = NB / NT;
-  static_assert(NB % NT == 0 && NB % 8 == 0 && NS % 8 == 0, "pass shape");
-  float2 v[PER][R];
-#pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    const int j = tid + NT * p;
-    const float2* src = buf + padx16(j);
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[p][r] = src[r * (NB + NB / 16)];
-    float2 w[R];
-    twiddle_pows<R>(bw[p], w);
-#pragma unroll
-    for (int r = 1; r < R; ++r) v[p][r] = cmul(v[p][r], w[r]);
+// W_16^r = exp(-2 pi i r / 16)
+__device__ __forceinline__ float2 w16(int r) {
+  constexpr float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f, h = 0.70710678118654752440f;
+  switch (r & 15) {
+    case 0: return make_float2(1.f, 0.f);
+    case 1: return make_float2(c1, -s1);
+    case 2: return make_float2(h, -h);
+    case 3: return make_float2(s1, -c1);
+    case 4: return make_float2(0.f, -1.f);
+    case 5: return make_float2(-s1, -c1);
+    case 6: return make_float2(-h, -h);
+    case 7: return make_float2(-c1, -s1);
+    case 8: return make_float2(-1.f, 0.f);
+    case 9: return make_float2(-c1, s1);
+    case 10: return make_float2(-h, h);
+    case 11: return make_float2(-s1, c1);
+    case 12: return make_float2(0.f, 1.f);
+    case 13: return make_float2(s1, c1);
+    case 14: return make_float2(h, h);
+    default: return make_float2(c1, s1);
   }
-  __syncthreads();  // every lane's reads precede the in-place writes of the other wave
-#pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    const int j = tid + NT * p, jm = j & (NS - 1);
-    dft<R>(v[p]);
-    float2* dst = buf + padx16((j / NS) * NS * R + jm);
-#pragma unroll
-    for (int r = 0; r < R; ++r) dst[r * (NS + NS / 16)] = v[p][r];
-  }
-  __syncthreads();
 }
 
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3)))
-k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restrict__ stats, int pad_mode, int power,
+// real-FFT bin from the complex bins zk = Z[k], zm = Z[2048 - k] and W_4096^k
+__device__ __forceinline__ float rbin_power(float2 zk, float2 zm, float2 rt) {
+  const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+  const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
+  const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
+  const float2 X = cadd(E, cmul(rt, O));
+  return X.x * X.x + X.y * X.y;
+}
+
+// LDS float2 at byte address a of the frame buffer
+__device__ __forceinline__ float2& lds2(float2* buf, unsigned a) {
+  return *reinterpret_cast<float2*>(reinterpret_cast<char*>(buf) + a);
+}
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
+k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restrict__ stats, int pad_mode, int power,
          int n_frames, int fpw, int hop, const float2* __restrict__ tw, const float2* __restrict__ rtw,
-         const float* __restrict__ win, const int* __restrict__ band, const float* __restrict__ vals, int n_mels,
-         int kmin, int kmax, float* __restrict__ out, int layout) {
-  constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16, NT = 128;
+         const int* __restrict__ band, const float* __restrict__ vals, int n_mels, int kmin, int kmax,
+         float* __restrict__ out, int layout) {
+  constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16;
   extern __shared__ float2 wbuf[];
+  float* pw = reinterpret_cast<float*>(wbuf);
   const int nk = kmax - kmin + 1;
-  const bool alias = nk <= 1024;
-  float* pw = alias ? reinterpret_cast<float*>(wbuf) : reinterpret_cast<float*>(wbuf + NC + NC / 16);
   const int tid = threadIdx.x;
   // XCD-aware work order: the hardware places workgroup L (x fastest) on XCD
   // L % 8, so consecutive frame groups of a clip -- whose 4096-sample frames
   // overlap by ~3.6 groups -- would land in eight different L2s and each
   // fetch the clip's samples again.  Give every XCD a contiguous range of
   // (clip, frame group) items instead (a bijection when the count is a
-  // multiple of 8; otherwise the plain order).
+  // multiple of 8; otherwise the plain order; r03: 1.35 -> 0.30 GB of HBM
+  // reads per launch).
   const int gx = gridDim.x, nwg = gx * gridDim.y, lin = blockIdx.x + gx * blockIdx.y;
   const int item = nwg % 8 == 0 ? (lin % 8) * (nwg / 8) + lin / 8 : lin;
   const int b = item / gx;
@@ -622,42 +634,61 @@ k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
   const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
   const float rinv = __fdiv_rn(1.0f, rng);
   const int f0 = (item - b * gx) * fpw;
-  // base twiddles: pass 2 (jm = j & 15), pass 3 (jm = j, two butterflies per lane)
-  float2 bw2[1][4], bw3[2][4];
+  const int j0 = tid, j1 = tid ? 256 - tid : 128;
+  // base twiddles held across frames: pass 2 W^{8 (t & 15) 2^q}, pass 3
+  // W^{t 2^q}, post W_4096^t; the j1 = 256 - t ones follow per frame as
+  // W^{256 2^q} conj(W^{t 2^q}) and W_16 conj(W_4096^t) (lane 0: j1 = 128)
+  float2 bw2[1][4], e0[3], rb0;
   {
     const int t = (tid & 15) * 8;
 #pragma unroll
     for (int q = 0; q < 4; ++q) bw2[0][q] = tw[(t << q) & (NC - 1)];
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) bw3[p][q] = tw[((tid + NT * p) << q) & (NC - 1)];
-      bw3[p][3] = make_float2(1.f, 0.f);
-    }
+    for (int q = 0; q < 3; ++q) e0[q] = tw[(j0 << q) & (NC - 1)];
+    rb0 = rtw[j0];
   }
+  // swizzled byte addresses: every access of a pass is its lane base XOR a
+  // compile-time constant (+ an immediate offset), see msw():
+  //   pass-1 rows  msw(16 j + r)            = msw(16 j) ^ r
+  //   pass-2 reads msw(j + 128 r)           = (msw(j) ^ C_r) + 128 r
+  //   pass-2 rows  msw(256 J + x + 16 r)    = (256 J + (x ^ 24 (J & 1)) ^ E_r) + 32 (r >> 1)
+  //   pass-3 reads msw(j + 256 r)           = (msw(j) ^ 24 (r & 1)) + 256 r
+  const unsigned ua = (unsigned)msw(16 * tid) * 8u, ub = (unsigned)msw(tid) * 8u;
+  const unsigned uc = (unsigned)(256 * (tid >> 4) + ((tid & 15) ^ (24 * ((tid >> 4) & 1)))) * 8u;
+  const unsigned ud0 = (unsigned)msw(j0) * 8u, ud1 = (unsigned)msw(j1) * 8u;
   for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
-    int zo;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
-    const float* winf = win + zo;
+    // (per frame: keeps the compiler from hoisting ~100 LDS addresses and
+    // twiddle products out of the loop into spilled registers)
+    unsigned aa = ua, ab = ub, ac = uc, ad0 = ud0, ad1 = ud1;
+    asm volatile("" : "+v"(aa), "+v"(ab), "+v"(ac), "+v"(ad0), "+v"(ad1));
+    asm volatile("" : "+v"(rb0.x), "+v"(rb0.y));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      asm volatile("" : "+v"(bw2[0][q].x), "+v"(bw2[0][q].y));
+    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(bw2[0][q].x), "+v"(bw2[0][q].y));
 #pragma unroll
-      for (int p = 0; p < 2; ++p) asm volatile("" : "+v"(bw3[p][q].x), "+v"(bw3[p][q].y));
-    }
+    for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(e0[q].x), "+v"(e0[q].y));
     const int start = (pad_mode == ACFE_PAD_END) ? f * hop : f * hop - L / 2;
     const bool inb = start >= 0 && start + L <= n;
-    __syncthreads();  // the previous frame's readers of wbuf / pw are done
+    __syncthreads();  // the previous frame's readers of pw are done
+    // ---- pass 1 (radix 16, span 1) straight from memory: rows 16 t + r
     {
       const int j = tid;
       float xa[16], xc[16], wa[16], wc[16];
-      // sample and window pairs as 8-B loads (4-B aligned: the hop is odd)
       typedef float f2a __attribute__((ext_vector_type(2), aligned(4)));
-      const float* ws = winf + 2 * j;
+      // periodic Hann w[n] = 0.5 - 0.5 cos(2 pi n / 4096) of samples
+      // n = 2 j + 256 r (+1): cos(theta + 2 pi r / 16) from the lane's
+      // cos / sin theta (theta_e = 2 pi j / 2048 = arg conj(W^j), theta_o =
+      // theta_e + 2 pi / 4096) -- no window loads, no window registers
+      {
+        const float ce = e0[0].x, se = -e0[0].y;
+        constexpr float c1 = 0.99999882345170190993f, s1 = 0.00153398018628476550f;  // cos / sin (2 pi / 4096)
+        const float co = ce * c1 - se * s1, so = se * c1 + ce * s1;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const f2a w2 = *reinterpret_cast<const f2a*>(ws + 2 * r * NB0);
-        wa[r] = w2[0], wc[r] = w2[1];
+        for (int r = 0; r < 16; ++r) {
+          const float2 u = w16(r);  // (cos phi, -sin phi), phi = 2 pi r / 16
+          // 0.5 - 0.5 (cos t cos phi - sin t sin phi)
+          wa[r] = __builtin_fmaf(se, -0.5f * u.y, __builtin_fmaf(ce, -0.5f * u.x, 0.5f));
+          wc[r] = __builtin_fmaf(so, -0.5f * u.y, __builtin_fmaf(co, -0.5f * u.x, 0.5f));
+        }
       }
       if (inb) {
         const float* xs = xb + start + 2 * j;
@@ -688,46 +719,83 @@ k_mel_w2(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
         for (int r = 0; r < 16; ++r) v[r] = make_float2(xa[r] * wa[r], xc[r] * wc[r]);
       }
       dft<16>(v);
-      float2* dst = wbuf + j * 17;  // padx16(16 j + r) = 17 j + r
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dst[r] = v[r];
+      for (int r = 0; r < 16; ++r) lds2(wbuf, aa ^ (8u * r)) = v[r];
     }
     __syncthreads();
-    stockham_pass_t<NC, 16, 16, NT>(wbuf, bw2, tid);
-    stockham_pass_t<NC, 8, 256, NT>(wbuf, bw3, tid);
-    for (int i0 = 0; i0 < nk; i0 += 1024) {  // uniform: every thread reaches the barrier
-      float2 rt[8];
-      float pv[8];
+    // ---- pass 2 (radix 16, span 16)
+    {
+      float2 v[16], w[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + tid + NT * u;
-        rt[u] = i < nk ? rtw[kmin + i] : make_float2(0.f, 0.f);
+      for (int r = 0; r < 16; ++r) {
+        const unsigned cr = (unsigned)((4 * r & 12) ^ (((r >> 1) & 1) << 4));
+        v[r] = lds2(wbuf, (ab ^ (8u * cr)) + 1024u * r);
       }
+      twiddle_pows<16>(bw2[0], w);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + tid + NT * u;
-        pv[u] = 0.f;
-        if (i < nk) {
-          const int k = kmin + i;
-          const float2 zk = wbuf[padx16(k & (NC - 1))];
-          const float2 zm = wbuf[padx16((NC - k) & (NC - 1))];
-          const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-          const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
-          const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
-          const float2 X = cadd(E, cmul(rt[u], O));
-          pv[u] = X.x * X.x + X.y * X.y;
+      for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], w[r]);
+      __syncthreads();
+      dft<16>(v);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned er = (unsigned)((r >> 1) ^ (16 * (r & 1)));
+        lds2(wbuf, (ac ^ (8u * er)) + 256u * (r >> 1)) = v[r];
+      }
+    }
+    __syncthreads();
+    // ---- pass 3 (radix 8, span 256): butterflies j0, j1 -> Z[j + 256 r] in registers
+    float2 z[2][8];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const unsigned ad = p ? ad1 : ad0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) z[p][r] = lds2(wbuf, (ad ^ (192u * (r & 1))) + 2048u * r);
+      float2 bw[4], w[8];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (p == 0) {
+          bw[q] = e0[q];
+        } else {  // W^{(256 - t) 2^q} = W_8^{2^q} conj(W^{t 2^q}); lane 0: W^{128 2^q} = W_16^{2^q}
+          const float2 a = w16(2 << q), c = make_float2(e0[q].x, -e0[q].y);
+          bw[q] = tid ? cmul(a, c) : w16(1 << q);
         }
       }
-      if (alias) __syncthreads();
+      twiddle_pows<8>(bw, w);
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (i0 + tid + NT * u < nk) pw[i0 + tid + NT * u] = pv[u];
+      for (int r = 1; r < 8; ++r) z[p][r] = cmul(z[p][r], w[r]);
+      dft<8>(z[p]);
+    }
+    __syncthreads();  // every lane's pass-3 reads precede the power writes (pw aliases the FFT buffer)
+    // W_4096^{256 - t} = W_16 conj(W_4096^t); lane 0: W_4096^128 = W_32
+    const float2 rb1 = tid ? cmul(w16(1), make_float2(rb0.x, -rb0.y))
+                           : make_float2(0.98078528040323044913f, -0.19509032201612826785f);
+    // ---- real-FFT bins k = j + 256 r: the partner 2048 - k is bin 7 - r of
+    // the other butterfly (lane 0: j0 = 0 pairs with itself at (8 - r) & 7,
+    // j1 = 128 likewise at 7 - r); W_4096^k = W_4096^j W_16^r
+    {
+      int tt = tid;  // (opaque per frame: no hoisted per-bin masks / addresses)
+      asm volatile("" : "+v"(tt));
+      const bool l0 = tt == 0;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int kb = (p ? (l0 ? 128 : 256 - tt) : tt) - kmin;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float2 zm = l0 ? (p == 0 ? z[0][(8 - r) & 7] : z[1][7 - r]) : z[p ^ 1][7 - r];
+          const float2 rt = cmul(p ? rb1 : rb0, w16(r));
+          float pv = rbin_power(z[p][r], zm, rt);
+          if (power != 2) pv = sqrtf(pv);
+          const int i = kb + 256 * r;
+          if ((unsigned)i < (unsigned)nk) pw[i] = pv;
+        }
+      }
+    }
+    if (tid == 0 && kmax == NC) {  // Nyquist bin: Z[0] with itself, W_4096^2048 = -1
+      float pv = rbin_power(z[0][0], z[0][0], make_float2(-1.f, 0.f));
+      if (power != 2) pv = sqrtf(pv);
+      pw[NC - kmin] = pv;
     }
     if (tid < 8) pw[nk + tid] = 0.f;
-    if (power != 2) {
-      __syncthreads();
-      for (int k = tid; k < nk; k += NT) pw[k] = sqrtf(pw[k]);
-    }
     __syncthreads();
     // band pairs (m, n_mels-1-m): wave 0 the low band, wave 1 the high band
     for (int q = tid & 63; q < (n_mels + 1) / 2; q += 64) {
@@ -760,11 +828,9 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   const int T = acfe_plan_num_frames(p, n, pad_mode);
   if (p->n_fft == 4096) {
     constexpr int fpw = 4;  // frames per workgroup (2: 1.51 ms, 8: equal, r01n/r02y; r03: 2 / 8 / 16 +3 / 0 / +2 %)
-    const int nk = p->kmax - p->kmin + 1;
-    const size_t shm2 = sizeof(float2) * (2048 + 2048 / 16) + (nk <= 1024 ? 0 : sizeof(float) * (nk + 8));
-    hipLaunchKernelGGL(k_mel_w2, dim3(cdiv(T, fpw), batch), dim3(128), shm2, strm(stream), raw, cs, n, stats,
-                       pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_win, p->d_band, p->d_vals,
-                       p->n_mels, p->kmin, p->kmax, out, layout);
+    hipLaunchKernelGGL(k_mel_w3, dim3(cdiv(T, fpw), batch), dim3(128), sizeof(float2) * 2048, strm(stream), raw, cs, n,
+                       stats, pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_band, p->d_vals, p->n_mels,
+                       p->kmin, p->kmax, out, layout);
     return launch_rc("acfe_mel_fwd");
   }
   const int fpb = 4;

@@ -29,13 +29,9 @@ for w in "$@"; do
     testsall) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/testsall.log 2>&1
               rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
               case $rc in 0|1) ;; *) exit $rc ;; esac ;;
-    melab) step mel_w3 300 python tools/mel_bench.py --iters 15
-           ACFE_MEL_W2=1 step mel_w2 300 python tools/mel_bench.py --iters 15
-           step mel_w3b 300 python tools/mel_bench.py --iters 15 ;;
-    dpold) ACFE_CONV1W64=0 step dpold 600 python -u -m pytest tests/test_dp_gpu.py -m gpu -v --timeout 240 --timeout-method thread ;;
+    mel) step mel 300 python tools/mel_bench.py --iters 15 ;;
+    sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
-    t1old) ACFE_CONV1W64=0 bp t1old --steps 20 --warmup 5 --no-cpu-baseline ;;
-    wrnold) ACFE_CONV1W64=0 bp wrnold --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     convtests) step convtests 600 python -u -m pytest tests/test_production_gpu.py tests/test_fused_gpu.py \
                  tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     wrn) bp wrn --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
