@@ -558,11 +558,13 @@ __device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
 // (k_mel_w2: padded LDS, pass-3 results stored and re-read by the
 // post-processing, 148 VGPRs): one LDS round trip fewer, no bank conflicts,
 // 128 VGPRs (4 waves per SIMD); T1 1.16 -> 0.91 ms per 512 clips.
-//  * LDS holds the 2048 points unpadded under the XOR swizzle msw(i): the low
-//    five bits (the float2's bank group in a 32-lane half-wave) are XORed with
-//    bits 5..8 (and bit 8 into bit 4), so the pass-1 rows (stride 16), the
-//    pass-2 / pass-3 reads (consecutive points per half-wave) and the pass-2
-//    stores (two 16-point runs 256 apart) all hit 32 distinct bank pairs.
+//  * LDS holds the 2048 points unpadded under the XOR swizzle msw(i) = i ^
+//    ((i >> 4) & 15): ds_write_b64 serves 16-lane groups on 32 banks (a
+//    float2 index mod 16 per lane), ds_read_b64 32-lane groups on 64 banks
+//    (mod 32), and under msw the pass-1 rows (stride 16), the pass-2 stores
+//    (16-point runs) and the pass-2 / pass-3 reads (consecutive points) are all
+//    conflict-free (the r04 first cut XORed bits 5..8 in: its pass-1 stores
+//    were 2-way, 32 % of the LDS cycles in conflicts, SQ counters r04c).
 //  * Pass 3 (radix 8, span 256) gives lane t the butterflies j0 = t and
 //    j1 = 256 - t (j1 = 128 for t = 0), i.e. the complex bins j + 256 r that
 //    the real-FFT post-processing pairs as k <-> 2048 - k: the |X|^power of
@@ -570,7 +572,7 @@ __device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
 //    W_4096^k = W_4096^j W_16^r from one per-lane base, and written straight
 //    into the power vector (aliased onto the FFT buffer: 16 KB of LDS per
 //    workgroup).
-__device__ __forceinline__ int msw(int i) { return i ^ ((i >> 5) & 15) ^ (((i >> 8) & 1) << 4); }
+__device__ __forceinline__ int msw(int i) { return i ^ ((i >> 4) & 15); }
 
 // W_16^r = exp(-2 pi i r / 16)
 __device__ __forceinline__ float2 w16(int r) {
@@ -650,11 +652,11 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
   // swizzled byte addresses: every access of a pass is its lane base XOR a
   // compile-time constant (+ an immediate offset), see msw():
   //   pass-1 rows  msw(16 j + r)            = msw(16 j) ^ r
-  //   pass-2 reads msw(j + 128 r)           = (msw(j) ^ C_r) + 128 r
-  //   pass-2 rows  msw(256 J + x + 16 r)    = (256 J + (x ^ 24 (J & 1)) ^ E_r) + 32 (r >> 1)
-  //   pass-3 reads msw(j + 256 r)           = (msw(j) ^ 24 (r & 1)) + 256 r
+  //   pass-2 reads msw(j + 128 r)           = (msw(j) ^ 8 (r & 1)) + 128 r
+  //   pass-2 rows  msw(256 J + x + 16 r)    = ((256 J + x) ^ r) + 16 r
+  //   pass-3 reads msw(j + 256 r)           = msw(j) + 256 r
   const unsigned ua = (unsigned)msw(16 * tid) * 8u, ub = (unsigned)msw(tid) * 8u;
-  const unsigned uc = (unsigned)(256 * (tid >> 4) + ((tid & 15) ^ (24 * ((tid >> 4) & 1)))) * 8u;
+  const unsigned uc = (unsigned)(256 * (tid >> 4) + (tid & 15)) * 8u;
   const unsigned ud0 = (unsigned)msw(j0) * 8u, ud1 = (unsigned)msw(j1) * 8u;
   for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
     // (per frame: keeps the compiler from hoisting ~100 LDS addresses and
@@ -727,20 +729,14 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
     {
       float2 v[16], w[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const unsigned cr = (unsigned)((4 * r & 12) ^ (((r >> 1) & 1) << 4));
-        v[r] = lds2(wbuf, (ab ^ (8u * cr)) + 1024u * r);
-      }
+      for (int r = 0; r < 16; ++r) v[r] = lds2(wbuf, (ab ^ (64u * (r & 1))) + 1024u * r);
       twiddle_pows<16>(bw2[0], w);
 #pragma unroll
       for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], w[r]);
       __syncthreads();
       dft<16>(v);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const unsigned er = (unsigned)((r >> 1) ^ (16 * (r & 1)));
-        lds2(wbuf, (ac ^ (8u * er)) + 256u * (r >> 1)) = v[r];
-      }
+      for (int r = 0; r < 16; ++r) lds2(wbuf, (ac ^ (8u * r)) + 128u * r) = v[r];
     }
     __syncthreads();
     // ---- pass 3 (radix 8, span 256): butterflies j0, j1 -> Z[j + 256 r] in registers
@@ -749,7 +745,7 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
     for (int p = 0; p < 2; ++p) {
       const unsigned ad = p ? ad1 : ad0;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) z[p][r] = lds2(wbuf, (ad ^ (192u * (r & 1))) + 2048u * r);
+      for (int r = 0; r < 8; ++r) z[p][r] = lds2(wbuf, ad + 2048u * r);
       float2 bw[4], w[8];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
