@@ -658,6 +658,12 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
   const unsigned ua = (unsigned)msw(16 * tid) * 8u, ub = (unsigned)msw(tid) * 8u;
   const unsigned uc = (unsigned)(256 * (tid >> 4) + (tid & 15)) * 8u;
   const unsigned ud0 = (unsigned)msw(j0) * 8u, ud1 = (unsigned)msw(j1) * 8u;
+  // the lane's first mel band (band pairs (m, n_mels - 1 - m): wave 0 the
+  // low band, wave 1 the high one): its descriptor and first MAXG 8-tap
+  // weight groups are loaded each frame before the power vector's barrier, so
+  // their latency hides behind it (the band loop waited on them otherwise)
+  constexpr int MAXG = 5;
+  const int q0 = tid & 63;
   for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
     // (per frame: keeps the compiler from hoisting ~100 LDS addresses and
     // twiddle products out of the loop into spilled registers)
@@ -792,20 +798,47 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
       pw[NC - kmin] = pv;
     }
     if (tid < 8) pw[nk + tid] = 0.f;
+    int tq = tid;  // (per frame: the band registers are not held across the FFT)
+    asm volatile("" : "+v"(tq));
+    const int m0 = tq < 64 ? q0 : n_mels - 1 - q0;
+    const bool b0ok = q0 < (n_mels + 1) / 2 && !(tq >= 64 && m0 == q0);
+    int bs0 = 0, bp0 = 0, bo0 = 0;
+    if (b0ok) bs0 = band[3 * m0], bp0 = (band[3 * m0 + 1] + 7) & ~7, bo0 = band[3 * m0 + 2];
+    float4 wv[MAXG][2];
+    {
+      const float4* v0 = reinterpret_cast<const float4*>(vals + bo0);
+#pragma unroll
+      for (int gi = 0; gi < MAXG; ++gi) {
+        const bool ok = b0ok && 8 * gi < bp0;
+        wv[gi][0] = ok ? v0[2 * gi] : make_float4(0.f, 0.f, 0.f, 0.f);
+        wv[gi][1] = ok ? v0[2 * gi + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
     __syncthreads();
-    // band pairs (m, n_mels-1-m): wave 0 the low band, wave 1 the high band
-    for (int q = tid & 63; q < (n_mels + 1) / 2; q += 64) {
+    auto dot8 = [](float acc, const float4 a, const float4 c, const float* p) __attribute__((always_inline)) {
+      return acc + a.x * p[0] + a.y * p[1] + a.z * p[2] + a.w * p[3] + c.x * p[4] + c.y * p[5] + c.z * p[6] +
+             c.w * p[7];
+    };
+    if (b0ok) {
+      const float* p0 = pw + (bs0 - kmin);
+      float acc = 0.f;
+#pragma unroll
+      for (int gi = 0; gi < MAXG; ++gi)
+        if (8 * gi < bp0) acc = dot8(acc, wv[gi][0], wv[gi][1], p0 + 8 * gi);
+      const float4* v0 = reinterpret_cast<const float4*>(vals + bo0);
+      for (int i0 = 8 * MAXG; i0 < bp0; i0 += 8) acc = dot8(acc, v0[i0 / 4], v0[i0 / 4 + 1], p0 + i0);
+      out[layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m0
+                                    : ((size_t)b * n_mels + m0) * n_frames + f] = acc;
+    }
+    // further band pairs (n_mels > 128)
+    for (int q = q0 + 64; q < (n_mels + 1) / 2; q += 64) {
       const int m = tid < 64 ? q : n_mels - 1 - q;
       if (tid >= 64 && m == q) continue;
       const int s0 = band[3 * m], pl = (band[3 * m + 1] + 7) & ~7, off = band[3 * m + 2];
       const float4* v0 = reinterpret_cast<const float4*>(vals + off);
       const float* p0 = pw + (s0 - kmin);
       float acc = 0.f;
-      for (int i0 = 0; i0 < pl; i0 += 8) {
-        const float4 a = v0[i0 / 4], c = v0[i0 / 4 + 1];
-        acc += a.x * p0[i0] + a.y * p0[i0 + 1] + a.z * p0[i0 + 2] + a.w * p0[i0 + 3] + c.x * p0[i0 + 4] +
-               c.y * p0[i0 + 5] + c.z * p0[i0 + 6] + c.w * p0[i0 + 7];
-      }
+      for (int i0 = 0; i0 < pl; i0 += 8) acc = dot8(acc, v0[i0 / 4], v0[i0 / 4 + 1], p0 + i0);
       out[layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m : ((size_t)b * n_mels + m) * n_frames + f] =
           acc;
     }

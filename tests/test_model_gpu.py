@@ -21,10 +21,12 @@ bf16 compute, vs the oracle with the same bf16 storage points (storage="bf16"):
   eval-mode BN: rel-L2(logits) <= 1e-2, rel-L2(gradient arena) <= 5e-2
     (floor measured between fp32- and fp64-accumulating bf16 oracles:
      1.2e-3 / 8.8e-3);
-  training-mode BN on a 2-clip batch is chaotic at init -- the same two
-    oracles differ by 3.6% (logits) and 61% (gradients) -- so logits are held
-    to rel-L2 <= 0.15 and every parameter gradient to the accuracy class of
-    the bf16 emulation against exact float64 math (see the test body).
+  training-mode BN: a whole-model bf16 training step at init is chaotic (two
+    bf16-storage oracles differ by 3.6 % in the logits and 61 % in the
+    gradients at N = 2), so it is not checked whole with a loose bound; the
+    benchmarked mode is checked at the T1 shape segment by segment with fixed
+    bounds (test_bird_t1_shape_bf16_train_segments) and per residual block
+    (test_block_bf16_train_fixed_bounds).
 """
 import math
 

@@ -29,16 +29,16 @@ for w in "$@"; do
     testsall) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/testsall.log 2>&1
               rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
               case $rc in 0|1) ;; *) exit $rc ;; esac ;;
-    mel) step mel 300 python tools/mel_bench.py --iters 15 ;;
+    mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
     fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r04 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
              'k_conv3x3_rows<64,8,4,true,true> (wr_resnet b1/b2 conv2a 3x3 64->64 @128x513 with the BN prologue + dropout + BN sums, batch 512)' \
              --model wrn --classes 2 --steps 2 --warmup 1 ;;
-    evinfer) step evinfer 900 bash tools/pmc_evidence.sh infer_fp32 r04 'k_conv_fwd_g<float, 128, 64' 7961208422 \
-             'k_conv_fwd_g<float,128,64> (wr_resnet stage-1 3x3 ->64 @128x513 fp32, batch 256; averaged over the 4 C=64 and 1 C=16 launches of that grid)' \
+    evinfer) SELECT=7:3 step evinfer 900 bash tools/pmc_evidence.sh infer_fp32 r04 'k_conv_fwd_g<float, 128, 64' 8606859264 \
+             'k_conv_fwd_g<float,128,64> (wr_resnet b1.conv2a 3x3 64->64 @128x513 fp32, batch 256)' \
              --workload infer --steps 2 --warmup 1 ;;
-    evstream) step evstream 900 bash tools/pmc_evidence.sh stream_fp32 r04 'k_conv_fwd_g<float, 128, 128' 34359738368 \
-             'k_conv_fwd_g<float,128,128> (wr_resnet_bird s1b0 conv21 3x3 128->128 @128x256 fp32, 1024 windows)' \
+    evstream) SELECT=12:1 step evstream 900 bash tools/pmc_evidence.sh stream_fp32 r04 'k_conv_fwd_g<float, 128, 128' 26832360789 \
+             'k_conv_fwd_g<float,128,128> (wr_resnet_bird s1b0 conv21 3x3 128->128 @128x256 fp32; the 3 launches of a step: 1024 / 1024 / 351 windows, averaged)' \
              --workload stream --dtype fp32 --steps 1 --warmup 1 ;;
     e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;
     sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;

@@ -5,7 +5,8 @@
 # time limit, the program directly after `--`.  tools/pmc_fold.py then writes
 # profiles/pmc_dominant_<key>_<round>.json and profiles/sq_dominant_<key>_<round>.json
 # (read by bench.py for roofline.traffic / roofline.counters).
-# usage: tools/pmc_evidence.sh <key> <round> <kernel regex> <algorithmic bytes per launch> <label> <bench args...>
+# usage: [SELECT=period:index] tools/pmc_evidence.sh <key> <round> <kernel regex> <algorithmic bytes per launch>
+#        <label> <bench args...>   (SELECT: the dominant layer's position among each step's dispatches of the kernel)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 KEY=$1 RND=$2 RX=$3 ALGO=$4 LABEL=$5
 shift 5
@@ -23,4 +24,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   fi
   i=$((i+1))
 done
-python tools/pmc_fold.py $O "$RX" "$KEY" "$RND" "$ALGO" "$LABEL" "$*"
+python tools/pmc_fold.py $O "$RX" "$KEY" "$RND" "$ALGO" "$LABEL" "$*" "$SELECT"

@@ -6,7 +6,8 @@ HBM section; averaged over the kernel's dispatches after the first) and
 profiles/sq_dominant_<key>_<round>.json (SQ counters of the last dispatch:
 MFMA-pipe busy per SIMD, share of wave time waiting, VALU per MFMA, LDS
 bank-conflict share; formulas of tools/sq_summary.py).
-usage: tools/pmc_fold.py <dir> <kernel regex> <key> <round> <algorithmic bytes> <label> <bench args>"""
+usage: tools/pmc_fold.py <dir> <kernel regex> <key> <round> <algorithmic bytes> <label> <bench args>
+                         [period:index]"""
 import csv
 import glob
 import json
@@ -16,23 +17,32 @@ from collections import defaultdict
 from pathlib import Path
 
 
+SELECT = None  # (period, index): keep dispatch i of every `period` consecutive ones
+
+
 def dispatches(d, rx):
-    """Counters per dispatch of the kernels matching rx, restricted to the
-    largest grid among them (the dominant layer: the same kernel also runs
-    smaller layers of the model)."""
-    rows = []
-    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        rows += [r for r in csv.DictReader(open(f)) if re.search(rx, r["Kernel_Name"])]
-    gmax = max((int(r["Grid_Size"]) for r in rows), default=0)
+    """Counters per dispatch of the kernels matching rx.  The same kernel also
+    runs other layers of the model: with SELECT only the dominant layer's
+    dispatches are kept (its position among each step's dispatches of the
+    kernel, in dispatch order; the grid size does not tell layers apart for the
+    grid-stride kernels)."""
     vals = defaultdict(lambda: defaultdict(float))
-    for r in rows:
-        if int(r["Grid_Size"]) == gmax:
-            vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if re.search(rx, r["Kernel_Name"]):
+                vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    if SELECT:
+        per, idx = SELECT
+        keep = sorted(vals)[idx::per]
+        vals = {k: vals[k] for k in keep}
     return vals
 
 
 def main():
+    global SELECT
     d, rx, key, rnd, algo, label, args = sys.argv[1:8]
+    if len(sys.argv) > 8 and sys.argv[8]:
+        SELECT = tuple(int(v) for v in sys.argv[8].split(":"))
     algo = float(algo)
     prof = Path(__file__).resolve().parent.parent / "profiles"
     traffic = {}
@@ -42,7 +52,7 @@ def main():
         traffic[c] = sum(v[k][c] for k in ks) / max(len(ks), 1)
         traffic[c + "_dispatches"] = len(ks)
     fetch, write = traffic["FETCH_SIZE"] * 1024 * 2, traffic["WRITE_SIZE"] * 1024
-    pmc = {"kernel": label, "kernel_regex": rx, "bench_args": args,
+    pmc = {"kernel": label, "kernel_regex": rx, "bench_args": args, "dispatch_select": SELECT,
            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes inside the bench command "
                      "(tools/pmc_evidence.sh)",
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
@@ -55,7 +65,7 @@ def main():
         if v:
             c.update(v[sorted(v)[-1]])
     cu = c["SQ_BUSY_CU_CYCLES"] / 256
-    sq = {"kernel": label, "kernel_regex": rx, "bench_args": args,
+    sq = {"kernel": label, "kernel_regex": rx, "bench_args": args, "dispatch_select": SELECT,
           "source": f"rocprofv3 --pmc, two passes inside the bench command (tools/pmc_evidence.sh); raw: {d}",
           "mfma_busy_per_simd": round(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / 1024 / cu, 4),
           "wave_time_waiting": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4),
