@@ -777,12 +777,20 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
     {
       int tt = tid;  // (opaque per frame: no hoisted per-bin masks / addresses)
       asm volatile("" : "+v"(tt));
+      // the r range of each butterfly set holding bins of [kmin, kmax]: set 0
+      // holds k = 256 r + [0, 127], set 1 k = 256 r + [128, 255]
+      int rhi0 = kmax >> 8, rhi1 = kmax >= 128 ? (kmax - 128) >> 8 : -1;
+      int rlo0 = kmin > 127 ? (kmin - 127 + 255) >> 8 : 0, rlo1 = kmin > 255 ? (kmin - 255 + 255) >> 8 : 0;
+      asm volatile("" : "+s"(rhi0), "+s"(rhi1), "+s"(rlo0), "+s"(rlo1));
       const bool l0 = tt == 0;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int kb = (p ? (l0 ? 128 : 256 - tt) : tt) - kmin;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
+          // (uniform: no lane of this (p, r) holds a bin in [kmin, kmax] -- T1:
+          // r >= 4, half of the post-processing)
+          if (r > (p ? rhi1 : rhi0) || r < (p ? rlo1 : rlo0)) continue;
           const float2 zm = l0 ? (p == 0 ? z[0][(8 - r) & 7] : z[1][7 - r]) : z[p ^ 1][7 - r];
           const float2 rt = cmul(p ? rb1 : rb0, w16(r));
           float pv = rbin_power(z[p][r], zm, rt);
