@@ -331,6 +331,8 @@ def main():
         },
         "roofline": {
             "kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t} " + (
+                "(k_conv_fwd_g<float,128,BN>: fp32 implicit-im2col GEMM on v_mfma_f32_16x16x4f32, LDS-staged tiles)"
+                if dtype != torch.bfloat16 else
                 "(k_conv3x3_1w<1,2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)"
                 if a.model == "bird" else
                 "(k_conv3x3_rows<64,8,4,true,true>: bn2a + ReLU applied while staging the input rows, dropout + BN sums epilogue; 8 rows x 64 px x 64 ch per workgroup of 8 waves)"),
