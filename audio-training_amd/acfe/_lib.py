@@ -51,6 +51,9 @@ SIGNATURES: dict[str, list] = {
                                 C.c_uint64, P],
     "acfe_conv2d_dgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P],
     "acfe_conv2d_dgrad_workspace": [I32] * 13,
+    "acfe_conv2d_dgrad_bn_rows": [I32] * 9,
+    "acfe_conv2d_dgrad_bn": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P, P, P, P,
+                             I32, P, I32, P],
     "acfe_conv2d_wgrad_workspace": [I32, I32, I32, I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_wgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, I32, P, P],
     "acfe_stem_blocks": [I32, I32, I32],
@@ -103,6 +106,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_maxpool2d_fused": [P, I32, I32, I32, I32, I32, I32, P, P, F32, C.c_uint64, P, I32, P],
     "acfe_bn_maxpool2d_fused": [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, P, P, I32, P],
     "acfe_maxpool2d_bwd_argmax": [P, P, I32, I32, I32, I32, I32, I32, F32, C.c_uint64, P, I32, P],
+    "acfe_maxpool2d_bwd_argmax_bn": [P, P, I32, I32, I32, I32, I32, I32, P, I32, P, P, P, P, P, I32, P, P],
     "acfe_avgpool2d": [P, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_avgpool2d_bwd": [P, I32, I32, I32, I32, I32, P, I32, P],
     "acfe_axis_pool": [P, I32, I64, I32, I32, F32, I32, P, P],

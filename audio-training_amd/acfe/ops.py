@@ -32,6 +32,9 @@ PROLOGUE = os.environ.get("ACFE_BN_PROLOGUE", "1") != "0"
 # measured 1 % slower per T1 step than the one apply pass it saves, r02ab)
 PRO_POOL = os.environ.get("ACFE_BN_PROLOGUE_POOL", "1") != "0"
 PRO_C1 = os.environ.get("ACFE_BN_PROLOGUE_C1", "0") != "0"
+# ACFE_BN_REDUCE_FUSE=0: the BatchNormalization backward reduce runs as its own
+# pass even where the kernel producing its gradient can form the sums (A/B)
+FUSE_BN_REDUCE = FUSE and os.environ.get("ACFE_BN_REDUCE_FUSE", "1") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -215,8 +218,16 @@ def grads_ready(*params):
                 fn(p)
 
 
-def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=None):
-    """dgrad / wgrad / bias gradient of _conv_fwd for the conv-output gradient dy."""
+def bn_src(x):
+    """The BatchNormalization behind x (x = its output) when a dgrad of a conv
+    reading x may form that BN's backward reduce (acfe_conv2d_dgrad_bn)."""
+    return getattr(x, "_acfe_bn_src", None) if FUSE_BN_REDUCE else None
+
+
+def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=None, bn=None):
+    """dgrad / wgrad / bias gradient of _conv_fwd for the conv-output gradient dy.
+    bn: bn_src(x) -- where acfe_conv2d_dgrad_bn covers the shape, dx comes back
+    tagged with that BN's backward reduce slab (consumed by its _bn_bwd)."""
     N, H, W, C = x.shape
     K, R, S, _ = w.shape
     dt = dtype_code(x.dtype)
@@ -227,12 +238,26 @@ def _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, need_dw, need_db, bias=No
         wf = pack_weights(w, x.dtype, True)
         dx = _empty(x.shape, x.dtype, x.device)
         ws = None
+        brows = 0
+        if bn is not None:
+            xb = bn[0]
+            brows = lib.acfe_conv2d_dgrad_bn_rows(N, H, W, C, K, R, S, stride, dt)
+            if not (brows and xb.shape == x.shape and xb.dtype == x.dtype and xb.is_contiguous()
+                    and xb.data_ptr() % 16 == 0 and P == H and Q == W):
+                brows = 0
         if stride > 1:  # sub-pixel phases: packed sub-kernels + one phase image
             nb = lib.acfe_conv2d_dgrad_workspace(N, P, Q, K, C, R, S, stride, pt, pl, H, W, dt)
             ws = _empty((max(nb, 1),), torch.uint8, x.device)
         with _Timed(w, "dgrad"):
-            call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
-                 ptr(ws), s)
+            if brows:
+                xb, scale, shift, mean, invstd, brelu = bn
+                part = _empty((brows, 2, C), F64, x.device)
+                call("acfe_conv2d_dgrad_bn", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
+                     ptr(xb), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), int(brelu), ptr(part), brows, s)
+                _tag(dx, "_acfe_bnpart", (part, brows, (xb.data_ptr(), tuple(xb.shape), brelu)))
+            else:
+                call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, S, stride, pt, pl, H, W, ptr(dx), dt,
+                     ptr(ws), s)
     if need_dw:
         # arena parameters: the split-K combine accumulates straight into the
         # flat gradient buffer (beta 1) and autograd gets None -- no separate
@@ -263,6 +288,7 @@ class _Conv2dFn(torch.autograd.Function):
         y, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pt, pl, P, Q, b is not None)
+        ctx.bn = bn_src(x)
         ctx.link = link
         ctx.mark_non_differentiable(stats)
         return y, stats
@@ -273,7 +299,7 @@ class _Conv2dFn(torch.autograd.Function):
         stride, pt, pl, P, Q, has_b = ctx.conf
         need_dx = ctx.needs_input_grad[0] or ctx.link is not None
         dx, dw, db = _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, ctx.needs_input_grad[1],
-                               has_b and ctx.needs_input_grad[2], bias=ctx.bias)
+                               has_b and ctx.needs_input_grad[2], bias=ctx.bias, bn=ctx.bn)
         if ctx.link is not None:  # the BN reading x adds this gradient in its own backward
             ctx.link.grad = dx
             dx = None
@@ -455,6 +481,9 @@ def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, o
     if out_dtype is None:  # affine only: the caller applies it (bn_max_pool)
         return None, (scale, shift, mean, invstd)
     y = _empty(x.shape, out_dtype, dev)
+    if FUSE_BN_REDUCE:
+        # a conv reading y may form this BN's backward reduce in its dgrad (_conv_bwd)
+        y._acfe_bn_src = (x, scale, shift, mean, invstd, bool(relu))
     if defer and out_dtype == x.dtype:
         y._acfe_bn_pending = (x, scale, shift, bool(relu))
         return y, (scale, shift, mean, invstd)
@@ -517,20 +546,30 @@ def _conv_fwd_bn(xb, w, b, want_stats, drop):
     return y, stats
 
 
-def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None, params=None):
+def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None, params=None, part=None):
     """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given;
     mask_in: x is a ReLU output (ops.add), its backward [x > 0] is applied to dx here
-    and dx is marked so that ops.add's backward skips its own pass."""
+    and dx is marked so that ops.add's backward skips its own pass.  part: the
+    reduce slab [acfe_reduce_blocks(rows)][2][C] already formed by the kernel
+    that produced dy (acfe_maxpool2d_bwd_argmax_bn): no reduce pass; the same
+    when dy carries the slab of the dgrad that produced it (acfe_conv2d_dgrad_bn,
+    tagged _acfe_bnpart for this x)."""
     scale, shift, mean, invstd = saved
     C = x.shape[-1]
     rows = x.numel() // C
     dev = x.device
     s = stream()
-    dy = dy.contiguous()
     nrows = lib.acfe_reduce_blocks(rows)
-    part = _empty((nrows * 2 * C,), F64, dev)
-    call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
-         ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
+    prow = nrows
+    if part is None:
+        lazy = _tagged(dy, "_acfe_bnpart")
+        if lazy is not None and lazy[2] == (x.data_ptr(), tuple(x.shape), bool(relu)):
+            part, prow = lazy[0], lazy[1]
+    dy = dy.contiguous()
+    if part is None:
+        part = _empty((nrows * 2 * C,), F64, dev)
+        call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+             ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
     # arena parameters (gamma, beta): the finalizer accumulates into their
     # gradient views and autograd gets None
     tg = tb = None
@@ -543,7 +582,7 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
     coef = _empty((3 * C,), F32, dev)
     # eval mode: statistics are constants -> count -> inf removes the mean terms
     count = float(rows) if training else 1e300
-    call("acfe_bn_bwd_finalize_ex", ptr(part), nrows, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
+    call("acfe_bn_bwd_finalize_ex", ptr(part), prow, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
          ptr(dbeta), ptr(coef), int(tg is not None), s)
     if tg is not None:
         dgamma = dbeta = None
@@ -623,6 +662,7 @@ class _ConvDropBNFn(torch.autograd.Function):
         ctx.gb = (gamma, beta)
         stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum, defer = conf
         drop = (rate, seed) if training and rate > 0.0 else None
+        ctx.bn = bn_src(x)
         u, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, training, drop)
         y, saved = _bn_fwd(u, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
                            u.dtype, defer)
@@ -638,7 +678,7 @@ class _ConvDropBNFn(torch.autograd.Function):
         stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum, _ = ctx.conf
         g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop, params=ctx.gb)
         dx, dw, db = _conv_bwd(x, w, g, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               ctx.has_b and ctx.needs_input_grad[2], bias=ctx.bias)
+                               ctx.has_b and ctx.needs_input_grad[2], bias=ctx.bias, bn=ctx.bn)
         return dx, dw, db, dgamma, dbeta, None, None, None
 
 
@@ -826,6 +866,7 @@ class _ConvAddFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, sc, relu, want_stats, link):
         ctx.bias = b
+        ctx.bn = bn_src(x)
         N, H, W, C = x.shape
         K, R, S, _ = w.shape
         _, pt = same_padding(H, R, 1)
@@ -873,7 +914,7 @@ class _ConvAddFn(torch.autograd.Function):
                 call("acfe_relu_bwd", ptr(g), ptr(z), g.numel(), ptr(d), dtype_code(g.dtype), stream())
             g = d
         dx, dw, db = _conv_bwd(x, w, g, 1, pt, pl, H, W, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                               has_b and ctx.needs_input_grad[2], bias=ctx.bias)
+                               has_b and ctx.needs_input_grad[2], bias=ctx.bias, bn=ctx.bn)
         if link is not None:  # the shortcut input's gradient is added by the linked BN backward
             link.grad = g
             return dx, dw, db, None, None, None, None
@@ -1026,8 +1067,20 @@ class _BNPoolFn(torch.autograd.Function):
     def backward(ctx, g, _gs):
         x, amax, *saved = ctx.saved_tensors
         kh, kw, training, relu, eps, momentum, want_stats = ctx.conf
-        gu = _maxpool_bwd(amax, g, x.shape, kh, kw, None)
-        dx, dgamma, dbeta = _bn_bwd(x, gu, saved, relu, training, params=ctx.gb)
+        if FUSE_BN_REDUCE and _sums_ok(x):
+            # the pool backward also forms the BN backward's reduce slab (it
+            # reads x at the pixels it expands to): no separate reduce pass
+            N, H, W, C = x.shape
+            g = g.contiguous()
+            gu = _empty(x.shape, g.dtype, g.device)
+            part = _empty((lib.acfe_reduce_blocks(N * H * W) * 2 * C,), F64, x.device)
+            scale, shift, mean, invstd = saved
+            call("acfe_maxpool2d_bwd_argmax_bn", ptr(amax), ptr(g), N, H, W, C, kh, kw, ptr(gu), dtype_code(g.dtype),
+                 ptr(x), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), stream())
+            dx, dgamma, dbeta = _bn_bwd(x, gu, saved, relu, training, params=ctx.gb, part=part)
+        else:
+            gu = _maxpool_bwd(amax, g, x.shape, kh, kw, None)
+            dx, dgamma, dbeta = _bn_bwd(x, gu, saved, relu, training, params=ctx.gb)
         return dx, dgamma, dbeta, None, None, None, None
 
 

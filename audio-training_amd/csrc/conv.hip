@@ -910,11 +910,15 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
   // the register limit) accumulates them with LDS double atomics per tile
   constexpr bool REGSTAT = KB == 64;
   constexpr int SMEMS = SMEM0 + (REGSTAT ? 0 : 2 * KB * 8);
-  constexpr int SMEM = SMEMS + (PRO ? 2 * 256 * 4 : 0);
+  // PM 5: the BN backward coefficient table [scale | shift | mean | invstd][KB]
+  static_assert(PM != 5 || (KB == 64 && CPERM && !PRO), "PM 5: the K = 64 dgrad");
+  constexpr int SMEMB = SMEMS + (PRO ? 2 * 256 * 4 : 0);
+  constexpr int SMEM = SMEMB + (PM == 5 ? 4 * KB * 4 : 0);
   static_assert(SMEM <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   double* sstat = reinterpret_cast<double*>(smem + SMEM0);
   float* pss = reinterpret_cast<float*>(smem + SMEMS);  // PRO: scale[256], shift[256]
+  float* bnt = reinterpret_cast<float*>(smem + SMEMB);  // PM 5
   auto xbuf = [&](int b) __attribute__((always_inline)) { return smem + (WDMA ? b * XBYTES : b * BUFB); };
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -930,6 +934,9 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
     for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
   if constexpr (PRO)
     for (int i = tid; i < g.C; i += 512) pss[i] = g.pro_sc[i], pss[256 + i] = g.pro_sh[i];
+  if constexpr (PM == 5)  // (read only by the epilogues, after the main loop's first barrier)
+    for (int i = tid; i < KB; i += 512)
+      bnt[i] = g.bn_sc[i], bnt[KB + i] = g.bn_sh[i], bnt[2 * KB + i] = g.bn_mu[i], bnt[3 * KB + i] = g.bn_is[i];
   // bias: lane l holds channel wk * KB/2 + (l mod KB/2), one VGPR across the
   // main loop (the K = 128 variants sit at the 256-VGPR limit; no LDS left for
   // a copy); each epilogue gathers its quads with ds_bpermute, once per
@@ -1263,7 +1270,30 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       }
     }
   };
+  // PM 5: the BN input x at the tile's pixels (the lane's 4 FN = 8 channels of
+  // each fragment row: one 16-B load), requested at the start of the epilogue
+  // (prefetched during the tile's last step, its 32 VGPRs spilled 163)
+  u32x4 xbn[PM == 5 ? FM : 1];
+  // (buffer loads of the tile's image, out-of-image pixels at an
+  // out-of-range offset: no branches; one image < 2^31 bytes, launcher)
+  auto xbn_load = [&](int tm) __attribute__((always_inline)) {
+    if constexpr (PM == 5) {
+      const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+      const int cq = wk * (KB / 2) + (lane >> 4) * 4 * FN;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(g.res + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int p = wp * (TR * 16) + fm * 16;
+        const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+        const bool inb = (h < g.P) & (w < g.Q);
+        const unsigned o = ((unsigned)(h * g.Q + w) * (unsigned)g.ldy + cq) * 2u;
+        xbn[fm] = __builtin_amdgcn_raw_buffer_load_b128(rr, inb ? o : 0x80000000u, 0, 0);
+      }
+    }
+  };
   auto epilogue = [&](int tm) __attribute__((always_inline)) {
+    xbn_load(tm);
     const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
     float sv[NV];
 #pragma unroll
@@ -1567,8 +1597,67 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
         }
       }
     };
+    // PM 5 (the dgrad, no bias): the dX rows rounded to bf16 (what the dgrad
+    // stores), packed and stored first -- the tile's x quads, loaded at the
+    // start of the epilogue, in flight meanwhile -- then acfe_bn_bwd_reduce's
+    // terms of the stored values: gm = dX masked by the BN's ReLU, summed as
+    // gm and gm * (x - mean) * invstd (its arithmetic).  Branch-free: masks
+    // combined bitwise, out-of-image rows stored to the sink.  (Forming the
+    // sums row by row beside the stores, with the coefficient quads re-read per
+    // row behind an opaque offset, spilled 150 VGPRs; the same order with the
+    // rows' packed values all live and per-element xhat, 7-11.)
+    auto epi5 = [&]() __attribute__((always_inline)) {
+      const int cq = wk * (KB / 2) + (lane >> 4) * 4 * FN;
+      const bool norelu = g.bn_relu == 0;
+      // rows rounded, packed and stored first (the x loads in flight), then the sums
+      unsigned pk[FM][2 * FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int p = wp * (TR * 16) + fm * 16;
+        const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+        const bool inb = (h < g.P) & (w < g.Q);
+        const long long pix = ((long long)n * g.P + h) * g.Q + w;
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          float r[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) r[jj] = bf2f(f2bf(acc[fm][fn][jj]));
+          pk[fm][2 * fn] = (__float_as_uint(r[0]) >> 16) | (__float_as_uint(r[1]) & 0xffff0000u);
+          pk[fm][2 * fn + 1] = (__float_as_uint(r[2]) >> 16) | (__float_as_uint(r[3]) & 0xffff0000u);
+          acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+        u32x4* dst = inb ? reinterpret_cast<u32x4*>(Y + pix * g.ldy + cq) : &g_store_sink16[lane];
+#pragma unroll
+        for (int hq = 0; hq < FN / 2; ++hq)
+          dst[inb ? hq : 0] = u32x4{pk[fm][4 * hq], pk[fm][4 * hq + 1], pk[fm][4 * hq + 2], pk[fm][4 * hq + 3]};
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const f4 csc = *reinterpret_cast<const f4*>(bnt + cq + fn * 4);
+        const f4 csh = *reinterpret_cast<const f4*>(bnt + KB + cq + fn * 4);
+        const f4 cmu = *reinterpret_cast<const f4*>(bnt + 2 * KB + cq + fn * 4);
+        const f4 cis = *reinterpret_cast<const f4*>(bnt + 3 * KB + cq + fn * 4);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int p = wp * (TR * 16) + fm * 16;
+          const int h = hb * TR + p / SEGW, w = wb * SEGW + (p % SEGW) + l16;
+          const bool inb = (h < g.P) & (w < g.Q);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const unsigned xw = xbn[fm][2 * fn + (jj >> 1)], gw = pk[fm][2 * fn + (jj >> 1)];
+            const float xf = __uint_as_float((jj & 1) ? (xw & 0xffff0000u) : (xw << 16));
+            const float gf = __uint_as_float((jj & 1) ? (gw & 0xffff0000u) : (gw << 16));
+            const bool on = inb & (norelu | (xf * csc[jj] + csh[jj] > 0.f));
+            const float gm = on ? gf : 0.f;
+            sv[fn * 4 + jj] += gm;
+            sv[FN * 4 + fn * 4 + jj] += gm * ((xf - cmu[jj]) * cis[jj]);
+          }
+        }
+      }
+    };
     // only PM 4 carries a Dropout, launched with 32-bit element indices (launch_fwd_t)
-    if constexpr (PM != 1) epi03(std::bool_constant<PM == 4>{}, std::true_type{});
+    if constexpr (PM == 5) epi5();
+    else if constexpr (PM != 1) epi03(std::bool_constant<PM == 4>{}, std::true_type{});
     if (stats && !SWP) {
       butterfly_step<NV, 8, 0x128>(sv, lane);
       butterfly_step<NV / 2, 4, 0x141>(sv, lane);
@@ -1674,11 +1763,19 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       }
     stp.mark(1);
     if (NBUF == 2 && more) sstore(buf ^ 1);
+    // PM 5: the tile's epilogue runs after the next chunk's rows are stored
+    // (below): its BN-input loads and sums need the registers the staged rows
+    // hold until then (before them: 9 VGPRs spilled, reloaded every step)
+    bool epi_late = false;
     if (++cst == nsteps_t) {
       cst = 0;
       ++ctl;
-      epilogue(ctm);
-      ctm += walk.step;
+      if constexpr (PM == 5) {
+        epi_late = true;
+      } else {
+        epilogue(ctm);
+        ctm += walk.step;
+      }
     }
     stp.mark(2);
     if constexpr (WDMA && NBUF == 2) wait_vmcnt<0>();  // next step's weight pieces landed
@@ -1693,6 +1790,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
       sstore(0);  // single buffer: every wave has finished reading it
       if constexpr (WDMA) wait_vmcnt<0>();  // next step's weight pieces landed
       __syncthreads();
+    }
+    if constexpr (PM == 5) {
+      if (epi_late) {
+        epilogue(ctm);
+        ctm += walk.step;
+      }
     }
     stp.mark(4);
   }
@@ -3050,6 +3153,8 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.pro_sc = g.pro_sh = nullptr;
   g.pro_relu = 0;
   g.pro_out = nullptr;
+  g.bn_sc = g.bn_sh = g.bn_mu = g.bn_is = nullptr;
+  g.bn_relu = 0;
   g.idx32 = g.M * K < (1ll << 32) ? 1 : 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
@@ -3694,6 +3799,45 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
     }
     return launch_rows_tr<KB, PM, 8, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
   }
+}
+
+// ------------------------------------------------------------------ dgrad + BN backward reduce
+// The stride-1 3x3 dgrad whose dX is the output gradient of a
+// BatchNormalization (+ReLU) -- wr_resnet's bn2a / bn2b -> conv2a / conv2b
+// (resnet/wr_resnet.py:56-80) -- with that BN's acfe_bn_bwd_reduce sums formed
+// in the dgrad's epilogue (k_conv3x3_rows PM 5): the reduce pass and its
+// re-read of dX are gone, the epilogue reads the BN input x instead.
+// 64 dX channels (k_conv3x3_rows PM 5), any K % 64 == 0 dY channels.  The
+// same sums in the one-wave K = C = 128 dgrad's units (r04p) cost more issue
+// time than the separate reduce pass (+0.85 ms vs 0.75 ms per wr_resnet stage-2
+// call): that kernel is issue-bound, the reduce runs at the copy rate.
+ACFE_API int acfe_conv2d_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int dtype) {
+  if (dtype != ACFE_DTYPE_BF16 || N <= 0 || H <= 0 || W <= 0 || stride != 1 || R != 3 || S != 3 || K <= 0 ||
+      C != 64 || K % 64 != 0 ||
+      (long long)N * ((H + 3) / 4) * ((W + 63) / 64) >= (1ll << 31) || (long long)H * W * C * 2 >= (1ll << 31))
+    return 0;
+  return grid_m_for((long long)N * H * W, 1);
+}
+
+ACFE_API int acfe_conv2d_dgrad_bn(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R,
+                                  int S, int stride, int pad_top, int pad_left, int H, int W, void* dx, int dtype,
+                                  const void* x_bn, const float* scale, const float* shift, const float* mean,
+                                  const float* invstd, int relu, double* part, int part_rows, void* stream) {
+  const int rows = acfe_conv2d_dgrad_bn_rows(N, H, W, C, K, R, S, stride, dtype);
+  if (!rows || part_rows != rows || !dy || !wflip || !dx || !x_bn || !scale || !shift || !mean || !invstd ||
+      !part || P != H || Q != W || pad_top < 0 || pad_top > 2 || pad_left < 0 || pad_left > 2 ||
+      ((uintptr_t)dx & 15) || ((uintptr_t)x_bn & 15))
+    return ACFE_E_INVAL;
+  // the dgrad as a forward conv of dY with the flipped weights (acfe_conv2d_dgrad)
+  ConvGeom g = make_geom(N, P, Q, K, C, R, S, 1, R - 1 - pad_top, S - 1 - pad_left, H, W, 64, 64);
+  g.res = (const uint16_t*)x_bn;
+  g.bn_sc = scale;
+  g.bn_sh = shift;
+  g.bn_mu = mean;
+  g.bn_is = invstd;
+  g.bn_relu = relu ? 1 : 0;
+  return launch_rows_tr<64, 5, 8, true>(g, dy, wflip, nullptr, dx, part, rows, nullptr, strm(stream),
+                                        "acfe_conv2d_dgrad_bn");
 }
 
 ACFE_API int acfe_conv2d_pool_supported(int N, int H, int W, int C, int K, int R, int S, int dtype) {

@@ -36,6 +36,15 @@ struct ConvGeom {
   const float* pro_sh;
   int pro_relu;
   uint16_t* pro_out;
+  // k_conv3x3_rows PM 5 (acfe_conv2d_dgrad_bn): the BatchNormalization whose
+  // output is this dgrad's dX -- its input x (g.res, Y's layout), affine
+  // scale / shift (ReLU mask x * bn_sc + bn_sh > 0 when bn_relu) and batch
+  // mean / invstd -- so the epilogue forms acfe_bn_bwd_reduce's sums
+  const float* bn_sc;
+  const float* bn_sh;
+  const float* bn_mu;
+  const float* bn_is;
+  int bn_relu;
 };
 
 // XCD-aware walk over the M tiles of a persistent grid.  Workgroups are

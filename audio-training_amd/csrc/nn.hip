@@ -1125,6 +1125,109 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd8i(const uint8_t* __restrict
   }
 }
 
+// k_maxpool_bwd8i + the BatchNormalization backward reduce of the BN in front
+// of the pool (the stem's BatchNormalization -> MaxPool2D((1, 2)),
+// wr_resnet_bird.py:29-30): each expanded gradient value g is also masked by
+// the BN's ReLU (x * scale + shift > 0 when relu) and summed as g and
+// g * (x - mean) * invstd per channel, with x read at the same pixels --
+// acfe_bn_bwd_reduce's slab [gridDim][2][C] without its second read of the
+// expanded gradient.  Grid = red_blocks(N * H * W) (the slab rows the BN
+// finalizer expects); positions outside the pooled windows (H, W not a
+// multiple of the window) carry a zero gradient and add nothing.
+template <typename T, int KH, int KW>
+__global__ void __launch_bounds__(256) k_maxpool_bwd8i_bn(const uint8_t* __restrict__ amax, const T* __restrict__ dy,
+                                                          int N, int H, int W, int C, int P, int Q,
+                                                          T* __restrict__ dx, const T* __restrict__ x,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, int relu,
+                                                          double* __restrict__ part) {
+  extern __shared__ double red[];
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.0;
+  __syncthreads();
+  // a workgroup walks pooled rows (n, p); its threads cover the row's Q * CV
+  // 16-B vectors, JU of them per pass with all their loads issued first.
+  // 256 % CV == 0 (stats8_ok): CV is a power of two and a thread's channel
+  // vector cv is the same in every pass
+  constexpr int JU = 2;
+  const int CV = C >> 3, lcv = __builtin_ctz(CV), RV = Q * CV;
+  const int cv = threadIdx.x & (CV - 1);
+  float sc[8], sh[8], mu[8], is[8], a[8], b[8];
+  double da[8], db[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[cv * 8 + j], sh[j] = shift[cv * 8 + j], mu[j] = mean[cv * 8 + j], is[j] = invstd[cv * 8 + j];
+    a[j] = b[j] = 0.f, da[j] = db[j] = 0.0;
+  }
+  const float z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int rows = N * P;
+  int cnt = 0;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+    const int n = r / P, p = r - n * P;
+    const size_t pin = (size_t)r * RV;                       // first vector of the pooled row
+    const size_t fin = ((size_t)n * H + p * KH) * W * CV;    // first vector of its full-resolution band
+    for (int j0 = threadIdx.x; j0 < RV; j0 += 256 * JU) {
+      float g[JU][8], xv[JU][KH * KW][8];
+      uint2 pk[JU];
+#pragma unroll
+      for (int u = 0; u < JU; ++u) {
+        const int j = j0 + 256 * u, jj = j < RV ? j : j0, q = jj >> lcv;
+        ld8(dy + (pin + jj) * 8, g[u]);
+        pk[u] = *reinterpret_cast<const uint2*>(amax + (pin + jj) * 8);
+#pragma unroll
+        for (int aa = 0; aa < KH; ++aa)
+#pragma unroll
+          for (int bb = 0; bb < KW; ++bb)
+            ld8(x + (fin + ((size_t)aa * W + q * KW + bb) * CV + cv) * 8, xv[u][aa * KW + bb]);
+      }
+#pragma unroll
+      for (int u = 0; u < JU; ++u) {
+        const int j = j0 + 256 * u;
+        if (j >= RV) break;
+        const int q = j >> lcv;
+        int am[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) am[k] = (pk[u].x >> (8 * k)) & 0xff, am[4 + k] = (pk[u].y >> (8 * k)) & 0xff;
+#pragma unroll
+        for (int aa = 0; aa < KH; ++aa)
+#pragma unroll
+          for (int bb = 0; bb < KW; ++bb) {
+            const float* xw = xv[u][aa * KW + bb];
+            float o[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              o[k] = am[k] == aa * KW + bb ? g[u][k] : 0.f;
+              const float gk = (relu && !(xw[k] * sc[k] + sh[k] > 0.f)) ? 0.f : o[k];
+              a[k] += gk;
+              b[k] += gk * ((xw[k] - mu[k]) * is[k]);
+            }
+            st8(dx + (fin + ((size_t)aa * W + q * KW + bb) * CV + cv) * 8, o);
+          }
+        // positions outside the pooled windows: zero gradient (no sums)
+        if (q == Q - 1)
+          for (int aa = 0; aa < KH; ++aa)
+            for (int w = Q * KW; w < W; ++w) st8(dx + (fin + ((size_t)aa * W + w) * CV + cv) * 8, z);
+        if (p == P - 1)
+          for (int h = P * KH; h < H; ++h) {
+            const size_t hr = ((size_t)n * H + h) * W;
+            for (int w = q * KW; w < q * KW + KW; ++w) st8(dx + ((hr + w) * CV + cv) * 8, z);
+            if (q == Q - 1)
+              for (int w = Q * KW; w < W; ++w) st8(dx + ((hr + w) * CV + cv) * 8, z);
+          }
+      }
+    }
+    if (++cnt == 16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) da[j] += a[j], db[j] += b[j], a[j] = b[j] = 0.f;
+      cnt = 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) da[j] += a[j], db[j] += b[j];
+  stats8_flush(da, db, cv, C, true, red, part);
+}
+
 
 static int maxpool_fused_impl(const void* x, int N, int H, int W, int C, int kh, int kw, void* y, uint8_t* argmax,
                               float drop_rate, unsigned long long seed, double* stats_part, int dtype,
@@ -1187,6 +1290,32 @@ ACFE_API int acfe_maxpool2d_bwd_argmax(const uint8_t* argmax, const void* dy, in
   }
   MAXPOOL_SHAPES(MPBI)
 #undef MPBI
+  return ACFE_E_INVAL;
+}
+
+// acfe_maxpool2d_bwd_argmax (no dropout) fused with acfe_bn_bwd_reduce of the
+// BatchNormalization whose output was pooled: x = that BN's input [N][H][W][C],
+// part = its reduce slab [acfe_reduce_blocks(N * H * W)][2][C].
+ACFE_API int acfe_maxpool2d_bwd_argmax_bn(const uint8_t* argmax, const void* dy, int N, int H, int W, int C, int kh,
+                                          int kw, void* dx, int dtype, const void* x, const float* scale,
+                                          const float* shift, const float* mean, const float* invstd, int relu,
+                                          double* part, void* stream) {
+  if (!argmax || !dy || !dx || !x || !scale || !shift || !mean || !invstd || !part || N <= 0 || kh <= 0 ||
+      kw <= 0 || H < kh || W < kw || !stats8_ok(C))
+    return ACFE_E_INVAL;
+  const int P = H / kh, Q = W / kw;
+  if (!vec_ok((long long)N * H * W * C, C, dy, dx, x) || ((uintptr_t)argmax & 7) || (long long)N * P >= (1ll << 31))
+    return ACFE_E_INVAL;
+  const int grid = red_blocks((long long)N * H * W);
+#define MPBB(A, B)                                                                                             \
+  if (kh == A && kw == B) {                                                                                    \
+    DISPATCH1(dtype, T, hipLaunchKernelGGL((k_maxpool_bwd8i_bn<T, A, B>), dim3(grid), dim3(256),               \
+                                           2 * C * sizeof(double), strm(stream), argmax, (const T*)dy, N, H, W, C, \
+                                           P, Q, (T*)dx, (const T*)x, scale, shift, mean, invstd, relu, part));   \
+    return launch_rc("acfe_maxpool2d_bwd_argmax_bn");                                                          \
+  }
+  MAXPOOL_SHAPES(MPBB)
+#undef MPBB
   return ACFE_E_INVAL;
 }
 

@@ -221,6 +221,19 @@ long long acfe_conv2d_dgrad_workspace(int N, int P, int Q, int K, int C, int R, 
 int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R, int S,
                       int stride, int pad_top, int pad_left, int H, int W, void* dx, int dtype,
                       void* workspace, void* stream);
+/* acfe_conv2d_dgrad (stride 1, 3x3) whose dX is the output gradient of a
+ * BatchNormalization (+ReLU) -- wr_resnet.py:56-80's bn2a / bn2b feeding
+ * conv2a / conv2b -- with that BN's acfe_bn_bwd_reduce slab formed in the same
+ * pass: x_bn = the BN input [N][H][W][C], scale / shift / mean / invstd its
+ * acfe_bn_finalize outputs, part = [part_rows][2][C] for
+ * acfe_bn_bwd_finalize_ex (nrows = part_rows).  _rows returns the slab rows,
+ * or 0 when the fused form does not cover the shape (then: acfe_conv2d_dgrad +
+ * acfe_bn_bwd_reduce). */
+int acfe_conv2d_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int dtype);
+int acfe_conv2d_dgrad_bn(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R, int S,
+                         int stride, int pad_top, int pad_left, int H, int W, void* dx, int dtype,
+                         const void* x_bn, const float* scale, const float* shift, const float* mean,
+                         const float* invstd, int relu, double* part, int part_rows, void* stream);
 /* float count of the wgrad split-K workspace. */
 long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q);
 /* dW (fp32 KRSC) = beta*dW + sum_pixels dY (x) im2col(X). */
@@ -439,6 +452,15 @@ int acfe_bn_maxpool2d_fused(const void* x, int N, int H, int W, int C, const flo
 /* Backward of acfe_maxpool2d_fused from its argmax bytes (x is not re-read). */
 int acfe_maxpool2d_bwd_argmax(const uint8_t* argmax, const void* dy, int N, int H, int W, int C, int kh, int kw,
                               float drop_rate, unsigned long long seed, void* dx, int dtype, void* stream);
+/* acfe_maxpool2d_bwd_argmax (no dropout) fused with the acfe_bn_bwd_reduce of
+ * the BatchNormalization in front of the pool (wr_resnet_bird.py:29-30, the
+ * stem's BN -> MaxPool2D((1, 2)); backward of acfe_bn_maxpool2d_fused): the
+ * expanded gradient dx is written and, with x = the BN input, the reduce slab
+ * part [acfe_reduce_blocks(N*H*W)][2][C] = {sum g, sum g * (x - mean) * invstd}
+ * (g = dx masked by the BN's ReLU when relu) for acfe_bn_bwd_finalize_ex. */
+int acfe_maxpool2d_bwd_argmax_bn(const uint8_t* argmax, const void* dy, int N, int H, int W, int C, int kh, int kw,
+                                 void* dx, int dtype, const void* x, const float* scale, const float* shift,
+                                 const float* mean, const float* invstd, int relu, double* part, void* stream);
 int acfe_avgpool2d(const void* x, int N, int H, int W, int C, int k, void* y, int dtype, void* stream);
 int acfe_avgpool2d_bwd(const void* dy, int N, int H, int W, int C, int k, void* dx, int dtype, void* stream);
 /* Reduce the middle axis of [outer][L][inner] to fp32 [outer][inner]:

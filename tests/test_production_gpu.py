@@ -563,3 +563,145 @@ def test_model_bn_prologue_matches_unfused(env, cuda):
     assert torch.equal(l0, l1)
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("N,H,W,C,kh,kw,relu", [(8, 128, 513, 16, 1, 2, False), (4, 33, 70, 64, 2, 2, True),
+                                                (2, 30, 45, 16, 3, 3, True)])
+def test_maxpool_bwd_bn_reduce_fused(env, cuda, N, H, W, C, kh, kw, relu):
+    """acfe_maxpool2d_bwd_argmax_bn (the stem BN -> MaxPool2D((1, 2)) backward,
+    wr_resnet_bird.py:29-30, at the T1 shape; odd sizes whose edge rows /
+    columns fall outside every window) against the unfused pair
+    acfe_maxpool2d_bwd_argmax -> acfe_bn_bwd_reduce: the expanded gradient
+    bit-identical, the reduce slab's per-channel column sums within 1e-9
+    relative (both sum in fp32 partials and doubles, in different orders)."""
+    ops, call, lib, ptr, stream = env
+    g = torch.Generator().manual_seed(17 + H)
+    x = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
+    sc = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    sh = (torch.randn(C, generator=g) * 0.3).to(cuda)
+    mu = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    inv = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    P, Q = H // kh, W // kw
+    y = torch.empty((N, P, Q, C), dtype=BF, device=cuda)
+    am = torch.empty((N, P, Q, C), dtype=torch.uint8, device=cuda)
+    call("acfe_bn_maxpool2d_fused", ptr(x), N, H, W, C, ptr(sc), ptr(sh), int(relu), kh, kw, ptr(y), ptr(am), None, 1,
+         stream())
+    dy = torch.randn((N, P, Q, C), generator=g).to(BF).to(cuda)
+    rows = N * H * W
+    nrows = lib.acfe_reduce_blocks(rows)
+    gu0 = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+    gu1 = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+    part0 = torch.empty((nrows, 2, C), dtype=F64, device=cuda)
+    part1 = torch.full((nrows, 2, C), float("nan"), dtype=F64, device=cuda)
+    call("acfe_maxpool2d_bwd_argmax", ptr(am), ptr(dy), N, H, W, C, kh, kw, 0.0, 0, ptr(gu0), 1, stream())
+    call("acfe_bn_bwd_reduce", ptr(gu0), 1, ptr(x), 1, rows, C, ptr(sc), ptr(sh), ptr(mu), ptr(inv), int(relu),
+         ptr(part0), stream())
+    call("acfe_maxpool2d_bwd_argmax_bn", ptr(am), ptr(dy), N, H, W, C, kh, kw, ptr(gu1), 1, ptr(x), ptr(sc), ptr(sh),
+         ptr(mu), ptr(inv), int(relu), ptr(part1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(gu1.view(torch.int16), gu0.view(torch.int16))
+    s0, s1 = part0.sum(0).cpu(), part1.sum(0).cpu()
+    assert torch.isfinite(s1).all()
+    # float64 reference of the sums
+    gx = gu0.cpu().to(F64)
+    xx = x.cpu().to(F64)
+    if relu:
+        gx = gx * ((xx * sc.cpu().to(torch.float32).to(F64) + sh.cpu().to(F64)) > 0)
+    ref = torch.stack([gx.sum((0, 1, 2)), (gx * (xx - mu.cpu().to(F64)) * inv.cpu().to(F64)).sum((0, 1, 2))])
+    scale_ = ref.abs().amax(1, keepdim=True).clamp_min(1.0)
+    assert ((s1 - s0).abs() / scale_).max().item() < 1e-6, ((s1 - s0).abs() / scale_).max()
+    assert ((s1 - ref).abs() / scale_).max().item() < 1e-5
+
+
+@pytest.mark.parametrize("model_name", ["bird", "wrn"])
+def test_model_bn_reduce_fusion_matches_unfused(env, cuda, model_name):
+    """A training step with the BN backward reduces formed by the kernels that
+    produce their gradients (ops.FUSE_BN_REDUCE: the stem BN's by the pool
+    backward on wr_resnet_bird, bn2a / bn2b's by the 64-channel dgrads on
+    wr_resnet) against the separate reduce passes: same loss and logits;
+    gradients equal up to the sums' summation order."""
+    ops = env[0]
+    from acfe.train import FrontEnd, Trainer
+    import bench
+
+    B = 4
+    outs = []
+    for fuse in (False, True):
+        ops.FUSE_BN_REDUCE = fuse
+        try:
+            torch.manual_seed(0)
+            if model_name == "bird":
+                from resnet.wr_resnet_bird import WRResNet
+                model = WRResNet(input_shape=(128, 513, 3), classes=10, dtype=BF).to(cuda)
+            else:
+                from resnet.wr_resnet import WRResNet
+                model = WRResNet(input_shape=(128, 513, 1), classes=10, dtype=BF).to(cuda)
+            fe = FrontEnd(n_mels=128, dtype=BF, device=cuda).to(cuda)
+            tr = Trainer(model, fe, lr=0.0, loss="cce", device=cuda)
+            x1, x2, lam, y = bench.make_batches(B, 10, cuda, n_sets=1)[0]
+            ops._seed_counter = itertools.count()  # same dropout seeds in both runs
+            loss, z = tr.step(x1, y, x2, lam)
+            torch.cuda.synchronize()
+            outs.append((loss.detach().clone(), z.detach().clone(), tr.arena.grad.detach().clone()))
+        finally:
+            ops.FUSE_BN_REDUCE = ops.FUSE
+    (l0, z0, g0), (l1, z1, g1) = outs
+    assert torch.equal(l0, l1) and torch.equal(z0, z1)
+    rel = ((g1.double() - g0.double()).norm() / g0.double().norm()).item()
+    # The fused sums differ from the reduce pass's in summation order only
+    # (~1e-7 relative: the first fused BN's gamma / beta gradients); each later
+    # BN backward in bf16 turns that into rounding flips of its dX, and at
+    # batch 4 the BN backwards amplify them ~3-10x per block towards the input
+    # (per-parameter profiles, tools/dbg_bnfuse.py: bird r04j 1e-7 at
+    # blocks.3.bn2b -> 5e-3 at the stem; wrn r04o 1e-7 at blocks.5.bn2b ->
+    # 6e-3 at the stem, whole arena 3.2e-3), as they do any rounding
+    # difference of the unfused chain.  The sums themselves: the op tests.
+    assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("N,H,W,C,K,relu", [(4, 128, 513, 64, 64, True), (2, 21, 70, 64, 128, True),
+                                              (3, 9, 64, 64, 64, False)])
+def test_conv_dgrad_bn_reduce_fused(env, cuda, N, H, W, C, K, relu):
+    """acfe_conv2d_dgrad_bn (wr_resnet's 64-channel bn2a / bn2b -> conv dgrads,
+    resnet/wr_resnet.py:56-80, at the stage-1 128 x 513 shape; partial row /
+    column tiles; no ReLU) against acfe_conv2d_dgrad ->
+    acfe_bn_bwd_reduce: dX bit-identical, the reduce slab's per-channel column
+    sums within 1e-6 of each other and 1e-5 of a float64 sum (relative to the
+    largest sum)."""
+    ops, call, lib, ptr, stream = env
+    g = torch.Generator().manual_seed(29 + W)
+    dy = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+    w = (torch.randn((K, 3, 3, C), generator=g) * 0.05).to(cuda)
+    xb = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
+    sc = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    sh = (torch.randn(C, generator=g) * 0.3).to(cuda)
+    mu = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    inv = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    wf = ops.pack_weights(w, BF, True)
+    rows = N * H * W
+    brows = lib.acfe_conv2d_dgrad_bn_rows(N, H, W, C, K, 3, 3, 1, 1)
+    assert brows > 0
+    assert lib.acfe_conv2d_dgrad_bn_rows(N, H, W, 32, K, 3, 3, 1, 1) == 0  # uncovered: C = 32
+    assert lib.acfe_conv2d_dgrad_bn_rows(N, H, W, 128, 128, 3, 3, 1, 1) == 0  # uncovered: C = 128
+    dx0 = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+    dx1 = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+    nrows = lib.acfe_reduce_blocks(rows)
+    part0 = torch.empty((nrows, 2, C), dtype=F64, device=cuda)
+    part1 = torch.full((brows, 2, C), float("nan"), dtype=F64, device=cuda)
+    call("acfe_conv2d_dgrad", ptr(dy), N, H, W, K, ptr(wf), C, 3, 3, 1, 1, 1, H, W, ptr(dx0), 1, None, stream())
+    call("acfe_bn_bwd_reduce", ptr(dx0), 1, ptr(xb), 1, rows, C, ptr(sc), ptr(sh), ptr(mu), ptr(inv), int(relu),
+         ptr(part0), stream())
+    call("acfe_conv2d_dgrad_bn", ptr(dy), N, H, W, K, ptr(wf), C, 3, 3, 1, 1, 1, H, W, ptr(dx1), 1, ptr(xb), ptr(sc),
+         ptr(sh), ptr(mu), ptr(inv), int(relu), ptr(part1), brows, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx1.view(torch.int16), dx0.view(torch.int16))
+    s0, s1 = part0.sum(0).cpu(), part1.sum(0).cpu()
+    assert torch.isfinite(s1).all()
+    gx = dx0.cpu().to(F64)
+    xx = xb.cpu().to(F64)
+    if relu:
+        gx = gx * ((xb.cpu().float() * sc.cpu() + sh.cpu()) > 0).to(F64)
+    ref = torch.stack([gx.sum((0, 1, 2)), (gx * ((xb.cpu().float() - mu.cpu()) * inv.cpu()).to(F64)).sum((0, 1, 2))])
+    scale_ = ref.abs().amax(1, keepdim=True).clamp_min(1.0)
+    assert ((s1 - s0).abs() / scale_).max().item() < 1e-6, ((s1 - s0).abs() / scale_).max()
+    assert ((s1 - ref).abs() / scale_).max().item() < 1e-5

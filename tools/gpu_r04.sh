@@ -45,6 +45,10 @@ for w in "$@"; do
     t1) bp t1 --steps 20 --warmup 5 ;;
     convtests) step convtests 600 python -u -m pytest tests/test_production_gpu.py tests/test_fused_gpu.py \
                  tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    fusetests) step fusetests 600 python -u -m pytest tests/test_production_gpu.py -m gpu -k "reduce_fus" -x -v \
+                 --timeout 120 --timeout-method thread ;;
+    wrn0) ACFE_BN_REDUCE_FUSE=0 step wrn0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    t10) ACFE_BN_REDUCE_FUSE=0 step t10_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     wrn) bp wrn --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     t1fp32) bp t1fp32 --dtype fp32 --steps 10 --warmup 3 --no-cpu-baseline ;;
     infer) bp infer --workload infer --steps 5 --warmup 2 ;;
