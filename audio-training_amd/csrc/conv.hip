@@ -3629,11 +3629,16 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
   return launch_rc("acfe_conv2d_wgrad");
 }
 
-// k_wgrad3x3_halo launch (3x3 stride 1, C % 64 == 0, K in {64, 128}, Q % 64 ==
-// 0): split count within the planned workspace (`splits`), returned in *used.
+// k_wgrad3x3_halo launch (3x3 stride 1; C % 64 == 0 with K in {32, 64, 128,
+// 256}, or C in {16, 32} with K in {128, 256}; a partial last 64-pixel column
+// segment is masked): split count within the planned workspace (`splits`),
+// returned in *used.
 static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
                              long long splits, hipStream_t s, int* used) {
-  const int cw = g.C % 64 == 0 ? 64 : g.C;  // 16 / 32-channel layers: one chunk of C
+  // 16 / 32-channel layers: one chunk of C; K = 256 (wr_resnet's stage-3
+  // 256 -> 256): 32-channel chunks, so the K x 9 x CW accumulators stay 36
+  // tiles per wave
+  const int cw = g.C % 64 == 0 ? (g.K == 256 ? 32 : 64) : g.C;
   // two output rows per step for the K = 64 (plain or pooled dY) and K = 32
   // layers (r02au-aw: 72 instead of 36 MFMAs per wave per barrier); the K =
   // 128 pooled-gradient variant spills at two rows (138 VGPRs) and keeps one
@@ -3714,7 +3719,7 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   g.ldy = K;
   int rc;
   if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 &&
-      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32)) ||
+      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) ||
        ((C == 32 && (K == 128 || K == 256)) || (C == 16 && K == 256))) &&
       (long long)N * P * ((Q + 63) / 64) < (1ll << 31)) {
     // halo-staged kernel; its split count stays within the planned workspace

@@ -432,15 +432,16 @@ def test_conv_narrow_production(env, cuda, C, K, H, W):
 
 
 @pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (32, 128, 32, 64), (32, 256, 16, 32), (16, 256, 16, 32),
-                                     (64, 64, 64, 128), (128, 64, 64, 128), (64, 64, 14, 100)],
+                                     (64, 64, 64, 128), (128, 64, 64, 128), (64, 64, 14, 100), (256, 256, 22, 86)],
                          ids=["s2-21", "s2-2b", "s3-2b-b6", "s3-2b", "k64-rowpair", "k64-rowpair-2chunks",
-                              "k64-rowpair-partial"])
+                              "k64-rowpair-partial", "wrn-s3-256"])
 def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
     """k_wgrad3x3_halo for the stage-2/3 layers whose channel count is the
     feature height: K = 32 (branch21 128 -> 32) and the 16 / 32-channel
     chunks (branch2b 32 -> 128 / 256, 16 -> 256), and the K = 64 layers'
     two-rows-per-step variant (k_wgrad3x3_halo<64, false, 64, 2>: 64 x 128
     stage-2 shapes, two 64-channel chunks, and a partial last column segment),
+    and wr_resnet's stage-3 256 -> 256 at 22 x 86 (32-channel chunks of C),
     at 32 clips and the production split count, against float64."""
     ops, call, lib, ptr, stream = env
     N = 32
