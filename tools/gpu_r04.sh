@@ -34,6 +34,9 @@ for w in "$@"; do
     evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r04 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
              'k_conv3x3_rows<64,8,4,true,true> (wr_resnet b1/b2 conv2a 3x3 64->64 @128x513 with the BN prologue + dropout + BN sums, batch 512)' \
              --model wrn --classes 2 --steps 2 --warmup 1 ;;
+    evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r04 'k_conv3x3_1w<1, 2, true, true>' 5905580032 \
+             'k_conv3x3_1w<1,2,true,true> (wr_resnet_bird s1b0 branch21 3x3 128->128 @128x256 + 2x2 max-pool + dropout + BN sums, batch 512)' \
+             --steps 3 --warmup 1 ;;
     evinfer) SELECT=7:3 step evinfer 900 bash tools/pmc_evidence.sh infer_fp32 r04 'k_conv_fwd_g<float, 128, 64' 8606859264 \
              'k_conv_fwd_g<float,128,64> (wr_resnet b1.conv2a 3x3 64->64 @128x513 fp32, batch 256)' \
              --workload infer --steps 2 --warmup 1 ;;
