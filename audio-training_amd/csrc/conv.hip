@@ -2309,12 +2309,15 @@ k_conv3x3_c16(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
   constexpr int XG = XR * HWX * 2;       // 16-B granules of the halo (two per pixel)
   constexpr int XPT = (XG + 511) / 512;
   __shared__ __attribute__((aligned(16))) unsigned char xs[XR * HWX * XRB];
-  __shared__ double sstat[2 * KB];
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // the wave's tile row
   const int tpi = tiles_h * tiles_w;
   const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
-  for (int i = tid; i < 2 * KB; i += 512) sstat[i] = 0.0;
+  // BN sums: per-lane f64 partials of the DPP butterfly's slots, one
+  // fixed-order cross-wave sum at the end (per-tile LDS f64 atomics of 16-lane
+  // shuffle sums before, r04)
+  constexpr int NV = 2 * FN * 4;
+  double dstat[NV / 16] = {0.0, 0.0};
   // A fragments: lane (l16, lg) of channel fragment fn holds W[fn * 16 + l16][q * 32 + lg * 8 .. + 7]
   uint4 wa[NQ][FN];
 #pragma unroll
@@ -2377,11 +2380,9 @@ k_conv3x3_c16(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     // epilogue (k_conv3x3_narrow's): pixel (row wid, column fm * 16 + l16), channels fn * 16 + lg * 4 + j
     const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
     const int h = hb * TR + wid;
-    float s1[FN][4], s2[FN][4];
+    float sv[NV];
 #pragma unroll
-    for (int fn = 0; fn < FN; ++fn)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s1[fn][j] = s2[fn][j] = 0.f;
+    for (int i = 0; i < NV; ++i) sv[i] = 0.f;
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
       const int w = wb * SEGW + fm * 16 + l16;
@@ -2404,8 +2405,8 @@ k_conv3x3_c16(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float f = inb ? r[j] : 0.f;
-          s1[fn][j] += f;
-          s2[fn][j] += f * f;
+          sv[fn * 4 + j] += f;
+          sv[FN * 4 + fn * 4 + j] += f * f;
         }
         uint2 v;
         v.x = (__float_as_uint(r[0]) >> 16) | (__float_as_uint(r[1]) & 0xffff0000u);
@@ -2415,29 +2416,37 @@ k_conv3x3_c16(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
       }
     }
     if (stats) {
+      // reduce-scatter over the 16 pixel lanes: lane l16 keeps values b0 + k of sv
+      butterfly_step<NV, 8, 0x128>(sv, lane);
+      butterfly_step<NV / 2, 4, 0x141>(sv, lane);
+      butterfly_step<NV / 4, 2, 0x4E>(sv, lane);
+      butterfly_step<NV / 8, 1, 0xB1>(sv, lane);
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-          for (int off = 1; off < 16; off <<= 1) {
-            s1[fn][j] += __shfl_xor(s1[fn][j], off, 64);
-            s2[fn][j] += __shfl_xor(s2[fn][j], off, 64);
-          }
-          if (l16 == 0) {
-            const int c = fn * 16 + lg * 4 + j;
-            atomicAdd(&sstat[c], (double)s1[fn][j]);
-            atomicAdd(&sstat[KB + c], (double)s2[fn][j]);
-          }
-        }
+      for (int k = 0; k < NV / 16; ++k) dstat[k] += (double)sv[k];
     }
   }
   if (stats) {
+    // fixed-order sum of the 8 waves' partials (same slots in the same lanes;
+    // the halo image is free after the loop)
     __syncthreads();
-    for (int c = tid; c < g.Kp; c += 512) {
-      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = c < KB ? sstat[c] : 0.0;
-      stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = c < KB ? sstat[KB + c] : 0.0;
+    double* red = reinterpret_cast<double*>(xs);
+#pragma unroll
+    for (int k = 0; k < NV / 16; ++k) red[(wid * 64 + lane) * (NV / 16) + k] = dstat[k];
+    __syncthreads();
+    if (wid == 0) {
+      const int b0 = ((l16 >> 3) & 1) * (NV / 2) + ((l16 >> 2) & 1) * (NV / 4) + ((l16 >> 1) & 1) * (NV / 8) +
+                     (l16 & 1) * (NV / 16);
+#pragma unroll
+      for (int k = 0; k < NV / 16; ++k) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v += red[(w * 64 + lane) * (NV / 16) + k];
+        const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
+        stats[((long long)blockIdx.x * 2 + st) * g.Kp + (rm >> 2) * 16 + lg * 4 + (rm & 3)] = v;
+      }
     }
+    for (int c = KB + tid; c < g.Kp; c += 512)  // (padded channels)
+      stats[((long long)blockIdx.x * 2 + 0) * g.Kp + c] = stats[((long long)blockIdx.x * 2 + 1) * g.Kp + c] = 0.0;
     for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
       for (int c = tid; c < 2 * g.Kp; c += 512) stats[((long long)rr * 2 + (c / g.Kp)) * g.Kp + (c % g.Kp)] = 0.0;
   }
