@@ -32,6 +32,8 @@ PROLOGUE = os.environ.get("ACFE_BN_PROLOGUE", "1") != "0"
 # measured 1 % slower per T1 step than the one apply pass it saves, r02ab)
 PRO_POOL = os.environ.get("ACFE_BN_PROLOGUE_POOL", "1") != "0"
 PRO_C1 = os.environ.get("ACFE_BN_PROLOGUE_C1", "0") != "0"
+# ACFE_BN_PROLOGUE_1W=0: no BN prologue on the K = C = 128 one-wave conv (A/B)
+PRO_1W = os.environ.get("ACFE_BN_PROLOGUE_1W", "1") != "0"
 # ACFE_BN_REDUCE_FUSE=0: the BatchNormalization backward reduce runs as its own
 # pass even where the kernel producing its gradient can form the sums (A/B)
 FUSE_BN_REDUCE = FUSE and os.environ.get("ACFE_BN_REDUCE_FUSE", "1") != "0"
@@ -499,6 +501,8 @@ def bn_prologue_ok(x_shape, dtype, w) -> bool:
         return False
     N, H, W, C = x_shape
     K, R, S, Cw = w.shape
+    if K == 128 and not PRO_1W:
+        return False
     return (R, S) == (3, 3) and Cw == C and bool(lib.acfe_conv2d_bn_prologue_supported(N, H, W, C, K, 1))
 
 

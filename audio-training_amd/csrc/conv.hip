@@ -4266,8 +4266,10 @@ ACFE_API int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, cons
 // writes x'; x' is still written (x_bn_out, nullable) for the weight gradient,
 // from the staging registers of the tile's own pixels.  Shapes: K = 64, C % 64
 // == 0, C <= 256, 3x3 stride-1 "same" bf16 (the stage-1 layers).
+// K = 64: k_conv3x3_rows PRO; K = C = 128: k_conv3x3_1w PRO (one image < 2^31 bytes)
 ACFE_API int acfe_conv2d_bn_prologue_supported(int N, int H, int W, int C, int K, int dtype) {
-  return acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, dtype) && K == 64 && C <= 256 &&
+  return acfe_conv2d_rows_supported(N, H, W, C, K, 3, 3, dtype) &&
+         ((K == 64 && C <= 256) || (K == 128 && C == 128 && (long long)H * W * 128 * 2 < (1ll << 31))) &&
          (long long)N * H * W * K < (1ll << 32);
 }
 
@@ -4289,6 +4291,7 @@ ACFE_API int acfe_conv2d_fwd_bn(const void* x, int N, int H, int W, int C, const
   g.pro_relu = bn_relu ? 1 : 0;
   g.pro_out = (uint16_t*)x_bn_out;
   const int srows = grid_m_for(g.M, 1);
+  if (K == 128) return launch_plain1w(g, x, wpacked, bias, y, stats_partial, srows, strm(stream), "acfe_conv2d_fwd_bn", 0);
   if (g.drop.on)
     return launch_rows<64, 4>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
                               "acfe_conv2d_fwd_bn");
@@ -4312,6 +4315,8 @@ ACFE_API int acfe_conv2d_fwd_add_bn(const void* x, int N, int H, int W, int C, c
   g.pro_relu = bn_relu ? 1 : 0;
   g.pro_out = (uint16_t*)x_bn_out;
   const int srows = grid_m_for(g.M, 1);
+  if (K == 128)
+    return launch_plain1w(g, x, wpacked, bias, y, stats_partial, srows, strm(stream), "acfe_conv2d_fwd_add_bn", 3);
   return launch_rows<64, 3>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
                             "acfe_conv2d_fwd_add_bn");
 }

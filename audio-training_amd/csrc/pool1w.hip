@@ -49,13 +49,19 @@ using namespace acfe;
 // segments, read back by acfe_debug_pool1w_stamps (tools/pool1w_stamps.py)
 __device__ unsigned long long g_p1w_stamps[4096 * 8];
 #endif
-template <int PM, int NCH, bool DROP, bool ST = true>
+template <int PM, int NCH, bool DROP, bool ST = true, bool PRO = false>
 __global__ void __launch_bounds__(256, 1)
 k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
              int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
   static_assert(NCH % 2 == 0, "even step count per tile: weight buffer parity is static");
   static_assert(PM == 0 || PM == 1 || ((PM == 2 || PM == 3) && !DROP), "modes");
+  // PRO: the BatchNormalization (+ReLU) of the input applied while staging it
+  // (acfe_conv2d_fwd_bn / fwd_add_bn at K = C = 128: wr_resnet's stage-2
+  // bn2a / bn2b -> conv2a / conv2b), x' = (ReLU)(x * pro_sc + pro_sh) rounded to
+  // bf16 (acfe_bn_apply's values); the tile's own pixels of x' also go to
+  // pro_out for the weight gradient
+  static_assert(!PRO || PM == 0 || PM == 3, "prologue: plain / residual forward");
   constexpr bool CPERM = PM != 1;     // weights x pixels operand order (PM 0 / 2 / 3)
   constexpr bool DENSE = PM == 0 || PM == 3;  // full-resolution output with bias (PM 3: + residual)
   constexpr int KB = 128, TR = 4, FM = 4, FN = 4, NH = 2, NF = NH * FN, SEGW = 64, HWX = SEGW + 2, XRB = 160;
@@ -65,7 +71,8 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   constexpr int XG = XROWS * HWX * 8, XPT = (XG + NT - 1) / NT;  // 16-B input granules
   constexpr int WPW = 3 * KB * 8 / 64 / (NT / 64);               // 12 weight pieces per wave per step
   constexpr int WPG = 4;                                         // pieces per MFMA group (groups 0..2)
-  constexpr int SMEM = XBYTES + 2 * WBYTES + (DENSE ? KB * 4 : 0);  // (PM 0 / 3: bias table)
+  constexpr int SMEMP = XBYTES + 2 * WBYTES + (DENSE ? KB * 4 : 0);  // (PM 0 / 3: bias table)
+  constexpr int SMEM = SMEMP + (PRO ? 2 * 64 * NCH * 4 : 0);          // (PRO: scale / shift of the C channels)
   static_assert(SMEM <= 163840, "LDS");
   static_assert(XPT * NT - XG <= 2 * XROWS * HWX, "spare granules fit the pixel pads");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
@@ -101,6 +108,9 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   for (int h = 0; h < NH; ++h)
     bch[h] = (PM == 1 && bias) ? *reinterpret_cast<const f4*>(bias + h * 64 + 4 * l16) : f4{0.f, 0.f, 0.f, 0.f};
   float* btab = reinterpret_cast<float*>(smem + XBYTES + 2 * WBYTES);
+  float* pss = reinterpret_cast<float*>(smem + SMEMP);  // PRO: scale[C], shift[C]
+  if constexpr (PRO)
+    for (int i = tid; i < 64 * NCH; i += NT) pss[i] = g.pro_sc[i], pss[64 * NCH + i] = g.pro_sh[i];
   if constexpr (DENSE)
     if (tid < KB) btab[tid] = bias ? bias[tid] : 0.f;
 
@@ -175,6 +185,10 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   int rel[XPT];
   int tbase = 0;
   unsigned cmask = 0, pos0 = 0, pos1 = 0;
+  // PRO: granules inside the image (zero after the transform otherwise: the
+  // conv pads x', not x) and the tile's own pixels (stored to pro_out)
+  unsigned vmask = 0, omask = 0;
+  __amdgpu_buffer_rsrc_t prs;
   if constexpr (PM != 2) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
@@ -201,6 +215,20 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         const unsigned xpix = (idx % (HWX * 8)) >> 3;
         const bool ok = idx < (unsigned)XG && (unsigned)(sw0 + (int)xpix) < (unsigned)g.W;
         cmask |= (ok ? 1u : 0u) << i;
+      }
+      if constexpr (PRO) {
+        prs = __builtin_amdgcn_make_buffer_rsrc((void*)(g.pro_out + (long long)n * g.H * g.W * g.C), (short)0,
+                                                g.H * g.W * CB, 0x00020000);
+        vmask = omask = 0;
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+          const unsigned idx = (unsigned)t0 + NT * i;
+          const int xrow = (int)(idx / (HWX * 8)), xpix = (int)((idx % (HWX * 8)) >> 3);
+          const bool ok = ((cmask >> i) & 1u) && (unsigned)(sh0 + xrow) < (unsigned)g.H;
+          const bool own = ok && xrow >= 1 && xrow <= TR && xpix >= 1 && xpix <= SEGW;
+          vmask |= (ok ? 1u : 0u) << i;
+          omask |= (own ? 1u : 0u) << i;
+        }
       }
     } else {
       // X = pooled gradient [N][H/2][W/2][C], amax its argmax bytes
@@ -245,11 +273,34 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     const int idx = tid + NT * i, e = idx - XG;
     return idx < XG ? (idx >> 3) * XRB + gr * 16 : (e >> 1) * XRB + 128 + (e & 1) * 16;
   };
-  auto sstore = [&]() __attribute__((always_inline)) {
+  auto sstore = [&](int scc) __attribute__((always_inline)) {
+    f4 sc0, sc1, sh0_, sh1_;
+    bool relu = false;
+    if constexpr (PRO) {  // this thread's 8 channels scc * 64 + gr * 8 ..
+      const f4* ps = reinterpret_cast<const f4*>(pss + scc * 64 + gr * 8);
+      sc0 = ps[0], sc1 = ps[1], sh0_ = ps[16 * NCH], sh1_ = ps[16 * NCH + 1];
+      relu = g.pro_relu != 0;
+    }
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       u32x4 v = rx[i];
       if constexpr (PM == 2) v &= unpool_mask(ra[i], ((i < 8 ? pos0 >> (4 * i) : pos1 >> (4 * (i - 8)))) & 3u);
+      if constexpr (PRO) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const float s0 = d < 2 ? sc0[2 * d] : sc1[2 * d - 4], s1 = d < 2 ? sc0[2 * d + 1] : sc1[2 * d - 3];
+          const float h0 = d < 2 ? sh0_[2 * d] : sh1_[2 * d - 4], h1 = d < 2 ? sh0_[2 * d + 1] : sh1_[2 * d - 3];
+          float lo = __builtin_fmaf(__uint_as_float(v[d] << 16), s0, h0);
+          float hi = __builtin_fmaf(__uint_as_float(v[d] & 0xffff0000u), s1, h1);
+          if (relu) lo = fmaxf(lo, 0.f), hi = fmaxf(hi, 0.f);
+          const b2v pk = __builtin_convertvector((f2v){lo, hi}, b2v);
+          v[d] = __builtin_bit_cast(unsigned, pk);
+        }
+        v = ((vmask >> i) & 1u) ? v : u32x4{0u, 0u, 0u, 0u};
+        __builtin_amdgcn_raw_buffer_store_b128(v, prs,
+                                               ((omask >> i) & 1u) ? (unsigned)(tbase + scc * 128 + rel[i]) : 0x80000000u,
+                                               0, 0);
+      }
       *reinterpret_cast<u32x4*>(smem + sslot(i)) = v;
     }
   };
@@ -633,7 +684,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       if constexpr (rs == 2) {
         __syncthreads();  // every wave has finished reading the chunk's rows
         stamp(3);
-        sstore();
+        sstore(cc + 1 == NCH ? 0 : cc + 1);
         stamp(4);
         wait_vmcnt<NLATE>();  // next step's weight pieces landed
         __syncthreads();
@@ -653,7 +704,8 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     wprep(0, 0);
 #pragma unroll
     for (int j = 0; j < WPW; ++j) wpiece(j);
-    sstore();
+    if constexpr (PRO) __syncthreads();  // pss
+    sstore(0);
   }
   wait_vmcnt<0>();
   __syncthreads();
@@ -764,10 +816,24 @@ int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float
   int th, tw, gp;
   long long nt;
   grid_1w(g, stats, srows, &th, &tw, &nt, &gp);
-#define P1W_L(PM_, D, S_)                                                                                     \
-  hipLaunchKernelGGL((k_conv3x3_1w<PM_, 2, D, S_>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x,        \
-                     (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows, nullptr)
-  if (pm == 3) {
+#define P1W_L(PM_, D, S_, ...)                                                                                \
+  hipLaunchKernelGGL((k_conv3x3_1w<PM_, 2, D, S_, ##__VA_ARGS__>), dim3(gp), dim3(256), 0, s, g,              \
+                     (const uint16_t*)x, (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows,  \
+                     nullptr)
+  if (g.pro_sc) {  // BN prologue (acfe_conv2d_fwd_bn / fwd_add_bn)
+    if (!g.pro_sh || !g.pro_out || ((uintptr_t)g.pro_out & 15) || ((uintptr_t)x & 15)) return ACFE_E_INVAL;
+    if (pm == 3) {
+      if (!g.res || g.drop.on) return ACFE_E_INVAL;
+      if (stats) P1W_L(3, false, true, true);
+      else P1W_L(3, false, false, true);
+    } else if (g.drop.on) {
+      P1W_L(0, true, true, true);
+    } else if (stats) {
+      P1W_L(0, false, true, true);
+    } else {
+      P1W_L(0, false, false, true);
+    }
+  } else if (pm == 3) {
     if (!g.res || g.drop.on) return ACFE_E_INVAL;
     if (stats) P1W_L(3, false, true);
     else P1W_L(3, false, false);

@@ -474,20 +474,23 @@ def _bn_affine(C, seed, device):
     return sc.to(device), sh.to(device)
 
 
-@pytest.mark.parametrize("N,H,W,C,mode", [(8, 64, 128, 64, "drop"), (8, 64, 128, 128, "add"),
-                                          (4, 64, 128, 64, "plain"), (3, 14, 100, 64, "add"),
-                                          (2, 9, 70, 128, "drop"), (8, 64, 128, 64, "pool"),
-                                          (3, 14, 100, 64, "pool")])
-def test_conv_bn_prologue(env, cuda, N, H, W, C, mode):
+@pytest.mark.parametrize("N,H,W,C,K,mode", [(8, 64, 128, 64, 64, "drop"), (8, 64, 128, 128, 64, "add"),
+                                            (4, 64, 128, 64, 64, "plain"), (3, 14, 100, 64, 64, "add"),
+                                            (2, 9, 70, 128, 64, "drop"), (8, 64, 128, 64, 64, "pool"),
+                                            (3, 14, 100, 64, 64, "pool"), (4, 64, 257, 128, 128, "drop"),
+                                            (4, 64, 257, 128, 128, "add"), (2, 9, 70, 128, 128, "plain"),
+                                            (3, 14, 100, 128, 128, "add")])
+def test_conv_bn_prologue(env, cuda, N, H, W, C, K, mode):
     """acfe_conv2d_fwd_bn / acfe_conv2d_fwd_add_bn (BatchNormalization + ReLU
     applied while staging the conv input, resnet/wr_resnet_bird.py:136-161)
     against the unfused chain acfe_bn_apply -> acfe_conv2d_fwd_dropout /
     acfe_conv2d_fwd_add: the conv output, its BN statistics and the written BN
     output x' all bit-identical; x' also against the float64 BN of x within one
     bf16 ulp.  Shapes: the stage-1 layers (K = 64, C = 64 / 128) at production
-    tile counts, plus partial 6-row / 64-column tiles."""
+    tile counts, plus partial 6-row / 64-column tiles; K = C = 128 (the
+    one-wave kernel's prologue: wr_resnet's stage-2 bn2a / bn2b -> conv2a /
+    conv2b at 64 x 257, a ragged image, no-dropout plain)."""
     ops, call, lib, ptr, stream = env
-    K = 64
     assert lib.acfe_conv2d_bn_prologue_supported(N, H, W, C, K, 1)
     x, w, b, g = _data(N, H, W, C, K, 131 + C + H, cuda)
     sc, sh = _bn_affine(C, 7 + C, cuda)

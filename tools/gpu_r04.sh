@@ -52,6 +52,9 @@ for w in "$@"; do
                  --timeout 120 --timeout-method thread ;;
     wrn0) ACFE_BN_REDUCE_FUSE=0 step wrn0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     t10) ACFE_BN_REDUCE_FUSE=0 step t10_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    wrnp0) ACFE_BN_PROLOGUE_1W=0 step wrnp0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    protests) step protests 600 python -u -m pytest tests/test_production_gpu.py tests/test_model_gpu.py -m gpu -k "prologue or model" -v \
+                 --timeout 120 --timeout-method thread ;;
     wrn) bp wrn --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     t1fp32) bp t1fp32 --dtype fp32 --steps 10 --warmup 3 --no-cpu-baseline ;;
     infer) bp infer --workload infer --steps 5 --warmup 2 ;;
