@@ -2062,38 +2062,45 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
   }
 }
 
-// ------------------------------------------------------------------ 3x3 stride 1, 32 -> 128 channels
-// wr_resnet_bird's stage-2 branch2b forward (32 -> 128 at 32 x 64,
-// resnet/wr_resnet_bird.py:150-152) and the branch21 dgrad (dY of 32 channels
-// -> dX of 128).  With C = 32 the im2col GEMM (k_conv_fwd_g) runs 5 K-tiles
-// per 128-pixel tile, its prologue / epilogue dominating (245 / 178 us per
-// call at T1, ~0.3 PFLOP/s).  Here, as in k_conv3x3_narrow: the packed weights
-// (9 taps x 32 x 128 bf16 = 72 KB) stay in LDS for the workgroup's lifetime,
-// a tile (256 pixels: TR rows x SEGW) stages its (TR + 2) x (SEGW + 2) input
-// halo once for all nine taps (80-B pixel pitch: 16 consecutive pixels of a
-// fragment read start on distinct 4-bank groups), and each tap is ONE k-step of
-// v_mfma_f32_16x16x32_bf16 over its 32 channels: 8 waves x 32 pixels x 128
-// channels, 144 MFMAs per wave per tile.  Weight rows are permuted (fragment fn,
-// A row m = output channel 32 (m >> 2) + 4 fn + (m & 3)) so a lane holds 32
-// consecutive channels of its pixel: four 16-B stores per pixel; granule slot
-// g ^ ((k >> 5) & 3) keeps the 16 rows of a fragment read on distinct banks.
-// Epilogue: bias (LDS table), bf16 rounding, the pair-hash Dropout or (ADD,
-// acfe_conv2d_fwd_add: the branch2b forward) the residual g.res (+ReLU) as
-// ops.add stores it, BN sums by a DPP butterfly into per-lane f64 partials (one
-// fixed-order cross-wave sum at the end).  The next tile's halo is in flight in
-// registers during the MFMAs.
-template <int SEGW, bool DROP, bool ADD = false>
+// ------------------------------------------------------------------ 3x3 stride 1, few input channels, wide output
+// k_conv3x3_cw<CW, KB>: CW = 32 -> KB = 128 (wr_resnet_bird's stage-2 branch2b
+// forward + residual and branch21 dgrad, 32 x 64; resnet/wr_resnet_bird.py:
+// 150-152) and CW = 16 -> KB = 256 (stage 3 at 16 x 32).  With C = 16 / 32 the
+// im2col GEMM (k_conv_fwd_g) runs 3-5 K-tiles per 128-pixel tile, its
+// prologue / epilogue dominating (T1: 245 / 178 us per 32 -> 128 call, ~0.3
+// PFLOP/s).  Here, as in k_conv3x3_narrow: the packed weights (9 x CW x KB
+// bf16, 72 / 80 KB) stay in LDS for the workgroup's lifetime as NQ 32-deep
+// k-steps (CW = 32: one tap each; CW = 16: taps 2 qs, 2 qs + 1, the last
+// step's second half the packing's zeros), a tile (256 pixels: TR rows x SEGW)
+// stages its (TR + 2) x (SEGW + 2) input halo once for all nine taps (80- /
+// 48-B pixel pitch: 16 consecutive pixels of a fragment read start on
+// distinct 4-bank groups), 8 waves x 32 pixels x KB channels, 9 / 5 k-steps of
+// v_mfma_f32_16x16x32_bf16 per tile.  Weight rows are permuted (fragment fn,
+// A row m = output channel 4 FN (m >> 2) + 4 fn + (m & 3)) so a lane holds
+// 4 FN consecutive channels of its pixel (16-B stores; granule slot
+// g ^ ((k >> LQ) & 3) keeps a fragment's 16 rows on distinct banks).
+// Epilogue per 32-channel half: bias (LDS table), bf16 rounding, the pair-hash
+// Dropout or (ADD, acfe_conv2d_fwd_add) the residual g.res (+ReLU) as ops.add
+// stores it, BN sums by a DPP butterfly into per-lane f64 partials (one
+// fixed-order cross-wave sum at the end).  The next tile's halo is in flight
+// in registers during the MFMAs (CW = 32: the residual words too).
+template <int CW, int KB, int SEGW, bool DROP, bool ADD = false>
 __global__ void __launch_bounds__(512, 1)
-k_conv3x3_c32(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
-              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
-              int tiles_w, int ntiles, int srows) {
-  constexpr int KB = 128, CW = 32, NT = 512, TR = 256 / SEGW, HWX = SEGW + 2, XR = TR + 2, XRB = 80;
-  constexpr int FM = 2, FN = 8, NV = 2 * FN * 4;
+k_conv3x3_cw(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+             const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
+             int tiles_w, int ntiles, int srows) {
+  static_assert((CW == 32 && KB == 128) || (CW == 16 && KB == 256), "shapes");
   static_assert(!(DROP && ADD), "modes");
-  constexpr int XBYTES = XR * HWX * XRB, WBYTES = 9 * KB * CW * 2;
-  constexpr int XG = XR * HWX * 4, XPT = (XG + NT - 1) / NT;
+  // FM pixel fragments per wave (KB = 256: one, the 128 accumulators of two spilled)
+  constexpr int FM = KB == 256 ? 1 : 2, TP = 128 * FM;  // tile pixels (8 waves x 16 FM)
+  constexpr int NT = 512, TR = TP / SEGW, HWX = SEGW + 2, XR = TR + 2, XRB = CW == 32 ? 80 : 48;
+  constexpr int NQ = (9 * CW + 31) / 32, FN = KB / 16, CPL = 4 * FN, LQ = CPL == 32 ? 5 : 6;
+  constexpr int NH = FN / 8, NV = 64;  // 32-channel epilogue halves; BN-sum values per half
+  constexpr int GPP = CW / 8, XG = XR * HWX * GPP, XPT = (XG + NT - 1) / NT;
+  constexpr int XBYTES = XR * HWX * XRB, WBYTES = NQ * KB * 64;
   constexpr int SMEM = XBYTES + WBYTES + KB * 4;
-  static_assert(SMEM <= 163840, "LDS");
+  static_assert(SMEM <= 163840 && 8 * 64 * NH * 4 * 8 <= SMEM, "LDS");
+  constexpr bool RPF = ADD && NH == 1;  // residual words prefetched before the MFMAs
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   unsigned char* Wl = smem + XBYTES;
   float* btab = reinterpret_cast<float*>(smem + XBYTES + WBYTES);
@@ -2101,11 +2108,12 @@ k_conv3x3_c32(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tpi = tiles_h * tiles_w;
   const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
-  // resident weights: row tap * KB + k (64 B = 32 channels), granule gw at slot gw ^ ((k >> 5) & 3)
-  for (int gi = tid; gi < 9 * KB * 4; gi += NT) {
-    const int row = gi >> 2, gw = gi & 3, k = row % KB, t = row / KB;
-    const u32x4 v = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + t * CW + gw * 8);
-    *reinterpret_cast<u32x4*>(Wl + row * 64 + ((gw ^ ((k >> 5) & 3)) << 4)) = v;
+  // resident weights: row qs * KB + k = k-dim [32 qs, 32 qs + 32) of output
+  // channel k (64 B), granule gw at slot gw ^ ((k >> LQ) & 3)
+  for (int gi = tid; gi < NQ * KB * 4; gi += NT) {
+    const int row = gi >> 2, gw = gi & 3, k = row % KB, qs = row / KB;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(Wp + (long long)k * g.Kdp + qs * 32 + gw * 8);
+    *reinterpret_cast<u32x4*>(Wl + row * 64 + ((gw ^ ((k >> LQ) & 3)) << 4)) = v;
   }
   for (int i = tid; i < KB; i += NT) btab[i] = bias ? bias[i] : 0.f;
   const TileWalk walk(ntiles);
@@ -2119,61 +2127,66 @@ k_conv3x3_c32(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + NT * i;
-      const int px = idx >> 2, xrow = px / HWX, xpix = px - xrow * HWX;
+      const int px = idx / GPP, xrow = px / HWX, xpix = px - xrow * HWX;
       const int hin = h0 + xrow, win = w0 + xpix;
       const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
-      rx[i] = *reinterpret_cast<const u32x4*>(ok ? img + ((long long)hin * g.W + win) * CW + (idx & 3) * 8 : zp);
+      rx[i] = *reinterpret_cast<const u32x4*>(ok ? img + ((long long)hin * g.W + win) * CW + (idx % GPP) * 8 : zp);
     }
   };
   auto sstore = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int idx = tid + NT * i;
-      if (idx < XG) *reinterpret_cast<u32x4*>(smem + (idx >> 2) * XRB + (idx & 3) * 16) = rx[i];
+      if (idx < XG) *reinterpret_cast<u32x4*>(smem + (idx / GPP) * XRB + (idx % GPP) * 16) = rx[i];
     }
   };
-  // fragment read offsets: weights (tap 0) of fragment fn, this lane's row
-  // k = 32 (l16 >> 2) + 4 fn + (l16 & 3), granule q; input pixels of fragment fm
-  int woff[FN], xoff[FM];
-#pragma unroll
-  for (int fn = 0; fn < FN; ++fn) {
-    const int k = 32 * (l16 >> 2) + 4 * fn + (l16 & 3);
-    woff[fn] = k * 64 + ((q ^ ((k >> 5) & 3)) << 4);
-  }
+  // fragment read offsets: weights of fragment fn (row k = CPL (l16 >> 2) +
+  // 4 fn + (l16 & 3), granule q); input pixels of fragment fm; per k-step the
+  // lane's tap (k-dim 32 qs + 8 q) and channel offset in the halo
+  // (k >> LQ) = l16 >> 2 for every fn: fragment fn is the lane's base + 256 fn B)
+  int xoff[FM], xq[NQ];
+  const int kw0 = CPL * (l16 >> 2) + (l16 & 3);
+  const int woff0 = kw0 * 64 + ((q ^ ((l16 >> 2) & 3)) << 4);
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm) {
-    const int p = wid * 32 + fm * 16 + l16;
-    xoff[fm] = ((p / SEGW) * HWX + (p % SEGW)) * XRB + q * 16;
+    const int p = wid * 16 * FM + fm * 16 + l16;
+    xoff[fm] = ((p / SEGW) * HWX + (p % SEGW)) * XRB;
   }
-  double dstat[NV / 16];
 #pragma unroll
-  for (int k = 0; k < NV / 16; ++k) dstat[k] = 0.0;
-  const int cq = 32 * q;  // this lane's 32 output channels
+  for (int qs = 0; qs < NQ; ++qs) {
+    const int kd = 32 * qs + 8 * q, t = kd / CW < 9 ? kd / CW : 8, c0 = kd % CW;  // (t 9: zero weights)
+    xq[qs] = ((t / 3) * HWX + (t % 3)) * XRB + c0 * 2;
+  }
+  double dstat[NH][NV / 16];
+#pragma unroll
+  for (int hh = 0; hh < NH; ++hh)
+#pragma unroll
+    for (int k = 0; k < NV / 16; ++k) dstat[hh][k] = 0.0;
+  const int cq = CPL * q;  // this lane's output channels cq + [0, CPL)
   f4 acc[FM][FN];
   if (ntl > 0) {
     gload(0);
     sstore();
   }
   __syncthreads();
-  // ADD: the tile's residual words (32 channels of the lane's two pixels),
-  // requested before its MFMAs so the epilogue does not wait on them
-  u32x4 rres[ADD ? FM : 1][ADD ? 4 : 1];
+  u32x4 rres[FM][4];
+  auto res_load = [&](int tm, int fm, int hh) __attribute__((always_inline)) {
+    const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    const int p = wid * 16 * FM + fm * 16 + l16;
+    const int h = hb * TR + p / SEGW, w = wb * SEGW + p % SEGW;
+    const bool inb = (h < g.P) & (w < g.Q);
+    const u32x4* rs =
+        inb ? reinterpret_cast<const u32x4*>(g.res + ((size_t)((unsigned)n * g.P + h) * g.Q + w) * g.ldy + cq + 32 * hh)
+            : reinterpret_cast<const u32x4*>(zp);
+#pragma unroll
+    for (int hq = 0; hq < 4; ++hq) rres[fm][hq] = rs[inb ? hq : 0];
+  };
   for (int tl = 0; tl < ntl; ++tl) {
+    const int tm = walk.tm + tl * walk.step;
     if (tl + 1 < ntl) gload(tl + 1);
-    if constexpr (ADD) {
-      const int tm = walk.tm + tl * walk.step;
-      const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
+    if constexpr (RPF) {
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const int p = wid * 32 + fm * 16 + l16;
-        const int h = hb * TR + p / SEGW, w = wb * SEGW + p % SEGW;
-        const bool inb = (h < g.P) & (w < g.Q);
-        const u32x4* rs = inb ? reinterpret_cast<const u32x4*>(g.res + ((size_t)((unsigned)n * g.P + h) * g.Q + w) *
-                                                                            g.ldy + cq)
-                              : reinterpret_cast<const u32x4*>(zp);
-#pragma unroll
-        for (int hq = 0; hq < 4; ++hq) rres[fm][hq] = rs[inb ? hq : 0];
-      }
+      for (int fm = 0; fm < FM; ++fm) res_load(tm, fm, 0);
     }
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm)
@@ -2181,79 +2194,87 @@ k_conv3x3_c32(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
       for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
     __builtin_amdgcn_iglp_opt(0);
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int r = tap / 3, sx = tap - 3 * r;
-      uint4 wf[FN], xf[FM];
+    for (int qs = 0; qs < NQ; ++qs) {
+      uint4 xf[FM];
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) wf[fn] = *reinterpret_cast<const uint4*>(Wl + tap * KB * 64 + woff[fn]);
+      for (int fm = 0; fm < FM; ++fm) xf[fm] = *reinterpret_cast<const uint4*>(smem + xoff[fm] + xq[qs]);
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-        xf[fm] = *reinterpret_cast<const uint4*>(smem + xoff[fm] + (r * HWX + sx) * XRB);
+      for (int f0 = 0; f0 < FN; f0 += 8) {  // weight fragments 8 at a time (KB = 256: registers)
+        uint4 wf[8];
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
+        for (int fn = 0; fn < 8; ++fn) wf[fn] = *reinterpret_cast<const uint4*>(Wl + woff0 + qs * KB * 64 + (f0 + fn) * 256);
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], wf[fn], xf[fm], uint16_t());
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 8; ++fn) mma(acc[fm][f0 + fn], wf[fn], xf[fm], uint16_t());
+      }
     }
-    // epilogue: lane = pixel l16 of fragment fm, channels cq + 4 fn + j
-    const int tm = walk.tm + tl * walk.step;
+    // epilogue: lane = pixel l16 of fragment fm, channels cq + 4 fn + j, by 32-channel halves
     const int n = tm / tpi, rem = tm - n * tpi, hb = rem / tiles_w, wb = rem - hb * tiles_w;
-    float sv[NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) sv[i] = 0.f;
+    for (int hh = 0; hh < NH; ++hh) {
+      if constexpr (ADD && !RPF) {
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
-      const int p = wid * 32 + fm * 16 + l16;
-      const int h = hb * TR + p / SEGW, w = wb * SEGW + p % SEGW;
-      const bool inb = (h < g.P) & (w < g.Q);
-      const unsigned pix = ((unsigned)n * g.P + h) * g.Q + w;  // < 2^32: launcher checks M * K < 2^32
-      unsigned pk[2 * FN];
+        for (int fm = 0; fm < FM; ++fm) res_load(tm, fm, hh);
+      }
+      float sv[NV];
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int c = cq + 4 * fn;
-        const f4 b4 = *reinterpret_cast<const f4*>(btab + c);
-        float rr[4];
+      for (int i = 0; i < NV; ++i) sv[i] = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) rr[j] = bf2f(f2bf(acc[fm][fn][j] + b4[j]));
-        if constexpr (ADD) {
-          // z = (ReLU)(conv + residual), rounded to bf16 (ops.add's values)
+      for (int fm = 0; fm < FM; ++fm) {
+        const int p = wid * 16 * FM + fm * 16 + l16;
+        const int h = hb * TR + p / SEGW, w = wb * SEGW + p % SEGW;
+        const bool inb = (h < g.P) & (w < g.Q);
+        const unsigned pix = ((unsigned)n * g.P + h) * g.Q + w;  // < 2^32: launcher checks M * K < 2^32
+        unsigned pk[16];
+#pragma unroll
+        for (int f8 = 0; f8 < 8; ++f8) {
+          const int fn = 8 * hh + f8, c = cq + 4 * fn;
+          const f4 b4 = *reinterpret_cast<const f4*>(btab + c);
+          float rr[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rr[j] = bf2f(f2bf(acc[fm][fn][j] + b4[j]));
+          if constexpr (ADD) {
+            // z = (ReLU)(conv + residual), rounded to bf16 (ops.add's values)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const unsigned rw = rres[fm][f8 >> 1][2 * (f8 & 1) + (j >> 1)];
+              float z = rr[j] + __uint_as_float((j & 1) ? (rw & 0xffff0000u) : (rw << 16));
+              if (g.res_relu) z = fmaxf(z, 0.f);
+              rr[j] = bf2f(f2bf(z));
+            }
+          }
+          if constexpr (DROP) {
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+              const uint32_t hs = drop_pair_hash32(g.drop, pix * (unsigned)KB + c + 2 * pr);
+              rr[2 * pr] = (hs & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(rr[2 * pr] * g.drop.scl)) : 0.f;
+              rr[2 * pr + 1] = (hs >> 16) >= g.drop.thr ? bf2f(f2bf(rr[2 * pr + 1] * g.drop.scl)) : 0.f;
+            }
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const unsigned rw = rres[fm][fn >> 1][2 * (fn & 1) + (j >> 1)];
-            float z = rr[j] + __uint_as_float((j & 1) ? (rw & 0xffff0000u) : (rw << 16));
-            if (g.res_relu) z = fmaxf(z, 0.f);
-            rr[j] = bf2f(f2bf(z));
+            const float f = inb ? rr[j] : 0.f;
+            sv[f8 * 4 + j] += f;
+            sv[32 + f8 * 4 + j] += f * f;
           }
+          pk[2 * f8] = (__float_as_uint(rr[0]) >> 16) | (__float_as_uint(rr[1]) & 0xffff0000u);
+          pk[2 * f8 + 1] = (__float_as_uint(rr[2]) >> 16) | (__float_as_uint(rr[3]) & 0xffff0000u);
         }
-        if constexpr (DROP) {
+        u32x4* dst = inb ? reinterpret_cast<u32x4*>(Y + (size_t)pix * g.ldy + cq + 32 * hh) : &g_store_sink16[lane];
 #pragma unroll
-          for (int pr = 0; pr < 2; ++pr) {
-            const uint32_t hh = drop_pair_hash32(g.drop, pix * (unsigned)KB + c + 2 * pr);
-            rr[2 * pr] = (hh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(rr[2 * pr] * g.drop.scl)) : 0.f;
-            rr[2 * pr + 1] = (hh >> 16) >= g.drop.thr ? bf2f(f2bf(rr[2 * pr + 1] * g.drop.scl)) : 0.f;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float f = inb ? rr[j] : 0.f;
-          sv[fn * 4 + j] += f;
-          sv[FN * 4 + fn * 4 + j] += f * f;
-        }
-        pk[2 * fn] = (__float_as_uint(rr[0]) >> 16) | (__float_as_uint(rr[1]) & 0xffff0000u);
-        pk[2 * fn + 1] = (__float_as_uint(rr[2]) >> 16) | (__float_as_uint(rr[3]) & 0xffff0000u);
+        for (int hq = 0; hq < 4; ++hq)
+          dst[inb ? hq : 0] = u32x4{pk[4 * hq], pk[4 * hq + 1], pk[4 * hq + 2], pk[4 * hq + 3]};
       }
-      u32x4* dst = inb ? reinterpret_cast<u32x4*>(Y + (size_t)pix * g.ldy + cq) : &g_store_sink16[lane];
+      if (stats) {
+        // reduce-scatter over the 16 pixel lanes: lane l16 keeps values b0 + k of sv
+        butterfly_step<NV, 8, 0x128>(sv, lane);
+        butterfly_step<NV / 2, 4, 0x141>(sv, lane);
+        butterfly_step<NV / 4, 2, 0x4E>(sv, lane);
+        butterfly_step<NV / 8, 1, 0xB1>(sv, lane);
 #pragma unroll
-      for (int hq = 0; hq < 4; ++hq)
-        dst[inb ? hq : 0] = u32x4{pk[4 * hq], pk[4 * hq + 1], pk[4 * hq + 2], pk[4 * hq + 3]};
-    }
-    if (stats) {
-      // reduce-scatter over the 16 pixel lanes: lane l16 keeps values b0 + k of sv
-      butterfly_step<NV, 8, 0x128>(sv, lane);
-      butterfly_step<NV / 2, 4, 0x141>(sv, lane);
-      butterfly_step<NV / 4, 2, 0x4E>(sv, lane);
-      butterfly_step<NV / 8, 1, 0xB1>(sv, lane);
-#pragma unroll
-      for (int k = 0; k < NV / 16; ++k) dstat[k] += (double)sv[k];
+        for (int k = 0; k < NV / 16; ++k) dstat[hh][k] += (double)sv[k];
+      }
     }
     __syncthreads();  // every wave is done with the halo
     if (tl + 1 < ntl) {
@@ -2266,19 +2287,23 @@ k_conv3x3_c32(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     __syncthreads();
     double* red = reinterpret_cast<double*>(smem);
 #pragma unroll
-    for (int k = 0; k < NV / 16; ++k) red[(wid * 64 + lane) * (NV / 16) + k] = dstat[k];
+    for (int hh = 0; hh < NH; ++hh)
+#pragma unroll
+      for (int k = 0; k < NV / 16; ++k) red[((wid * 64 + lane) * NH + hh) * (NV / 16) + k] = dstat[hh][k];
     __syncthreads();
     if (wid == 0) {
       const int b0 = ((l16 >> 3) & 1) * (NV / 2) + ((l16 >> 2) & 1) * (NV / 4) + ((l16 >> 1) & 1) * (NV / 8) +
                      (l16 & 1) * (NV / 16);
 #pragma unroll
-      for (int k = 0; k < NV / 16; ++k) {
-        double v = 0.0;
+      for (int hh = 0; hh < NH; ++hh)
 #pragma unroll
-        for (int w = 0; w < 8; ++w) v += red[(w * 64 + lane) * (NV / 16) + k];
-        const int idx = b0 + k, st = idx / (FN * 4), rm = idx - st * (FN * 4);
-        stats[((long long)blockIdx.x * 2 + st) * g.Kp + cq + rm] = v;
-      }
+        for (int k = 0; k < NV / 16; ++k) {
+          double v = 0.0;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) v += red[((w * 64 + lane) * NH + hh) * (NV / 16) + k];
+          const int idx = b0 + k, st = idx / 32, rm = idx - st * 32;
+          stats[((long long)blockIdx.x * 2 + st) * g.Kp + cq + 32 * hh + rm] = v;
+        }
     }
     for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
       for (int c = tid; c < 2 * KB; c += NT) stats[((long long)rr * 2 + (c / KB)) * g.Kp + (c % KB)] = 0.0;
@@ -3512,11 +3537,11 @@ general:
         return launch_rc("acfe_conv2d_fwd(c16)");
       }
     }
-    if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W && g.C == 32 &&
-        g.K == 128 && g.Kp == 128 && g.ldy == g.K && g.M * g.K < (1ll << 32) && ((uintptr_t)x & 15) == 0 &&
-        ((uintptr_t)wp & 15) == 0 && ((uintptr_t)y & 15) == 0) {
-      // 32 -> 128 (k_conv3x3_c32): 256-pixel tiles, 64 x 4 (32 x 8 for narrow images)
-      const int segw = g.Q <= 32 ? 32 : 64, tr = 256 / segw;
+    if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W &&
+        ((g.C == 32 && g.K == 128) || (g.C == 16 && g.K == 256 && g.Kdp >= 160)) && g.Kp == g.K && g.ldy == g.K &&
+        g.M * g.K < (1ll << 32) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wp & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+      // 32 -> 128 / 16 -> 256 (k_conv3x3_cw): 256- / 128-pixel tiles, 64 (32 for narrow images) wide
+      const int segw = g.Q <= 32 ? 32 : 64, tr = (g.K == 256 ? 128 : 256) / segw;
       const int tiles_h = (g.P + tr - 1) / tr, tiles_w = (g.Q + segw - 1) / segw;
       const long long nt = (long long)g.N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
@@ -3524,16 +3549,19 @@ general:
         if (gp > nt) gp = (int)nt;
         if (gp >= 64) gp &= ~7;
         if (stats && gp > grid_m) gp = grid_m;  // one statistics slab row per workgroup
-#define C32(SW_, D_)                                                                                        \
-  hipLaunchKernelGGL((k_conv3x3_c32<SW_, D_>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,             \
+#define CWL(CW_, KB_, SW_, D_)                                                                              \
+  hipLaunchKernelGGL((k_conv3x3_cw<CW_, KB_, SW_, D_>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x,    \
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m)
-        if (segw == 64) {
-          if (g.drop.on) C32(64, true); else C32(64, false);
-        } else {
-          if (g.drop.on) C32(32, true); else C32(32, false);
-        }
-#undef C32
-        return launch_rc("acfe_conv2d_fwd(c32)");
+#define CWD(CW_, KB_)                                                                                       \
+  if (segw == 64) {                                                                                         \
+    if (g.drop.on) CWL(CW_, KB_, 64, true); else CWL(CW_, KB_, 64, false);                                  \
+  } else {                                                                                                  \
+    if (g.drop.on) CWL(CW_, KB_, 32, true); else CWL(CW_, KB_, 32, false);                                  \
+  }
+        if (g.C == 32) { CWD(32, 128) } else { CWD(16, 256) }
+#undef CWD
+#undef CWL
+        return launch_rc("acfe_conv2d_fwd(cw)");
       }
     }
     if (g.R == 3 && g.S == 3 && g.st == 1 && g.pt == 1 && g.pl == 1 && g.P == g.H && g.Q == g.W &&
@@ -4220,27 +4248,29 @@ ACFE_API int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, cons
     g.res_relu = relu ? 1 : 0;
     const int ny = g.Kp / 128, gm = grid_m_for(g.M, ny);
     const int tiles_m = (int)((g.M + 127) / 128);
-    if (C == 32 && K == 128 && pad_top == 1 && pad_left == 1 && g.M * K < (1ll << 32) && ((uintptr_t)x & 15) == 0 &&
-        ((uintptr_t)wpacked & 15) == 0) {
-      // k_conv3x3_c32 with the residual epilogue (wr_resnet_bird's stage-2 branch2b)
-      const int segw = W <= 32 ? 32 : 64, tr = 256 / segw;
+    if (((C == 32 && K == 128) || (C == 16 && K == 256 && g.Kdp >= 160)) && pad_top == 1 && pad_left == 1 &&
+        g.M * K < (1ll << 32) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wpacked & 15) == 0) {
+      // k_conv3x3_cw with the residual epilogue (wr_resnet_bird's stage-2 / 3 branch2b)
+      const int segw = W <= 32 ? 32 : 64, tr = (K == 256 ? 128 : 256) / segw;
       const int tiles_h = (H + tr - 1) / tr, tiles_w = (W + segw - 1) / segw;
       const long long nt = (long long)N * tiles_h * tiles_w;
       if (nt < (1ll << 31)) {
         int gp = 256;
         if (gp > nt) gp = (int)nt;
         if (gp >= 64) gp &= ~7;
-        const int srows = grid_m_for(g.M, 1);
+        const int srows = acfe_conv2d_stats_rows(g.M, K);  // (the caller's slab rows)
         if (stats_partial && gp > srows) gp = srows;
-        if (segw == 64)
-          hipLaunchKernelGGL((k_conv3x3_c32<64, false, true>), dim3(gp), dim3(512), 0, strm(stream), g,
-                             (const uint16_t*)x, (const uint16_t*)wpacked, bias, (uint16_t*)y, stats_partial,
-                             tiles_h, tiles_w, (int)nt, srows);
-        else
-          hipLaunchKernelGGL((k_conv3x3_c32<32, false, true>), dim3(gp), dim3(512), 0, strm(stream), g,
-                             (const uint16_t*)x, (const uint16_t*)wpacked, bias, (uint16_t*)y, stats_partial,
-                             tiles_h, tiles_w, (int)nt, srows);
-        return launch_rc("acfe_conv2d_fwd_add(c32)");
+#define CWA(CW_, KB_, SW_)                                                                                  \
+  hipLaunchKernelGGL((k_conv3x3_cw<CW_, KB_, SW_, false, true>), dim3(gp), dim3(512), 0, strm(stream), g,    \
+                     (const uint16_t*)x, (const uint16_t*)wpacked, bias, (uint16_t*)y, stats_partial, tiles_h, \
+                     tiles_w, (int)nt, srows)
+        if (C == 32) {
+          if (segw == 64) CWA(32, 128, 64); else CWA(32, 128, 32);
+        } else {
+          if (segw == 64) CWA(16, 256, 64); else CWA(16, 256, 32);
+        }
+#undef CWA
+        return launch_rc("acfe_conv2d_fwd_add(cw)");
       }
     }
     hipLaunchKernelGGL((k_conv_fwd_g<uint16_t, 128, 128, 2, 2, true>), dim3(gm, ny), dim3(256), 0, strm(stream), g,

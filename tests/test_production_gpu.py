@@ -156,12 +156,13 @@ def test_conv_unpool_backward_production(env, cuda, N, H, W, C, K):
 
 
 @pytest.mark.parametrize("relu,shape", [(False, (32, 64, 128, 64, 64)), (True, (32, 64, 128, 64, 64)),
-                                        (True, (32, 32, 64, 32, 128)), (False, (8, 13, 70, 32, 128))],
-                         ids=["rows", "rows-relu", "c32-relu", "c32-ragged"])
+                                        (True, (32, 32, 64, 32, 128)), (False, (8, 13, 70, 32, 128)),
+                                        (True, (32, 16, 32, 16, 256)), (False, (8, 13, 70, 16, 256))],
+                         ids=["rows", "rows-relu", "c32-relu", "c32-ragged", "c16-256-relu", "c16-256-ragged"])
 def test_conv_fwd_add_production(env, cuda, relu, shape):
     """acfe_conv2d_fwd_add at the stage-1 conv2b shape (64x128, 64 -> 64) for 32
-    clips and at wr_resnet_bird's stage-2 branch2b (32 -> 128 at 32 x 64,
-    k_conv3x3_c32; a ragged image): (ReLU)(conv + bias + shortcut) within one
+    clips and at wr_resnet_bird's stage-2 / 3 branch2b (32 -> 128 at 32 x 64,
+    16 -> 256 at 16 x 32, k_conv3x3_cw; ragged images): (ReLU)(conv + bias + shortcut) within one
     ulp of the exact value of the bf16 sum, BN sums of the stored output."""
     ops, call, lib, ptr, stream = env
     N, H, W, C, K = shape
@@ -392,19 +393,20 @@ def test_head_conv_wgrad_row_halo(env, cuda):
 
 
 @pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (256, 16, 16, 32), (64, 32, 20, 70), (32, 128, 32, 64),
-                                     (32, 128, 13, 70), (32, 128, 16, 32)],
-                         ids=["s2-128to32", "s3-256to16", "ragged", "c32-s2-32to128", "c32-ragged", "c32-narrow"])
+                                     (32, 128, 13, 70), (32, 128, 16, 32), (16, 256, 16, 32), (16, 256, 13, 70)],
+                         ids=["s2-128to32", "s3-256to16", "ragged", "c32-s2-32to128", "c32-ragged", "c32-narrow",
+                              "c16-s3-16to256", "c16-256-ragged"])
 def test_conv_narrow_production(env, cuda, C, K, H, W):
     """k_conv3x3_narrow (resident weights, halo staged once for all nine taps)
     at wr_resnet_bird's stage-2/3 branch21 shapes (128 -> 32 at 32 x 64,
     256 -> 16 at 16 x 32; 32 clips: more tiles than workgroups) and a ragged
-    one (partial row and column tiles), and k_conv3x3_c32 (32 -> 128: the
-    stage-2 branch2b forward and the branch21 dgrad; 64- and 32-pixel-wide
-    tiles, a ragged image): outputs within 1 bf16 ulp of the float64 conv, BN
+    one (partial row and column tiles), and k_conv3x3_cw (32 -> 128 and
+    16 -> 256: the stage-2 / 3 branch2b forwards and branch21 dgrads; 64- and
+    32-pixel-wide tiles, ragged images): outputs within 1 bf16 ulp of the float64 conv, BN
     sums of the stored values to 1e-6, the fused Dropout's mask equal to
     acfe_dropout's, and the dgrad of the matching conv (dY K' = C channels ->
-    dX K channels: K = 32 -> 128 runs on k_conv3x3_c32, 128 -> 32 on the narrow
-    kernel)."""
+    dX K channels: 32 -> 128 / 16 -> 256 run on k_conv3x3_cw, 128 -> 32 and
+    256 -> 16 on the narrow kernel)."""
     ops, call, lib, ptr, stream = env
     N = 32 if H * W <= 2048 else 8
     x, w, b, g = _data(N, H, W, C, K, 211 + K, cuda)
