@@ -3007,8 +3007,15 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   // are WC = CW / 16 channel blocks x WK = 8 / WC slices of K; a wave's nine
   // blocks are the nine taps of its channel block (CW = 64: 2 K halves x 4
   // groups of 9 (tap, block) pairs)
-  static_assert(CW == 64 || (CW == 32 && !UNP) || (CW == 16 && !UNP), "chunk");
-  constexpr int WC = CW == 64 ? 4 : CW / 16, WK = 8 / WC;
+  // CW = 128 (K = 16: wr_resnet_bird's stage-3 branch21, 256 -> 16): the 8
+  // waves are the 8 channel blocks of the chunk, each all 16 K rows x 9 taps.
+  // K < 16 * 8 / WC (wr_resnet's stage-1 conv2a, 16 -> 64): WP pixel groups
+  // of waves take alternate 32-pixel halves and write separate split slabs
+  // (the combine adds them like any other split).
+  static_assert(CW == 64 || (CW == 32 && !UNP) || (CW == 16 && !UNP) || (CW == 128 && KB == 16 && !UNP), "chunk");
+  constexpr int WC = CW == 64 ? 4 : CW / 16;
+  constexpr int WK = 8 / WC < KB / 16 ? 8 / WC : KB / 16, WP = 8 / (WC * WK);
+  static_assert(WC * WK * WP == 8 && (2 * NR) % WP == 0, "wave split");
   constexpr int LDD = KB + 16, LDX = CW + 16;
   constexpr int DS = NR * SEGW * LDD, XS = HR * HW * LDX;
   constexpr int FM = KB / (16 * WK), FN = 9;
@@ -3019,7 +3026,8 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (DS + XS)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wk = wid / WC, wc = wid - (wid / WC) * WC;
+  const int wp = wid / (WC * WK), wkc = wid - wp * (WC * WK);
+  const int wk = wkc / WC, wc = wkc - (wkc / WC) * WC;
   const int xcd = blockIdx.x & 7, bi = blockIdx.x >> 3;
   const int cc = bi % nchunk, split = (bi / nchunk) * 8 + xcd;
   const int sbeg = split * segs_per_split;
@@ -3115,13 +3123,14 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   // 32-pixel half's MFMAs (their issue stalls then overlap MFMA work)
   // (K = 64: no measurable difference, r02as: 0.518-0.522 vs 0.521-0.530 ms)
   constexpr bool WGI = KB >= 128;
+  static_assert(!WGI || WP == 1, "split halves");
   for (int sg = sbeg; sg < send; ++sg) {
     const bool more = sg + 1 < send;
     if (more) gload(sg + 1, WGI ? 1 : 3);
     const uint16_t* Ds = smem + buf * (DS + XS);
     const uint16_t* Xh = Ds + DS;
 #pragma unroll
-    for (int kq = 0; kq < 2 * NR; ++kq) {
+    for (int kq = WP > 1 ? wp : 0; kq < 2 * NR; kq += WP) {
       const int kc = kq & 1, ro = kq >> 1;  // 32-pixel half, output row of the group
       if constexpr (WGI) {
         if (kq == NR) {
@@ -3170,7 +3179,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int k = wk * (KB / WK) + fm * 16 + (lane >> 4) * 4 + jj;
-        ws[((long long)split * g.K + k) * kd + col] = acc[fm][fn][jj];
+        ws[((long long)(split * WP + wp) * g.K + k) * kd + col] = acc[fm][fn][jj];
       }
     }
 }
@@ -3922,14 +3931,21 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   // 16 / 32-channel layers: one chunk of C; K = 256 (wr_resnet's stage-3
   // 256 -> 256): 32-channel chunks, so the K x 9 x CW accumulators stay 36
   // tiles per wave
-  const int cw = g.C % 64 == 0 ? (g.K == 256 ? 32 : 64) : g.C;
+  // tiles per wave; K = 16 (wr_resnet_bird's stage-3 256 -> 16): 128-channel
+  // chunks, one 16-channel block per wave
+  const int cw = g.C % 64 == 0 ? (g.K == 256 ? 32 : (g.K == 16 ? 128 : 64)) : g.C;
   // two output rows per step for the K = 64 (plain or pooled dY) and K = 32
   // layers (r02au-aw: 72 instead of 36 MFMAs per wave per barrier); the K =
   // 128 pooled-gradient variant spills at two rows (138 VGPRs) and keeps one
-  const int nr = (cw == 64 && g.P % 2 == 0 && (g.K == 64 || (g.K == 32 && !amax))) ? 2 : 1;
+  // C = 16 -> K = 64 (wr_resnet's stage-1 conv2a): two pixel groups of 4
+  // waves, each its own split slab (the caller guarantees splits >= 16)
+  const bool c16k64 = cw == 16 && g.K == 64;
+  const int nr = ((cw == 64 || c16k64) && g.P % 2 == 0 && (g.K == 64 || (g.K == 32 && !amax))) ? 2 : 1;
+  const int wp = c16k64 ? 2 : 1;
   const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * ((g.Q + 63) / 64));
-  int sp = 256 / nchunk;
-  if (sp > splits) sp = (int)splits;
+  // c16k64: 75 KB of LDS and 114 VGPRs -> two workgroups per CU
+  int sp = (c16k64 ? 512 : 256) / nchunk;
+  if (sp > splits / wp) sp = (int)(splits / wp);
   sp &= ~7;
   if (sp < 8) sp = 8;
   if (sp > splits) sp = (int)splits;  // splits is a multiple of 8 (wgrad_plan)
@@ -3941,7 +3957,14 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
 #define WHC(KB_, CW_)                                                                                              \
   hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_>), gr, dim3(512), 0, s, g, (const uint16_t*)x,               \
                      (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
-  if (cw == 32) {  // the stage-2/3 branch2b (32 -> 128 / 256)
+  if (cw == 128) {  // wr_resnet_bird stage 3 (256 -> 16)
+    WHC(16, 128);
+  } else if (c16k64) {
+    if (nr == 2)
+      hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 16, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
+                         (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);
+    else WHC(64, 16);
+  } else if (cw == 32) {  // the stage-2/3 branch2b (32 -> 128 / 256)
     if (g.K == 128) WHC(128, 32); else WHC(256, 32);
   } else if (cw == 16) {  // stage 3 (16 -> 256)
     WHC(256, 16);
@@ -3964,7 +3987,7 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   }
 #undef WHC
 #undef WH
-  *used = sp;
+  *used = sp * wp;
   return launch_rc(amax ? "acfe_conv2d_wgrad_unpool" : "acfe_conv2d_wgrad(halo)");
 }
 
@@ -4003,8 +4026,8 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   g.ldy = K;
   int rc;
   if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 &&
-      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) ||
-       ((C == 32 && (K == 128 || K == 256)) || (C == 16 && K == 256))) &&
+      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) || (C % 128 == 0 && K == 16) ||
+       ((C == 32 && (K == 128 || K == 256)) || (C == 16 && (K == 256 || (K == 64 && splits >= 16))))) &&
       (long long)N * P * ((Q + 63) / 64) < (1ll << 31)) {
     // halo-staged kernel; its split count stays within the planned workspace
     int used = 0;

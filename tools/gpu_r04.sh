@@ -46,6 +46,7 @@ for w in "$@"; do
     e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;
     sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
+    ptk) step ptk 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$PTK" ;;
     convtests) step convtests 600 python -u -m pytest tests/test_production_gpu.py tests/test_fused_gpu.py \
                  tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     fusetests) step fusetests 600 python -u -m pytest tests/test_production_gpu.py -m gpu -k "reduce_fus" -x -v \
