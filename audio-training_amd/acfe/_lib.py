@@ -61,6 +61,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_stem_fwd": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, I32, P, P],
     "acfe_stem_dgrad": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P],
     "acfe_stem_wgrad": [P, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, P, P],
+    "acfe_stem_bwd_bn": [P, P, P, I32, I32, I32, I32, I32, I32, I32, P, P, P, P, I32, P, I32, P, F32, P, P, P],
     "acfe_reduce_blocks": [I64],
     "acfe_bn_stats": [P, I64, I32, I32, P, P],
     "acfe_bn_finalize": [P, I32, I32, I32, F64, P, P, F32, F32, P, P, I32, P, P, P, P, P],

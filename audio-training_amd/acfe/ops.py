@@ -37,6 +37,9 @@ PRO_1W = os.environ.get("ACFE_BN_PROLOGUE_1W", "1") != "0"
 # ACFE_BN_REDUCE_FUSE=0: the BatchNormalization backward reduce runs as its own
 # pass even where the kernel producing its gradient can form the sums (A/B)
 FUSE_BN_REDUCE = FUSE and os.environ.get("ACFE_BN_REDUCE_FUSE", "1") != "0"
+# ACFE_STEM_BN_FUSE=0: wr_resnet_bird's stem backward as separate BN apply,
+# dgrad, wgrad and bias-sum passes instead of acfe_stem_bwd_bn (A/B)
+STEM_BN_FUSE = os.environ.get("ACFE_STEM_BN_FUSE", "1") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -418,6 +421,94 @@ class _StemFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+class _StemBNPoolFn(torch.autograd.Function):
+    """conv1_1 -> BatchNormalization -> MaxPool2D((kh, kw)) of wr_resnet_bird
+    (wr_resnet_bird.py:22-30) as one node.  Forward: the _StemFn and _BNPoolFn
+    kernels.  Backward: the pool backward forms the BN reduce slab
+    (acfe_maxpool2d_bwd_argmax_bn) and acfe_stem_bwd_bn applies the BN backward
+    while staging the stem's dgrad / wgrad / bias sums, so the BN input
+    gradient is never stored (k_bn_bwd_apply8's 3 x 1.07 GB per T1 step)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, mmean, mvar, conf):
+        pt, pl, out_dtype, kh, kw, relu, eps, momentum, want_stats = conf
+        N, H, W = x.shape
+        K, R, S, rep = w.shape
+        dev = x.device
+        s = stream()
+        weff = _empty((R, S, K), F32, dev)
+        call("acfe_stem_fold_weights", ptr(w), K, R, S, rep, ptr(weff), s)
+        y = _empty((N, H, W, K), out_dtype, dev)
+        st = _empty((lib.acfe_stem_blocks(N, H, W), 2, K), F64, dev)
+        call("acfe_stem_fwd", ptr(x), dtype_code(x.dtype), N, H, W, R, S, pt, pl, ptr(weff), ptr(b), ptr(y),
+             dtype_code(out_dtype), ptr(st), s)
+        _, saved = _bn_fwd(y, gamma, beta, st, mmean, mvar, True, relu, eps, momentum, None)
+        P, Q = H // kh, W // kw
+        yp = _empty((N, P, Q, K), y.dtype, dev)
+        amax = _empty((N, P, Q, K), torch.uint8, dev)
+        pst = _no_stats(dev)
+        if want_stats:
+            pst = _empty((lib.acfe_reduce_blocks(N * P * Q), 2, K), F64, dev)
+        call("acfe_bn_maxpool2d_fused", ptr(y), N, H, W, K, ptr(saved[0]), ptr(saved[1]), int(relu), kh, kw, ptr(yp),
+             ptr(amax), ptr(pst) if want_stats else None, dtype_code(y.dtype), s)
+        ctx.save_for_backward(x, w, weff, y, amax, *saved)
+        ctx.conf, ctx.gb = conf, (gamma, beta)
+        ctx.mark_non_differentiable(pst)
+        return yp, pst
+
+    @staticmethod
+    def backward(ctx, g, _gs):
+        x, w, weff, y, amax, *saved = ctx.saved_tensors
+        pt, pl, out_dtype, kh, kw, relu, eps, momentum, want_stats = ctx.conf
+        N, H, W, K = y.shape
+        _, R, S, rep = w.shape
+        dev = y.device
+        s = stream()
+        scale, shift, mean, invstd = saved
+        g = g.contiguous()
+        gu = _empty(y.shape, g.dtype, dev)
+        rows = N * H * W
+        nrows = lib.acfe_reduce_blocks(rows)
+        part = _empty((nrows * 2 * K,), F64, dev)
+        call("acfe_maxpool2d_bwd_argmax_bn", ptr(amax), ptr(g), N, H, W, K, kh, kw, ptr(gu), dtype_code(g.dtype),
+             ptr(y), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
+        coef, dgamma, dbeta = _bn_bwd_coef(part, nrows, K, rows, saved, True, ctx.gb, dev)
+        nb = lib.acfe_stem_blocks(N, H, W)
+        dx = _empty(x.shape, x.dtype, dev)
+        dw = _empty(w.shape, F32, dev)
+        ws = _empty((nb * K * R * S,), F64, dev)
+        bp = _empty((nb, 2, K), F64, dev)
+        call("acfe_stem_bwd_bn", ptr(gu), ptr(y), ptr(x), N, H, W, R, S, pt, pl, ptr(weff), ptr(scale), ptr(shift),
+             ptr(coef), int(relu), ptr(dx), rep, ptr(dw), 0.0, ptr(bp), ptr(ws), s)
+        db = None
+        if ctx.needs_input_grad[2]:
+            db = _empty((K,), F32, dev)
+            call("acfe_channel_sum_finalize", ptr(bp), nb, K, 0.0, ptr(db), s)
+        return (dx if ctx.needs_input_grad[0] else None), dw, db, dgamma, dbeta, None, None, None
+
+
+def stem_bn_pool_ok(x, w, b, out_dtype, kh, kw) -> bool:
+    """_StemBNPoolFn's shapes: training with autograd on, bf16 in and out, a
+    bias, the 16-channel 5 x 5 / 3 x 3 stem and a fused pool shape."""
+    K, R, S, _ = w.shape
+    return (FUSE and FUSE_BN_REDUCE and STEM_BN_FUSE and torch.is_grad_enabled() and b is not None
+            and x.dtype == torch.bfloat16 and out_dtype == torch.bfloat16 and x.dim() == 3 and x.is_contiguous()
+            and K == 16 and R == S and R in (3, 5) and (kh, kw) in ((1, 2), (2, 2), (3, 3)))
+
+
+def stem_bn_max_pool(x, w, b, out_dtype, gamma, beta, mmean, mvar, kh, kw, relu=False, eps=1e-3, momentum=0.99,
+                     want_stats=False):
+    """MaxPool2D((kh, kw))(BatchNormalization(stem_conv(x, w, b))) in training
+    (stem_bn_pool_ok) -> (y, stats slab of y or None)."""
+    N, H, W = x.shape
+    _, R, S, _ = w.shape
+    _, pt = same_padding(H, R, 1)
+    _, pl = same_padding(W, S, 1)
+    conf = (pt, pl, out_dtype, kh, kw, bool(relu), float(eps), float(momentum), bool(want_stats))
+    y, st = _StemBNPoolFn.apply(x, w, b, gamma, beta, mmean, mvar, conf)
+    return y, (st if want_stats else None)
+
+
 def stem_conv(x, w, b, out_dtype, want_stats=False):
     """'same' stride-1 conv of a one-channel map x [N,H,W] whose Cin copies are folded."""
     N, H, W = x.shape
@@ -550,6 +641,29 @@ def _conv_fwd_bn(xb, w, b, want_stats, drop):
     return y, stats
 
 
+def _bn_bwd_coef(part, prow, C, rows, saved, training, params, dev):
+    """acfe_bn_bwd_finalize_ex over a reduce slab of prow rows -> (coef [3][C],
+    dgamma, dbeta); arena parameters (gamma, beta): the finalizer accumulates
+    into their gradient views and autograd gets None for them."""
+    scale, shift, mean, invstd = saved
+    tg = tb = None
+    if params is not None:
+        tg, tb = direct_grad(params[0]), direct_grad(params[1])
+        if tg is None or tb is None:
+            tg = tb = None
+    dgamma = tg if tg is not None else _empty((C,), F32, dev)
+    dbeta = tb if tb is not None else _empty((C,), F32, dev)
+    coef = _empty((3 * C,), F32, dev)
+    # eval mode: statistics are constants -> count -> inf removes the mean terms
+    count = float(rows) if training else 1e300
+    call("acfe_bn_bwd_finalize_ex", ptr(part), prow, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
+         ptr(dbeta), ptr(coef), int(tg is not None), stream())
+    if tg is not None:
+        dgamma = dbeta = None
+        grads_ready(*params)
+    return coef, dgamma, dbeta
+
+
 def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None, params=None, part=None):
     """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given;
     mask_in: x is a ReLU output (ops.add), its backward [x > 0] is applied to dx here
@@ -574,23 +688,7 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
         part = _empty((nrows * 2 * C,), F64, dev)
         call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
              ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
-    # arena parameters (gamma, beta): the finalizer accumulates into their
-    # gradient views and autograd gets None
-    tg = tb = None
-    if params is not None:
-        tg, tb = direct_grad(params[0]), direct_grad(params[1])
-        if tg is None or tb is None:
-            tg = tb = None
-    dgamma = tg if tg is not None else _empty((C,), F32, dev)
-    dbeta = tb if tb is not None else _empty((C,), F32, dev)
-    coef = _empty((3 * C,), F32, dev)
-    # eval mode: statistics are constants -> count -> inf removes the mean terms
-    count = float(rows) if training else 1e300
-    call("acfe_bn_bwd_finalize_ex", ptr(part), prow, C, count, ptr(scale), ptr(mean), ptr(invstd), ptr(dgamma),
-         ptr(dbeta), ptr(coef), int(tg is not None), s)
-    if tg is not None:
-        dgamma = dbeta = None
-        grads_ready(*params)
+    coef, dgamma, dbeta = _bn_bwd_coef(part, prow, C, rows, saved, training, params, dev)
     dx = _empty(x.shape, x.dtype, dev)
     rate, seed = drop if drop is not None and drop[0] > 0.0 else (0.0, 0)
     if add is not None:

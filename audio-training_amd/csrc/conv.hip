@@ -4885,6 +4885,171 @@ k_stem_wgrad_mfma(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
 }
 
 
+// ------------------------------------------------------------------ stem backward with the BN backward apply
+// wr_resnet_bird's stem conv1_1 (5 x 5, 16 filters, bias) -> BatchNormalization
+// -> MaxPool2D((1, 2)) (resnet/wr_resnet_bird.py:22-30).  The BN backward's
+// elementwise pass dX_bn = a*g*[x*scale+shift > 0] + b*x + c (k_bn_bwd_apply8:
+// reads g and x, writes dX_bn, 3 x 1.07 GB per T1 step) is formed while the
+// stem dgrad stages its dY halo; the weight gradient and the conv-bias sums
+// read the same LDS image, so dX_bn is never stored and the separate wgrad's
+// re-read of it is gone.  dX and dW bit-identical to the apply8 ->
+// k_stem_dgrad_mfma / k_stem_wgrad_mfma chain (the same bf16 dX_bn, tile order
+// and MFMA operands); bias sums [block][2][16] of the bf16 dX_bn values over
+// each tile's own pixels.
+template <int R, int S>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+k_stem_bwd_bn(const uint16_t* __restrict__ g, const uint16_t* __restrict__ xb, const uint16_t* __restrict__ xin,
+              int N, int H, int W, int pt, int pl, const float* __restrict__ weff, const float* __restrict__ scale,
+              const float* __restrict__ shift, const float* __restrict__ coef, int relu, uint16_t* __restrict__ dxin,
+              double* __restrict__ wpart, double* __restrict__ bpart, int tiles_h, int tiles_w) {
+  constexpr int XH = STEM_TH + R - 1, XW = STEM_TW + S - 1, NT = R * S, NKT = (NT + 1) / 2;
+  constexpr int GSZ = XH * XW * STEM_K;
+  static_assert(GSZ * 2 >= 4 * STEM_K * 32 * 4, "the wgrad reduction aliases the dY image");
+  __shared__ __attribute__((aligned(16))) uint16_t gs[GSZ];
+  __shared__ uint16_t xs[XH * XW];
+  __shared__ double bred[4][STEM_K];
+  __shared__ __attribute__((aligned(16))) float bnc[5][STEM_K];  // scale, shift, coef a, b, c
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4, wid = tid >> 6;
+  if (tid < 5 * STEM_K) {
+    const int a = tid / STEM_K, k = tid - a * STEM_K;
+    bnc[a][k] = a == 0 ? scale[k] : (a == 1 ? shift[k] : coef[(a - 2) * STEM_K + k]);
+  }
+  // dgrad A operand (k_stem_dgrad_mfma): flipped folded weights, k-slot q*8 + j <-> (tap 2kt + (q >> 1), ch (q & 1)*8 + j)
+  uint4 wa[NKT];
+  int goff[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int t = 2 * kt + (q >> 1), r = t / S, s = t % S;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t < NT ? weff[t * STEM_K + (q & 1) * 8 + j] : 0.f;
+    wa[kt] = uint4{stem_pack2(v[0], v[1]), stem_pack2(v[2], v[3]), stem_pack2(v[4], v[5]), stem_pack2(v[6], v[7])};
+    goff[kt] = t < NT ? ((R - 1 - r) * XW + (S - 1 - s)) * STEM_K + (q & 1) * 8 : -1;
+  }
+  // wgrad B operand (k_stem_wgrad_mfma): tap of column l16 / 16 + l16
+  const int grp = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  int tof0, tof1;
+  {
+    const int t0 = l16, t1 = 16 + l16;
+    tof0 = t0 < NT ? (t0 / S) * XW + (t0 % S) : -1;
+    tof1 = t1 < NT ? (t1 / S) * XW + (t1 % S) : -1;
+  }
+  // this thread's 8 staging channels: its index parity
+  const int c8 = (tid & 1) * 8;
+  double s1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = 0.0;
+  f4 d0 = f4{0.f, 0.f, 0.f, 0.f}, d1 = d0;
+  const uint4 z4 = {0u, 0u, 0u, 0u};
+  const long long ntiles = (long long)N * tiles_h * tiles_w;
+  for (long long tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    const int tw = (int)(tt % tiles_w), th = (int)((tt / tiles_w) % tiles_h);
+    const int n = (int)(tt / ((long long)tiles_w * tiles_h));
+    const int h0 = th * STEM_TH, w0 = tw * STEM_TW;
+    const int gh0 = h0 - (R - 1 - pt), gw0 = w0 - (S - 1 - pl);
+    __syncthreads();
+    for (int i = tid; i < XH * XW * 2; i += 256) {
+      const int pos = i >> 1;
+      const int yy = pos / XW, xx = pos - yy * XW;
+      const int h = gh0 + yy, w = gw0 + xx;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+        const long long e = (((long long)n * H + h) * W + w) * STEM_K + c8;
+        const u32x4 gv = *reinterpret_cast<const u32x4*>(g + e);
+        const u32x4 xv = *reinterpret_cast<const u32x4*>(xb + e);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const unsigned gw = gv[j >> 1], xw = xv[j >> 1];
+          const float gf = __uint_as_float((j & 1) ? (gw & 0xffff0000u) : (gw << 16));
+          const float xf = __uint_as_float((j & 1) ? (xw & 0xffff0000u) : (xw << 16));
+          const float gj = (relu && !(xf * bnc[0][c8 + j] + bnc[1][c8 + j] > 0.f)) ? 0.f : gf;
+          o[j] = __builtin_fmaf(bnc[2][c8 + j], gj, __builtin_fmaf(bnc[3][c8 + j], xf, bnc[4][c8 + j]));  // as k_bn_bwd_apply8
+        }
+        v = u32x4{stem_pack2(o[0], o[1]), stem_pack2(o[2], o[3]), stem_pack2(o[4], o[5]), stem_pack2(o[6], o[7])};
+        if ((unsigned)(yy - (R - 1 - pt)) < (unsigned)STEM_TH && (unsigned)(xx - (S - 1 - pl)) < (unsigned)STEM_TW) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const unsigned vw = v[j >> 1];
+            s1[j] += (double)__uint_as_float((j & 1) ? (vw & 0xffff0000u) : (vw << 16));
+          }
+        }
+      }
+      *reinterpret_cast<u32x4*>(gs + (long long)i * 8) = v;
+    }
+    for (int i = tid; i < XH * XW; i += 256) {
+      const int yy = i / XW, xx = i - yy * XW;
+      const int h = h0 - pt + yy, w = w0 - pl + xx;
+      xs[i] = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? xin[((long long)n * H + h) * W + w] : 0;
+    }
+    __syncthreads();
+    // dX of the stem input (k_stem_dgrad_mfma)
+#pragma unroll 2
+    for (int blk = 0; blk < 16; ++blk) {
+      const int ry = wid * 4 + (blk >> 2), cx = (blk & 3) * 16 + l16;
+      const uint16_t* base = gs + (ry * XW + cx) * STEM_K;
+      f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const uint4 b = goff[kt] >= 0 ? *reinterpret_cast<const uint4*>(base + goff[kt]) : z4;
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, wa[kt]), __builtin_bit_cast(bf8, b), acc,
+                                                      0, 0, 0);
+      }
+      const int h = h0 + ry, w = w0 + cx;
+      if (q == 0 && h < H && w < W) dxin[((long long)n * H + h) * W + w] = f2bf(acc[0]);
+    }
+    // dW (k_stem_wgrad_mfma): dY^T chunks read from the tile's own pixels of the image
+    for (int c = 0; c < 8; ++c) {
+      const int ry = wid * 4 + (c >> 1), cx0 = (c & 1) * 32;
+      const uint16_t* gw = gs + ((ry + R - 1 - pt) * XW + cx0 + S - 1 - pl) * STEM_K;
+      const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (stem_lp)(reinterpret_cast<const __bf16*>(gw + (4 * grp + qq) * STEM_K + 4 * pp)));
+      const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (stem_lp)(reinterpret_cast<const __bf16*>(gw + (16 + 4 * grp + qq) * STEM_K + 4 * pp)));
+      const bf8 a = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const uint16_t* src = xs + ry * XW + cx0;
+      unsigned b0[8], b1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int px = j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4);
+        b0[j] = tof0 >= 0 ? src[px + tof0] : 0u;
+        b1[j] = tof1 >= 0 ? src[px + tof1] : 0u;
+      }
+      const uint4 B0 = uint4{b0[0] | (b0[1] << 16), b0[2] | (b0[3] << 16), b0[4] | (b0[5] << 16), b0[6] | (b0[7] << 16)};
+      const uint4 B1 = uint4{b1[0] | (b1[1] << 16), b1[2] | (b1[3] << 16), b1[4] | (b1[5] << 16), b1[6] | (b1[7] << 16)};
+      d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf8, B0), d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf8, B1), d1, 0, 0, 0);
+    }
+  }
+  // bias sums: lanes of one parity hold the same 8 channels
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) s1[j] += __shfl_xor(s1[j], o, 64);
+  }
+  __syncthreads();  // last tile's image reads done: the wgrad reduction reuses it
+  float(*red)[STEM_K][32] = reinterpret_cast<float(*)[STEM_K][32]>(gs);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[wid][q * 4 + r][l16] = d0[r];
+    red[wid][q * 4 + r][16 + l16] = d1[r];
+  }
+  if (lane < 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bred[wid][lane * 8 + j] = s1[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < STEM_K * NT; i += 256) {
+    const int k = i / NT, t = i - k * NT;
+    wpart[(long long)blockIdx.x * STEM_K * NT + i] =
+        ((double)red[0][k][t] + (double)red[1][k][t]) + ((double)red[2][k][t] + (double)red[3][k][t]);
+  }
+  // row 1 of the [2][16] slab (sums of squares in the statistics layout) is not used by the channel sums
+  if (tid < 2 * STEM_K)
+    bpart[(long long)blockIdx.x * 2 * STEM_K + tid] =
+        tid < STEM_K ? (bred[0][tid] + bred[1][tid]) + (bred[2][tid] + bred[3][tid]) : 0.0;
+}
+
 ACFE_API int acfe_stem_blocks(int N, int H, int W) {
   const long long t = (long long)N * ((H + STEM_TH - 1) / STEM_TH) * ((W + STEM_TW - 1) / STEM_TW);
   return (int)(t < STEM_CAP ? t : STEM_CAP);
@@ -4978,4 +5143,35 @@ ACFE_API int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_
   if (rep > 256) return ACFE_E_INVAL;
   hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3(n), dim3(256), 0, strm(stream), workspace, grid, n, rep, beta, dw);
   return launch_rc("acfe_stem_wgrad(reduce)");
+}
+
+// The stem backward with the BN backward apply folded in (k_stem_bwd_bn): g =
+// the BN output gradient (bf16 [N][H][W][16], e.g. acfe_maxpool2d_bwd_argmax_bn's
+// dX), xb = the BN input (= the stem output), coef = acfe_bn_bwd_finalize_ex's
+// [3][16] coefficients.  dxin: the stem input gradient (bf16 [N][H][W]); dw: [16][R][S][rep] fp32 (beta as acfe_stem_wgrad); bias_part:
+// double[acfe_stem_blocks(N,H,W)][2][16] channel sums of dX_bn (for
+// acfe_channel_sum_finalize); workspace: double[acfe_stem_blocks(N,H,W) * 16 * R * S].
+ACFE_API int acfe_stem_bwd_bn(const void* g, const void* xb, const void* xin, int N, int H, int W, int R, int S,
+                              int pad_top, int pad_left, const float* weff, const float* scale, const float* shift,
+                              const float* coef, int relu, void* dxin, int rep, float* dw, float beta,
+                              double* bias_part, double* workspace, void* stream) {
+  if (!g || !xb || !xin || !weff || !scale || !shift || !coef || !dw || !bias_part || !workspace || N <= 0 ||
+      H <= 0 || W <= 0 || R != S || (R != 5 && R != 3) || rep <= 0 || rep > 256 || ((uintptr_t)g & 15) ||
+      ((uintptr_t)xb & 15))
+    return ACFE_E_INVAL;
+  const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
+  const int grid = acfe_stem_blocks(N, H, W);
+  uint16_t* dxo = (uint16_t*)dxin;
+  if (!dxo) return ACFE_E_INVAL;
+#define SB(RR)                                                                                                \
+  hipLaunchKernelGGL((k_stem_bwd_bn<RR, RR>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)g,        \
+                     (const uint16_t*)xb, (const uint16_t*)xin, N, H, W, pad_top, pad_left, weff, scale, shift, coef, \
+                     relu, dxo, workspace, bias_part, th, tw)
+  if (R == 5) SB(5); else SB(3);
+#undef SB
+  int rc = launch_rc("acfe_stem_bwd_bn");
+  if (rc) return rc;
+  const int n = STEM_K * R * S;
+  hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3(n), dim3(256), 0, strm(stream), workspace, grid, n, rep, beta, dw);
+  return launch_rc("acfe_stem_bwd_bn(reduce)");
 }

@@ -539,7 +539,7 @@ __global__ void k_bn_bwd_apply(const TG* __restrict__ dy, const TX* __restrict__
     const float xv = ld(x, i);
     float g = ld(dy, i);
     if ((relu & 1) && !(xv * scale[c] + shift[c] > 0.f)) g = 0.f;
-    float v = coef[c] * g + coef[C + c] * xv + coef[2 * C + c];
+    float v = __builtin_fmaf(coef[c], g, __builtin_fmaf(coef[C + c], xv, coef[2 * C + c]));
     if (add) v += ld(add, i);
     if ((relu & 2) && !(xv > 0.f)) v = 0.f;  // x = ReLU output upstream: its backward
     if (drop.on) v = drop_apply<TO>(drop, (uint64_t)i, rnd(v, TO()));
@@ -601,7 +601,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + j;
       const float gj = ((relu & 1) && !(xv[j] * sm[c] + sm[C + c] > 0.f)) ? 0.f : g[j];
-      const float r = sm[2 * C + c] * gj + sm[3 * C + c] * xv[j] + sm[4 * C + c];
+      const float r = __builtin_fmaf(sm[2 * C + c], gj, __builtin_fmaf(sm[3 * C + c], xv[j], sm[4 * C + c]));
       o[j] = has_add ? o[j] + r : r;
       if ((relu & 2) && !(xv[j] > 0.f)) o[j] = 0.f;  // x = ReLU output upstream: its backward
     }

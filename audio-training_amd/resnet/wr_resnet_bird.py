@@ -134,10 +134,17 @@ class WRResNet(nn.Module):
         (wr_resnet_bird.py:69-70), before the two logmeanexp poolings."""
         if x.dim() == 4:
             x = x[..., 0]
-        y, st = self.conv1_1(x, want_stats=True)
-        bn = self.bn_stem  # BN -> MaxPool2D((1, 2)) as one node: the normalised stem output is never stored
-        y, st = ops.bn_max_pool(y, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance, self.training, 1, 2,
-                                stats=st, eps=bn.eps, momentum=bn.momentum, want_stats=self.training)
+        bn, c1 = self.bn_stem, self.conv1_1
+        if self.training and ops.stem_bn_pool_ok(x, c1.weight, c1.bias, c1.out_dtype, 1, 2):
+            # conv1_1 -> BN -> MaxPool2D((1, 2)) as one node: its backward applies
+            # the BN backward inside the stem's dgrad / wgrad staging
+            y, st = ops.stem_bn_max_pool(x, c1.weight, c1.bias, c1.out_dtype, bn.gamma, bn.beta, bn.moving_mean,
+                                         bn.moving_variance, 1, 2, eps=bn.eps, momentum=bn.momentum, want_stats=True)
+        else:
+            y, st = c1(x, want_stats=True)
+            # BN -> MaxPool2D((1, 2)) as one node: the normalised stem output is never stored
+            y, st = ops.bn_max_pool(y, bn.gamma, bn.beta, bn.moving_mean, bn.moving_variance, self.training, 1, 2,
+                                    stats=st, eps=bn.eps, momentum=bn.momentum, want_stats=self.training)
         for blk in self.blocks:
             y, st = blk(y, st)
         y = self.final_bn(y, relu=True, stats=st)

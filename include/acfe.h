@@ -256,6 +256,20 @@ int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, int R, in
 int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, int N, int H, int W, int R,
                     int S, int pad_top, int pad_left, int rep, float* dw, float beta, double* workspace,
                     void* stream);
+/* The stem backward with its BatchNormalization's backward apply folded in
+ * (wr_resnet_bird.py:22-30: conv1_1 -> BN -> MaxPool2D((1, 2))): g = the BN
+ * output gradient, xb = the BN input (the stem output), both bf16
+ * [N][H][W][16] and 16-B aligned; coef = acfe_bn_bwd_finalize_ex's [3][16]
+ * coefficients.  Writes dxin (bf16 [N][H][W]), dw (as acfe_stem_wgrad) and
+ * bias_part double[acfe_stem_blocks(N,H,W)][2][16] (the conv-bias sums for
+ * acfe_channel_sum_finalize) without storing dX_bn.  Replaces
+ * acfe_bn_bwd_apply_ex + acfe_stem_dgrad + acfe_stem_wgrad + acfe_channel_sum
+ * on that chain (the reference's autodiff of tf.keras Conv2D + BatchNormalization,
+ * wr_resnet_bird.py:22-30). */
+int acfe_stem_bwd_bn(const void* g, const void* xb, const void* xin, int N, int H, int W, int R, int S,
+                     int pad_top, int pad_left, const float* weff, const float* scale, const float* shift,
+                     const float* coef, int relu, void* dxin, int rep, float* dw, float beta,
+                     double* bias_part, double* workspace, void* stream);
 
 /* BatchNormalization(axis=3) (Keras: eps 1e-3, momentum 0.99, biased variance).
  * Partial slabs are double[acfe_reduce_blocks(rows)][2][C]. */

@@ -440,6 +440,100 @@ def test_conv_narrow_production(env, cuda, C, K, H, W):
     _within_ulp(dx, F.conv_transpose2d(gd, wd, padding=1).permute(0, 2, 3, 1), what="narrow dgrad")
 
 
+@pytest.mark.parametrize("N,H,W,R,relu", [(3, 40, 130, 5, 0), (2, 37, 71, 3, 1), (2, 128, 513, 5, 0),
+                                          (2, 33, 65, 5, 1)],
+                         ids=["odd-5x5", "odd-3x3-relu", "t1-shape", "edge-5x5-relu"])
+def test_stem_bwd_bn_fused(env, cuda, N, H, W, R, relu):
+    """acfe_stem_bwd_bn (wr_resnet_bird.py:22-30: the stem conv's backward with
+    its BN's backward apply folded into the dY staging) against the unfused
+    chain acfe_bn_bwd_apply_ex -> acfe_stem_dgrad + acfe_stem_wgrad +
+    acfe_channel_sum: dX and dW bit-identical (same bf16 dX_bn, tile order and
+    MFMA operands), the bias sums within 1e-6 of the sum of |dX_bn| (both add
+    the same bf16 values in float64, in different orders)."""
+    ops, call, lib, ptr, stream = env
+    K, rep = 16, 3
+    S = R
+    pt = pl = (R - 1) // 2
+    g = torch.Generator().manual_seed(29 + H + R)
+    gy = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+    xb = (torch.randn((N, H, W, K), generator=g) * 2).to(BF).to(cuda)
+    xin = torch.randn((N, H, W), generator=g).to(BF).to(cuda)
+    w = (torch.randn((K, R, S, rep), generator=g) * 0.2).to(cuda)
+    sc = ((torch.rand(K, generator=g) + 0.5) * torch.where(torch.rand(K, generator=g) < 0.2, -1.0, 1.0)).to(cuda)
+    sh = (torch.randn(K, generator=g) * 0.3).to(cuda)
+    coef = (torch.randn(3 * K, generator=g) * 0.5).to(cuda)
+    weff = torch.empty((R, S, K), device=cuda)
+    call("acfe_stem_fold_weights", ptr(w), K, R, S, rep, ptr(weff), stream())
+    rows = N * H * W
+    nb = lib.acfe_stem_blocks(N, H, W)
+    # unfused chain
+    dxb = torch.empty((N, H, W, K), dtype=BF, device=cuda)
+    call("acfe_bn_bwd_apply_ex", ptr(gy), 1, ptr(xb), 1, rows, K, ptr(sc), ptr(sh), relu, ptr(coef), None, 0.0, 0,
+         ptr(dxb), 1, None, stream())
+    dx0 = torch.empty((N, H, W), dtype=BF, device=cuda)
+    call("acfe_stem_dgrad", ptr(dxb), 1, N, H, W, R, S, pt, pl, ptr(weff), ptr(dx0), 1, stream())
+    dw0 = torch.empty((K, R, S, rep), device=cuda)
+    ws0 = torch.empty((nb * K * R * S,), dtype=F64, device=cuda)
+    call("acfe_stem_wgrad", ptr(xin), 1, ptr(dxb), 1, N, H, W, R, S, pt, pl, rep, ptr(dw0), 0.0, ptr(ws0), stream())
+    db0 = torch.empty((K,), device=cuda)
+    cpart = torch.empty((lib.acfe_reduce_blocks(rows) * 2 * K,), dtype=F64, device=cuda)
+    call("acfe_channel_sum", ptr(dxb), rows, K, 1, ptr(cpart), ptr(db0), 0.0, stream())
+    # fused
+    dx1 = torch.full((N, H, W), float("nan"), dtype=BF, device=cuda)
+    dw1 = torch.full((K, R, S, rep), float("nan"), device=cuda)
+    ws1 = torch.empty((nb * K * R * S,), dtype=F64, device=cuda)
+    bp = torch.full((nb, 2, K), float("nan"), dtype=F64, device=cuda)
+    call("acfe_stem_bwd_bn", ptr(gy), ptr(xb), ptr(xin), N, H, W, R, S, pt, pl, ptr(weff), ptr(sc), ptr(sh),
+         ptr(coef), relu, ptr(dx1), rep, ptr(dw1), 0.0, ptr(bp), ptr(ws1), stream())
+    db1 = torch.empty((K,), device=cuda)
+    call("acfe_channel_sum_finalize", ptr(bp), nb, K, 0.0, ptr(db1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx1.view(torch.int16), dx0.view(torch.int16))
+    assert torch.equal(dw1, dw0)
+    scale_ = dxb.float().abs().sum((0, 1, 2)).clamp_min(1.0)
+    assert ((db1 - db0).abs() / scale_).max().item() < 1e-6
+    ref = dxb.cpu().to(F64).sum((0, 1, 2))
+    assert ((db1.cpu().to(F64) - ref).abs() / scale_.cpu().to(F64)).max().item() < 1e-6
+
+
+def test_model_stem_bn_fusion(env, cuda):
+    """A wr_resnet_bird training step with the stem node (acfe_stem_bwd_bn) on
+    and off (ops.STEM_BN_FUSE): identical loss and every parameter gradient
+    bit-identical except the stem conv bias (its channel sums are added in
+    another order: within 1e-6 of its largest element)."""
+    ops = env[0]
+    from acfe.train import FrontEnd, Trainer
+    from resnet.wr_resnet_bird import WRResNet
+    import bench
+
+    outs = []
+    old = ops.STEM_BN_FUSE
+    try:
+        for f in (False, True):
+            ops.STEM_BN_FUSE = f
+            torch.manual_seed(0)
+            model = WRResNet(input_shape=(128, 513, 3), classes=10, dtype=BF).to(cuda)
+            fe = FrontEnd(n_mels=128, dtype=BF, device=cuda).to(cuda)
+            tr = Trainer(model, fe, lr=0.0, loss="cce", device=cuda)
+            x1, x2, lam, y = bench.make_batches(4, 10, cuda, n_sets=1)[0]
+            ops._seed_counter = itertools.count()  # same dropout seeds in both runs
+            loss, _ = tr.step(x1, y, x2, lam)
+            torch.cuda.synchronize()
+            names = [n for n, p in tr.holder.named_parameters() if p.requires_grad]
+            outs.append((loss.detach().clone(), {n: tr.arena.grad[o:o + k].detach().clone()
+                                                 for n, (o, k) in zip(names, tr.arena.offsets)}))
+    finally:
+        ops.STEM_BN_FUSE = old
+    (l0, g0), (l1, g1) = outs
+    assert torch.equal(l0, l1)
+    assert any("conv1_1" in n for n in g0)
+    for n in g0:
+        if "conv1_1" in n and g0[n].numel() == 16:  # the stem bias
+            assert ((g1[n] - g0[n]).abs().max() / g0[n].abs().max().clamp_min(1e-30)).item() < 1e-6, n
+        else:
+            assert torch.equal(g1[n], g0[n]), n
+
+
 @pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (32, 128, 32, 64), (32, 256, 16, 32), (16, 256, 16, 32),
                                      (64, 64, 64, 128), (128, 64, 64, 128), (64, 64, 14, 100), (256, 256, 22, 86),
                                      (256, 16, 16, 32), (128, 16, 16, 40), (16, 64, 64, 100), (16, 64, 15, 70)],
