@@ -5114,6 +5114,15 @@ ACFE_API int acfe_stem_dgrad(const void* dy, int dy_dtype, int N, int H, int W, 
   return launch_rc("acfe_stem_dgrad");
 }
 
+// Workgroups of k_stem_bwd_bn: one resident round (3 per CU: 168 VGPRs, 46 KB
+// of LDS) each walking its share of the tiles, instead of acfe_stem_blocks'
+// 2048 in 2.7 rounds.  <= acfe_stem_blocks, which sizes the workspaces.
+static int stem_bwd_grid(int N, int H, int W) {
+  static const int cap = getenv("ACFE_STEM_BWD_GRID") ? atoi(getenv("ACFE_STEM_BWD_GRID")) : 768;
+  const int nb = acfe_stem_blocks(N, H, W);
+  return cap > 0 && cap < nb ? cap : nb;
+}
+
 // workspace: double[acfe_stem_blocks(N,H,W) * 16 * R * S]
 ACFE_API int acfe_stem_wgrad(const void* x, int x_dtype, const void* dy, int dy_dtype, int N, int H, int W,
                              int R, int S, int pad_top, int pad_left, int rep, float* dw, float beta,
@@ -5160,7 +5169,12 @@ ACFE_API int acfe_stem_bwd_bn(const void* g, const void* xb, const void* xin, in
       ((uintptr_t)xb & 15))
     return ACFE_E_INVAL;
   const int th = (H + STEM_TH - 1) / STEM_TH, tw = (W + STEM_TW - 1) / STEM_TW;
-  const int grid = acfe_stem_blocks(N, H, W);
+  const int nb = acfe_stem_blocks(N, H, W), grid = stem_bwd_grid(N, H, W);
+  if (grid < nb) {  // bias slab rows past the grid: zero
+    const hipError_t e =
+        hipMemsetAsync(bias_part + (size_t)grid * 2 * STEM_K, 0, sizeof(double) * 2 * STEM_K * (nb - grid), strm(stream));
+    if (e != hipSuccess) return hip_rc(e, "acfe_stem_bwd_bn");
+  }
   uint16_t* dxo = (uint16_t*)dxin;
   if (!dxo) return ACFE_E_INVAL;
 #define SB(RR)                                                                                                \

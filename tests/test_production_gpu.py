@@ -447,9 +447,10 @@ def test_stem_bwd_bn_fused(env, cuda, N, H, W, R, relu):
     """acfe_stem_bwd_bn (wr_resnet_bird.py:22-30: the stem conv's backward with
     its BN's backward apply folded into the dY staging) against the unfused
     chain acfe_bn_bwd_apply_ex -> acfe_stem_dgrad + acfe_stem_wgrad +
-    acfe_channel_sum: dX and dW bit-identical (same bf16 dX_bn, tile order and
-    MFMA operands), the bias sums within 1e-6 of the sum of |dX_bn| (both add
-    the same bf16 values in float64, in different orders)."""
+    acfe_channel_sum: dX bit-identical (same bf16 dX_bn and MFMA operands), dW
+    within 1e-6 (the fused pass walks the tiles with fewer workgroups: another
+    fp32 summation order) and the bias sums within 1e-6 of the sum of |dX_bn|
+    (both add the same bf16 values in float64, in different orders)."""
     ops, call, lib, ptr, stream = env
     K, rep = 16, 3
     S = R
@@ -489,7 +490,7 @@ def test_stem_bwd_bn_fused(env, cuda, N, H, W, R, relu):
     call("acfe_channel_sum_finalize", ptr(bp), nb, K, 0.0, ptr(db1), stream())
     torch.cuda.synchronize()
     assert torch.equal(dx1.view(torch.int16), dx0.view(torch.int16))
-    assert torch.equal(dw1, dw0)
+    assert ((dw1 - dw0).norm() / dw0.norm()).item() < 1e-6
     scale_ = dxb.float().abs().sum((0, 1, 2)).clamp_min(1.0)
     assert ((db1 - db0).abs() / scale_).max().item() < 1e-6
     ref = dxb.cpu().to(F64).sum((0, 1, 2))
@@ -499,8 +500,8 @@ def test_stem_bwd_bn_fused(env, cuda, N, H, W, R, relu):
 def test_model_stem_bn_fusion(env, cuda):
     """A wr_resnet_bird training step with the stem node (acfe_stem_bwd_bn) on
     and off (ops.STEM_BN_FUSE): identical loss and every parameter gradient
-    bit-identical except the stem conv bias (its channel sums are added in
-    another order: within 1e-6 of its largest element)."""
+    bit-identical except the stem conv's weight and bias (their sums are added
+    in another order: within 1e-5)."""
     ops = env[0]
     from acfe.train import FrontEnd, Trainer
     from resnet.wr_resnet_bird import WRResNet
@@ -528,8 +529,8 @@ def test_model_stem_bn_fusion(env, cuda):
     assert torch.equal(l0, l1)
     assert any("conv1_1" in n for n in g0)
     for n in g0:
-        if "conv1_1" in n and g0[n].numel() == 16:  # the stem bias
-            assert ((g1[n] - g0[n]).abs().max() / g0[n].abs().max().clamp_min(1e-30)).item() < 1e-6, n
+        if "conv1_1" in n:  # the stem weight and bias
+            assert ((g1[n] - g0[n]).abs().max() / g0[n].abs().max().clamp_min(1e-30)).item() < 1e-5, n
         else:
             assert torch.equal(g1[n], g0[n]), n
 
