@@ -1597,17 +1597,26 @@ __global__ void k_dense_bwd_x(const float* __restrict__ dz, const float* __restr
     dx[t] = acc;
   }
 }
-__global__ void k_dense_bwd_w(const float* __restrict__ x, const float* __restrict__ dz, int B, int I, int O,
-                              float* __restrict__ dw, float* __restrict__ db) {
-  for (int t = blockIdx.x * 256 + threadIdx.x; t < (I + 1) * O; t += gridDim.x * 256) {
+// dw[i][o] = sum_b x[b][i] dz[b][o], db[o] = sum_b dz[b][o]: one wave per
+// output, its lanes striding the batch (a thread-serial loop over B = 512 was
+// bound by its dependent load latency: 132 us per T1 step), fixed-order
+// butterfly sum in float64
+__global__ void __launch_bounds__(256) k_dense_bwd_w(const float* __restrict__ x, const float* __restrict__ dz, int B,
+                                                     int I, int O, float* __restrict__ dw, float* __restrict__ db) {
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < (I + 1) * O; t += gridDim.x * 4) {
     const int i = t / O, o = t % O;
+    if (i == I && !db) continue;
     double acc = 0.0;
-    if (i < I) {
-      for (int b = 0; b < B; ++b) acc += (double)x[(long long)b * I + i] * dz[(long long)b * O + o];
-      dw[t] = (float)acc;
-    } else if (db) {
-      for (int b = 0; b < B; ++b) acc += dz[(long long)b * O + o];
-      db[o] = (float)acc;
+    for (int b = lane; b < B; b += 64) {
+      const double g = dz[(long long)b * O + o];
+      acc += i < I ? (double)x[(long long)b * I + i] * g : g;
+    }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+    if (lane == 0) {
+      if (i < I) dw[t] = (float)acc;
+      else db[o] = (float)acc;
     }
   }
 }
@@ -1617,8 +1626,9 @@ ACFE_API int acfe_dense_bwd(const float* x, const float* w, const float* dz, int
   if (dx && B > 0)
     hipLaunchKernelGGL(k_dense_bwd_x, dim3(grid_for((long long)B * I)), dim3(256), 0, strm(stream), dz, w, B, I, O,
                        dx);
-  hipLaunchKernelGGL(k_dense_bwd_w, dim3(grid_for((long long)(I + 1) * O)), dim3(256), 0, strm(stream), x, dz, B, I,
-                     O, dw, db);
+  const long long nw = (long long)(I + 1) * O;  // one wave per output
+  hipLaunchKernelGGL(k_dense_bwd_w, dim3((unsigned)std::min<long long>((nw + 3) / 4, 8192)), dim3(256), 0,
+                     strm(stream), x, dz, B, I, O, dw, db);
   return launch_rc("acfe_dense_bwd");
 }
 

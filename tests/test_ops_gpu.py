@@ -266,6 +266,20 @@ def test_pools_dropout_add(ops, cuda, dtype):
     assert rel(z.float(), torch.relu(a.double().cpu() + b.double().cpu())) < (1e-7 if dtype == torch.float32 else 5e-3)
 
 
+@pytest.mark.parametrize("B,I,O", [(512, 32, 50), (70, 17, 3), (1, 5, 2)])
+def test_dense_backward_batch_sizes(ops, cuda, B, I, O):
+    """acfe_dense_bwd's weight / bias gradients (one wave per output striding
+    the batch, float64 butterfly) against float64 autograd, at the T1 head's
+    [512, 32] x [32, 50] and ragged batches."""
+    x, w, b = rnd((B, I), 41), rnd((I, O), 42, 0.5), rnd((O,), 43, 0.1)
+    dz = rnd((B, O), 44)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    (xr @ wr + br).backward(dz)
+    xd, wd, bd = (t.float().to(cuda).requires_grad_(True) for t in (x, w, b))
+    ops.dense(xd, wd, bd).backward(dz.float().to(cuda))
+    assert rel(wd.grad, wr.grad) < 1e-6 and rel(bd.grad, br.grad) < 1e-6 and rel(xd.grad, xr.grad) < 1e-6
+
+
 def test_lme_dense_loss_adam(ops, cuda):
     from oracle.models import keras_adam, keras_loss
 
