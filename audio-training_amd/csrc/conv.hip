@@ -3933,18 +3933,25 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   // tiles per wave
   // tiles per wave; K = 16 (wr_resnet_bird's stage-3 256 -> 16): 128-channel
   // chunks, one 16-channel block per wave
-  const int cw = g.C % 64 == 0 ? (g.K == 256 ? 32 : (g.K == 16 ? 128 : 64)) : g.C;
+  // (ACFE_WG16_CW=64: the 64-channel-chunk form below for C % 128 == 0 too;
+  // r04g7: 120.5 vs 103.9 us for the 256 -> 16 layer at 512 clips)
+  static const int cw16 = getenv("ACFE_WG16_CW") ? atoi(getenv("ACFE_WG16_CW")) : 128;
+  const int cw = g.C % 64 == 0 ? (g.K == 256 ? 32 : (g.K == 16 && cw16 == 128 && g.C % 128 == 0 ? 128 : 64)) : g.C;
   // two output rows per step for the K = 64 (plain or pooled dY) and K = 32
   // layers (r02au-aw: 72 instead of 36 MFMAs per wave per barrier); the K =
   // 128 pooled-gradient variant spills at two rows (138 VGPRs) and keeps one
   // C = 16 -> K = 64 (wr_resnet's stage-1 conv2a): two pixel groups of 4
   // waves, each its own split slab (the caller guarantees splits >= 16)
   const bool c16k64 = cw == 16 && g.K == 64;
+  // K = 16 on 64-channel chunks (C = 64 * odd): the 4 wave groups' 9 (tap,
+  // block) pairs x two pixel groups (one 32-pixel half each), 72 KB of LDS ->
+  // 2 workgroups per CU
+  const bool k16c64 = cw == 64 && g.K == 16;
   const int nr = ((cw == 64 || c16k64) && g.P % 2 == 0 && (g.K == 64 || (g.K == 32 && !amax))) ? 2 : 1;
-  const int wp = c16k64 ? 2 : 1;
+  const int wp = (c16k64 || k16c64) ? 2 : 1;
   const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * ((g.Q + 63) / 64));
   // c16k64: 75 KB of LDS and 114 VGPRs -> two workgroups per CU
-  int sp = (c16k64 ? 512 : 256) / nchunk;
+  int sp = (c16k64 || k16c64 ? 512 : 256) / nchunk;
   if (sp > splits / wp) sp = (int)(splits / wp);
   sp &= ~7;
   if (sp < 8) sp = 8;
@@ -3959,6 +3966,8 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
                      (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
   if (cw == 128) {  // wr_resnet_bird stage 3 (256 -> 16)
     WHC(16, 128);
+  } else if (k16c64) {
+    WHC(16, 64);
   } else if (c16k64) {
     if (nr == 2)
       hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 16, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
@@ -4026,7 +4035,7 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   g.ldy = K;
   int rc;
   if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 &&
-      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) || (C % 128 == 0 && K == 16) ||
+      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) || (C % 64 == 0 && K == 16 && splits >= 16) ||
        ((C == 32 && (K == 128 || K == 256)) || (C == 16 && (K == 256 || (K == 64 && splits >= 16))))) &&
       (long long)N * P * ((Q + 63) / 64) < (1ll << 31)) {
     // halo-staged kernel; its split count stays within the planned workspace

@@ -537,10 +537,11 @@ def test_model_stem_bn_fusion(env, cuda):
 
 @pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (32, 128, 32, 64), (32, 256, 16, 32), (16, 256, 16, 32),
                                      (64, 64, 64, 128), (128, 64, 64, 128), (64, 64, 14, 100), (256, 256, 22, 86),
-                                     (256, 16, 16, 32), (128, 16, 16, 40), (16, 64, 64, 100), (16, 64, 15, 70)],
+                                     (256, 16, 16, 32), (128, 16, 16, 40), (16, 64, 64, 100), (16, 64, 15, 70),
+                                     (64, 16, 20, 70)],
                          ids=["s2-21", "s2-2b", "s3-2b-b6", "s3-2b", "k64-rowpair", "k64-rowpair-2chunks",
                               "k64-rowpair-partial", "wrn-s3-256", "s3-21-k16", "k16-1chunk-partial",
-                              "wrn-s1-2a-c16", "c16-k64-oddrows"])
+                              "wrn-s1-2a-c16", "c16-k64-oddrows", "k16-c64-chunks"])
 def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
     """k_wgrad3x3_halo for the stage-2/3 layers whose channel count is the
     feature height: K = 32 (branch21 128 -> 32) and the 16 / 32-channel
@@ -548,7 +549,8 @@ def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
     two-rows-per-step variant (k_wgrad3x3_halo<64, false, 64, 2>: 64 x 128
     stage-2 shapes, two 64-channel chunks, and a partial last column segment),
     and wr_resnet's stage-3 256 -> 256 at 22 x 86 (32-channel chunks of C),
-    the K = 16 layers (128-channel chunks, one 16-channel block per wave) and
+    the K = 16 layers (128-channel chunks, one 16-channel block per wave; 64-
+    channel chunks with two pixel groups when C = 64 * odd) and
     wr_resnet's stage-1 16 -> 64 (two pixel groups of waves writing separate
     split slabs; two rows per step, one for an odd row count), at 32 clips and
     the production split count, against float64."""
