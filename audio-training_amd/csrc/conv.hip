@@ -4901,10 +4901,11 @@ k_stem_wgrad_mfma(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
 // reads g and x, writes dX_bn, 3 x 1.07 GB per T1 step) is formed while the
 // stem dgrad stages its dY halo; the weight gradient and the conv-bias sums
 // read the same LDS image, so dX_bn is never stored and the separate wgrad's
-// re-read of it is gone.  dX and dW bit-identical to the apply8 ->
-// k_stem_dgrad_mfma / k_stem_wgrad_mfma chain (the same bf16 dX_bn, tile order
-// and MFMA operands); bias sums [block][2][16] of the bf16 dX_bn values over
-// each tile's own pixels.
+// re-read of it is gone.  dX bit-identical to the apply8 -> k_stem_dgrad_mfma
+// chain (the same bf16 dX_bn and MFMA operands); dW the k_stem_wgrad_mfma
+// arithmetic over stem_bwd_grid's workgroups (its fp32 partials summed in
+// another grouping than acfe_stem_wgrad's); bias sums [block][2][16] of the
+// bf16 dX_bn values over each tile's own pixels.
 template <int R, int S>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 k_stem_bwd_bn(const uint16_t* __restrict__ g, const uint16_t* __restrict__ xb, const uint16_t* __restrict__ xin,
