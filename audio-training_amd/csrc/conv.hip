@@ -5084,11 +5084,19 @@ ACFE_API int acfe_stem_fwd(const void* x, int x_dtype, int N, int H, int W, int 
                      pad_top, pad_left, weff, bias, (TO*)y, stats_partial, th, tw)
 #define SF(TI, TO) if (R == 5) SF1(TI, TO, 5); else SF1(TI, TO, 3)
   if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16) {
+    // one resident round (7 workgroups per CU at 62 VGPRs) instead of 2048 in
+    // 1.14 rounds; the statistics slab rows past the grid are zeroed
+    const int g1 = grid < 7 * 256 ? grid : 7 * 256;
+    if (stats_partial && g1 < grid) {
+      const hipError_t e = hipMemsetAsync(stats_partial + (size_t)g1 * 2 * STEM_K, 0,
+                                          sizeof(double) * 2 * STEM_K * (grid - g1), strm(stream));
+      if (e != hipSuccess) return hip_rc(e, "acfe_stem_fwd");
+    }
     if (R == 5)
-      hipLaunchKernelGGL((k_stem_fwd_mfma<5, 5>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, N, H, W,
+      hipLaunchKernelGGL((k_stem_fwd_mfma<5, 5>), dim3(g1), dim3(256), 0, strm(stream), (const uint16_t*)x, N, H, W,
                          pad_top, pad_left, weff, bias, (uint16_t*)y, stats_partial, th, tw);
     else
-      hipLaunchKernelGGL((k_stem_fwd_mfma<3, 3>), dim3(grid), dim3(256), 0, strm(stream), (const uint16_t*)x, N, H, W,
+      hipLaunchKernelGGL((k_stem_fwd_mfma<3, 3>), dim3(g1), dim3(256), 0, strm(stream), (const uint16_t*)x, N, H, W,
                          pad_top, pad_left, weff, bias, (uint16_t*)y, stats_partial, th, tw);
   } else if (x_dtype == ACFE_DTYPE_BF16 && y_dtype == ACFE_DTYPE_BF16) SF(uint16_t, uint16_t);
   else if (x_dtype == ACFE_DTYPE_BF16) SF(uint16_t, float);
