@@ -1007,16 +1007,28 @@ __global__ void __launch_bounds__(256) k_pcen_fwd(const float* __restrict__ mel,
   float lmin = INFINITY, lmax = -INFINITY;
   const int nrow = (int)((rows - row0) < PCEN_RB ? (rows - row0) : PCEN_RB);
   constexpr int PER = PCEN_TCH / 4;
+  // the next chunk's x values are loaded into registers while this chunk is
+  // scanned, transformed and stored (the chunk loop was load-latency bound)
+  float px[PER];
+  auto ldx = [&](int t0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int tt = sub * PER + k;
+      px[k] = (valid && t0 + tt < T) ? xr[(int64_t)(t0 + tt) * M] : 0.f;
+    }
+  };
+  ldx(0);
   for (int t0 = 0; t0 < T; t0 += PCEN_TCH) {
     const int tn = (T - t0) < PCEN_TCH ? (T - t0) : PCEN_TCH;
     if (valid) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const int tt = sub * PER + k;
-        if (tt < tn) xs[tt][r] = xr[(int64_t)(t0 + tt) * M];
+        if (tt < tn) xs[tt][r] = px[k];
       }
     }
     __syncthreads();
+    if (t0 + PCEN_TCH < T) ldx(t0 + PCEN_TCH);
     if (valid && sub == 0) {
       float xv[PCEN_TCH];
 #pragma unroll
@@ -1168,6 +1180,17 @@ __global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel,
   for (int i = 0; i < PCEN_NACC; ++i) acc[i] = 0.f;
   float a = (valid && sub == 0) ? xr[0] : 0.f, da = 0.f;
   const float lnb = logf(P.b);
+  // the next chunk's x values prefetched as in k_pcen_fwd (prefetching the
+  // dL/dout chunk too measured slower: 180 -> 219 us, r04g11)
+  float px[PER];
+  auto ldx = [&](int t0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int tt = sub * PER + k;
+      px[k] = (valid && t0 + tt < T) ? xr[(int64_t)(t0 + tt) * M] : 0.f;
+    }
+  };
+  ldx(0);
   for (int t0 = 0; t0 < T; t0 += PCEN_TCH) {
     const int tn = (T - t0) < PCEN_TCH ? (T - t0) : PCEN_TCH;
     for (int i = threadIdx.x; i < nrow * PCEN_TCH; i += 256) {
@@ -1182,10 +1205,11 @@ __global__ void __launch_bounds__(256) k_pcen_bwd(const float* __restrict__ mel,
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         const int tt = sub * PER + k;
-        if (tt < tn) xs[tt][r] = xr[(int64_t)(t0 + tt) * M];
+        if (tt < tn) xs[tt][r] = px[k];
       }
     }
     __syncthreads();
+    if (t0 + PCEN_TCH < T) ldx(t0 + PCEN_TCH);
     if (valid && sub == 0) {
       float xv[PCEN_TCH];
 #pragma unroll
