@@ -545,8 +545,10 @@ class ResidualLink:
         return p
 
 
-def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, defer=False):
+def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, defer=False, grad=False):
     """Batch statistics (given slab or acfe_bn_stats) -> finalize -> apply. Returns (y, saved).
+    grad: a backward can run (the node's ctx.needs_input_grad); only then is y
+    tagged with its BN input for a consumer dgrad's fused reduce.
     defer: y is returned unwritten, marked pending (x, scale, shift, relu); the
     consuming conv applies the BN in its input staging and fills y, or
     materialize(y) runs the apply pass."""
@@ -574,7 +576,7 @@ def _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, o
     if out_dtype is None:  # affine only: the caller applies it (bn_max_pool)
         return None, (scale, shift, mean, invstd)
     y = _empty(x.shape, out_dtype, dev)
-    if FUSE_BN_REDUCE:
+    if FUSE_BN_REDUCE and training and grad:
         # a conv reading y may form this BN's backward reduce in its dgrad (_conv_bwd)
         y._acfe_bn_src = (x, scale, shift, mean, invstd, bool(relu))
     if defer and out_dtype == x.dtype:
@@ -725,7 +727,8 @@ class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, link, defer):
         ctx.gb = (gamma, beta)
-        y, saved = _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, defer)
+        y, saved = _bn_fwd(x, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, out_dtype, defer,
+                           any(ctx.needs_input_grad))
         ctx.save_for_backward(x, *saved)
         ctx.conf = (relu, training, link)
         ctx.mask_in = FUSE and getattr(x, "_acfe_relu_out", False)
@@ -767,7 +770,7 @@ class _ConvDropBNFn(torch.autograd.Function):
         ctx.bn = bn_src(x)
         u, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, training, drop)
         y, saved = _bn_fwd(u, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
-                           u.dtype, defer)
+                           u.dtype, defer, any(ctx.needs_input_grad))
         ctx.save_for_backward(x, w, u, *saved)
         ctx.conf = conf
         ctx.has_b = b is not None
@@ -1217,7 +1220,7 @@ class _PoolDropBNFn(torch.autograd.Function):
         drop = (rate, seed) if training and rate > 0.0 else None
         u, amax, stats = _maxpool_fwd(x, kh, kw, drop, training)
         y, saved = _bn_fwd(u, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
-                           u.dtype)
+                           u.dtype, False, any(ctx.needs_input_grad))
         ctx.save_for_backward(u, amax, *saved)
         ctx.conf, ctx.drop, ctx.shape = conf, drop, x.shape
         return y
@@ -1286,7 +1289,8 @@ class _ConvPoolBNFn(torch.autograd.Function):
             else:
                 call("acfe_conv2d_fwd_pool", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(u), ptr(amax),
                      float(r_), int(s_), ptr(stats), dtype_code(x.dtype), stream())
-        y, saved = _bn_fwd(u, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, u.dtype, defer)
+        y, saved = _bn_fwd(u, gamma, beta, stats, mmean, mvar, training, relu, eps, momentum, u.dtype, defer,
+                           any(ctx.needs_input_grad))
         ctx.save_for_backward(x, w, u, amax, *saved)
         ctx.conf, ctx.drop, ctx.has_b = conf, drop, b is not None
         return y

@@ -312,8 +312,14 @@ class AudioDataset:
         n = self.count()
         budget = self.cache_bytes
         if budget is None:
-            budget = (torch.cuda.get_device_properties(self.device).total_memory // 2 if self.device.type == "cuda"
-                      else 1 << 30)
+            if self.device.type == "cuda":
+                # what is free now, less a quarter of the device for the
+                # activations / workspaces the training step has yet to take
+                free, total = torch.cuda.mem_get_info(self.device)
+                budget = max(0, min(total // 2, free - total // 4))
+            else:
+                budget = 1 << 30
+            logging.info("dataset cache budget %.1f GB", budget / 1e9)
         need = (n + self.per_chunk) * 4 * self.nfloats
         if need > budget:
             logging.warning("dataset cache: %d clips need %.1f GB > budget %.1f GB; streaming every epoch", n,
@@ -523,7 +529,7 @@ class AudioDataset:
                         break
                 pick, partner = self._draw(rng, live, used, target, done, augment)
                 yield pick, partner, lab, slots
-            if caching and done and self.error is None:
+            if caching and done and self.error is None and slots.keep:
                 # the whole epoch went through: later epochs run from the device
                 self._cached = (order, lab.copy())
         finally:
@@ -583,18 +589,26 @@ class _SlotPool:
         self.free = list(range(rows - 1, -1, -1))
         self.ev = ev
         self.keep = False  # dataset cache: released slots keep their clips
+        self.held: list[int] = []  # slots released while keeping (given back if the cache is abandoned)
         self.cv = threading.Condition()
 
     def release(self, rows, ev):
         with self.cv:
-            if not self.keep:
-                self.free.extend(rows)
+            (self.held if self.keep else self.free).extend(rows)
             if ev is not None:
                 self.ev = ev
             self.cv.notify_all()
 
     def acquire(self, n, stop):
         with self.cv:
+            if self.keep and len(self.free) < n:
+                # the epoch holds more clips than the pool was sized for (a
+                # caller's epoch_size below the true record count): stop
+                # caching rather than wait for releases that never come back
+                logging.warning("dataset cache: more clips than planned; this epoch streams, nothing is cached")
+                self.keep = False
+                self.free.extend(self.held)
+                self.held = []
             while len(self.free) < n:
                 if stop.is_set():
                     return None

@@ -87,6 +87,26 @@ def normalize(x):
     return (x - 0.5) * 2
 
 
+def normalize_f32(x):
+    """The same in float32, operation for operation (predict_utils.py:153-160,
+    audiodataset.py:1334-1341 -- numpy float32; tfdataset.py:1923-1929 has the
+    same order in TF): pinned bit for bit to tests/golden/normalize_golden.npz,
+    which oracle/gen_golden_normalize.py made with the reference functions."""
+    x = np.asarray(x, dtype=np.float32)
+    x = x - np.min(x, -1, keepdims=True)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        x = x / np.max(x, -1, keepdims=True) + np.float32(0.000001)
+    x = x - np.float32(0.5)
+    return x * np.float32(2)
+
+
+def mix_up_f32(x1, x2, lam):
+    """tfdataset.py:950 image blend in float32 (x1 * l + x2 * (1 - l), one
+    rounding per operation); lam [B]."""
+    lam = np.asarray(lam, np.float32).reshape(-1, 1)
+    return np.asarray(x1, np.float32) * lam + np.asarray(x2, np.float32) * (np.float32(1) - lam)
+
+
 def mix_up(x1, y1, x2, y2, lam, single_label=True):
     """tfdataset.py:930-955 with the per-row lambda supplied (the reference draws
     it from Beta(a,a)*Bernoulli(chance), :942-946)."""

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import synth_clips
+from conftest import GOLDEN, synth_clips
 from oracle import frontend as of
 
 pytestmark = pytest.mark.gpu
@@ -214,3 +214,56 @@ def test_stored_spectrogram_path_matches_raw_path(fe, cuda):
     mel = np.einsum("mf,bft->btm", plan.weights.astype(np.float64), spec.double().cpu().numpy())
     ref = of.pcen(mel).transpose(0, 2, 1)
     assert np.abs(got - ref).max() < 5e-5
+
+
+def test_normalize_reference_golden_bitexact(fe, cuda):
+    """Row a1 pinned to the reference itself (tests/golden/normalize_golden.npz,
+    made by oracle/gen_golden_normalize.py from predict_utils.normalize_data /
+    audiodataset.normalize_data, float32): acfe_normalize_stats +
+    acfe_normalize_apply bit for bit on every clip (3 s clips batched as
+    tfdataset.normalize sees them, a 5 000-sample clip, a lone spike, a
+    constant clip whose 0 / 0 is NaN) and on the load_samples(normalize=True)
+    windows (zero-padded short tracks: the pads take part in the min / max).
+    The fused users of the same arithmetic: acfe_mixup (normalize-on-load of
+    both inputs, tfdataset.py:950 blend) bit for bit against the float32
+    oracle composition that the fixture pins, and acfe_mel_fwd's
+    normalize-on-load (Markstein reciprocal division, frontend.hip norm1r) ==
+    mel of the separately normalised clips, bit for bit."""
+    from oracle.gen_golden_normalize import N, SR, STRIDE, clip_set, hash_audio, sha
+
+    z = np.load(GOLDEN / "normalize_golden.npz")
+    clips = clip_set()
+    full = np.stack([clips["full0"], clips["full1"], clips["full2"]])
+    y = fe.normalize(torch.from_numpy(full).to(cuda)).cpu().numpy()
+    for r, name in enumerate(("full0", "full1", "full2")):
+        assert np.array_equal(y[r, ::STRIDE], z[f"norm_{name}_sample"]), name
+        assert sha(y[r]) == str(z[f"norm_{name}_sha"]), name
+    for name in ("short", "spike", "const"):
+        yy = fe.normalize(torch.from_numpy(clips[name][None]).to(cuda)).cpu().numpy()[0]
+        assert np.array_equal(yy, z[f"norm_{name}"], equal_nan=True), name
+
+    recs = {}
+    wins = []
+    for k, ti, first, src, cnt in z["ls_rows"]:
+        rec = recs.setdefault(int(k), hash_audio(SR * 20, 100 + int(k), 0.8))
+        w = np.zeros(N, np.float32)
+        w[first:first + cnt] = rec[src:src + cnt]
+        wins.append(w)
+    yw = fe.normalize(torch.from_numpy(np.stack(wins)).to(cuda)).cpu().numpy()
+    for r in range(len(wins)):
+        assert sha(yw[r]) == str(z["ls_sha"][r]), r
+
+    # mix_up with both normalizations on load, then the second normalize
+    x1 = torch.from_numpy(full).to(cuda)
+    x2 = torch.from_numpy(full[::-1].copy()).to(cuda)
+    lam = torch.tensor([0.3, 1.0, 0.0], device=cuda)
+    mixed = fe.mix_up(x1, x2, lam, fe.normalize_stats(x1), fe.normalize_stats(x2))
+    ref = of.mix_up_f32(of.normalize_f32(full), of.normalize_f32(full[::-1]), lam.cpu().numpy())
+    assert np.array_equal(mixed.cpu().numpy(), ref)
+    assert np.array_equal(fe.normalize(mixed).cpu().numpy(), of.normalize_f32(ref))
+
+    # the mel kernel's normalize-on-load == mel of the normalised clips
+    plan = fe.MelPlan(n_mels=128)
+    a = plan.mel(x1, fe.normalize_stats(x1))
+    b = plan.mel(fe.normalize(x1), None)
+    assert torch.equal(a, b)

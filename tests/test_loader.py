@@ -266,6 +266,29 @@ def test_dataset_cache_over_budget_streams(shards):
     assert ds._cached is None and not ds.cache
 
 
+def test_dataset_cache_with_short_epoch_size_does_not_hang(shards, monkeypatch):
+    """cache=True with a caller epoch_size below the true record count (ADVICE
+    r04 medium): the pool is planned for too few clips, so the caching epoch
+    runs out of slots; it must fall back to streaming (every kept example once,
+    nothing cached) instead of waiting for slot releases that never come."""
+    import tfdataset
+
+    monkeypatch.setattr(tfdataset, "CHUNK_BYTES", 4 * 4 * N)
+    d, keep = shards
+    ds = tfdataset.AudioDataset(tfdataset._files(d), ["bird", "noise"], batch_size=3, device="cpu", threads=3,
+                                shuffle_buffer=6, augment=True, cache=True, epoch_size=5)
+    for _ in range(2):
+        t0 = time.perf_counter()
+        seen = []
+        for (x1, y1), _ in ds:
+            for k, row in zip(_ids(x1), y1):
+                assert _label_ok(k, row), k
+            seen += _ids(x1)
+        assert time.perf_counter() - t0 < 60
+        assert sorted(seen) == keep
+        assert ds._cached is None
+
+
 @pytest.mark.gpu
 def test_dataset_cache_on_device(shards, cuda):
     """The HBM-resident cache on the GPU: epochs 2-3 gather every kept clip

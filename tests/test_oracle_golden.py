@@ -112,3 +112,49 @@ def test_ema_initializer_semantics():
     e = of.ema(x, 0.3)
     np.testing.assert_allclose(e[:, 0], x[:, 0])
     np.testing.assert_allclose(e[:, 1], 0.3 * x[:, 1] + 0.7 * x[:, 0])
+
+
+# ---------------------------------------------------------------- normalize
+def _norm_golden():
+    return np.load(GOLDEN / "normalize_golden.npz")
+
+
+def test_oracle_normalize_f32_bitexact():
+    """of.normalize_f32 against the reference predict_utils / audiodataset
+    normalize_data outputs (oracle/gen_golden_normalize.py): every clip of the
+    set bit for bit (SHA-256 of the float32 bytes for the 3 s clips, the
+    values themselves for the short ones; the constant clip is 0 / 0 = NaN
+    everywhere), and the float64 oracle within 2 float32 ulps of it."""
+    from oracle.gen_golden_normalize import STRIDE, clip_set, sha
+
+    z = _norm_golden()
+    for name, x in clip_set().items():
+        y = of.normalize_f32(x)
+        assert y.dtype == np.float32
+        if f"norm_{name}_sha" in z:
+            assert np.array_equal(y[::STRIDE], z[f"norm_{name}_sample"]), name
+            assert sha(y) == str(z[f"norm_{name}_sha"]), name
+        else:
+            ref = z[f"norm_{name}"]
+            assert np.array_equal(y, ref, equal_nan=True), name
+        if name != "const":
+            assert np.abs(of.normalize(x) - y).max() <= 2 * np.spacing(np.float32(1)), name
+    assert np.isnan(z["norm_const"]).all()
+
+
+def test_oracle_normalize_load_samples_windows():
+    """load_samples(normalize=True) windows (zero-padded short tracks are
+    normalised after padding): rebuilt from the fixture's window layout and
+    normalised by of.normalize_f32, bit for bit."""
+    from oracle.gen_golden_normalize import N, SR, STRIDE, hash_audio, sha
+
+    z = _norm_golden()
+    recs = {}
+    for r, (k, ti, first, src, cnt) in enumerate(z["ls_rows"]):
+        rec = recs.setdefault(int(k), hash_audio(SR * 20, 100 + int(k), 0.8))
+        win = np.zeros(N, np.float32)
+        win[first:first + cnt] = rec[src:src + cnt]
+        y = of.normalize_f32(win)
+        assert np.array_equal(y[::STRIDE], z["ls_sample"][r]), r
+        assert sha(y) == str(z["ls_sha"][r]), r
+    assert (z["ls_rows"][:, 4] < N).any()  # some windows are padded

@@ -1,0 +1,65 @@
+#!/bin/bash
+# Round-5 GPU session: GPU parity tests + smoke, then for each workload a bench
+# line and a rocprofv3 kernel-trace summary of the same command.  Every GPU step
+# has its own time limit; the first failing step ends the script.
+# usage: tools/gpu_r04.sh <tag> [workloads...]   (workloads: tests t1 wrn t1fp32 infer stream)
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=${1:-r05}; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+step() { # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 $t "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -c 400 $O/$name.log; echo
+  [ $rc -eq 0 ] || exit $rc
+}
+bp() { # name benchargs...  (bench line + rocprof of the same command)
+  local name=$1; shift
+  step ${name}_bench 600 python bench.py "$@"
+  step ${name}_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${name}_prof -o run -- \
+      python bench.py --no-cpu-baseline "$@"
+}
+for w in "$@"; do
+  case $w in
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+           step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    testsall) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/testsall.log 2>&1
+              rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
+              case $rc in 0|1) ;; *) exit $rc ;; esac ;;
+    mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
+    fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r04 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
+             'k_conv3x3_rows<64,8,4,true,true> (wr_resnet b1/b2 conv2a 3x3 64->64 @128x513 with the BN prologue + dropout + BN sums, batch 512)' \
+             --model wrn --classes 2 --steps 2 --warmup 1 ;;
+    evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r04 'k_conv3x3_1w<1, 2, true, true>' 5905580032 \
+             'k_conv3x3_1w<1,2,true,true> (wr_resnet_bird s1b0 branch21 3x3 128->128 @128x256 + 2x2 max-pool + dropout + BN sums, batch 512)' \
+             --steps 3 --warmup 1 ;;
+    evinfer) SELECT=7:3 step evinfer 900 bash tools/pmc_evidence.sh infer_fp32 r04 'k_conv_fwd_g<float, 128, 64' 8606859264 \
+             'k_conv_fwd_g<float,128,64> (wr_resnet b1.conv2a 3x3 64->64 @128x513 fp32, batch 256)' \
+             --workload infer --steps 2 --warmup 1 ;;
+    evstream) SELECT=12:1 step evstream 900 bash tools/pmc_evidence.sh stream_fp32 r04 'k_conv_fwd_g<float, 128, 128' 26832360789 \
+             'k_conv_fwd_g<float,128,128> (wr_resnet_bird s1b0 conv21 3x3 128->128 @128x256 fp32; the 3 launches of a step: 1024 / 1024 / 351 windows, averaged)' \
+             --workload stream --dtype fp32 --steps 1 --warmup 1 ;;
+    e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;
+    sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;
+    t1) bp t1 --steps 20 --warmup 5 ;;
+    ptk) step ptk 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$PTK" ;;
+    convtests) step convtests 600 python -u -m pytest tests/test_production_gpu.py tests/test_fused_gpu.py \
+                 tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    fusetests) step fusetests 600 python -u -m pytest tests/test_production_gpu.py -m gpu -k "reduce_fus" -x -v \
+                 --timeout 120 --timeout-method thread ;;
+    wrn0) ACFE_BN_REDUCE_FUSE=0 step wrn0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    t10) ACFE_BN_REDUCE_FUSE=0 step t10_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    wrnp0) ACFE_BN_PROLOGUE_1W=0 step wrnp0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    protests) step protests 600 python -u -m pytest tests/test_production_gpu.py tests/test_model_gpu.py -m gpu -k "prologue or model" -v \
+                 --timeout 120 --timeout-method thread ;;
+    wrn) bp wrn --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    t1fp32) bp t1fp32 --dtype fp32 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    infer) bp infer --workload infer --steps 5 --warmup 2 ;;
+    stream) bp stream --workload stream --dtype fp32 --steps 3 --warmup 1 ;;
+  esac
+done
+echo done
