@@ -40,6 +40,10 @@ FUSE_BN_REDUCE = FUSE and os.environ.get("ACFE_BN_REDUCE_FUSE", "1") != "0"
 # ACFE_STEM_BN_FUSE=0: wr_resnet_bird's stem backward as separate BN apply,
 # dgrad, wgrad and bias-sum passes instead of acfe_stem_bwd_bn (A/B)
 STEM_BN_FUSE = os.environ.get("ACFE_STEM_BN_FUSE", "1") != "0"
+# ACFE_BN_BWD_FUSE=0: the backward of Conv2D -> Dropout -> BatchNormalization
+# runs the BN backward apply as its own pass instead of inside the conv's
+# weight gradient (acfe_conv2d_wgrad_bnbwd) (A/B, tests)
+FUSE_BN_BWD = FUSE and os.environ.get("ACFE_BN_BWD_FUSE", "1") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -781,10 +785,79 @@ class _ConvDropBNFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, u, *saved = ctx.saved_tensors
         stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum, _ = ctx.conf
+        if _bnbwd_fold_ok(x, w, u, dy, stride, pt, pl, P, Q) and ctx.needs_input_grad[1]:
+            return _conv_bn_bwd_fold(ctx, x, w, u, dy, saved, relu, training)
         g, dgamma, dbeta = _bn_bwd(u, dy, saved, relu, training, drop=ctx.drop, params=ctx.gb)
         dx, dw, db = _conv_bwd(x, w, g, stride, pt, pl, P, Q, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                                ctx.has_b and ctx.needs_input_grad[2], bias=ctx.bias, bn=ctx.bn)
         return dx, dw, db, dgamma, dbeta, None, None, None
+
+
+def _bnbwd_fold_ok(x, w, u, dy, stride, pt, pl, P, Q) -> bool:
+    """acfe_conv2d_wgrad_bnbwd covers the node: bf16 3x3 stride-1 "same", the
+    halo wgrad shapes (acfe_conv2d_wgrad_bnbwd_rows), 16-B aligned operands."""
+    if not FUSE_BN_BWD or x.dtype != torch.bfloat16 or u.dtype != x.dtype or dy.dtype != x.dtype:
+        return False
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    if (R, S, stride, pt, pl, P, Q) != (3, 3, 1, 1, 1, H, W) or not (x.is_contiguous() and u.is_contiguous()):
+        return False
+    if u.data_ptr() % 16 or x.data_ptr() % 16:
+        return False
+    return lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K) > 0
+
+
+def _conv_bn_bwd_fold(ctx, x, w, u, dy, saved, relu, training):
+    """Backward of BN(Dropout(Conv2D(x))) with the BN backward apply inside the
+    conv's weight gradient (acfe_conv2d_wgrad_bnbwd): the wgrad stages the BN
+    output gradient dy and the BN input u, forms the conv output gradient g
+    (written for the dgrad, its channel sums = the bias gradient) -- the apply
+    pass over the tensor is gone.  Same values as _bn_bwd -> _conv_bwd."""
+    N, H, W, C = x.shape
+    K = w.shape[0]
+    dev = x.device
+    s = stream()
+    scale, shift, mean, invstd = saved
+    rows = u.numel() // K
+    dy = dy.contiguous()
+    part = None
+    prow = nrows = lib.acfe_reduce_blocks(rows)
+    lazy = _tagged(dy, "_acfe_bnpart")
+    if lazy is not None and lazy[2] == (u.data_ptr(), tuple(u.shape), bool(relu)):
+        part, prow = lazy[0], lazy[1]
+    if part is None:
+        part = _empty((nrows * 2 * K,), F64, dev)
+        call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(u), dtype_code(u.dtype), rows, K, ptr(scale),
+             ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
+    coef, dgamma, dbeta = _bn_bwd_coef(part, prow, K, rows, saved, training, ctx.gb, dev)
+    g = _empty(u.shape, u.dtype, dev)  # the conv output gradient
+    tgt = direct_grad(w)
+    dwt = tgt if tgt is not None else _empty(w.shape, F32, dev)
+    ws = _empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), F32, dev)
+    srows = lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K)
+    sums = _empty((srows, 2, K), F64, dev)
+    rate, seed = ctx.drop if ctx.drop is not None else (0.0, 0)
+    with _Timed(w, "wgrad"):
+        call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(scale), ptr(shift), int(relu),
+             ptr(coef), float(rate), int(seed), ptr(g), ptr(dwt), 1.0 if tgt is not None else 0.0, ptr(ws),
+             ptr(sums), s)
+    dw = dwt
+    if tgt is not None:
+        dw = None
+        grads_ready(w)
+    db = None
+    if ctx.has_b and ctx.needs_input_grad[2]:
+        tb = direct_grad(ctx.bias)
+        out = tb if tb is not None else _empty((K,), F32, dev)
+        call("acfe_channel_sum_finalize", ptr(sums), srows, K, 1.0 if tb is not None else 0.0, ptr(out), s)
+        db = out
+        if tb is not None:
+            db = None
+            grads_ready(ctx.bias)
+    dx = None
+    if ctx.needs_input_grad[0]:
+        dx, _, _ = _conv_bwd(x, w, g, 1, 1, 1, H, W, True, False, False, bias=ctx.bias, bn=ctx.bn)
+    return dx, dw, db, dgamma, dbeta, None, None, None
 
 
 def conv_dropout_bn(x, w, b, gamma, beta, mmean, mvar, training, rate=0.0, seed=None, relu=True, stride=1,

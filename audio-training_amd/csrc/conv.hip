@@ -2998,10 +2998,18 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 // NR: output rows per pipeline step (a "segment" = NR rows x 64 pixels, P % NR
 // == 0): NR = 2 doubles the MFMAs per barrier for K = 64 (36 -> 72 per wave),
 // the halo then being NR + 2 input rows.
-template <int KB, bool UNP, int CW = 64, int NR = 1>
+// BWD (acfe_conv2d_wgrad_bnbwd): dY is not stored; the kernel stages the
+// output gradient of the BatchNormalization (+ReLU) -> Dropout that follows the
+// conv and that BN's input x, forms dY = Dropout'(a g [x sc + sh > 0] + b x + c)
+// exactly as acfe_bn_bwd_apply_ex rounds and drops it, writes it (g.fb_out: the
+// dgrad reads it next) and sums it per channel (the conv bias gradient) -- the
+// BN backward apply pass over the tensor is gone.  Each dY element is staged
+// by one workgroup of chunk 0 (the others only read it).
+template <int KB, bool UNP, int CW = 64, int NR = 1, bool BWD = false>
 __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
                 float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
+  static_assert(!(BWD && UNP), "BN backward fold: plain dY");
   constexpr int SEGW = 64, HW = SEGW + 2, HR = NR + 2;
   // CW-channel chunks (C = 16 / 32 layers: the stage-2/3 branch2b): the 8 waves
   // are WC = CW / 16 channel blocks x WK = 8 / WC slices of K; a wave's nine
@@ -3034,10 +3042,28 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   const int send = sbeg + segs_per_split < nseg ? sbeg + segs_per_split : nseg;
   const int QS = (g.Q + SEGW - 1) / SEGW;  // the last segment of a row may be partial
   const T16* zp = reinterpret_cast<const T16*>(g_zero_page);
+  // BWD: [scale | shift | a | b | c][KB] and the channel sums of this workgroup
+  __shared__ float ftab[BWD ? 5 * KB : 1];
+  __shared__ double fsum[BWD ? KB : 1];
+  if constexpr (BWD) {
+    for (int i = tid; i < 5 * KB; i += 512)
+      ftab[i] = i < KB ? g.fb_sc[i] : (i < 2 * KB ? g.fb_sh[i - KB] : g.fb_coef[i - 2 * KB]);
+    for (int i = tid; i < KB; i += 512) fsum[i] = 0.0;
+    __syncthreads();  // (read by the first sstore)
+  }
 
   u32x4 rd[DPT], rx[XPT];
   uint2 rda[UNP ? DPT : 1];  // UNP: argmax bytes + window taps, applied at the LDS store
   unsigned dpos = 0;
+  // BWD: the BN input x at the staged dY granules, the staged segment's first
+  // element index and column, and the lane's channel sums (its 8 channels
+  // cg * 8 + j are fixed: 512 is a multiple of DGR)
+  u32x4 rdx[BWD ? DPT : 1];
+  long long fbase = 0;
+  int fw0 = 0;
+  float fs[BWD ? 8 : 1];
+#pragma unroll
+  for (int j = 0; j < (BWD ? 8 : 1); ++j) fs[j] = 0.f;
   // part bit 0: the dY granules, bit 1: the input halo granules
   auto gload = [&](int sg, int part = 3) __attribute__((always_inline)) {
     // segments walk down a 64-pixel column (row fastest): consecutive steps
@@ -3062,8 +3088,14 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         dpos |= (unsigned)(((hh & 1) << 1) | (w & 1)) << (2 * i);
       } else {
         const int ro = px / SEGW, pw = px - ro * SEGW;  // row of the group, pixel of the segment
-        rd[i] = *reinterpret_cast<const u32x4*>(idx < DG && w0 + pw < g.Q
-                                                    ? dyrow + ((long long)ro * g.Q + pw) * g.K + cg * 8 : zp);
+        const long long eo = ((long long)ro * g.Q + pw) * g.K + cg * 8;
+        const bool okd = idx < DG && w0 + pw < g.Q;
+        rd[i] = *reinterpret_cast<const u32x4*>(okd ? dyrow + eo : zp);
+        if constexpr (BWD) {
+          const long long e0 = (((long long)n * g.P + h) * g.Q + w0) * g.K;
+          rdx[i] = *reinterpret_cast<const u32x4*>(okd ? g.fb_x + e0 + eo : zp);
+          if (i == 0) fbase = e0, fw0 = w0;
+        }
       }
     }
 #pragma unroll
@@ -3086,6 +3118,36 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       if constexpr (UNP) {
         if (idx < DG)
           *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i] & unpool_mask(rda[i], (dpos >> (2 * i)) & 3u);
+      } else if constexpr (BWD) {
+        // acfe_bn_bwd_apply_ex's arithmetic per element (k_bn_bwd_apply8):
+        // g masked by the BN's ReLU, a g + b x + c, rounded to bf16, then the
+        // Dropout backward of the rounded value (keep: round(v * scale))
+        const int ro = px / SEGW, pw = px - ro * SEGW;
+        const bool ok = idx < DG && fw0 + pw < g.Q;
+        const long long e = fbase + ((long long)ro * g.Q + pw) * g.K + cg * 8;
+        const f4* tb = reinterpret_cast<const f4*>(ftab + cg * 8);
+        u32x4 v;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const f4 sc = tb[d >> 1], sh = tb[KB / 4 + (d >> 1)], ca = tb[2 * (KB / 4) + (d >> 1)],
+                   cb = tb[3 * (KB / 4) + (d >> 1)], c0 = tb[4 * (KB / 4) + (d >> 1)];
+          unsigned pk = 0;
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            const int jj = (d & 1) * 2 + hf, j = 2 * d + hf;
+            const float xv = __uint_as_float(hf ? (rdx[i][d] & 0xffff0000u) : (rdx[i][d] << 16));
+            const float gv = __uint_as_float(hf ? (rd[i][d] & 0xffff0000u) : (rd[i][d] << 16));
+            const float gj = (g.fb_relu && !(__builtin_fmaf(xv, sc[jj], sh[jj]) > 0.f)) ? 0.f : gv;
+            float o = bf2f(f2bf(__builtin_fmaf(ca[jj], gj, __builtin_fmaf(cb[jj], xv, c0[jj]))));
+            if (g.drop.on) o = drop_keep(g.drop, (uint64_t)(e + j)) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
+            o = ok ? o : 0.f;
+            fs[j] += o;
+            pk |= hf ? (__float_as_uint(o) & 0xffff0000u) : (__float_as_uint(o) >> 16);
+          }
+          v[d] = pk;
+        }
+        if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = v;
+        if (ok && g.fb_out && cc == 0) *reinterpret_cast<u32x4*>(g.fb_out + e) = v;
       } else {
         if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i];
       }
@@ -3113,6 +3175,21 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   const int grp = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   typedef __attribute__((address_space(3))) bf4* lp;
 
+  // BWD: the lanes' channel sums over the 64 / DGR lanes of a wave that hold
+  // the same channels, added into the workgroup's LDS doubles (every 16
+  // segments: f32 partials of at most 16 * DPT values)
+  auto fflush = [&]() __attribute__((always_inline)) {
+    if constexpr (BWD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = fs[j];
+#pragma unroll
+        for (int m = DGR; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+        if (lane < DGR) atomicAdd(&fsum[lane * 8 + j], (double)v);
+        fs[j] = 0.f;
+      }
+    }
+  };
   if (sbeg < send) {
     gload(sbeg);
     sstore(0);
@@ -3165,8 +3242,21 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       }
     }
     if (more) sstore(buf ^ 1);
+    if constexpr (BWD) {
+      if (((sg - sbeg) & 15) == 15) fflush();
+    }
     __syncthreads();
     buf ^= 1;
+  }
+  if constexpr (BWD) {
+    // this workgroup's slab row of the channel sums (zeros for chunks > 0,
+    // whose staged values chunk 0 also summed)
+    fflush();
+    __syncthreads();
+    for (int c = tid; c < KB; c += 512) {
+      g.fb_sums[((long long)blockIdx.x * 2 + 0) * KB + c] = cc == 0 ? fsum[c] : 0.0;
+      g.fb_sums[((long long)blockIdx.x * 2 + 1) * KB + c] = 0.0;
+    }
   }
   // slab write: D[k][c] -> ws[split][k][tap * C + cc * 64 + c]
   const long long kd = 9ll * g.C;
@@ -3421,6 +3511,11 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.pro_out = nullptr;
   g.bn_sc = g.bn_sh = g.bn_mu = g.bn_is = nullptr;
   g.bn_relu = 0;
+  g.fb_x = nullptr;
+  g.fb_sc = g.fb_sh = g.fb_coef = nullptr;
+  g.fb_relu = 0;
+  g.fb_out = nullptr;
+  g.fb_sums = nullptr;
   g.idx32 = g.M * K < (1ll << 32) ? 1 : 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
@@ -3926,8 +4021,12 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
 // 256}, or C in {16, 32} with K in {128, 256}; a partial last 64-pixel column
 // segment is masked): split count within the planned workspace (`splits`),
 // returned in *used.
-static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
-                             long long splits, hipStream_t s, int* used) {
+struct HaloPlan {
+  int cw, nr, wp, nchunk, nseg, sp, per;
+  bool c16k64, k16c64;
+};
+static HaloPlan halo_plan(const ConvGeom& g, bool amax, long long splits) {
+  HaloPlan hp;
   // 16 / 32-channel layers: one chunk of C; K = 256 (wr_resnet's stage-3
   // 256 -> 256): 32-channel chunks, so the K x 9 x CW accumulators stay 36
   // tiles per wave
@@ -3956,8 +4055,37 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   sp &= ~7;
   if (sp < 8) sp = 8;
   if (sp > splits) sp = (int)splits;  // splits is a multiple of 8 (wgrad_plan)
-  const int per = (nseg + sp - 1) / sp;
+  hp.cw = cw;
+  hp.nr = nr;
+  hp.wp = wp;
+  hp.nchunk = nchunk;
+  hp.nseg = nseg;
+  hp.sp = sp;
+  hp.per = (nseg + sp - 1) / sp;
+  hp.c16k64 = c16k64;
+  hp.k16c64 = k16c64;
+  return hp;
+}
+
+static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, const uint8_t* amax, float* ws,
+                             long long splits, hipStream_t s, int* used) {
+  const HaloPlan hp = halo_plan(g, amax != nullptr, splits);
+  const int cw = hp.cw, nr = hp.nr, wp = hp.wp, nchunk = hp.nchunk, nseg = hp.nseg, sp = hp.sp, per = hp.per;
+  const bool c16k64 = hp.c16k64, k16c64 = hp.k16c64;
   const dim3 gr(nchunk * sp);
+  if (g.fb_sc) {  // acfe_conv2d_wgrad_bnbwd: the BN backward formed while staging dY
+#define WB(KB_, CW_, NR_)                                                                                       \
+  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_, NR_, true>), gr, dim3(512), 0, s, g, (const uint16_t*)x,  \
+                     (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
+    if (amax || wp != 1 && !c16k64) return ACFE_E_INVAL;
+    if (c16k64 && nr == 2) WB(64, 16, 2);
+    else if (cw == 64 && g.K == 64 && nr == 2) WB(64, 64, 2);
+    else if (cw == 64 && g.K == 32 && nr == 2) WB(32, 64, 2);
+    else return ACFE_E_INVAL;
+#undef WB
+    *used = sp * wp;
+    return launch_rc("acfe_conv2d_wgrad_bnbwd");
+  }
 #define WH(KB_, U_)                                                                                              \
   hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, U_>), gr, dim3(512), 0, s, g, (const uint16_t*)x, (const uint16_t*)dy, \
                      ws, nchunk, nseg, per, amax)
@@ -4019,6 +4147,13 @@ static int wgrad_row_halo_launch(const ConvGeom& g, const void* x, const void* d
   return launch_rc("acfe_conv2d_wgrad(row halo)");
 }
 
+static bool halo_ok(int N, int C, int K, int R, int S, int stride, int P, int Q, long long splits) {
+  return R == 3 && S == 3 && stride == 1 &&
+         ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) || (C % 64 == 0 && K == 16 && splits >= 16) ||
+          ((C == 32 && (K == 128 || K == 256)) || (C == 16 && (K == 256 || (K == 64 && splits >= 16))))) &&
+         (long long)N * P * ((Q + 63) / 64) < (1ll << 31);
+}
+
 // dW[k][r][s][c] (fp32, KRSC) = sum over pixels.  beta: dW = beta*dW + grad.
 ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy, int K, int R, int S,
                                int stride, int pad_top, int pad_left, int P, int Q, float* dw, float beta,
@@ -4034,10 +4169,7 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   ConvGeom g = make_geom(N, H, W, C, K, R, S, stride, pad_top, pad_left, P, Q, 64, 128);
   g.ldy = K;
   int rc;
-  if (dtype == ACFE_DTYPE_BF16 && R == 3 && S == 3 && stride == 1 &&
-      ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) || (C % 64 == 0 && K == 16 && splits >= 16) ||
-       ((C == 32 && (K == 128 || K == 256)) || (C == 16 && (K == 256 || (K == 64 && splits >= 16))))) &&
-      (long long)N * P * ((Q + 63) / 64) < (1ll << 31)) {
+  if (dtype == ACFE_DTYPE_BF16 && halo_ok(N, C, K, R, S, stride, P, Q, splits)) {
     // halo-staged kernel; its split count stays within the planned workspace
     int used = 0;
     rc = wgrad_halo_launch(g, x, dy, nullptr, workspace, splits, strm(stream), &used);
@@ -4065,6 +4197,62 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
   if (grid > 2048) grid = 2048;
   wgrad_combine(workspace, (int)splits, n, beta, dw, grid, strm(stream));
   return launch_rc("acfe_conv2d_wgrad(reduce)");
+}
+
+// ------------------------------------------------------------------ wgrad + BN backward apply
+// The weight gradient of a 3x3 stride-1 "same" bf16 conv whose output u feeds
+// [Dropout ->] BatchNormalization (+ReLU) (resnet/wr_resnet.py:58-71: conv2a ->
+// Dropout -> bn2b -> ReLU; resnet/wr_resnet_bird.py:139-154: conv21 -> Dropout
+// -> bn2b -> ReLU), given that BN's OUTPUT gradient gy, its input u_bn (the
+// dropped-out conv output) and its backward coefficients: the conv output
+// gradient dy = acfe_bn_bwd_apply_ex(gy, u_bn, scale, shift, relu, coef, NULL,
+// rate, seed) is formed while the wgrad stages it, written to `dy` (the dgrad
+// reads it) and summed per channel into `sums` ([rows][2][K], rows =
+// acfe_conv2d_wgrad_bnbwd_rows; the conv bias gradient via
+// acfe_channel_sum_finalize) -- the separate apply pass over the tensor is not
+// run.  Same dW as acfe_conv2d_wgrad on that dy.
+ACFE_API int acfe_conv2d_wgrad_bnbwd_rows(int N, int H, int W, int C, int K) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || K <= 0) return 0;
+  long long splits, chunk;
+  wgrad_plan((long long)N * H * W, 9 * C, K, &splits, &chunk);
+  if (!halo_ok(N, C, K, 3, 3, 1, H, W, splits)) return 0;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, 1, 1, H, W, 64, 128);
+  const HaloPlan hp = halo_plan(g, false, splits);
+  // (K = 128, one row per step: 19 VGPRs spilled -- not covered)
+  const bool ok = (hp.c16k64 && hp.nr == 2) || (hp.cw == 64 && ((K == 64 || K == 32) && hp.nr == 2));
+  return ok ? hp.nchunk * hp.sp : 0;
+}
+
+ACFE_API int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn,
+                                     int K, const float* scale, const float* shift, int relu, const float* coef,
+                                     float drop_rate, unsigned long long seed, void* dy, float* dw, float beta,
+                                     float* workspace, double* sums, void* stream) {
+  if (!x || !gy || !u_bn || !scale || !shift || !coef || !dy || !dw || !workspace || !sums || drop_rate < 0.f ||
+      drop_rate >= 1.f)
+    return ACFE_E_INVAL;
+  if (((uintptr_t)gy | (uintptr_t)u_bn | (uintptr_t)dy) & 15) return ACFE_E_INVAL;
+  const int rows = acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K);
+  if (!rows) return ACFE_E_INVAL;
+  long long splits, chunk;
+  wgrad_plan((long long)N * H * W, 9 * C, K, &splits, &chunk);
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, 1, 1, H, W, 64, 128);
+  g.ldy = K;
+  g.drop = make_drop(drop_rate, seed);
+  g.fb_x = (const uint16_t*)u_bn;
+  g.fb_sc = scale;
+  g.fb_sh = shift;
+  g.fb_coef = coef;
+  g.fb_relu = relu & 1;
+  g.fb_out = (uint16_t*)dy;
+  g.fb_sums = sums;
+  int used = 0;
+  int rc = wgrad_halo_launch(g, x, gy, nullptr, workspace, splits, strm(stream), &used);
+  if (rc) return rc;
+  const long long n = (long long)K * 9 * C;
+  int grid = cdiv((n + 3) / 4, 256);
+  if (grid > 2048) grid = 2048;
+  wgrad_combine(workspace, used, n, beta, dw, grid, strm(stream));
+  return launch_rc("acfe_conv2d_wgrad_bnbwd(reduce)");
 }
 
 // ------------------------------------------------------------------ conv + 2x2 max-pool

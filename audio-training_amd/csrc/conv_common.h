@@ -45,6 +45,20 @@ struct ConvGeom {
   const float* bn_mu;
   const float* bn_is;
   int bn_relu;
+  // k_wgrad3x3_halo BWD (acfe_conv2d_wgrad_bnbwd): the wgrad's dY is the
+  // backward of a BatchNormalization (+ReLU) -> Dropout (g.drop) whose output
+  // gradient is the kernel's dY argument and whose input is fb_x (dY's layout),
+  // formed while staging as acfe_bn_bwd_apply_ex forms it: fb_sc / fb_sh [K]
+  // (ReLU mask), fb_coef [3][K] = a, b, c (dY = a g + b x + c); the values are
+  // also stored to fb_out (for the dgrad) and summed per channel into fb_sums
+  // (slab [gridDim][2][K], the conv bias gradient)
+  const uint16_t* fb_x;
+  const float* fb_sc;
+  const float* fb_sh;
+  const float* fb_coef;
+  int fb_relu;
+  uint16_t* fb_out;
+  double* fb_sums;
 };
 
 // XCD-aware walk over the M tiles of a persistent grid.  Workgroups are

@@ -258,6 +258,9 @@ ACFE_API int acfe_normalize_apply(const float* x, int64_t cs, int batch, int n, 
 __global__ void k_mixup(const float* __restrict__ x1, const float* __restrict__ s1,
                         const float* __restrict__ x2, const float* __restrict__ s2,
                         const float* __restrict__ lam, int n, float* __restrict__ y) {
+  // tfdataset.py:950 is two products and a sum, each rounded (TF ops, no
+  // fusion): without this the a * l + (c * l1) pair contracts to an FMA
+#pragma clang fp contract(off)
   const int b = blockIdx.y;
   const float l = lam[b];
   const float l1 = __fsub_rn(1.0f, l);
@@ -266,7 +269,10 @@ __global__ void k_mixup(const float* __restrict__ x1, const float* __restrict__ 
     float a = x1[o], c = x2[o];
     if (s1) a = norm1(a, s1[2 * b], s1[2 * b + 1]);
     if (s2) c = norm1(c, s2[2 * b], s2[2 * b + 1]);
-    y[o] = __fadd_rn(__fmul_rn(a, l), __fmul_rn(c, l1));  // tfdataset.py:950
+    // (plain operators: the contraction state of __fmul_rn / __fadd_rn is
+    // their header's, where the pair still fuses)
+    const float p1 = a * l, p2 = c * l1;
+    y[o] = p1 + p2;  // tfdataset.py:950
   }
 }
 

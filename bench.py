@@ -153,7 +153,7 @@ def dominant_evidence(key: str, same_shape: bool):
     the earlier rounds' unsuffixed files.  Only used when this run has the
     measured launch shape (same_shape)."""
     if not same_shape:
-        return None, None
+        return None, None, None
     prof = ROOT / "profiles"
 
     def newest(kind):
@@ -162,11 +162,16 @@ def dominant_evidence(key: str, same_shape: bool):
             names += [f"{kind}_r03.json", f"{kind}_r02b.json"]
         return next((prof / n for n in names if (prof / n).exists()), None)
 
-    traffic = counters = None
+    traffic = counters = src = None
     pmc = newest("pmc_dominant")
     if pmc is not None:
         try:
-            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            d = json.loads(pmc.read_text())
+            traffic = d.get("hbm_bytes_per_launch")
+            # replayed from the committed PMC fold (rocprofv3 --pmc cannot run
+            # inside this timed process): its file and the tree it measured
+            src = {"file": f"profiles/{pmc.name}", "commit": d.get("commit"),
+                   "over_algorithmic": d.get("traffic_over_algorithmic")}
         except ValueError:
             traffic = None
     sq = newest("sq_dominant")
@@ -176,9 +181,10 @@ def dominant_evidence(key: str, same_shape: bool):
             counters = {k: d[k] for k in ("mfma_busy_per_simd", "wave_time_waiting", "valu_insts_per_mfma",
                                           "lds_bank_conflict_share")}
             counters["source"] = f"profiles/{sq.name}"
+            counters["commit"] = d.get("commit")
         except (ValueError, KeyError):
             counters = None
-    return traffic, counters
+    return traffic, src, counters
 
 
 def main():
@@ -191,6 +197,8 @@ def main():
     ap.add_argument("--model", choices=["bird", "wrn"], default="bird")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", dest="extra", action="store_false",
+                    help="skip the secondary workloads (wr_resnet training, configs I and S) of the default run")
     ap.add_argument("--cpu-batch", type=int, default=8)
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--clips", type=int, default=4096, help="e2e: clips written to the TFRecord set")
@@ -203,7 +211,8 @@ def main():
     if a.workload == "e2e":
         return run_e2e(a)
     if a.workload != "train":
-        return run_inference(a)
+        print(json.dumps(run_inference(a)), flush=True)
+        return 0
 
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # `bench.py --gpus N` started directly: one process per GPU under
@@ -227,28 +236,70 @@ def main():
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     from acfe import ops
-    from acfe.train import FrontEnd, Trainer
 
     ops.set_seed_rank(rank)  # per-replica dropout masks
-
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    if a.model == "bird":
+    out, _ = train_line(a.model, dtype, a.classes, a.batch, a.steps, a.warmup, rank, world, dev, dist)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps, a.model, a.classes)
+        suite = ROOT / "profiles" / "r02_cpu_baseline.json"
+        if suite.exists():  # the other workloads' CPU rows (tools/cpu_baseline.py, same host type)
+            try:
+                out["cpu_baseline"]["suite"] = {"source": "profiles/r02_cpu_baseline.json",
+                                                **json.loads(suite.read_text())["rows"]}
+            except (ValueError, KeyError):
+                pass
+    if rank == 0 and world == 1 and a.extra and a.model == "bird" and a.dtype == "bf16" and a.batch == 512:
+        # the secondary workloads of BASELINE.json at reduced step counts, so
+        # the driver's own run observes them: the metric's named model
+        # (wr_resnet training, T1 shape), config I and config S
+        torch.cuda.empty_cache()
+        w, _ = train_line("wrn", torch.bfloat16, 2, 512, 5, 2, 0, 1, dev, dist)
+        out["wrn"] = _summary(w)
+        torch.cuda.empty_cache()
+        out["infer"] = _summary(run_inference(a, workload="infer", steps=5, warmup=2, emit=False))
+        torch.cuda.empty_cache()
+        out["stream"] = _summary(run_inference(a, workload="stream", steps=2, warmup=1, emit=False))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _summary(o):
+    """The fields of a secondary workload's line kept in the main line."""
+    keep = ("metric", "value", "unit", "ms_per_step", "ms_per_step_median", "steps", "warmup", "dtype", "config",
+            "roofline", "mel_pipeline", "model_tflops_fwd_bwd", "final_loss")
+    r = {k: o[k] for k in keep if k in o}
+    if "roofline" in r:
+        r["roofline"] = {k: v for k, v in r["roofline"].items() if k != "kernel"}
+    return r
+
+
+def train_line(model_name, dtype, classes, batch, steps, warmup, rank, world, dev, dist):
+    """Time `steps` training steps (after `warmup`) of model_name on HBM-resident
+    synthetic batches; returns (the bench line without cpu_baseline, trainer)."""
+    from acfe import ops
+    from acfe.train import FrontEnd, Trainer
+
+    if model_name == "bird":
         from resnet.wr_resnet_bird import WRResNet, flops_per_clip
     else:
         from resnet.wr_resnet import WRResNet
         flops_per_clip = None
     torch.manual_seed(1234 + rank)
-    model = WRResNet(input_shape=(128, 513, 3), classes=a.classes, dtype=dtype).to(dev)
+    model = WRResNet(input_shape=(128, 513, 3), classes=classes, dtype=dtype).to(dev)
     if world > 1:  # replicas start from rank 0's weights
         with torch.no_grad():
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, 0)
     frontend = FrontEnd(n_mels=128, dtype=dtype, device=dev).to(dev)
     trainer = Trainer(model, frontend, lr=0.01, loss="cce", device=dev)
-    sets = make_batches(a.batch, a.classes, dev, n_sets=2, seed=rank)
+    sets = make_batches(batch, classes, dev, n_sets=2, seed=rank)
 
     # dominant kernel: stage-1 block-0 3x3 conv (128 -> 128 ch at 128 x 256)
-    target = model.blocks[0].conv21 if a.model == "bird" else model.blocks[1].conv2a
+    target = model.blocks[0].conv21 if model_name == "bird" else model.blocks[1].conv2a
     K, R, S, C = target.weight.shape
     events: list = []
     mel_events: list = []
@@ -257,7 +308,7 @@ def main():
         x1, x2, lam, y = sets[i % len(sets)]
         return trainer.step(x1, y, x2, lam)
 
-    for i in range(a.warmup):
+    for i in range(warmup):
         step(i)
     torch.cuda.synchronize()
     ops.watch_conv(target.weight, events)
@@ -267,17 +318,17 @@ def main():
     torch.cuda.synchronize()
     # per-step HIP events on the launch stream (no host sync inside the
     # timed region): the median step time is reported beside the mean
-    sev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+    sev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
     sev[0].record()
-    for i in range(a.steps):
+    for i in range(steps):
         loss, _ = step(i)
         sev[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    step_ms = [sev[i].elapsed_time(sev[i + 1]) for i in range(a.steps)]
+    step_ms = [sev[i].elapsed_time(sev[i + 1]) for i in range(steps)]
     ops.watch_conv(target.weight, None)
     frontend.timer = None
     own = elapsed
@@ -290,7 +341,7 @@ def main():
         elapsed = max(per_rank)
     loss_v = float(loss.item())
     if rank != 0:  # each rank's own line, on stderr (stdout carries rank 0's one JSON line)
-        print(f"bench rank {rank}/{world}: {a.batch * a.steps / own:.1f} clips/s, {own / a.steps * 1e3:.3f} ms/step, "
+        print(f"bench rank {rank}/{world}: {batch * steps / own:.1f} clips/s, {own / steps * 1e3:.3f} ms/step, "
               f"loss {loss_v:.5f}", file=sys.stderr, flush=True)
 
     def avg_ms(kind, evs):
@@ -300,22 +351,23 @@ def main():
     fwd_ms, dgrad_ms, wgrad_ms = avg_ms("fwd", events), avg_ms("dgrad", events), avg_ms("wgrad", events)
     mel_ms = avg_ms("mel", mel_events)
     H_t = 128
-    W_t = 256 if a.model == "bird" else 513
-    flops_launch = 2.0 * a.batch * H_t * W_t * K * R * S * C
+    W_t = 256 if model_name == "bird" else 513
+    flops_launch = 2.0 * batch * H_t * W_t * K * R * S * C
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
-    key = ("t1" if a.model == "bird" else "wrn") + ("" if dtype == torch.bfloat16 else "_fp32")
-    traffic, counters = dominant_evidence(key, a.batch == 512)
-    clips = world * a.batch * a.steps
+    key = ("t1" if model_name == "bird" else "wrn") + ("" if dtype == torch.bfloat16 else "_fp32")
+    traffic, tsrc, counters = dominant_evidence(key, batch == 512)
+    clips = world * batch * steps
     value = clips / elapsed
+    bird = model_name == "bird"
     out = {
         "metric": "clips/sec training (3s@48kHz, wr_resnet) at 1/2/4/8 GPU; mel pipeline GB/s",
         "value": round(value, 2),
         "unit": "clips/s",
         "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 3),
         "ms_per_step_median": round(float(np.median(step_ms)), 3),
         "higher_is_better": True,
         "scaling": "weak",
@@ -323,10 +375,10 @@ def main():
         "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
         "data": "synthetic (SURVEY 8d chirps+noise, resident in HBM; random-init weights)",
         "config": {
-            "workload": f"T1 training step: normalize/mix_up/STFT-mel/PCEN + {'wr_resnet_bird' if a.model == 'bird' else 'wr_resnet'} fwd/bwd + Adam",
-            "model": "wr_resnet_bird" if a.model == "bird" else "wr_resnet",
-            "input": [128, 513, 3], "classes": a.classes, "global_batch": world * a.batch,
-            "batch_per_gpu": a.batch, "seq_len": 513, "parallelism": f"dp{world}",
+            "workload": f"T1 training step: normalize/mix_up/STFT-mel/PCEN + {'wr_resnet_bird' if bird else 'wr_resnet'} fwd/bwd + Adam",
+            "model": "wr_resnet_bird" if bird else "wr_resnet",
+            "input": [128, 513, 3], "classes": classes, "global_batch": world * batch,
+            "batch_per_gpu": batch, "seq_len": 513, "parallelism": f"dp{world}",
             "loss": "categorical_crossentropy", "optimizer": "adam(lr=0.01)",
         },
         "roofline": {
@@ -334,10 +386,10 @@ def main():
                 "(k_conv_fwd_g<float,128,BN>: fp32 implicit-im2col GEMM on v_mfma_f32_16x16x4f32, LDS-staged tiles)"
                 if dtype != torch.bfloat16 else
                 "(k_conv3x3_1w<1,2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)"
-                if a.model == "bird" else
+                if bird else
                 "(k_conv3x3_rows<64,8,4,true,true>: bn2a + ReLU applied while staging the input rows, dropout + BN sums epilogue; 8 rows x 64 px x 64 ch per workgroup of 8 waves)"),
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": traffic,
+            "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
             "counters": counters,
             "dgrad_ms": round(dgrad_ms, 4), "wgrad_ms": round(wgrad_ms, 4),
@@ -347,12 +399,12 @@ def main():
         "mel_pipeline": {
             "kernel": "k_mel_w3 (two waves per frame: frame+Hann+4096 rFFT+|X|^2+banded mel)",
             "avg_launch_ms": round(mel_ms, 4),
-            "GBps": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2),
-            "hbm_frac": round(a.batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9 / MI355X_PEAK_HBM_GBS, 4),
+            "GBps": round(batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2),
+            "hbm_frac": round(batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9 / MI355X_PEAK_HBM_GBS, 4),
             "bytes_per_clip": FRONTEND_BYTES_PER_CLIP,
             # 68.87 MFLOP per clip (FFT + power + banded mel), fp32 VALU peak 157.3 TFLOP/s
-            "valu_tflops": round(a.batch * 68.87e6 / (mel_ms * 1e-3) / 1e12, 2),
-            "valu_frac": round(a.batch * 68.87e6 / (mel_ms * 1e-3) / 1e12 / 157.3, 4),
+            "valu_tflops": round(batch * 68.87e6 / (mel_ms * 1e-3) / 1e12, 2),
+            "valu_frac": round(batch * 68.87e6 / (mel_ms * 1e-3) / 1e12 / 157.3, 4),
         },
         "per_rank_s": [round(v, 4) for v in per_rank],
         "grad_allreduce": ({"buckets": len(trainer.buckets.buckets), "bucket_bytes": 4 << 20,
@@ -361,20 +413,7 @@ def main():
         "model_tflops_fwd_bwd": round(3 * (flops_per_clip(model) if flops_per_clip else 64.956e9) * value / 1e12, 2),
         "final_loss": round(loss_v, 5),
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps, a.model, a.classes)
-        suite = ROOT / "profiles" / "r02_cpu_baseline.json"
-        if suite.exists():  # the other workloads' CPU rows (tools/cpu_baseline.py, same host type)
-            try:
-                out["cpu_baseline"]["suite"] = {"source": "profiles/r02_cpu_baseline.json",
-                                                **json.loads(suite.read_text())["rows"]}
-            except (ValueError, KeyError):
-                pass
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    return out, trainer
 
 
 def launch_ranks(n: int) -> int:
@@ -505,24 +544,36 @@ def run_e2e(a):
     print(json.dumps(out), flush=True)
 
 
-def run_inference(a):
+def run_inference(a, workload=None, steps=None, warmup=None, emit=True):
     """Configs I and S of BASELINE.json (one GPU; shards over ranks with no
-    collective, so only the single-GPU replica is measured here).
+    collective, so only the single-GPU replica is measured here).  Returns the
+    line.  `workload` given (the default run's secondary lines): the config's
+    own settings, not the command line's.
 
     I: fused normalize/STFT/mel/PCEN + wr_resnet forward, batch 256, fp32.
     S: one 60-min 48 kHz recording resident in HBM, 3 s windows every 1.5 s
        read in place by the front-end kernel (centred STFT, constant padding as
        predict_utils.get_spect), PCEN per window batch, model forward, sigmoid;
-       batch 1024 windows.  A step = the whole recording."""
+       batch 1024 windows, fp32 (the reference default).  A step = the whole
+       recording."""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     from acfe import ops
     from acfe.train import FrontEnd
 
-    stream = a.workload == "stream"
-    model_name = a.model if (stream or "--model" in sys.argv) else "wrn"
-    dtype = torch.float32 if (a.dtype == "fp32" or ("--dtype" not in sys.argv and not stream)) else torch.bfloat16
-    classes = a.classes if "--classes" in sys.argv else (2 if model_name == "wrn" else 50)
+    if workload is None:  # command line
+        stream = a.workload == "stream"
+        model_name = a.model if (stream or "--model" in sys.argv) else "wrn"
+        dtype = torch.float32 if (a.dtype == "fp32" or ("--dtype" not in sys.argv and not stream)) else torch.bfloat16
+        classes = a.classes if "--classes" in sys.argv else (2 if model_name == "wrn" else 50)
+        bs_arg = a.batch if "--batch" in sys.argv else None
+        steps, warmup = a.steps, a.warmup
+    else:
+        stream = workload == "stream"
+        model_name = "bird" if stream else "wrn"
+        dtype = torch.float32
+        classes = 50 if stream else 2
+        bs_arg = None
     if model_name == "bird":
         from resnet.wr_resnet_bird import WRResNet
     else:
@@ -537,7 +588,7 @@ def run_inference(a):
         sr, n, hop = 48000, 144000, 72000
         rec = torch.from_numpy(np.tile(synth_bank(8, seed=4242).reshape(-1), 1500)[: 60 * 60 * sr].copy()).to(dev)
         n_win = 1 + (rec.numel() - n) // hop
-        bs = 1024 if "--batch" not in sys.argv else a.batch
+        bs = bs_arg or 1024
 
         @torch.no_grad()
         def step(i):
@@ -548,21 +599,21 @@ def run_inference(a):
             return outs
         units = n_win
     else:
-        bs = 256 if "--batch" not in sys.argv else a.batch
+        bs = bs_arg or 256
         x = make_batches(bs, classes, dev, n_sets=1)[0][0]
 
         @torch.no_grad()
         def step(i):
             return ops.sigmoid(model(frontend(x)))
         units = bs
-    for i in range(a.warmup):
+    for i in range(warmup):
         step(i)
     torch.cuda.synchronize()
     ops.watch_conv(target.weight, events)
     frontend.timer = mel_events
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
+    for i in range(steps):
         step(i)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -580,14 +631,14 @@ def run_inference(a):
     flops_launch = 2.0 * avg_clips * H_t * W_t * K * R * S * C
     peak = MI355X_PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else MI355X_PEAK_FP32_TFLOPS
     ach = flops_launch / (fwd_ms * 1e-3) / 1e12
-    value = units * a.steps / elapsed
+    value = units * steps / elapsed
     key = ("stream" if stream else "infer") + ("_fp32" if dtype == torch.float32 else "_bf16")
-    traffic, counters = dominant_evidence(key, bs == (1024 if stream else 256))
+    traffic, tsrc, counters = dominant_evidence(key, bs == (1024 if stream else 256))
     out = {
         "metric": ("windows/sec streaming inference (60-min 48 kHz recording, 3 s / 1.5 s windows)" if stream
                    else "clips/sec inference (3s@48kHz, front end + PCEN + wr_resnet fwd)"),
         "value": round(value, 2), "unit": "windows/s" if stream else "clips/s", "n_gpus": 1,
-        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
         "data": "synthetic (SURVEY 8d chirps+noise, resident in HBM; random-init weights)",
@@ -597,12 +648,12 @@ def run_inference(a):
                    "units_per_step": units, "batch": bs},
         "roofline": {"kernel": f"conv2d_fwd {R}x{S} {C}->{K} @ {H_t}x{W_t}", "bound": "mfma",
                      "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                     "traffic": traffic, "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,
-                     "counters": counters},
+                     "traffic": traffic, "traffic_source": tsrc, "avg_launch_ms": round(fwd_ms, 4),
+                     "flops_per_launch": flops_launch, "counters": counters},
         "mel_pipeline": {"avg_launch_ms": round(mel_ms, 4),
                          "GBps": round(avg_clips * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2)},
     }
-    print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":

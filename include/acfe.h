@@ -240,6 +240,23 @@ long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K, int R, 
 int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy, int K, int R, int S,
                       int stride, int pad_top, int pad_left, int P, int Q, float* dw, float beta, int dtype,
                       float* workspace, void* stream);
+/* The wgrad of a bf16 3x3 stride-1 "same" conv whose output feeds [Dropout ->]
+ * BatchNormalization (+ReLU) -- resnet/wr_resnet.py:58-71 (conv2a -> Dropout ->
+ * bn2b -> ReLU), resnet/wr_resnet_bird.py:139-154 (conv21 -> Dropout -> bn2b)
+ * -- taking that BN's OUTPUT gradient gy and its input u_bn: the conv output
+ * gradient dy = acfe_bn_bwd_apply_ex(gy, u_bn, scale, shift, relu, coef, NULL,
+ * drop_rate, seed, ...) is formed while the wgrad stages it (no separate apply
+ * pass over the tensor), written to dy (bit-identical to the apply pass's;
+ * the dgrad reads it next) and summed per channel into sums
+ * [acfe_conv2d_wgrad_bnbwd_rows][2][K] (finalize with
+ * acfe_channel_sum_finalize: the conv bias gradient).  dw / beta / workspace as
+ * acfe_conv2d_wgrad.  _rows: 0 when the shape is not covered (then
+ * acfe_bn_bwd_apply_ex + acfe_conv2d_wgrad). */
+int acfe_conv2d_wgrad_bnbwd_rows(int N, int H, int W, int C, int K);
+int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn, int K,
+                            const float* scale, const float* shift, int relu, const float* coef, float drop_rate,
+                            unsigned long long seed, void* dy, float* dw, float beta, float* workspace,
+                            double* sums, void* stream);
 
 /* Stem convolution with one (folded) input channel and 16 outputs ("same",
  * stride 1, R = S = 5 (wr_resnet_bird) or 3 (wr_resnet)): the three identical

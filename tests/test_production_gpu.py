@@ -835,3 +835,116 @@ def test_conv_dgrad_bn_reduce_fused(env, cuda, N, H, W, C, K, relu):
     scale_ = ref.abs().amax(1, keepdim=True).clamp_min(1.0)
     assert ((s1 - s0).abs() / scale_).max().item() < 1e-6, ((s1 - s0).abs() / scale_).max()
     assert ((s1 - ref).abs() / scale_).max().item() < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,C,K,rate,relu", [(4, 128, 513, 64, 64, 0.1, 1), (8, 64, 128, 64, 64, 0.1, 1),
+                                                 (2, 128, 513, 16, 64, 0.1, 1), (4, 32, 64, 128, 32, 0.1, 1),
+                                                 (3, 14, 100, 64, 64, 0.0, 1), (2, 20, 70, 64, 64, 0.1, 0),
+                                                 (2, 16, 64, 192, 64, 0.1, 1)],
+                         ids=["wrn-s1-2a", "bird-s1-21", "wrn-s1b0-2a-c16", "bird-s2-21-k32", "partial-nodrop",
+                              "norelu", "3chunks"])
+def test_conv_wgrad_bnbwd_fused(env, cuda, N, H, W, C, K, rate, relu):
+    """acfe_conv2d_wgrad_bnbwd (the BN backward apply of Conv2D -> Dropout ->
+    BatchNormalization -> ReLU, resnet/wr_resnet.py:58-71 and
+    resnet/wr_resnet_bird.py:139-154, formed while the halo wgrad stages its
+    dY) against the unfused chain acfe_bn_bwd_apply_ex -> acfe_conv2d_wgrad +
+    the apply pass's channel sums: the conv output gradient bit-identical, dW
+    bit-identical (same staged values, same kernel and split), the bias sums
+    within 1e-6 of the sum of |dy| (f32 partials of 16 segments vs per-element
+    doubles).  Shapes: wr_resnet stage-1 (128 x 513, C = 64 and the C = 16
+    block-0 conv2a), wr_resnet_bird stage 1 / stage-2 K = 32, a partial last
+    column segment, no dropout, no ReLU, three chunks of C (only chunk 0's
+    workgroups store and sum)."""
+    ops, call, lib, ptr, stream = env
+    srows = lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K)
+    assert srows > 0
+    g = torch.Generator().manual_seed(41 + H + C)
+    x = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
+    gy = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+    u = (torch.randn((N, H, W, K), generator=g) * 1.5).to(BF).to(cuda)
+    sc = ((torch.rand(K, generator=g) + 0.5) * torch.where(torch.rand(K, generator=g) < 0.2, -1.0, 1.0)).to(cuda)
+    sh = (torch.randn(K, generator=g) * 0.3).to(cuda)
+    coef = (torch.randn(3 * K, generator=g) * 0.5).to(cuda)
+    rows = N * H * W
+    seed = 12345
+    # unfused chain
+    dy0 = torch.full((N, H, W, K), float("nan"), dtype=BF, device=cuda)
+    nr = lib.acfe_reduce_blocks(rows)
+    sums0 = torch.empty((nr, 2, K), dtype=F64, device=cuda)
+    call("acfe_bn_bwd_apply_ex", ptr(gy), 1, ptr(u), 1, rows, K, ptr(sc), ptr(sh), relu, ptr(coef), None, rate,
+         seed, ptr(dy0), 1, ptr(sums0), stream())
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+    dw0 = torch.empty((K, 3, 3, C), device=cuda)
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dy0), K, 3, 3, 1, 1, 1, H, W, ptr(dw0), 0.0, 1, ptr(ws),
+         stream())
+    db0 = torch.empty((K,), device=cuda)
+    call("acfe_channel_sum_finalize", ptr(sums0), nr, K, 0.0, ptr(db0), stream())
+    # fused
+    dy1 = torch.full((N, H, W, K), float("nan"), dtype=BF, device=cuda)
+    dw1 = torch.full((K, 3, 3, C), float("nan"), device=cuda)
+    sums1 = torch.full((srows, 2, K), float("nan"), dtype=F64, device=cuda)
+    ws1 = torch.empty_like(ws)
+    call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(gy), ptr(u), K, ptr(sc), ptr(sh), relu, ptr(coef),
+         rate, seed, ptr(dy1), ptr(dw1), 0.0, ptr(ws1), ptr(sums1), stream())
+    db1 = torch.empty((K,), device=cuda)
+    call("acfe_channel_sum_finalize", ptr(sums1), srows, K, 0.0, ptr(db1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dy1.view(torch.int16), dy0.view(torch.int16)), "conv output gradient"
+    assert torch.equal(dw1, dw0), ((dw1 - dw0).abs().max(), dw0.abs().max())
+    scale_ = dy0.float().abs().sum((0, 1, 2)).clamp_min(1.0)
+    assert ((db1 - db0).abs() / scale_).max().item() < 1e-6
+    ref = dy0.cpu().to(F64).sum((0, 1, 2))
+    assert ((db1.cpu().to(F64) - ref).abs() / scale_.cpu().to(F64)).max().item() < 1e-6
+    # accumulate into an existing dW (beta 1, the arena path)
+    dw2 = dw0.clone()
+    call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(gy), ptr(u), K, ptr(sc), ptr(sh), relu, ptr(coef),
+         rate, seed, ptr(dy1), ptr(dw2), 1.0, ptr(ws1), ptr(sums1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dw2, dw0 + dw0)
+
+
+@pytest.mark.parametrize("model_name", ["bird", "wrn"])
+def test_model_bn_bwd_fold_matches_unfused(env, cuda, model_name):
+    """A training step with the Conv2D -> Dropout -> BN backward apply inside
+    the wgrad (ops.FUSE_BN_BWD) against the separate apply pass: identical
+    loss and logits, every parameter gradient bit-identical except the biases
+    of the folded convs (their channel sums are added in another order: within
+    1e-5 of max |grad|)."""
+    ops = env[0]
+    from acfe.train import FrontEnd, Trainer
+    import bench
+
+    outs = []
+    old = ops.FUSE_BN_BWD
+    try:
+        for f in (False, True):
+            ops.FUSE_BN_BWD = f
+            torch.manual_seed(0)
+            if model_name == "bird":
+                from resnet.wr_resnet_bird import WRResNet
+                model = WRResNet(input_shape=(128, 513, 3), classes=10, dtype=BF).to(cuda)
+            else:
+                from resnet.wr_resnet import WRResNet
+                model = WRResNet(input_shape=(128, 513, 1), classes=10, dtype=BF).to(cuda)
+            fe = FrontEnd(n_mels=128, dtype=BF, device=cuda).to(cuda)
+            tr = Trainer(model, fe, lr=0.0, loss="cce", device=cuda)
+            x1, x2, lam, y = bench.make_batches(4, 10, cuda, n_sets=1)[0]
+            ops._seed_counter = itertools.count()  # same dropout seeds in both runs
+            loss, z = tr.step(x1, y, x2, lam)
+            torch.cuda.synchronize()
+            names = [n for n, p in tr.holder.named_parameters() if p.requires_grad]
+            outs.append((loss.detach().clone(), z.detach().clone(), tr.arena.grad.detach().clone()))
+    finally:
+        ops.FUSE_BN_BWD = old
+    (l0, z0, g0), (l1, z1, g1) = outs
+    assert torch.equal(l0, l1) and torch.equal(z0, z1)
+    nbias = 0
+    for n, (o, k) in zip(names, tr.arena.offsets):
+        a, b = g0[o:o + k], g1[o:o + k]
+        if torch.equal(a, b):
+            continue
+        # only conv biases may differ (summation order of the folded channel sums)
+        assert n.endswith("bias") and "bn" not in n, n
+        assert ((a - b).abs().max() / a.abs().max().clamp_min(1e-30)).item() < 1e-5, n
+        nbias += 1
+    assert nbias > 0, "no conv bias differed: was the fold exercised?"

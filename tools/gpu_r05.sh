@@ -47,6 +47,9 @@ for w in "$@"; do
     sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
     ptk) step ptk 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$PTK" ;;
+    ptka) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$PTK" > $O/ptka.log 2>&1
+          rc=$?; echo "== ptka rc=$rc"; grep -E "PASSED|FAILED|ERROR|passed|failed" $O/ptka.log | tail -40
+          case $rc in 0|1|5) ;; *) exit $rc ;; esac ;;
     convtests) step convtests 600 python -u -m pytest tests/test_production_gpu.py tests/test_fused_gpu.py \
                  tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     fusetests) step fusetests 600 python -u -m pytest tests/test_production_gpu.py -m gpu -k "reduce_fus" -x -v \

@@ -44,7 +44,12 @@ def main():
     if len(sys.argv) > 8 and sys.argv[8]:
         SELECT = tuple(int(v) for v in sys.argv[8].split(":"))
     algo = float(algo)
-    prof = Path(__file__).resolve().parent.parent / "profiles"
+    root = Path(__file__).resolve().parent.parent
+    prof = root / "profiles"
+    # the tree the counters were measured on (tools/gpurun.sh writes it before
+    # the snapshot travels: the GPU box has no .git)
+    bc = root / "BUILD_COMMIT"
+    commit = bc.read_text().strip() if bc.exists() else None
     traffic = {}
     for i, c in ((0, "FETCH_SIZE"), (1, "WRITE_SIZE")):
         v = dispatches(f"{d}/p{i}", rx)
@@ -57,7 +62,8 @@ def main():
                      "(tools/pmc_evidence.sh)",
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
            "algorithmic_bytes_per_launch": algo, "traffic_over_algorithmic": (fetch + write) / algo,
-           "raw": traffic, "corrections": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB->B"}
+           "raw": traffic, "corrections": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB->B",
+           "commit": commit}
     (prof / f"pmc_dominant_{key}_{rnd}.json").write_text(json.dumps(pmc, indent=1) + "\n")
     c = {}
     for i in (2, 3):
@@ -72,7 +78,7 @@ def main():
           "valu_insts_per_mfma": round(c.get("SQ_INSTS_VALU", 0) / max(c.get("SQ_INSTS_MFMA", 1), 1), 3),
           "valu_insts_per_wave": round(c.get("SQ_INSTS_VALU", 0) / max(c.get("SQ_WAVES", 1), 1), 1),
           "lds_bank_conflict_share": round(c.get("SQ_LDS_BANK_CONFLICT", 0) / max(c.get("SQ_LDS_IDX_ACTIVE", 1), 1), 3),
-          "raw": c}
+          "raw": c, "commit": commit}
     (prof / f"sq_dominant_{key}_{rnd}.json").write_text(json.dumps(sq, indent=1) + "\n")
     print(json.dumps({"traffic": pmc["hbm_bytes_per_launch"], "over_algo": round(pmc["traffic_over_algorithmic"], 3),
                       **{k: sq[k] for k in ("mfma_busy_per_simd", "wave_time_waiting", "valu_insts_per_mfma",
