@@ -121,6 +121,20 @@ __device__ __forceinline__ uint32_t drop_pair_hash32(const Drop& d, uint32_t e) 
   return hash_u32_lo(d.seed, e >> 1);
 }
 __device__ __forceinline__ uint32_t drop_pair_hash(const Drop& d, uint64_t e) { return hash_u32(d.seed, e >> 1); }
+// Dropout of 8 consecutive elements from the even flat index e0: the 4 pair
+// hashes of drop_keep's mask (one hash_u32 per element pair instead of per
+// element, and the 32-bit form when every index is < 2^32 -- i32, uniform):
+// the hashes' three 32-bit multiplies made the dropout passes VALU-bound
+template <typename T>
+__device__ __forceinline__ void drop_apply8(const Drop& d, uint64_t e0, bool i32, float (&v)[8]) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const uint64_t e = e0 + 2 * p;
+    const uint32_t h = i32 ? hash_u32_lo(d.seed, (uint32_t)(e >> 1)) : hash_u32(d.seed, e >> 1);
+    v[2 * p] = (h & 0xFFFFu) >= d.thr ? rnd(v[2 * p] * d.scl, T()) : 0.f;
+    v[2 * p + 1] = (h >> 16) >= d.thr ? rnd(v[2 * p + 1] * d.scl, T()) : 0.f;
+  }
+}
 template <typename T>
 __device__ __forceinline__ float drop_apply32(const Drop& d, uint32_t idx, float v) {
   const uint32_t h = hash_u32_lo(d.seed, idx >> 1);

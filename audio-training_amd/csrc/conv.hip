@@ -3131,6 +3131,12 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         for (int d = 0; d < 4; ++d) {
           const f4 sc = tb[d >> 1], sh = tb[KB / 4 + (d >> 1)], ca = tb[2 * (KB / 4) + (d >> 1)],
                    cb = tb[3 * (KB / 4) + (d >> 1)], c0 = tb[4 * (KB / 4) + (d >> 1)];
+          // one pair hash per dword (channels 2d, 2d + 1; e is even)
+          uint32_t hh = 0;
+          if (g.drop.on) {
+            const uint64_t ep = (uint64_t)(e + 2 * d);
+            hh = g.idx32 ? hash_u32_lo(g.drop.seed, (uint32_t)(ep >> 1)) : hash_u32(g.drop.seed, ep >> 1);
+          }
           unsigned pk = 0;
 #pragma unroll
           for (int hf = 0; hf < 2; ++hf) {
@@ -3139,7 +3145,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
             const float gv = __uint_as_float(hf ? (rd[i][d] & 0xffff0000u) : (rd[i][d] << 16));
             const float gj = (g.fb_relu && !(__builtin_fmaf(xv, sc[jj], sh[jj]) > 0.f)) ? 0.f : gv;
             float o = bf2f(f2bf(__builtin_fmaf(ca[jj], gj, __builtin_fmaf(cb[jj], xv, c0[jj]))));
-            if (g.drop.on) o = drop_keep(g.drop, (uint64_t)(e + j)) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
+            if (g.drop.on) o = ((hf ? hh >> 16 : hh & 0xFFFFu) >= g.drop.thr) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
             o = ok ? o : 0.f;
             fs[j] += o;
             pk |= hf ? (__float_as_uint(o) & 0xffff0000u) : (__float_as_uint(o) >> 16);

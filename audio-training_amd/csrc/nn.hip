@@ -575,6 +575,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
   }
   __syncthreads();
   const unsigned CV = C >> 3;
+  const bool i32 = (uint64_t)nvec * 8 <= (1ull << 32);  // every element index < 2^32
   double sa[8], sb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
@@ -607,7 +608,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
     }
     if (drop.on) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = drop_apply<TO>(drop, (uint64_t)v * 8 + j, rnd(o[j], TO()));
+      for (int j = 0; j < 8; ++j) o[j] = rnd(o[j], TO());
+      drop_apply8<TO>(drop, (uint64_t)v * 8, i32, o);
     }
     st8(dx + (size_t)v * 8, o);
     if (sum_part) {
@@ -1055,10 +1057,7 @@ __global__ void __launch_bounds__(256) k_maxpool8x(const T* __restrict__ x, int 
         for (int j = 0; j < 8; ++j)
           if (f[j] > m[j]) m[j] = f[j], am[j] = a * KW + b;
       }
-    if (drop.on) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = drop_apply<T>(drop, (uint64_t)v * 8 + j, m[j]);
-    }
+    if (drop.on) drop_apply8<T>(drop, (uint64_t)v * 8, (uint64_t)total * 8 <= (1ull << 32), m);
     st8(y + (size_t)v * 8, m);
     if (amax) {
       uint2 pk;
@@ -1095,10 +1094,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd8i(const uint8_t* __restrict
     const int n = (int)(t / P);
     float g[8];
     ld8(dy + (size_t)v * 8, g);
-    if (drop.on) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = drop_apply<T>(drop, (uint64_t)v * 8 + j, g[j]);
-    }
+    if (drop.on) drop_apply8<T>(drop, (uint64_t)v * 8, (uint64_t)total * 8 <= (1ull << 32), g);
     const uint2 pk = *reinterpret_cast<const uint2*>(amax + (size_t)v * 8);
     int am[8];
 #pragma unroll

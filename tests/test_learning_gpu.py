@@ -12,8 +12,18 @@ Trainer.predict (eval-mode BN).  This is the behavioural check that the whole
 bf16 training-mode path (every BN backward, dropout, the fused nodes) moves the
 model the way fp32 does, which the per-block tests cannot show.
 
-Bounds: held-out accuracy >= 90 % for both; the bf16 loss, averaged over the
-5 steps ending at every 25th step, within LOSS_BAND of the fp32 one there.
+Evaluation: Keras's moving statistics (momentum 0.99) still lag the weights
+after a few hundred steps (tools/bn_moving_probe.py, tools/learn_probe.py:
+held-out accuracy at chance with them, 99-100 % with current statistics), so
+before predicting, one training-mode forward over 128 training clips with
+momentum 0 sets every BatchNormalization's moving statistics to the current
+batch statistics ("BN recalibration"; the reference fit loop instead runs many
+epochs).
+
+Bounds: held-out accuracy >= 90 % for both; the bf16 loss, averaged over each
+25-step window, within LOSS_BAND of the fp32 one (the two runs leave the
+ln(4) plateau within ~20 steps of each other: 0.27 apart at worst in the
+probe).
 """
 import numpy as np
 import pytest
@@ -24,8 +34,8 @@ pytestmark = pytest.mark.gpu
 SR = 48000
 N = 3 * SR
 BANDS = [(600.0, 1400.0), (1800.0, 3200.0), (4000.0, 6000.0), (7000.0, 10500.0)]
-B, STEPS, TRAIN, HELD = 32, 150, 512, 128
-LOSS_BAND = 0.3  # |mean bf16 loss - mean fp32 loss| over each 5-step window
+B, STEPS, TRAIN, HELD = 32, 300, 512, 128
+LOSS_BAND = 0.4  # |mean bf16 loss - mean fp32 loss| over each 25-step window
 
 
 def band_clip(rng, k):
@@ -77,6 +87,14 @@ def train(dtype, data, cuda):
         loss, _ = tr.step(xtr[idx].contiguous(), eye[ytr[idx]])
         losses.append(float(loss))
     torch.cuda.synchronize()
+    bns = [m for m in model.modules() if hasattr(m, "moving_mean")]
+    for m in bns:
+        m.momentum, m._m = 0.0, m.momentum
+    with torch.no_grad():
+        model.train()
+        model(fe(xtr[:128].contiguous()))
+    for m in bns:
+        m.momentum = m._m
     pred = []
     for i in range(0, HELD, 64):
         pred.append(tr.predict(xte[i:i + 64].contiguous()).float().argmax(1).cpu().numpy())
@@ -87,11 +105,11 @@ def train(dtype, data, cuda):
 def test_training_learns_bf16_and_fp32(data, cuda):
     l16, a16 = train(torch.bfloat16, data, cuda)
     l32, a32 = train(torch.float32, data, cuda)
-    w16 = [l16[s - 5:s].mean() for s in range(25, STEPS + 1, 25)]
-    w32 = [l32[s - 5:s].mean() for s in range(25, STEPS + 1, 25)]
+    w16 = [l16[s - 25:s].mean() for s in range(25, STEPS + 1, 25)]
+    w32 = [l32[s - 25:s].mean() for s in range(25, STEPS + 1, 25)]
     print("loss bf16", np.round(w16, 4), "acc", a16)
     print("loss fp32", np.round(w32, 4), "acc", a32)
     assert np.isfinite(l16).all() and np.isfinite(l32).all()
-    assert w32[-1] < 0.5 * l32[:5].mean() and w16[-1] < 0.5 * l16[:5].mean()
+    assert w32[-1] < 0.2 * w32[0] and w16[-1] < 0.2 * w16[0]
     assert a32 >= 0.9 and a16 >= 0.9, (a16, a32)
     assert max(abs(a - b) for a, b in zip(w16, w32)) <= LOSS_BAND, (w16, w32)

@@ -20,7 +20,7 @@ bp() { # name benchargs...  (bench line + rocprof of the same command)
   local name=$1; shift
   step ${name}_bench 600 python bench.py "$@"
   step ${name}_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${name}_prof -o run -- \
-      python bench.py --no-cpu-baseline "$@"
+      python bench.py --no-cpu-baseline --no-extra "$@"
 }
 for w in "$@"; do
   case $w in
@@ -46,6 +46,10 @@ for w in "$@"; do
     e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;
     sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
+    t1nx) step t1nx_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
+    t1f0) ACFE_BN_BWD_FUSE=0 step t1f0_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
+    wrnnx) step wrnnx_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    wrnf0) ACFE_BN_BWD_FUSE=0 step wrnf0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
     ptk) step ptk 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$PTK" ;;
     ptka) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$PTK" > $O/ptka.log 2>&1
           rc=$?; echo "== ptka rc=$rc"; grep -E "PASSED|FAILED|ERROR|passed|failed" $O/ptka.log | tail -40
