@@ -57,7 +57,8 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_wgrad_workspace": [I32, I32, I32, I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_wgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, I32, P, P],
     "acfe_conv2d_wgrad_bnbwd_rows": [I32] * 5,
-    "acfe_conv2d_wgrad_bnbwd": [P, I32, I32, I32, I32, P, P, I32, P, P, I32, P, F32, C.c_uint64, P, P, F32, P, P, P],
+    "acfe_conv2d_wgrad_bnbwd": [P, I32, I32, I32, I32, P, P, I32, P, P, I32, P, P, F32, C.c_uint64, P, P, F32, P, P,
+                                P],
     "acfe_stem_blocks": [I32, I32, I32],
     "acfe_stem_fold_weights": [P, I32, I32, I32, I32, P, P],
     "acfe_stem_fwd": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, I32, P, P],

@@ -736,6 +736,9 @@ class _BNFn(torch.autograd.Function):
         ctx.save_for_backward(x, *saved)
         ctx.conf = (relu, training, link)
         ctx.mask_in = FUSE and getattr(x, "_acfe_relu_out", False)
+        # x is the residual output of a _ConvAddFn whose wgrad can form this
+        # BN's backward apply (acfe_conv2d_wgrad_bnbwd with `add`)
+        ctx.fold = FUSE_BN_BWD and getattr(x, "_acfe_fold_consumer", False)
         return y
 
     @staticmethod
@@ -747,9 +750,75 @@ class _BNFn(torch.autograd.Function):
             add, pool = link.take(), link.take_pool()
             if add is None and pool is None and not link.declined:
                 raise RuntimeError("ResidualLink: the shortcut gradient was not delivered before this BN's backward")
-        dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool,
-                                    params=ctx.gb)
+        if ctx.fold and pool is None and (link is None or not link.declined):
+            # x's only autograd consumer is this BN (a shortcut's gradient came
+            # through the link): dx is returned unwritten, its apply pending for
+            # the producing conv's backward (_ConvAddFn), which forms it inside
+            # its weight gradient or, failing that, runs the apply pass
+            dx, dgamma, dbeta = _bn_bwd_pending(x, dy, saved, relu, training, add, ctx.mask_in, ctx.gb)
+        else:
+            dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool,
+                                        params=ctx.gb)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
+
+
+def _bn_bwd_pending(x, dy, saved, relu, training, add, mask_in, params):
+    """_bn_bwd up to its apply pass: the reduce (or the slab the producing
+    dgrad formed) and the coefficients run now; dx comes back UNWRITTEN with
+    the apply's arguments attached (_acfe_bwd_pending), for _take_pending."""
+    scale, shift, mean, invstd = saved
+    C = x.shape[-1]
+    rows = x.numel() // C
+    dev = x.device
+    nrows = lib.acfe_reduce_blocks(rows)
+    prow = nrows
+    part = None
+    lazy = _tagged(dy, "_acfe_bnpart")
+    if lazy is not None and lazy[2] == (x.data_ptr(), tuple(x.shape), bool(relu)):
+        part, prow = lazy[0], lazy[1]
+    dy = dy.contiguous()
+    if part is None:
+        part = _empty((nrows * 2 * C,), F64, dev)
+        call("acfe_bn_bwd_reduce", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+             ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), stream())
+    coef, dgamma, dbeta = _bn_bwd_coef(part, prow, C, rows, saved, training, params, dev)
+    if add is not None:
+        add = add.contiguous()
+        assert add.dtype == x.dtype and add.shape == x.shape
+    dx = _empty(x.shape, x.dtype, dev)
+    flags = int(relu) | (2 if mask_in else 0)
+    dx._acfe_bwd_pending = ((dy, x, scale, shift, flags, coef, add), dx._version)
+    return dx, dgamma, dbeta
+
+
+def _take_pending(g):
+    """The pending BN backward apply of gradient g (None when g is written).
+    g must be the very tensor _bn_bwd_pending returned, untouched: an autograd
+    accumulation into it would have read unwritten memory."""
+    p = getattr(g, "_acfe_bwd_pending", None)
+    if p is None:
+        return None
+    g._acfe_bwd_pending = None
+    args, ver = p
+    if g._version != ver:
+        raise RuntimeError("pending BatchNormalization gradient was modified before its apply ran")
+    return args
+
+
+def _apply_pending(g, args):
+    """Write the pending gradient g with the apply pass (acfe_bn_bwd_apply_ex),
+    its channel sums attached as _bn_bwd does."""
+    dy, x, scale, shift, flags, coef, add = args
+    C = x.shape[-1]
+    rows = x.numel() // C
+    want_sum = FUSE and _sums_ok(g) and _sums_ok(dy) and _sums_ok(x) and (add is None or _sums_ok(add))
+    sums = _empty((lib.acfe_reduce_blocks(rows), 2, C), F64, x.device) if want_sum else None
+    call("acfe_bn_bwd_apply_ex", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), rows, C, ptr(scale),
+         ptr(shift), flags, ptr(coef), ptr(add), 0.0, 0, ptr(g), dtype_code(x.dtype), ptr(sums), stream())
+    if want_sum:
+        _attach_sum(g, sums, rows)
+    if flags & 2:
+        _tag(g, "_acfe_relu_masked", True)
 
 
 def batch_norm(x, gamma, beta, mmean, mvar, training, relu=False, stats=None, eps=1e-3, momentum=0.99, link=None,
@@ -807,6 +876,42 @@ def _bnbwd_fold_ok(x, w, u, dy, stride, pt, pl, P, Q) -> bool:
     return lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K) > 0
 
 
+def _wgrad_bnbwd(x, w, g, pend, need_db, bias, rate=0.0, seed=0):
+    """acfe_conv2d_wgrad_bnbwd: dW (and the bias gradient from its channel
+    sums) of conv(x, w) whose output gradient g it forms and writes from the
+    BN backward apply `pend` = (dy, x_bn, scale, shift, flags, coef, add)."""
+    N, H, W, C = x.shape
+    K = w.shape[0]
+    dev = x.device
+    s = stream()
+    dy, u, scale, shift, flags, coef, add = pend
+    tgt = direct_grad(w)
+    dwt = tgt if tgt is not None else _empty(w.shape, F32, dev)
+    ws = _empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), F32, dev)
+    srows = lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K)
+    sums = _empty((srows, 2, K), F64, dev)
+    with _Timed(w, "wgrad"):
+        call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(scale), ptr(shift), int(flags),
+             ptr(coef), ptr(add), float(rate), int(seed), ptr(g), ptr(dwt), 1.0 if tgt is not None else 0.0, ptr(ws),
+             ptr(sums), s)
+    if flags & 2:
+        _tag(g, "_acfe_relu_masked", True)
+    dw = dwt
+    if tgt is not None:
+        dw = None
+        grads_ready(w)
+    db = None
+    if need_db:
+        tb = direct_grad(bias)
+        out = tb if tb is not None else _empty((K,), F32, dev)
+        call("acfe_channel_sum_finalize", ptr(sums), srows, K, 1.0 if tb is not None else 0.0, ptr(out), s)
+        db = out
+        if tb is not None:
+            db = None
+            grads_ready(bias)
+    return dw, db
+
+
 def _conv_bn_bwd_fold(ctx, x, w, u, dy, saved, relu, training):
     """Backward of BN(Dropout(Conv2D(x))) with the BN backward apply inside the
     conv's weight gradient (acfe_conv2d_wgrad_bnbwd): the wgrad stages the BN
@@ -831,29 +936,9 @@ def _conv_bn_bwd_fold(ctx, x, w, u, dy, saved, relu, training):
              ptr(shift), ptr(mean), ptr(invstd), int(relu), ptr(part), s)
     coef, dgamma, dbeta = _bn_bwd_coef(part, prow, K, rows, saved, training, ctx.gb, dev)
     g = _empty(u.shape, u.dtype, dev)  # the conv output gradient
-    tgt = direct_grad(w)
-    dwt = tgt if tgt is not None else _empty(w.shape, F32, dev)
-    ws = _empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), F32, dev)
-    srows = lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K)
-    sums = _empty((srows, 2, K), F64, dev)
     rate, seed = ctx.drop if ctx.drop is not None else (0.0, 0)
-    with _Timed(w, "wgrad"):
-        call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(scale), ptr(shift), int(relu),
-             ptr(coef), float(rate), int(seed), ptr(g), ptr(dwt), 1.0 if tgt is not None else 0.0, ptr(ws),
-             ptr(sums), s)
-    dw = dwt
-    if tgt is not None:
-        dw = None
-        grads_ready(w)
-    db = None
-    if ctx.has_b and ctx.needs_input_grad[2]:
-        tb = direct_grad(ctx.bias)
-        out = tb if tb is not None else _empty((K,), F32, dev)
-        call("acfe_channel_sum_finalize", ptr(sums), srows, K, 1.0 if tb is not None else 0.0, ptr(out), s)
-        db = out
-        if tb is not None:
-            db = None
-            grads_ready(ctx.bias)
+    dw, db = _wgrad_bnbwd(x, w, g, (dy, u, scale, shift, int(relu), coef, None),
+                          ctx.has_b and ctx.needs_input_grad[2], ctx.bias, rate, seed)
     dx = None
     if ctx.needs_input_grad[0]:
         dx, _, _ = _conv_bwd(x, w, g, 1, 1, 1, H, W, True, False, False, bias=ctx.bias, bn=ctx.bn)
@@ -1071,6 +1156,8 @@ class _ConvAddFn(torch.autograd.Function):
         ctx.conf = (pt, pl, relu, b is not None, link)
         if relu:
             z._acfe_relu_out = True  # a BatchNormalization reading z folds in the ReLU backward
+        if FUSE_BN_BWD:
+            z._acfe_fold_consumer = True  # its BN's backward apply may be left pending for this node
         ctx.mark_non_differentiable(stats)
         return z, stats
 
@@ -1080,6 +1167,20 @@ class _ConvAddFn(torch.autograd.Function):
         pt, pl, relu, has_b, link = ctx.conf
         N, H, W, C = x.shape
         K = w.shape[0]
+        pend = _take_pending(g)
+        if pend is not None:
+            if (ctx.needs_input_grad[1] and _bnbwd_fold_ok(x, w, pend[1], g, 1, pt, pl, H, W)
+                    and pend[0].data_ptr() % 16 == 0 and (pend[6] is None or pend[6].data_ptr() % 16 == 0)):
+                # the BN backward apply inside this conv's wgrad, writing g
+                dw, db = _wgrad_bnbwd(x, w, g, pend, has_b and ctx.needs_input_grad[2], ctx.bias)
+                dx = None
+                if ctx.needs_input_grad[0]:
+                    dx, _, _ = _conv_bwd(x, w, g, 1, pt, pl, H, W, True, False, False, bias=ctx.bias, bn=ctx.bn)
+                if link is not None:
+                    link.grad = g
+                    return dx, dw, db, None, None, None, None
+                return dx, dw, db, g, None, None, None
+            _apply_pending(g, pend)
         g = g.contiguous()
         if relu and not _tagged(g, "_acfe_relu_masked"):
             d = torch.empty_like(g)

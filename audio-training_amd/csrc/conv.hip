@@ -3010,6 +3010,10 @@ __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
                 float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
   static_assert(!(BWD && UNP), "BN backward fold: plain dY");
+#ifndef ACFE_FB_MID
+#define ACFE_FB_MID 0
+#endif
+  constexpr int FBMID = ACFE_FB_MID < 2 * NR ? ACFE_FB_MID : 0;
   constexpr int SEGW = 64, HW = SEGW + 2, HR = NR + 2;
   // CW-channel chunks (C = 16 / 32 layers: the stage-2/3 branch2b): the 8 waves
   // are WC = CW / 16 channel blocks x WK = 8 / WC slices of K; a wave's nine
@@ -3058,7 +3062,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   // BWD: the BN input x at the staged dY granules, the staged segment's first
   // element index and column, and the lane's channel sums (its 8 channels
   // cg * 8 + j are fixed: 512 is a multiple of DGR)
-  u32x4 rdx[BWD ? DPT : 1];
+  u32x4 rdx[BWD ? DPT : 1], rdr[BWD ? DPT : 1];  // BN input x, residual gradient
   long long fbase = 0;
   int fw0 = 0;
   float fs[BWD ? 8 : 1];
@@ -3094,6 +3098,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         if constexpr (BWD) {
           const long long e0 = (((long long)n * g.P + h) * g.Q + w0) * g.K;
           rdx[i] = *reinterpret_cast<const u32x4*>(okd ? g.fb_x + e0 + eo : zp);
+          if (g.fb_add) rdr[i] = *reinterpret_cast<const u32x4*>(okd ? g.fb_add + e0 + eo : zp);
           if (i == 0) fbase = e0, fw0 = w0;
         }
       }
@@ -3143,8 +3148,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
             const int jj = (d & 1) * 2 + hf, j = 2 * d + hf;
             const float xv = __uint_as_float(hf ? (rdx[i][d] & 0xffff0000u) : (rdx[i][d] << 16));
             const float gv = __uint_as_float(hf ? (rd[i][d] & 0xffff0000u) : (rd[i][d] << 16));
-            const float gj = (g.fb_relu && !(__builtin_fmaf(xv, sc[jj], sh[jj]) > 0.f)) ? 0.f : gv;
-            float o = bf2f(f2bf(__builtin_fmaf(ca[jj], gj, __builtin_fmaf(cb[jj], xv, c0[jj]))));
+            const float gj = ((g.fb_relu & 1) && !(__builtin_fmaf(xv, sc[jj], sh[jj]) > 0.f)) ? 0.f : gv;
+            float o = __builtin_fmaf(ca[jj], gj, __builtin_fmaf(cb[jj], xv, c0[jj]));
+            if (g.fb_add) o += __uint_as_float(hf ? (rdr[i][d] & 0xffff0000u) : (rdr[i][d] << 16));
+            if ((g.fb_relu & 2) && !(xv > 0.f)) o = 0.f;  // x = a ReLU output upstream: its backward
+            o = bf2f(f2bf(o));
             if (g.drop.on) o = ((hf ? hh >> 16 : hh & 0xFFFFu) >= g.drop.thr) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
             o = ok ? o : 0.f;
             fs[j] += o;
@@ -3222,6 +3230,14 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      // BWD: the next segment's dY transform (and LDS store into the other
+      // buffer) between the MFMA halves, so its VALU runs beside the partner
+      // wave's MFMAs instead of after every wave's MFMAs (FBMID)
+      if constexpr (BWD && FBMID) {
+        if (kq == FBMID) {
+          if (more) sstore(buf ^ 1);
+        }
+      }
       const int rb = ro * SEGW + kc * 32;  // dY pixel row of this half
       const int xr = kc * 32;              // its pixel offset in the halo rows (tap row + ro below)
       bf8 af[FM];
@@ -3247,7 +3263,9 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
           acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bv, acc[fm][fn], 0, 0, 0);
       }
     }
-    if (more) sstore(buf ^ 1);
+    if constexpr (!BWD || !FBMID) {
+      if (more) sstore(buf ^ 1);
+    }
     if constexpr (BWD) {
       if (((sg - sbeg) & 15) == 15) fflush();
     }
@@ -3518,6 +3536,7 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.bn_sc = g.bn_sh = g.bn_mu = g.bn_is = nullptr;
   g.bn_relu = 0;
   g.fb_x = nullptr;
+  g.fb_add = nullptr;
   g.fb_sc = g.fb_sh = g.fb_coef = nullptr;
   g.fb_relu = 0;
   g.fb_out = nullptr;
@@ -4212,7 +4231,11 @@ ACFE_API int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const 
 // -> bn2b -> ReLU), given that BN's OUTPUT gradient gy, its input u_bn (the
 // dropped-out conv output) and its backward coefficients: the conv output
 // gradient dy = acfe_bn_bwd_apply_ex(gy, u_bn, scale, shift, relu, coef, NULL,
-// rate, seed) is formed while the wgrad stages it, written to `dy` (the dgrad
+// rate, seed) -- or, with `add`, acfe_bn_bwd_apply_ex(gy, u_bn, ..., relu
+// (bit 1: u_bn is a ReLU output), coef, add, 0, 0): a BN whose input is this
+// conv's (ReLU'd) residual output z and whose gradient carries the identity
+// shortcut's (resnet/wr_resnet.py:82-89, bn2a of the next block) -- is formed
+// while the wgrad stages it, written to `dy` (the dgrad
 // reads it) and summed per channel into `sums` ([rows][2][K], rows =
 // acfe_conv2d_wgrad_bnbwd_rows; the conv bias gradient via
 // acfe_channel_sum_finalize) -- the separate apply pass over the tensor is not
@@ -4231,12 +4254,12 @@ ACFE_API int acfe_conv2d_wgrad_bnbwd_rows(int N, int H, int W, int C, int K) {
 
 ACFE_API int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn,
                                      int K, const float* scale, const float* shift, int relu, const float* coef,
-                                     float drop_rate, unsigned long long seed, void* dy, float* dw, float beta,
-                                     float* workspace, double* sums, void* stream) {
+                                     const void* add, float drop_rate, unsigned long long seed, void* dy, float* dw,
+                                     float beta, float* workspace, double* sums, void* stream) {
   if (!x || !gy || !u_bn || !scale || !shift || !coef || !dy || !dw || !workspace || !sums || drop_rate < 0.f ||
-      drop_rate >= 1.f)
+      drop_rate >= 1.f || (add && drop_rate > 0.f))
     return ACFE_E_INVAL;
-  if (((uintptr_t)gy | (uintptr_t)u_bn | (uintptr_t)dy) & 15) return ACFE_E_INVAL;
+  if (((uintptr_t)gy | (uintptr_t)u_bn | (uintptr_t)dy | (uintptr_t)add) & 15) return ACFE_E_INVAL;
   const int rows = acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K);
   if (!rows) return ACFE_E_INVAL;
   long long splits, chunk;
@@ -4248,7 +4271,8 @@ ACFE_API int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, 
   g.fb_sc = scale;
   g.fb_sh = shift;
   g.fb_coef = coef;
-  g.fb_relu = relu & 1;
+  g.fb_add = (const uint16_t*)add;
+  g.fb_relu = relu & 3;
   g.fb_out = (uint16_t*)dy;
   g.fb_sums = sums;
   int used = 0;

@@ -53,10 +53,11 @@ struct ConvGeom {
   // also stored to fb_out (for the dgrad) and summed per channel into fb_sums
   // (slab [gridDim][2][K], the conv bias gradient)
   const uint16_t* fb_x;
+  const uint16_t* fb_add;  // nullable: the residual gradient added to a g + b x + c (ResidualLink)
   const float* fb_sc;
   const float* fb_sh;
   const float* fb_coef;
-  int fb_relu;
+  int fb_relu;  // bit 0: the BN's ReLU mask on g; bit 1: x is a ReLU output, dY zeroed where x <= 0
   uint16_t* fb_out;
   double* fb_sums;
 };

@@ -244,8 +244,11 @@ int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy,
  * BatchNormalization (+ReLU) -- resnet/wr_resnet.py:58-71 (conv2a -> Dropout ->
  * bn2b -> ReLU), resnet/wr_resnet_bird.py:139-154 (conv21 -> Dropout -> bn2b)
  * -- taking that BN's OUTPUT gradient gy and its input u_bn: the conv output
- * gradient dy = acfe_bn_bwd_apply_ex(gy, u_bn, scale, shift, relu, coef, NULL,
+ * gradient dy = acfe_bn_bwd_apply_ex(gy, u_bn, scale, shift, relu, coef, add,
  * drop_rate, seed, ...) is formed while the wgrad stages it (no separate apply
+ * pass; add != NULL: the residual form -- the conv's output z = (ReLU)(conv +
+ * shortcut) is the next block's bn2a input (resnet/wr_resnet.py:82-89), add
+ * its identity shortcut's gradient, relu bit 1 the ReLU of z; no dropout)
  * pass over the tensor), written to dy (bit-identical to the apply pass's;
  * the dgrad reads it next) and summed per channel into sums
  * [acfe_conv2d_wgrad_bnbwd_rows][2][K] (finalize with
@@ -254,9 +257,9 @@ int acfe_conv2d_wgrad(const void* x, int N, int H, int W, int C, const void* dy,
  * acfe_bn_bwd_apply_ex + acfe_conv2d_wgrad). */
 int acfe_conv2d_wgrad_bnbwd_rows(int N, int H, int W, int C, int K);
 int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn, int K,
-                            const float* scale, const float* shift, int relu, const float* coef, float drop_rate,
-                            unsigned long long seed, void* dy, float* dw, float beta, float* workspace,
-                            double* sums, void* stream);
+                            const float* scale, const float* shift, int relu, const float* coef, const void* add,
+                            float drop_rate, unsigned long long seed, void* dy, float* dw, float beta,
+                            float* workspace, double* sums, void* stream);
 
 /* Stem convolution with one (folded) input channel and 16 outputs ("same",
  * stride 1, R = S = 5 (wr_resnet_bird) or 3 (wr_resnet)): the three identical

@@ -885,7 +885,7 @@ def test_conv_wgrad_bnbwd_fused(env, cuda, N, H, W, C, K, rate, relu):
     sums1 = torch.full((srows, 2, K), float("nan"), dtype=F64, device=cuda)
     ws1 = torch.empty_like(ws)
     call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(gy), ptr(u), K, ptr(sc), ptr(sh), relu, ptr(coef),
-         rate, seed, ptr(dy1), ptr(dw1), 0.0, ptr(ws1), ptr(sums1), stream())
+         None, rate, seed, ptr(dy1), ptr(dw1), 0.0, ptr(ws1), ptr(sums1), stream())
     db1 = torch.empty((K,), device=cuda)
     call("acfe_channel_sum_finalize", ptr(sums1), srows, K, 0.0, ptr(db1), stream())
     torch.cuda.synchronize()
@@ -898,7 +898,7 @@ def test_conv_wgrad_bnbwd_fused(env, cuda, N, H, W, C, K, rate, relu):
     # accumulate into an existing dW (beta 1, the arena path)
     dw2 = dw0.clone()
     call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(gy), ptr(u), K, ptr(sc), ptr(sh), relu, ptr(coef),
-         rate, seed, ptr(dy1), ptr(dw2), 1.0, ptr(ws1), ptr(sums1), stream())
+         None, rate, seed, ptr(dy1), ptr(dw2), 1.0, ptr(ws1), ptr(sums1), stream())
     torch.cuda.synchronize()
     assert torch.equal(dw2, dw0 + dw0)
 
@@ -948,3 +948,52 @@ def test_model_bn_bwd_fold_matches_unfused(env, cuda, model_name):
         assert ((a - b).abs().max() / a.abs().max().clamp_min(1e-30)).item() < 1e-5, n
         nbias += 1
     assert nbias > 0, "no conv bias differed: was the fold exercised?"
+
+
+@pytest.mark.parametrize("N,H,W,C,K,mask_in", [(4, 128, 513, 64, 64, True), (8, 64, 128, 64, 64, False),
+                                               (3, 14, 100, 64, 64, True)],
+                         ids=["wrn-s1-2b", "bird-s1b0-2b-norelu", "partial"])
+def test_conv_wgrad_bnbwd_residual(env, cuda, N, H, W, C, K, mask_in):
+    """The residual form of acfe_conv2d_wgrad_bnbwd: conv2b's weight gradient
+    forming the NEXT block's bn2a backward apply (resnet/wr_resnet.py:54-89:
+    z = ReLU(conv2b + shortcut) is bn2a's input, the identity shortcut's
+    gradient `add` is summed in, the ReLU of z masks the result) against
+    acfe_bn_bwd_apply_ex(add, relu bit 1) -> acfe_conv2d_wgrad: dz
+    bit-identical, dW bit-identical, bias sums within 1e-6."""
+    ops, call, lib, ptr, stream = env
+    srows = lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K)
+    assert srows > 0
+    g = torch.Generator().manual_seed(53 + H)
+    x = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
+    gy = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+    z = torch.randn((N, H, W, K), generator=g)
+    z = (z.clamp_min(0) if mask_in else z).to(BF).to(cuda)
+    add = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+    sc = ((torch.rand(K, generator=g) + 0.5) * torch.where(torch.rand(K, generator=g) < 0.2, -1.0, 1.0)).to(cuda)
+    sh = (torch.randn(K, generator=g) * 0.3).to(cuda)
+    coef = (torch.randn(3 * K, generator=g) * 0.5).to(cuda)
+    flags = 1 | (2 if mask_in else 0)
+    rows = N * H * W
+    dz0 = torch.full((N, H, W, K), float("nan"), dtype=BF, device=cuda)
+    nr = lib.acfe_reduce_blocks(rows)
+    sums0 = torch.empty((nr, 2, K), dtype=F64, device=cuda)
+    call("acfe_bn_bwd_apply_ex", ptr(gy), 1, ptr(z), 1, rows, K, ptr(sc), ptr(sh), flags, ptr(coef), ptr(add), 0.0,
+         0, ptr(dz0), 1, ptr(sums0), stream())
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+    dw0 = torch.empty((K, 3, 3, C), device=cuda)
+    call("acfe_conv2d_wgrad", ptr(x), N, H, W, C, ptr(dz0), K, 3, 3, 1, 1, 1, H, W, ptr(dw0), 0.0, 1, ptr(ws),
+         stream())
+    db0 = torch.empty((K,), device=cuda)
+    call("acfe_channel_sum_finalize", ptr(sums0), nr, K, 0.0, ptr(db0), stream())
+    dz1 = torch.full((N, H, W, K), float("nan"), dtype=BF, device=cuda)
+    dw1 = torch.full((K, 3, 3, C), float("nan"), device=cuda)
+    sums1 = torch.full((srows, 2, K), float("nan"), dtype=F64, device=cuda)
+    call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(gy), ptr(z), K, ptr(sc), ptr(sh), flags, ptr(coef),
+         ptr(add), 0.0, 0, ptr(dz1), ptr(dw1), 0.0, ptr(ws), ptr(sums1), stream())
+    db1 = torch.empty((K,), device=cuda)
+    call("acfe_channel_sum_finalize", ptr(sums1), srows, K, 0.0, ptr(db1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dz1.view(torch.int16), dz0.view(torch.int16)), "dz"
+    assert torch.equal(dw1, dw0)
+    scale_ = dz0.float().abs().sum((0, 1, 2)).clamp_min(1.0)
+    assert ((db1 - db0).abs() / scale_).max().item() < 1e-6

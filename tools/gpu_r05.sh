@@ -46,6 +46,10 @@ for w in "$@"; do
     e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;
     sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
+    t1p) step t1p_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t1p_prof -o run -- \
+           python bench.py --no-cpu-baseline --no-extra --steps 10 --warmup 3 ;;
+    wrnp) step wrnp_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wrnp_prof -o run -- \
+           python bench.py --no-cpu-baseline --no-extra --model wrn --classes 2 --steps 5 --warmup 2 ;;
     t1nx) step t1nx_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     t1f0) ACFE_BN_BWD_FUSE=0 step t1f0_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     wrnnx) step wrnnx_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
