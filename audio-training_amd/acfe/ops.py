@@ -334,11 +334,13 @@ def _tagged(t: torch.Tensor, name: str):
     return v[0] if v is not None and v[1] == t._version else None
 
 
-def _attach_sum(t: torch.Tensor, part: torch.Tensor, rows: int):
+def _attach_sum(t: torch.Tensor, part: torch.Tensor, rows: int, nrows: int | None = None):
     """Finalize a fused channel-sum slab and cache it on the gradient tensor it
     sums, so the convolution receiving `t` as its output gradient takes its
     bias gradient from there instead of re-reading `t` (channel_sum)."""
-    _tag(t, "_acfe_chpart", (part, rows))  # finalized by channel_sum, possibly into an arena gradient
+    # finalized by channel_sum, possibly into an arena gradient; nrows: the
+    # slab's row count when it is not acfe_reduce_blocks(rows) (a kernel's grid)
+    _tag(t, "_acfe_chpart", (part, lib.acfe_reduce_blocks(rows) if nrows is None else nrows))
 
 
 def channel_sum(x: torch.Tensor, C: int, into: torch.Tensor | None = None) -> torch.Tensor:
@@ -348,8 +350,8 @@ def channel_sum(x: torch.Tensor, C: int, into: torch.Tensor | None = None) -> to
     beta = 1.0 if into is not None else 0.0
     lazy = _tagged(x, "_acfe_chpart")
     if lazy is not None and lazy[0].shape[-1] == C:
-        part, prow = lazy
-        call("acfe_channel_sum_finalize", ptr(part), lib.acfe_reduce_blocks(prow), C, beta, ptr(out), stream())
+        part, nrows = lazy
+        call("acfe_channel_sum_finalize", ptr(part), nrows, C, beta, ptr(out), stream())
         return out
     rows = x.numel() // C
     part = _empty((lib.acfe_reduce_blocks(rows) * 2 * C,), F64, x.device)
@@ -896,6 +898,9 @@ def _wgrad_bnbwd(x, w, g, pend, need_db, bias, rate=0.0, seed=0):
              ptr(sums), s)
     if flags & 2:
         _tag(g, "_acfe_relu_masked", True)
+    # g's channel sums: the bias gradient here and of any other conv receiving
+    # g (a conv shortcut's, through autograd: channel_sum)
+    _attach_sum(g, sums, g.numel() // K, srows)
     dw = dwt
     if tgt is not None:
         dw = None

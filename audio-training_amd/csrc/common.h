@@ -121,16 +121,39 @@ __device__ __forceinline__ uint32_t drop_pair_hash32(const Drop& d, uint32_t e) 
   return hash_u32_lo(d.seed, e >> 1);
 }
 __device__ __forceinline__ uint32_t drop_pair_hash(const Drop& d, uint64_t e) { return hash_u32(d.seed, e >> 1); }
+// hash_u32_lo(seed, q) from its Weyl term w = q * 0x9E3779B1 + (uint32)seed
+__device__ __forceinline__ uint32_t hash_u32_lo_w(uint64_t seed, uint32_t w) {
+  uint32_t x = w ^ (uint32_t)(seed >> 32);
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+// hash_u32_lo of the NP consecutive indices q0 .. q0 + NP - 1: the first
+// (Weyl) multiply advances by a constant, so only the first index pays it
+// (v_mul_lo_u32 is a quarter-rate instruction; identical values)
+template <int NP>
+__device__ __forceinline__ void hash_u32_lo_run(uint64_t seed, uint32_t q0, uint32_t (&h)[NP]) {
+  const uint32_t b = q0 * 0x9E3779B1u + (uint32_t)seed;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) h[p] = hash_u32_lo_w(seed, b + (uint32_t)p * 0x9E3779B1u);
+}
+
 // Dropout of 8 consecutive elements from the even flat index e0: the 4 pair
-// hashes of drop_keep's mask (one hash_u32 per element pair instead of per
-// element, and the 32-bit form when every index is < 2^32 -- i32, uniform):
-// the hashes' three 32-bit multiplies made the dropout passes VALU-bound
+// hashes of drop_keep's mask (one hash per element pair instead of per
+// element, the 32-bit form when every index is < 2^32 -- i32, uniform -- with
+// one Weyl multiply for the four): the hashes' 32-bit multiplies made the
+// dropout passes VALU-bound
 template <typename T>
 __device__ __forceinline__ void drop_apply8(const Drop& d, uint64_t e0, bool i32, float (&v)[8]) {
+  uint32_t hl[4];
+  if (i32) hash_u32_lo_run<4>(d.seed, (uint32_t)(e0 >> 1), hl);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const uint64_t e = e0 + 2 * p;
-    const uint32_t h = i32 ? hash_u32_lo(d.seed, (uint32_t)(e >> 1)) : hash_u32(d.seed, e >> 1);
+    const uint32_t h = i32 ? hl[p] : hash_u32(d.seed, e >> 1);
     v[2 * p] = (h & 0xFFFFu) >= d.thr ? rnd(v[2 * p] * d.scl, T()) : 0.f;
     v[2 * p + 1] = (h >> 16) >= d.thr ? rnd(v[2 * p + 1] * d.scl, T()) : 0.f;
   }

@@ -1541,10 +1541,12 @@ k_conv3x3_rows(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __res
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) r[jj] = bf2f(f2bf(acc[fm][fn][jj] + rb[jj]));
           if constexpr (DRP) {
+            uint32_t h2[2];
+            if constexpr (I32) hash_u32_lo_run<2>(g.drop.seed, ((unsigned)pix * (unsigned)g.K + c) >> 1, h2);
 #pragma unroll
             for (int pr = 0; pr < 2; ++pr) {
               uint32_t hh;
-              if constexpr (I32) hh = drop_pair_hash32(g.drop, (unsigned)pix * (unsigned)g.K + c + 2 * pr);
+              if constexpr (I32) hh = h2[pr];
               else hh = drop_pair_hash(g.drop, (uint64_t)pix * g.K + c + 2 * pr);
               r[2 * pr] = (hh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(r[2 * pr] * g.drop.scl)) : 0.f;
               r[2 * pr + 1] = (hh >> 16) >= g.drop.thr ? bf2f(f2bf(r[2 * pr + 1] * g.drop.scl)) : 0.f;
@@ -1957,9 +1959,11 @@ k_conv3x3_narrow(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __r
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = bf2f(f2bf(acc[fm][fn][j] + bq[fn][j]));
         if constexpr (DROP) {
+          uint32_t h2[2];
+          hash_u32_lo_run<2>(g.drop.seed, (pix * (unsigned)g.K + c) >> 1, h2);
 #pragma unroll
           for (int pr = 0; pr < 2; ++pr) {
-            const uint32_t hh = drop_pair_hash32(g.drop, pix * (unsigned)g.K + c + 2 * pr);
+            const uint32_t hh = h2[pr];
             r[2 * pr] = (hh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(r[2 * pr] * g.drop.scl)) : 0.f;
             r[2 * pr + 1] = (hh >> 16) >= g.drop.thr ? bf2f(f2bf(r[2 * pr + 1] * g.drop.scl)) : 0.f;
           }
@@ -2245,9 +2249,11 @@ k_conv3x3_cw(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
             }
           }
           if constexpr (DROP) {
+            uint32_t h2[2];
+            hash_u32_lo_run<2>(g.drop.seed, (pix * (unsigned)KB + c) >> 1, h2);
 #pragma unroll
             for (int pr = 0; pr < 2; ++pr) {
-              const uint32_t hs = drop_pair_hash32(g.drop, pix * (unsigned)KB + c + 2 * pr);
+              const uint32_t hs = h2[pr];
               rr[2 * pr] = (hs & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(rr[2 * pr] * g.drop.scl)) : 0.f;
               rr[2 * pr + 1] = (hs >> 16) >= g.drop.thr ? bf2f(f2bf(rr[2 * pr + 1] * g.drop.scl)) : 0.f;
             }
@@ -2420,9 +2426,11 @@ k_conv3x3_c16(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = bf2f(f2bf(acc[fm][fn][j] + bq[fn][j]));
         if constexpr (DROP) {
+          uint32_t h2[2];
+          hash_u32_lo_run<2>(g.drop.seed, (pix * (unsigned)g.K + c) >> 1, h2);
 #pragma unroll
           for (int pr = 0; pr < 2; ++pr) {
-            const uint32_t hh = drop_pair_hash32(g.drop, pix * (unsigned)g.K + c + 2 * pr);
+            const uint32_t hh = h2[pr];
             r[2 * pr] = (hh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(r[2 * pr] * g.drop.scl)) : 0.f;
             r[2 * pr + 1] = (hh >> 16) >= g.drop.thr ? bf2f(f2bf(r[2 * pr + 1] * g.drop.scl)) : 0.f;
           }
@@ -3132,16 +3140,22 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         const long long e = fbase + ((long long)ro * g.Q + pw) * g.K + cg * 8;
         const f4* tb = reinterpret_cast<const f4*>(ftab + cg * 8);
         u32x4 v;
+        // one pair hash per dword (channels 2d, 2d + 1; e is even), the four
+        // from one Weyl multiply when the indices fit 32 bits
+        uint32_t hl[4] = {0u, 0u, 0u, 0u};
+        if (g.drop.on) {
+          if (g.idx32) {
+            hash_u32_lo_run<4>(g.drop.seed, (uint32_t)((uint64_t)e >> 1), hl);
+          } else {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) hl[d] = hash_u32(g.drop.seed, ((uint64_t)e >> 1) + d);
+          }
+        }
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           const f4 sc = tb[d >> 1], sh = tb[KB / 4 + (d >> 1)], ca = tb[2 * (KB / 4) + (d >> 1)],
                    cb = tb[3 * (KB / 4) + (d >> 1)], c0 = tb[4 * (KB / 4) + (d >> 1)];
-          // one pair hash per dword (channels 2d, 2d + 1; e is even)
-          uint32_t hh = 0;
-          if (g.drop.on) {
-            const uint64_t ep = (uint64_t)(e + 2 * d);
-            hh = g.idx32 ? hash_u32_lo(g.drop.seed, (uint32_t)(ep >> 1)) : hash_u32(g.drop.seed, ep >> 1);
-          }
+          const uint32_t hh = hl[d];
           unsigned pk = 0;
 #pragma unroll
           for (int hf = 0; hf < 2; ++hf) {
@@ -3149,19 +3163,27 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
             const float xv = __uint_as_float(hf ? (rdx[i][d] & 0xffff0000u) : (rdx[i][d] << 16));
             const float gv = __uint_as_float(hf ? (rd[i][d] & 0xffff0000u) : (rd[i][d] << 16));
             const float gj = ((g.fb_relu & 1) && !(__builtin_fmaf(xv, sc[jj], sh[jj]) > 0.f)) ? 0.f : gv;
+#ifdef ACFE_FB_NOXFORM
+            float o = gv;
+#else
             float o = __builtin_fmaf(ca[jj], gj, __builtin_fmaf(cb[jj], xv, c0[jj]));
+#endif
             if (g.fb_add) o += __uint_as_float(hf ? (rdr[i][d] & 0xffff0000u) : (rdr[i][d] << 16));
             if ((g.fb_relu & 2) && !(xv > 0.f)) o = 0.f;  // x = a ReLU output upstream: its backward
             o = bf2f(f2bf(o));
             if (g.drop.on) o = ((hf ? hh >> 16 : hh & 0xFFFFu) >= g.drop.thr) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
             o = ok ? o : 0.f;
+#ifndef ACFE_FB_NOSUM
             fs[j] += o;
+#endif
             pk |= hf ? (__float_as_uint(o) & 0xffff0000u) : (__float_as_uint(o) >> 16);
           }
           v[d] = pk;
         }
         if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = v;
+#ifndef ACFE_FB_NOSTORE
         if (ok && g.fb_out && cc == 0) *reinterpret_cast<u32x4*>(g.fb_out + e) = v;
+#endif
       } else {
         if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = rd[i];
       }
