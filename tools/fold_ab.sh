@@ -6,6 +6,6 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for v in "$@"; do
   for shp in "512 128 513 64 64" "512 64 128 64 64"; do
     echo "== fbmid$v $shp"
-    ACFE_LIB=$PWD/abtest/fbmid$v.so timeout -k 10 120 python tools/fold_bench.py $shp 10 || exit 1
+    ACFE_LIB=$PWD/abtest/fbmid$v.so timeout -k 10 120 python tools/fold_bench.py $shp 10 ${RATE:-0.1} || exit 1
   done
 done

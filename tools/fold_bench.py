@@ -2,7 +2,7 @@
 """Time the Conv2D -> Dropout -> BN backward fold (acfe_conv2d_wgrad_bnbwd)
 against its unfused chain (acfe_bn_bwd_apply_ex with dropout + channel sums,
 then acfe_conv2d_wgrad), HIP events on the launch stream.
-usage: python tools/fold_bench.py N H W C K [iters]   (ACFE_LIB selects a library variant)"""
+usage: python tools/fold_bench.py N H W C K [iters] [rate]   (ACFE_LIB selects a library variant)"""
 import sys
 from pathlib import Path
 
@@ -15,6 +15,7 @@ from acfe._torch import ptr, stream  # noqa: E402
 
 N, H, W, C, K = (int(v) for v in sys.argv[1:6])
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 10
+rate = float(sys.argv[7]) if len(sys.argv) > 7 else 0.1
 dev = torch.device("cuda", 0)
 BF = torch.bfloat16
 x = (torch.randn((N, H, W, C), device=dev) * 0.5).to(BF)
@@ -32,7 +33,7 @@ sums1 = torch.empty((max(srows, 1), 2, K), dtype=torch.float64, device=dev)
 
 
 def apply():
-    call("acfe_bn_bwd_apply_ex", ptr(gy), 1, ptr(u), 1, rows, K, ptr(sc), ptr(sh), 1, ptr(coef), None, 0.1, 7,
+    call("acfe_bn_bwd_apply_ex", ptr(gy), 1, ptr(u), 1, rows, K, ptr(sc), ptr(sh), 1, ptr(coef), None, rate, 7,
          ptr(dy), 1, ptr(sums0), stream())
 
 
@@ -41,7 +42,7 @@ def wgrad():
 
 
 def fused():
-    call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(gy), ptr(u), K, ptr(sc), ptr(sh), 1, ptr(coef), None, 0.1, 7,
+    call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(gy), ptr(u), K, ptr(sc), ptr(sh), 1, ptr(coef), None, rate, 7,
          ptr(dy), ptr(dw), 0.0, ptr(ws), ptr(sums1), stream())
 
 
@@ -59,5 +60,5 @@ def t(f):
 
 
 ta, tw, tf = t(apply), t(wgrad), t(fused)
-print(f"fold N={N} {H}x{W} C={C} K={K}: apply {ta:.1f} us + wgrad {tw:.1f} us = {ta + tw:.1f} us; "
+print(f"fold rate {rate} N={N} {H}x{W} C={C} K={K}: apply {ta:.1f} us + wgrad {tw:.1f} us = {ta + tw:.1f} us; "
       f"fused {tf:.1f} us ({tf - tw:+.1f} over the wgrad)", flush=True)
