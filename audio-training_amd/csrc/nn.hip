@@ -613,12 +613,11 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
     }
     st8(dx + (size_t)v * 8, o);
     if (sum_part) {
+      // (the slab's sum-of-squares row stays zero: only the bias gradient --
+      // the first row, acfe_channel_sum_finalize -- reads this slab, and the
+      // f64 square-sum was half of this pass's double-precision work)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float r = rnd(o[j], TO());  // the stored value
-        sa[j] += r;
-        sb[j] += (double)r * r;
-      }
+      for (int j = 0; j < 8; ++j) sa[j] += rnd(o[j], TO());  // the stored value
     }
   }
   if (sum_part) stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, sum_part);

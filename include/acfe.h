@@ -325,8 +325,10 @@ int acfe_bn_bwd_apply_dropout(const void* dy, int dy_dtype, const void* x, int x
  * the upstream ReLU's backward folded in. */
 /* General form: residual `add` (nullable), Dropout backward (drop_rate > 0,
  * then add must be NULL), and per-channel sums of the stored dx into
- * sum_partial (nullable; slab as acfe_add_stats) -- the bias gradient of the
- * convolution whose output is this BatchNormalization's input. */
+ * sum_partial (nullable; slab [acfe_reduce_blocks(rows)][2][C] as
+ * acfe_add_stats, its second (sum-of-squares) row left zero) -- the bias
+ * gradient of the convolution whose output is this BatchNormalization's
+ * input, via acfe_channel_sum_finalize. */
 int acfe_bn_bwd_apply_ex(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                          const float* scale, const float* shift, int relu, const float* coef, const void* add,
                          float drop_rate, unsigned long long seed, void* dx, int dx_dtype, double* sum_partial,

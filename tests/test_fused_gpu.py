@@ -240,6 +240,7 @@ def test_fused_channel_sums(env, cuda, C):
         call("acfe_bn_bwd_apply_ex", ptr(dy), 1, ptr(x), 1, rows, C, ptr(scale), ptr(shift), 1, ptr(coef), None,
              rate, 5, ptr(d1), 1, ptr(part), stream())
         assert torch.equal(d0, d1)
+        assert not part[:, 1].any()  # the sum-of-squares row is not formed (acfe.h)
         s = torch.empty((C,), device=cuda)
         call("acfe_channel_sum_finalize", ptr(part), nb, C, 0.0, ptr(s), stream())
         torch.testing.assert_close(s, ops.channel_sum(d0, C), rtol=1e-5, atol=1e-4)
