@@ -327,6 +327,13 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
 #pragma unroll
   for (int j = 0; j < BJ; ++j) wrow[j] = Wp + (long long)(n0 + (wid * BJ + j) * 8 + lrow) * g.Kdp + gsw * GR;
 
+  // fp32 (configs I / S): K-tiles ordered filter row fastest (s, chunk, r)
+  // instead of tap-major, so the tiles of neighbouring output rows -- resident
+  // side by side on one XCD (TileWalk) -- read each input row within a few
+  // K-tiles of each other and the re-reads hit that XCD's L2; tap-major put
+  // 12 K-tiles (~12 MB per XCD) between them and re-read the 4-byte input
+  // from HBM (1.86x algorithmic on S, profiles/pmc_dominant_stream_fp32_r04.json)
+  const bool rin = sizeof(T) == 4 && g.rin && g.R > 1 && g.C % BK == 0;
   const TileWalk walk(tiles_m);
   for (int tm = walk.tm; tm < walk.end; tm += walk.step) {
     const long long m0 = (long long)tm * BM;
@@ -362,13 +369,22 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
         glds16_async(ok ? (const void*)(rowp[j] + off) : (const void*)zp,                        \
                      (BUF) + ((wid * AJ + j) * 8) * 128);                                         \
       }                                                                                           \
+      const int wcol = rin ? (r * g.S + s) * g.C + c0 - gsw * GR : (KT) * BK;                     \
       _Pragma("unroll") for (int j = 0; j < BJ; ++j)                                              \
-        glds16_async(wrow[j] + (KT) * BK, (BUF) + (BM + (wid * BJ + j) * 8) * 128);               \
+        glds16_async(wrow[j] + wcol, (BUF) + (BM + (wid * BJ + j) * 8) * 128);                    \
       kk0 += BK;                                                                                  \
-      c0 += BK;                                                                                   \
-      while (c0 >= g.C) {                                                                         \
-        c0 -= g.C;                                                                                \
-        if (++s == g.S) { s = 0; ++r; }                                                           \
+      if (rin) {                                                                                  \
+        if (++r == g.R) {                                                                         \
+          r = 0;                                                                                  \
+          c0 += BK;                                                                               \
+          if (c0 >= g.C) { c0 -= g.C; ++s; }                                                      \
+        }                                                                                         \
+      } else {                                                                                    \
+        c0 += BK;                                                                                 \
+        while (c0 >= g.C) {                                                                       \
+          c0 -= g.C;                                                                              \
+          if (++s == g.S) { s = 0; ++r; }                                                         \
+        }                                                                                         \
       }                                                                                           \
     }
     f4 acc[FM][FN];
@@ -599,7 +615,7 @@ __device__ uint2 g_store_sink[64];  // never read: target of masked-off epilogue
 __device__ u32x4 g_store_sink16[64];  // the same for 16-B stores
 
 
-template <int BN>
+template <int BN, bool S2D = false>
 __global__ void __launch_bounds__(512, 1)
 k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_m,
@@ -767,6 +783,15 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     for (int fm = 0; fm < FM; ++fm) {
       const int pix = pbase + fm * 16;
       const bool inb = pix < M;
+      // super-pixel store (g.s2d): this pixel's dX block origin
+      int sn = 0, sh = 0, sw = 0;
+      if constexpr (S2D) {
+        const int pp = inb ? pix : 0;
+        sn = pp / PQ;
+        const int rem = pp - sn * PQ, u = rem / g.Q;
+        sh = u * g.s2d - g.s2d_pt;
+        sw = (rem - u * g.Q) * g.s2d - g.s2d_pl;
+      }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
@@ -783,6 +808,13 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         v.x = (unsigned)h[0] | ((unsigned)h[1] << 16);
         v.y = (unsigned)h[2] | ((unsigned)h[3] << 16);
         uint2* dst = inb ? reinterpret_cast<uint2*>(Y + (long long)pix * g.ldy + c) : &g_store_sink[lane];
+        if constexpr (S2D) {
+          const int ab = g.s2d_fill ? 0 : c / g.s2d_C, cc = c - ab * g.s2d_C, a = ab / g.s2d, b = ab - a * g.s2d;
+          const int h = sh + a, w = sw + b;
+          dst = (inb && c < g.K && (unsigned)h < (unsigned)g.s2d_H && (unsigned)w < (unsigned)g.s2d_W)
+                    ? reinterpret_cast<uint2*>(Y + (((long long)sn * g.s2d_H + h) * g.s2d_W + w) * g.s2d_C + cc)
+                    : &g_store_sink[lane];
+        }
         *dst = v;
         acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
       }
@@ -3563,6 +3595,9 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.fb_relu = 0;
   g.fb_out = nullptr;
   g.fb_sums = nullptr;
+  g.s2d = g.s2d_C = g.s2d_H = g.s2d_W = g.s2d_pt = g.s2d_pl = g.s2d_fill = 0;
+  static const int rin = !getenv("ACFE_CONVG_RIN") || atoi(getenv("ACFE_CONVG_RIN")) != 0;
+  g.rin = rin;
   g.idx32 = g.M * K < (1ll << 32) ? 1 : 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
@@ -3895,6 +3930,62 @@ __global__ void k_pack_phase(const T* __restrict__ wflip, int ld_flip, int K, in
   }
 }
 
+// Super-pixel (space-to-depth) form of the strided bf16 dgrad.  With
+// h + pt = st u + a (a in [0, st)), dX row h receives dY row u - m through
+// filter row r = a + st m only (m = 0 .. Mr - 1, Mr = ceil(R / st)); so the
+// st x st blocks of dX -- block (u, v), channel o = (a st + b) C + c -- are ONE
+// stride-1 conv of dY (K channels) with an Mr x Ms window (pad Mr - 1 / Ms - 1)
+// and st^2 C output channels, run by k_conv_fwd_p with its super-pixel store
+// (ConvGeom::s2d), no phase buffer and no scatter pass.  The window's packed
+// weights hold w[k][a + st m][b + st n][c], zero where that tap lies past the
+// filter (wr_resnet: 9 of 16 at 3x3 / stride 2, all 9 at stride 3, 1 of 4 / 9
+// for the 1x1 shortcuts, whose zero rows write the tap-less pixels' zeros).
+namespace {
+struct S2dPlan {
+  int mr, ms, kout, bn, rows_p, cols_p;
+  bool ok, fill;
+};
+S2dPlan s2d_plan(int N, int P, int Q, int K, int C, int R, int S, int st, int pt, int pl, int H, int W,
+                 int dtype) {
+  static const bool on = !getenv("ACFE_DGRAD_S2D") || atoi(getenv("ACFE_DGRAD_S2D")) != 0;
+  S2dPlan p{};
+  p.mr = (R + st - 1) / st;
+  p.ms = (S + st - 1) / st;
+  // a 1x1 "valid" shortcut feeds only block position (0, 0): C outputs into
+  // a zeroed dX (ConvGeom::s2d_fill)
+  p.fill = R == 1 && S == 1 && pt == 0 && pl == 0;
+  p.kout = p.fill ? C : st * st * C;
+  p.bn = p.kout % 128 == 0 ? 128 : 64;
+  p.rows_p = (p.kout + p.bn - 1) / p.bn * p.bn;
+  p.cols_p = p.mr * p.ms * K;
+  const long long U = (H + pt + st - 1) / st, V = (W + pl + st - 1) / st;
+  const long long img = (long long)P * Q * K * 2;
+  const long long span = ((256 + (long long)P * Q - 1) / ((long long)P * Q) + 1) * img;
+  p.ok = on && dtype == ACFE_DTYPE_BF16 && st > 1 && K % 64 == 0 && p.kout % p.bn == 0 && p.mr * p.ms <= 64 &&
+         pt >= 0 && pl >= 0 && pt < st && pl < st && (long long)N * U * V < (1ll << 31) && span < (1ll << 31);
+  return p;
+}
+}  // namespace
+
+// out[o][(tr * ms + tc) * K + k] = w[k][a + st (mr-1-tr)][b + st (ms-1-tc)][c] for
+// o = (a st + b) C + c (0 past the filter or past kout), read from the dgrad
+// packing wflip[c][((R-1-r) * S + (S-1-s)) * K + k]
+__global__ void k_pack_s2d(const uint16_t* __restrict__ wflip, int ld_flip, int K, int C, int R, int S, int st,
+                           int mr, int ms, int kout, int rows_p, int cols_p, uint16_t* __restrict__ out) {
+  const long long total = (long long)rows_p * cols_p;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int o = (int)(i / cols_p), col = (int)(i - (long long)o * cols_p);
+    uint16_t v = 0;
+    if (o < kout) {
+      const int ab = o / C, c = o - ab * C, a = ab / st, b = ab - a * st;
+      const int k = col % K, tap = col / K, tr = tap / ms, tc = tap - tr * ms;
+      const int r = a + st * (mr - 1 - tr), sx = b + st * (ms - 1 - tc);
+      if (r < R && sx < S) v = wflip[(long long)c * ld_flip + ((R - 1 - r) * S + (S - 1 - sx)) * K + k];
+    }
+    out[i] = v;
+  }
+}
+
 // dX[n][a + st i][b + st j][:] = ph[n][off_r + i][off_c + j][:] (ph == NULL: zeros)
 template <typename T>
 __global__ void k_phase_scatter(const T* __restrict__ ph, int N, int PH, int PW, int C, int off_r, int off_c, int a,
@@ -3921,6 +4012,8 @@ ACFE_API long long acfe_conv2d_dgrad_workspace(int N, int P, int Q, int K, int C
       (dtype != 0 && dtype != 1))
     return ACFE_E_INVAL;
   if (stride == 1) return 0;
+  const S2dPlan sp = s2d_plan(N, P, Q, K, C, R, S, stride, pad_top, pad_left, H, W, dtype);
+  if (sp.ok) return (long long)align256((size_t)sp.rows_p * sp.cols_p * 2);
   const size_t es = dtype == ACFE_DTYPE_BF16 ? 2 : 4;
   const int BK = dtype == ACFE_DTYPE_BF16 ? 64 : 32;
   const int rows_p = (C + pick_bn(C) - 1) / pick_bn(C) * pick_bn(C);
@@ -3955,6 +4048,45 @@ ACFE_API int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const
   {
     int rc = acfe_conv2d_packed_shape(K, R, S, C, dtype, 1, &rp_full, &ld_flip);
     if (rc) return rc;
+  }
+  const S2dPlan sp = s2d_plan(N, P, Q, K, C, R, S, stride, pad_top, pad_left, H, W, dtype);
+  if (sp.ok) {
+    hipStream_t s = strm(stream);
+    uint16_t* wp = static_cast<uint16_t*>(workspace);
+    const long long tot = (long long)sp.rows_p * sp.cols_p;
+    const int grid = (int)std::min<long long>(cdiv(tot, 256), 2048);
+    hipLaunchKernelGGL(k_pack_s2d, dim3(grid), dim3(256), 0, s, (const uint16_t*)wflip, ld_flip, K, C, R, S, stride,
+                       sp.mr, sp.ms, sp.kout, sp.rows_p, sp.cols_p, wp);
+    int rc = launch_rc("acfe_conv2d_dgrad(pack_s2d)");
+    if (rc) return rc;
+    const int pt = sp.mr - 1, pl = sp.ms - 1;
+    const int U = (H + pad_top + stride - 1) / stride, V = (W + pad_left + stride - 1) / stride;
+    ConvGeom g = make_geom(N, P, Q, K, sp.kout, sp.mr, sp.ms, 1, pt, pl, U, V, 64, sp.bn);
+    g.s2d = stride;
+    g.s2d_fill = sp.fill;
+    g.s2d_C = C;
+    g.s2d_H = H;
+    g.s2d_W = W;
+    g.s2d_pt = pad_top;
+    g.s2d_pl = pad_left;
+    if (sp.fill) {
+      // the tap-less pixels' zeros: one memset of dX ahead of the conv (as
+      // extra epilogue stores they held the vmcnt waits of every K-tile)
+      rc = hip_rc(hipMemsetAsync(dx, 0, (size_t)N * H * W * C * 2, s), "acfe_conv2d_dgrad(zero)");
+      if (rc) return rc;
+    }
+    const int ny = g.Kp / sp.bn, tiles = (int)((g.M + 255) / 256);
+    int gp = 256 / ny;
+    if (gp < 8) gp = 8;
+    if (gp > tiles) gp = tiles;
+    if (gp >= 64) gp &= ~7;
+    if (sp.bn == 128)
+      hipLaunchKernelGGL((k_conv_fwd_p<128, true>), dim3(gp, ny), dim3(512), 0, s, g, (const uint16_t*)dy,
+                         (const uint16_t*)wp, nullptr, (uint16_t*)dx, nullptr, tiles, 0);
+    else
+      hipLaunchKernelGGL((k_conv_fwd_p<64, true>), dim3(gp, ny), dim3(512), 0, s, g, (const uint16_t*)dy,
+                         (const uint16_t*)wp, nullptr, (uint16_t*)dx, nullptr, tiles, 0);
+    return launch_rc("acfe_conv2d_dgrad(s2d)");
   }
   // weights of every phase first (one region each), then the phase image buffer
   size_t wbytes = 0;

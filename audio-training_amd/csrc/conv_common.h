@@ -60,6 +60,14 @@ struct ConvGeom {
   int fb_relu;  // bit 0: the BN's ReLU mask on g; bit 1: x is a ReLU output, dY zeroed where x <= 0
   uint16_t* fb_out;
   double* fb_sums;
+  // k_conv_fwd_p super-pixel store (the strided dgrad, acfe_conv2d_dgrad): s2d
+  // = the stride st of the forward conv (0: plain NHWC store).  Output pixel
+  // (n, u, v) x channel o = (a st + b) s2d_C + c is dX[n][st u + a - s2d_pt]
+  // [st v + b - s2d_pl][c] of an s2d_H x s2d_W image, stored when inside it;
+  // s2d_fill: the output channels are position (0, 0)'s only (o = c; the
+  // caller zeroes the block's other st^2 - 1 pixels)
+  int s2d, s2d_C, s2d_H, s2d_W, s2d_pt, s2d_pl, s2d_fill;
+  int rin;  // k_conv_fwd_g fp32: K-tiles filter row fastest (ACFE_CONVG_RIN=0: tap-major)
 };
 
 // XCD-aware walk over the M tiles of a persistent grid.  Workgroups are

@@ -31,16 +31,16 @@ for w in "$@"; do
               case $rc in 0|1) ;; *) exit $rc ;; esac ;;
     mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
     fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
-    evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r04 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
+    evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r05 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
              'k_conv3x3_rows<64,8,4,true,true> (wr_resnet b1/b2 conv2a 3x3 64->64 @128x513 with the BN prologue + dropout + BN sums, batch 512)' \
              --model wrn --classes 2 --steps 2 --warmup 1 ;;
-    evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r04 'k_conv3x3_1w<1, 2, true, true>' 5905580032 \
+    evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r05 'k_conv3x3_1w<1, 2, true, true, false>' 5905580032 \
              'k_conv3x3_1w<1,2,true,true> (wr_resnet_bird s1b0 branch21 3x3 128->128 @128x256 + 2x2 max-pool + dropout + BN sums, batch 512)' \
              --steps 3 --warmup 1 ;;
-    evinfer) SELECT=7:3 step evinfer 900 bash tools/pmc_evidence.sh infer_fp32 r04 'k_conv_fwd_g<float, 128, 64' 8606859264 \
+    evinfer) SELECT=7:3 step evinfer 900 bash tools/pmc_evidence.sh infer_fp32 r05 'k_conv_fwd_g<float, 128, 64' 8606859264 \
              'k_conv_fwd_g<float,128,64> (wr_resnet b1.conv2a 3x3 64->64 @128x513 fp32, batch 256)' \
              --workload infer --steps 2 --warmup 1 ;;
-    evstream) SELECT=12:1 step evstream 900 bash tools/pmc_evidence.sh stream_fp32 r04 'k_conv_fwd_g<float, 128, 128' 26832360789 \
+    evstream) SELECT=12:1 step evstream 900 bash tools/pmc_evidence.sh stream_fp32 r05 'k_conv_fwd_g<float, 128, 128' 26832360789 \
              'k_conv_fwd_g<float,128,128> (wr_resnet_bird s1b0 conv21 3x3 128->128 @128x256 fp32; the 3 launches of a step: 1024 / 1024 / 351 windows, averaged)' \
              --workload stream --dtype fp32 --steps 1 --warmup 1 ;;
     e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;
@@ -50,6 +50,16 @@ for w in "$@"; do
            python bench.py --no-cpu-baseline --no-extra --steps 10 --warmup 3 ;;
     wrnp) step wrnp_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wrnp_prof -o run -- \
            python bench.py --no-cpu-baseline --no-extra --model wrn --classes 2 --steps 5 --warmup 2 ;;
+    layers) step layers_wrn 300 python tools/layer_profile.py 512 wrn && step layers_t1 300 python tools/layer_profile.py 512 ;;
+    wrns2d0) ACFE_DGRAD_S2D=0 step wrns2d0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra ;;
+    wrnx) step wrnx_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra ;;
+    infx) step infx_bench 600 python bench.py --workload infer --steps 5 --warmup 2 --no-cpu-baseline ;;
+    strx) step strx_bench 600 python bench.py --workload stream --dtype fp32 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    inf0) ACFE_CONVG_RIN=0 step inf0_bench 600 python bench.py --workload infer --steps 5 --warmup 2 --no-cpu-baseline ;;
+    str0) ACFE_CONVG_RIN=0 step str0_bench 600 python bench.py --workload stream --dtype fp32 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    wrnp0) ACFE_DGRAD_S2D=0 step wrnp0_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wrnp0_prof -o run -- \
+           python bench.py --no-cpu-baseline --no-extra --model wrn --classes 2 --steps 5 --warmup 2 ;;
+    s2db) step s2db 300 python tools/s2d_bench.py && ACFE_DGRAD_S2D=0 step s2db0 300 python tools/s2d_bench.py ;;
     t1nx) step t1nx_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     t1f0) ACFE_BN_BWD_FUSE=0 step t1f0_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     wrnnx) step wrnnx_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
