@@ -80,6 +80,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_dgrad_unpool": [P, P, I32, I32, I32, I32, P, I32, I32, I32, P, I32, P],
     "acfe_conv2d_wgrad_unpool": [P, I32, I32, I32, I32, P, P, I32, I32, I32, P, F32, I32, P, P],
     "acfe_bn_bwd_apply_pool": [P, I32, P, I32, I32, I32, I32, I32, P, P, I32, P, P, I32, P, I32, P, P],
+    "acfe_bn_bwd_apply_sub": [P, I32, P, I32, I32, I32, I32, I32, P, P, I32, P, P, I32, P, I32, P, P],
     "acfe_conv2d_rows_supported": [I32, I32, I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_fwd_add_supported": [I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_fwd_add": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, I32, P, P, I32, P],

@@ -44,6 +44,10 @@ STEM_BN_FUSE = os.environ.get("ACFE_STEM_BN_FUSE", "1") != "0"
 # runs the BN backward apply as its own pass instead of inside the conv's
 # weight gradient (acfe_conv2d_wgrad_bnbwd) (A/B, tests)
 FUSE_BN_BWD = FUSE and os.environ.get("ACFE_BN_BWD_FUSE", "1") != "0"
+# ACFE_SUB_FUSE=0: a 1x1 "valid" stride-k conv shortcut hands its full-resolution
+# dX (zero off the (k p, k q) pixels) to the BN backward instead of the P x Q
+# values for acfe_bn_bwd_apply_sub (A/B, tests)
+FUSE_SUB = FUSE and os.environ.get("ACFE_SUB_FUSE", "1") != "0"
 
 
 def same_padding(n: int, k: int, s: int) -> tuple[int, int]:
@@ -307,6 +311,23 @@ class _Conv2dFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         stride, pt, pl, P, Q, has_b = ctx.conf
         need_dx = ctx.needs_input_grad[0] or ctx.link is not None
+        N, H, W, C = x.shape
+        K = w.shape[0]
+        sub = (FUSE_SUB and ctx.link is not None and stride > 1 and w.shape[1] == 1 and w.shape[2] == 1
+               and pt == 0 and pl == 0 and P == (H - 1) // stride + 1 and Q == (W - 1) // stride + 1
+               and x.dtype == torch.bfloat16 and C % 8 == 0)
+        if sub:
+            # 1x1 "valid" stride-k shortcut: its dX is the 1x1 dgrad at the pixels
+            # (k p, k q) only -- computed at P x Q (a stride-1 1x1 dgrad) and added
+            # there by the BN's backward apply (acfe_bn_bwd_apply_sub)
+            dyc = dy.contiguous()
+            xs = x[:, ::stride, ::stride, :]
+            dxc, dw, db = _conv_bwd(xs, w, dyc, 1, 0, 0, P, Q, True, False, has_b and ctx.needs_input_grad[2],
+                                    bias=ctx.bias)
+            if ctx.needs_input_grad[1]:
+                _, dw, _ = _conv_bwd(x, w, dyc, stride, pt, pl, P, Q, False, True, False, bias=ctx.bias)
+            ctx.link.sub = (dxc, stride)
+            return None, dw, db, None, None, None, None, None, None, None
         dx, dw, db = _conv_bwd(x, w, dy, stride, pt, pl, P, Q, need_dx, ctx.needs_input_grad[1],
                                has_b and ctx.needs_input_grad[2], bias=ctx.bias, bn=ctx.bn)
         if ctx.link is not None:  # the BN reading x adds this gradient in its own backward
@@ -534,6 +555,9 @@ class ResidualLink:
     def __init__(self):
         self.grad = None
         self.pool = None  # (pooled gradient, k) from an avg_pool_same(x, k, link=...) shortcut
+        # (dX at the pixels (k p, k q), k) from a 1x1 "valid" stride-k conv shortcut
+        # (wr_resnet's transition blocks): its other pixels' gradient is zero
+        self.sub = None
         # set by a consumer that could not take the link after all (ops.conv2d on a
         # non-contiguous x): its gradient reaches x through autograd instead
         self.declined = False
@@ -548,6 +572,10 @@ class ResidualLink:
 
     def take_pool(self):
         p, self.pool = self.pool, None
+        return p
+
+    def take_sub(self):
+        p, self.sub = self.sub, None
         return p
 
 
@@ -672,7 +700,8 @@ def _bn_bwd_coef(part, prow, C, rows, saved, training, params, dev):
     return coef, dgamma, dbeta
 
 
-def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None, params=None, part=None):
+def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, pool=None, params=None, part=None,
+            sub=None):
     """(dx, dgamma, dbeta); dx += add; dx passed back through Dropout `drop` when given;
     mask_in: x is a ReLU output (ops.add), its backward [x > 0] is applied to dx here
     and dx is marked so that ops.add's backward skips its own pass.  part: the
@@ -707,6 +736,18 @@ def _bn_bwd(x, dy, saved, relu, training, add=None, drop=None, mask_in=False, po
     want_sum = FUSE and _sums_ok(dx) and _sums_ok(dy) and _sums_ok(x) and (add is None or _sums_ok(add))
     sums = _empty((nrows, 2, C), F64, dev) if want_sum else None
     flags = int(relu) | (2 if mask_in else 0)
+    if sub is not None:  # 1x1 stride-k shortcut's dX (pixels (k p, k q) only) folded in
+        gs, k = sub
+        gs = gs.contiguous()
+        assert rate == 0.0 and add is None and pool is None and gs.dtype == x.dtype
+        N, H, W, _ = x.shape
+        call("acfe_bn_bwd_apply_sub", ptr(dy), dtype_code(dy.dtype), ptr(x), dtype_code(x.dtype), N, H, W, C,
+             ptr(scale), ptr(shift), flags, ptr(coef), ptr(gs), int(k), ptr(dx), dtype_code(x.dtype), ptr(sums), s)
+        if want_sum:
+            _attach_sum(dx, sums, rows)
+        if mask_in:
+            _tag(dx, "_acfe_relu_masked", True)
+        return dx, dgamma, dbeta
     if pool is not None:  # shortcut AveragePooling2D(x) backward folded in
         gp, k = pool
         gp = gp.contiguous()
@@ -747,12 +788,12 @@ class _BNFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, *saved = ctx.saved_tensors
         relu, training, link = ctx.conf
-        add = pool = None
+        add = pool = sub = None
         if link is not None:
-            add, pool = link.take(), link.take_pool()
-            if add is None and pool is None and not link.declined:
+            add, pool, sub = link.take(), link.take_pool(), link.take_sub()
+            if add is None and pool is None and sub is None and not link.declined:
                 raise RuntimeError("ResidualLink: the shortcut gradient was not delivered before this BN's backward")
-        if ctx.fold and pool is None and (link is None or not link.declined):
+        if ctx.fold and pool is None and sub is None and (link is None or not link.declined):
             # x's only autograd consumer is this BN (a shortcut's gradient came
             # through the link): dx is returned unwritten, its apply pending for
             # the producing conv's backward (_ConvAddFn), which forms it inside
@@ -760,7 +801,7 @@ class _BNFn(torch.autograd.Function):
             dx, dgamma, dbeta = _bn_bwd_pending(x, dy, saved, relu, training, add, ctx.mask_in, ctx.gb)
         else:
             dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool,
-                                        params=ctx.gb)
+                                        params=ctx.gb, sub=sub)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
 
 

@@ -327,13 +327,6 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
 #pragma unroll
   for (int j = 0; j < BJ; ++j) wrow[j] = Wp + (long long)(n0 + (wid * BJ + j) * 8 + lrow) * g.Kdp + gsw * GR;
 
-  // fp32 (configs I / S): K-tiles ordered filter row fastest (s, chunk, r)
-  // instead of tap-major, so the tiles of neighbouring output rows -- resident
-  // side by side on one XCD (TileWalk) -- read each input row within a few
-  // K-tiles of each other and the re-reads hit that XCD's L2; tap-major put
-  // 12 K-tiles (~12 MB per XCD) between them and re-read the 4-byte input
-  // from HBM (1.86x algorithmic on S, profiles/pmc_dominant_stream_fp32_r04.json)
-  const bool rin = sizeof(T) == 4 && g.rin && g.R > 1 && g.C % BK == 0;
   const TileWalk walk(tiles_m);
   for (int tm = walk.tm; tm < walk.end; tm += walk.step) {
     const long long m0 = (long long)tm * BM;
@@ -369,22 +362,13 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
         glds16_async(ok ? (const void*)(rowp[j] + off) : (const void*)zp,                        \
                      (BUF) + ((wid * AJ + j) * 8) * 128);                                         \
       }                                                                                           \
-      const int wcol = rin ? (r * g.S + s) * g.C + c0 - gsw * GR : (KT) * BK;                     \
       _Pragma("unroll") for (int j = 0; j < BJ; ++j)                                              \
-        glds16_async(wrow[j] + wcol, (BUF) + (BM + (wid * BJ + j) * 8) * 128);                    \
+        glds16_async(wrow[j] + (KT) * BK, (BUF) + (BM + (wid * BJ + j) * 8) * 128);               \
       kk0 += BK;                                                                                  \
-      if (rin) {                                                                                  \
-        if (++r == g.R) {                                                                         \
-          r = 0;                                                                                  \
-          c0 += BK;                                                                               \
-          if (c0 >= g.C) { c0 -= g.C; ++s; }                                                      \
-        }                                                                                         \
-      } else {                                                                                    \
-        c0 += BK;                                                                                 \
-        while (c0 >= g.C) {                                                                       \
-          c0 -= g.C;                                                                              \
-          if (++s == g.S) { s = 0; ++r; }                                                         \
-        }                                                                                         \
+      c0 += BK;                                                                                   \
+      while (c0 >= g.C) {                                                                         \
+        c0 -= g.C;                                                                                \
+        if (++s == g.S) { s = 0; ++r; }                                                           \
       }                                                                                           \
     }
     f4 acc[FM][FN];
@@ -779,18 +763,42 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 #pragma unroll
     for (int i = 0; i < NV; ++i) sv[i] = 0.f;
     const int pbase = ctm * BM + wm * TWM + (lane & 15);
+    // S2D: per fragment column fn, the lane's channel quad c -> block position
+    // (a, b) and channel cc (s2d_C a power of two, a = ab * amul >> 5 for the
+    // st^2 < 32 positions), as an element offset from the block origin
+    int s2a[S2D ? FN : 1], s2b[S2D ? FN : 1], s2o[S2D ? FN : 1];
+    if constexpr (S2D) {
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
+        const int ab = g.s2d_fill ? 0 : c >> g.s2d_lc, cc = c & (g.s2d_C - 1);
+        const int a = (ab * g.s2d_amul) >> 5, b = ab - a * g.s2d;
+        s2a[fn] = a;
+        s2b[fn] = c < g.K ? b : -(1 << 20);  // (past K: never stored)
+        s2o[fn] = (a * g.s2d_W + b) * g.s2d_C + cc;
+      }
+    }
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
       const int pix = pbase + fm * 16;
       const bool inb = pix < M;
-      // super-pixel store (g.s2d): this pixel's dX block origin
-      int sn = 0, sh = 0, sw = 0;
+      // super-pixel store (g.s2d): this pixel's dX block origin (sn, sh, sw),
+      // the divisions by P Q and Q through a float reciprocal (pix < 2^24) and
+      // one correction step
+      int sh = 0, sw = 0;
+      long long sbase = 0;
       if constexpr (S2D) {
         const int pp = inb ? pix : 0;
-        sn = pp / PQ;
-        const int rem = pp - sn * PQ, u = rem / g.Q;
+        int sn = (int)((float)pp * g.s2d_rpq);
+        sn -= sn * PQ > pp ? 1 : 0;
+        sn += (sn + 1) * PQ <= pp ? 1 : 0;
+        const int rem = pp - sn * PQ;
+        int u = (int)((float)rem * g.s2d_rq);
+        u -= u * g.Q > rem ? 1 : 0;
+        u += (u + 1) * g.Q <= rem ? 1 : 0;
         sh = u * g.s2d - g.s2d_pt;
         sw = (rem - u * g.Q) * g.s2d - g.s2d_pl;
+        sbase = (((long long)sn * g.s2d_H + sh) * g.s2d_W + sw) * g.s2d_C;
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
@@ -800,19 +808,19 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         for (int jj = 0; jj < 4; ++jj) {
           h[jj] = f2bf(acc[fm][fn][jj] + bv[fn][jj]);
           if (g.drop.on) h[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(h[jj])));
-          const float f = inb ? bf2f(h[jj]) : 0.f;
-          sv[fn * 4 + jj] += f;
-          sv[FN * 4 + fn * 4 + jj] += f * f;
+          if constexpr (!S2D) {  // (the dgrad has no statistics)
+            const float f = inb ? bf2f(h[jj]) : 0.f;
+            sv[fn * 4 + jj] += f;
+            sv[FN * 4 + fn * 4 + jj] += f * f;
+          }
         }
         uint2 v;
         v.x = (unsigned)h[0] | ((unsigned)h[1] << 16);
         v.y = (unsigned)h[2] | ((unsigned)h[3] << 16);
         uint2* dst = inb ? reinterpret_cast<uint2*>(Y + (long long)pix * g.ldy + c) : &g_store_sink[lane];
         if constexpr (S2D) {
-          const int ab = g.s2d_fill ? 0 : c / g.s2d_C, cc = c - ab * g.s2d_C, a = ab / g.s2d, b = ab - a * g.s2d;
-          const int h = sh + a, w = sw + b;
-          dst = (inb && c < g.K && (unsigned)h < (unsigned)g.s2d_H && (unsigned)w < (unsigned)g.s2d_W)
-                    ? reinterpret_cast<uint2*>(Y + (((long long)sn * g.s2d_H + h) * g.s2d_W + w) * g.s2d_C + cc)
+          dst = (inb && (unsigned)(sh + s2a[fn]) < (unsigned)g.s2d_H && (unsigned)(sw + s2b[fn]) < (unsigned)g.s2d_W)
+                    ? reinterpret_cast<uint2*>(Y + sbase + s2o[fn])
                     : &g_store_sink[lane];
         }
         *dst = v;
@@ -3595,9 +3603,8 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.fb_relu = 0;
   g.fb_out = nullptr;
   g.fb_sums = nullptr;
-  g.s2d = g.s2d_C = g.s2d_H = g.s2d_W = g.s2d_pt = g.s2d_pl = g.s2d_fill = 0;
-  static const int rin = !getenv("ACFE_CONVG_RIN") || atoi(getenv("ACFE_CONVG_RIN")) != 0;
-  g.rin = rin;
+  g.s2d = g.s2d_C = g.s2d_H = g.s2d_W = g.s2d_pt = g.s2d_pl = g.s2d_fill = g.s2d_lc = g.s2d_amul = 0;
+  g.s2d_rpq = g.s2d_rq = 0.f;
   g.idx32 = g.M * K < (1ll << 32) ? 1 : 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
@@ -3961,7 +3968,8 @@ S2dPlan s2d_plan(int N, int P, int Q, int K, int C, int R, int S, int st, int pt
   const long long U = (H + pt + st - 1) / st, V = (W + pl + st - 1) / st;
   const long long img = (long long)P * Q * K * 2;
   const long long span = ((256 + (long long)P * Q - 1) / ((long long)P * Q) + 1) * img;
-  p.ok = on && dtype == ACFE_DTYPE_BF16 && st > 1 && K % 64 == 0 && p.kout % p.bn == 0 && p.mr * p.ms <= 64 &&
+  p.ok = on && dtype == ACFE_DTYPE_BF16 && st > 1 && st * st < 32 && (C & (C - 1)) == 0 && K % 64 == 0 &&
+         p.kout % p.bn == 0 && p.mr * p.ms <= 64 && (long long)N * ((H + pt + st - 1) / st) * ((W + pl + st - 1) / st) < (1 << 24) &&
          pt >= 0 && pl >= 0 && pt < st && pl < st && (long long)N * U * V < (1ll << 31) && span < (1ll << 31);
   return p;
 }
@@ -4064,6 +4072,10 @@ ACFE_API int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const
     ConvGeom g = make_geom(N, P, Q, K, sp.kout, sp.mr, sp.ms, 1, pt, pl, U, V, 64, sp.bn);
     g.s2d = stride;
     g.s2d_fill = sp.fill;
+    g.s2d_lc = __builtin_ctz((unsigned)C);
+    g.s2d_amul = (32 + stride - 1) / stride;
+    g.s2d_rpq = 1.0f / (float)((long long)U * V);
+    g.s2d_rq = 1.0f / (float)V;
     g.s2d_C = C;
     g.s2d_H = H;
     g.s2d_W = W;

@@ -67,7 +67,8 @@ struct ConvGeom {
   // s2d_fill: the output channels are position (0, 0)'s only (o = c; the
   // caller zeroes the block's other st^2 - 1 pixels)
   int s2d, s2d_C, s2d_H, s2d_W, s2d_pt, s2d_pl, s2d_fill;
-  int rin;  // k_conv_fwd_g fp32: K-tiles filter row fastest (ACFE_CONVG_RIN=0: tap-major)
+  int s2d_lc, s2d_amul;     // log2(s2d_C); block position a = (ab * s2d_amul) >> 5
+  float s2d_rpq, s2d_rq;    // 1 / (P Q), 1 / Q of the block grid
 };
 
 // XCD-aware walk over the M tiles of a persistent grid.  Workgroups are

@@ -549,9 +549,12 @@ __global__ void k_bn_bwd_apply(const TG* __restrict__ dy, const TX* __restrict__
 // Gradient of an AveragePooling2D(k, strides=k, "same") whose input is this
 // BN's input x, added on the fly (the pooled gradient g [N][P][Q][C] spread
 // over the window's in-bounds elements, as acfe_avgpool2d_bwd stores it).
+// sub: instead, the input gradient of a 1x1 "valid" conv of stride k reading x
+// (wr_resnet's transition shortcuts): g [N][P][Q][C] lands on the pixels
+// (k p, k q) only -- the other pixels' shortcut gradient is zero.
 struct PoolAdd {
   const void* g;
-  int H, W, k, P, Q, pt, pl;
+  int H, W, k, P, Q, pt, pl, sub;
 };
 
 template <typename TG, typename TX, typename TO>
@@ -586,7 +589,17 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
     ld8(dy + (size_t)v * 8, g);
     ld8(x + (size_t)v * 8, xv);
     if (add) ld8(add + (size_t)v * 8, o);
-    if (pa.g) {
+    if (pa.g && pa.sub) {
+      const unsigned row = v / CV, t = row / (unsigned)pa.W;
+      const int w = (int)(row - t * (unsigned)pa.W), h = (int)(t % (unsigned)pa.H), nn = (int)(t / (unsigned)pa.H);
+      const int p = h / pa.k, q = w / pa.k;
+      if (h == p * pa.k && w == q * pa.k && p < pa.P && q < pa.Q) {
+        ld8(reinterpret_cast<const TO*>(pa.g) + (((size_t)nn * pa.P + p) * pa.Q + q) * C + c0, o);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = 0.f;  // (0 + r, as the materialised zero gradient adds)
+      }
+    } else if (pa.g) {
       const unsigned row = v / CV, t = row / (unsigned)pa.W;
       const int w = (int)(row - t * (unsigned)pa.W), h = (int)(t % (unsigned)pa.H), nn = (int)(t / (unsigned)pa.H);
       const int p = (h + pa.pt) / pa.k, q = (w + pa.pl) / pa.k;
@@ -626,7 +639,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
 static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
                              const float* scale, const float* shift, int relu, const float* coef, const void* add,
                              const Drop& d, void* dx, int dx_dtype, double* sum_part, void* stream,
-                             PoolAdd pa = PoolAdd{nullptr, 0, 0, 0, 0, 0, 0, 0}) {
+                             PoolAdd pa = PoolAdd{nullptr, 0, 0, 0, 0, 0, 0, 0, 0}) {
   if (!dy || !x || !scale || !shift || !coef || !dx || rows < 0 || C <= 0) return ACFE_E_INVAL;
   const long long n = rows * C;
   if (n == 0) return ACFE_OK;
@@ -694,6 +707,28 @@ ACFE_API int acfe_bn_bwd_apply_pool(const void* dy, int dy_dtype, const void* x,
   pa.Q = (W + k - 1) / k;
   pa.pt = ((pa.P - 1) * k + k - H) / 2;
   pa.pl = ((pa.Q - 1) * k + k - W) / 2;
+  pa.sub = 0;
+  return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, (long long)N * H * W, C, scale, shift, relu, coef, nullptr,
+                           make_drop(0.f, 0), dx, dx_dtype, sum_partial, stream, pa);
+}
+
+// acfe_bn_bwd_apply_ex with, instead of `add`, the input gradient of a 1x1
+// "valid" Conv2D of stride k reading x: gsub [N][(H-1)/k+1][(W-1)/k+1][C] at
+// the pixels (k p, k q), zero elsewhere (never materialised at H x W).
+ACFE_API int acfe_bn_bwd_apply_sub(const void* dy, int dy_dtype, const void* x, int x_dtype, int N, int H, int W,
+                                   int C, const float* scale, const float* shift, int relu, const float* coef,
+                                   const void* gsub, int k, void* dx, int dx_dtype, double* sum_partial,
+                                   void* stream) {
+  if (!gsub || N <= 0 || H <= 0 || W <= 0 || k <= 0) return ACFE_E_INVAL;
+  PoolAdd pa;
+  pa.g = gsub;
+  pa.H = H;
+  pa.W = W;
+  pa.k = k;
+  pa.P = (H - 1) / k + 1;
+  pa.Q = (W - 1) / k + 1;
+  pa.pt = pa.pl = 0;
+  pa.sub = 1;
   return bn_bwd_apply_impl(dy, dy_dtype, x, x_dtype, (long long)N * H * W, C, scale, shift, relu, coef, nullptr,
                            make_drop(0.f, 0), dx, dx_dtype, sum_partial, stream, pa);
 }

@@ -445,6 +445,16 @@ int acfe_bn_bwd_apply_pool(const void* dy, int dy_dtype, const void* x, int x_dt
                            const float* scale, const float* shift, int relu, const float* coef, const void* gpool,
                            int k, void* dx, int dx_dtype, double* sum_partial, void* stream);
 
+/* acfe_bn_bwd_apply_ex whose residual term is the input gradient of a 1x1
+ * "valid" Conv2D with stride k reading x (wr_resnet's transition-block
+ * shortcut, resnet/wr_resnet.py:84-86, whose dX is nonzero only at the pixels
+ * (k p, k q)): gsub = that gradient at those pixels, [N][(H-1)/k+1][(W-1)/k+1][C]
+ * (same dtype as dx) -- the full-resolution shortcut gradient is never stored.
+ * Bit-identical to acfe_bn_bwd_apply_ex with add = gsub scattered into zeros. */
+int acfe_bn_bwd_apply_sub(const void* dy, int dy_dtype, const void* x, int x_dtype, int N, int H, int W, int C,
+                          const float* scale, const float* shift, int relu, const float* coef, const void* gsub,
+                          int k, void* dx, int dx_dtype, double* sum_partial, void* stream);
+
 /* out[c] = beta*out[c] + sum_rows x[r][c] (bias gradients); partial as acfe_bn_stats. */
 int acfe_channel_sum(const void* x, long long rows, int C, int dtype, double* partial, float* out, float beta,
                      void* stream);

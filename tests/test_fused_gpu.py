@@ -427,6 +427,82 @@ def test_pool_link(env, cuda):
         assert rel(p, r) < (5e-3 if i in (1, 2) else 2e-3), (i, rel(p, r))
 
 
+@pytest.mark.parametrize("k,H,W", [(2, 16, 33), (3, 22, 31), (2, 12, 20)])
+@pytest.mark.parametrize("relu", [1, 3])
+def test_bn_bwd_apply_sub_bitexact(env, cuda, k, H, W, relu):
+    """acfe_bn_bwd_apply_sub (the 1x1 stride-k shortcut's dX at the pixels
+    (k p, k q) only) == acfe_bn_bwd_apply_ex with that gradient scattered into
+    a zero tensor as `add`: dx bit-identical, channel sums equal."""
+    ops, call, lib, ptr, stream = env
+    N, C = 2, 64
+    P, Q = (H - 1) // k + 1, (W - 1) // k + 1
+    g = torch.Generator(device="cpu").manual_seed(17 + k)
+    BF = torch.bfloat16
+    dy = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
+    x = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
+    gs = torch.randn((N, P, Q, C), generator=g).to(BF).to(cuda)
+    sc = (torch.rand((C,), generator=g) + 0.5).to(cuda)
+    sh = (torch.randn((C,), generator=g) * 0.2).to(cuda)
+    coef = (torch.randn((3 * C,), generator=g) * 0.5).to(cuda)
+    full = torch.zeros((N, H, W, C), dtype=BF, device=cuda)
+    full[:, ::k, ::k, :] = gs
+    rows = N * H * W
+    nb = lib.acfe_reduce_blocks(rows)
+    outs = []
+    for mode in ("ex", "sub"):
+        dx = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+        sums = torch.empty((nb, 2, C), dtype=torch.float64, device=cuda)
+        if mode == "ex":
+            call("acfe_bn_bwd_apply_ex", ptr(dy), 1, ptr(x), 1, rows, C, ptr(sc), ptr(sh), relu, ptr(coef), ptr(full),
+                 0.0, 0, ptr(dx), 1, ptr(sums), stream())
+        else:
+            call("acfe_bn_bwd_apply_sub", ptr(dy), 1, ptr(x), 1, N, H, W, C, ptr(sc), ptr(sh), relu, ptr(coef),
+                 ptr(gs), k, ptr(dx), 1, ptr(sums), stream())
+        torch.cuda.synchronize()
+        outs.append((dx, sums[:, 0].sum(0)))
+    assert torch.equal(outs[1][0].view(torch.int16), outs[0][0].view(torch.int16))
+    assert torch.equal(outs[1][1], outs[0][1])
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_sub_link_node(env, cuda, k):
+    """wr_resnet's transition block shape (resnet/wr_resnet.py:46-90):
+    BN(x) -> 3x3 conv stride k, plus a 1x1 "valid" stride-k conv shortcut of x
+    whose dX reaches bn(x)'s backward through the ResidualLink at P x Q
+    (acfe_bn_bwd_apply_sub) == the shortcut's full-resolution dX handed over
+    (ACFE_SUB_FUSE=0 path) and == plain autograd accumulation."""
+    ops = env[0]
+    N, H, W, C, K = 2, 12 * k, 10 * k + 1, 64, 128
+    g = torch.Generator(device="cpu").manual_seed(23 + k)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((K, 3, 3, C), generator=g) * 0.05).to(cuda)
+    ws0 = (torch.randn((K, 1, 1, C), generator=g) * 0.1).to(cuda)
+    P = -(-H // k)
+    Q = -(-W // k)
+    gz = torch.randn((N, P, Q, K), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    old = ops.FUSE_SUB
+    try:
+        for mode in ("autograd", "full", "sub"):
+            ops.FUSE_SUB = mode == "sub"
+            x = x0.clone().requires_grad_(True)
+            w, ws = w0.clone().requires_grad_(True), ws0.clone().requires_grad_(True)
+            gamma, beta, mm, mv = _bn_params(C, cuda, 29)
+            link = None if mode == "autograd" else ops.ResidualLink()
+            u = ops.batch_norm(x, gamma, beta, mm, mv, True, relu=True, link=link)
+            y, _ = ops.conv2d(u, w, None, k, "same")
+            s, _ = ops.conv2d(x, ws, None, k, "valid", link=link)
+            z = ops.add(y, s)
+            z.backward(gz)
+            outs.append([z, x.grad, w.grad, ws.grad, gamma.grad, beta.grad])
+    finally:
+        ops.FUSE_SUB = old
+    for i, (a, b) in enumerate(zip(outs[2], outs[1])):  # sub vs full hand-over: same arithmetic
+        assert rel(a, b) < 1e-6, ("full", i, rel(a, b))
+    for i, (a, b) in enumerate(zip(outs[2], outs[0])):
+        assert rel(a, b) < 2e-3, ("autograd", i, rel(a, b))
+
+
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128), (32, 128), (16, 256), (32, 256), (128, 128)])
 def test_conv_add_node(env, cuda, relu, C, K):

@@ -62,6 +62,7 @@ for w in "$@"; do
     s2db) step s2db 300 python tools/s2d_bench.py && ACFE_DGRAD_S2D=0 step s2db0 300 python tools/s2d_bench.py ;;
     trwrn) step trwrn 700 bash tools/step_traffic.sh wrn_r05 --model wrn --classes 2 ;;
     trt1) step trt1 700 bash tools/step_traffic.sh t1_r05 ;;
+    wrnsub0) ACFE_SUB_FUSE=0 step wrnsub0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra ;;
     t1nx) step t1nx_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     t1f0) ACFE_BN_BWD_FUSE=0 step t1f0_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     wrnnx) step wrnnx_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
