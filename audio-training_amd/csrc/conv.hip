@@ -327,6 +327,14 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
 #pragma unroll
   for (int j = 0; j < BJ; ++j) wrow[j] = Wp + (long long)(n0 + (wid * BJ + j) * 8 + lrow) * g.Kdp + gsw * GR;
 
+  // fp32 (configs I / S): K-tiles chunk-major (32-channel chunk outermost,
+  // then the taps) instead of tap-major.  The tiles resident on one XCD cover
+  // ~32 output rows; tap-major, each reads all C channels of its three input
+  // rows over the tile, a live set of ~4.5 MB per XCD at 128 fp32 channels --
+  // more than the 4 MB L2, so rows came from HBM again (S: 1.86x algorithmic,
+  // profiles/pmc_dominant_stream_fp32_r04.json).  Chunk-major, the live set is
+  // one chunk of those rows (a quarter)
+  const bool cmaj = sizeof(T) == 4 && g.cmaj && g.R * g.S > 1 && g.C % BK == 0;
   const TileWalk walk(tiles_m);
   for (int tm = walk.tm; tm < walk.end; tm += walk.step) {
     const long long m0 = (long long)tm * BM;
@@ -362,13 +370,21 @@ k_conv_fwd_g(ConvGeom g, const T* __restrict__ X, const T* __restrict__ Wp, cons
         glds16_async(ok ? (const void*)(rowp[j] + off) : (const void*)zp,                        \
                      (BUF) + ((wid * AJ + j) * 8) * 128);                                         \
       }                                                                                           \
+      const int wcol = cmaj ? (r * g.S + s) * g.C + c0 - gsw * GR : (KT) * BK;                    \
       _Pragma("unroll") for (int j = 0; j < BJ; ++j)                                              \
-        glds16_async(wrow[j] + (KT) * BK, (BUF) + (BM + (wid * BJ + j) * 8) * 128);               \
+        glds16_async(wrow[j] + wcol, (BUF) + (BM + (wid * BJ + j) * 8) * 128);                    \
       kk0 += BK;                                                                                  \
-      c0 += BK;                                                                                   \
-      while (c0 >= g.C) {                                                                         \
-        c0 -= g.C;                                                                                \
-        if (++s == g.S) { s = 0; ++r; }                                                           \
+      if (cmaj) {                                                                                 \
+        if (++s == g.S) {                                                                         \
+          s = 0;                                                                                  \
+          if (++r == g.R) { r = 0; c0 += BK; }                                                    \
+        }                                                                                         \
+      } else {                                                                                    \
+        c0 += BK;                                                                                 \
+        while (c0 >= g.C) {                                                                       \
+          c0 -= g.C;                                                                              \
+          if (++s == g.S) { s = 0; ++r; }                                                         \
+        }                                                                                         \
       }                                                                                           \
     }
     f4 acc[FM][FN];
@@ -3605,6 +3621,8 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.fb_sums = nullptr;
   g.s2d = g.s2d_C = g.s2d_H = g.s2d_W = g.s2d_pt = g.s2d_pl = g.s2d_fill = g.s2d_lc = g.s2d_amul = 0;
   g.s2d_rpq = g.s2d_rq = 0.f;
+  static const int cmaj = !getenv("ACFE_CONVG_CMAJ") || atoi(getenv("ACFE_CONVG_CMAJ")) != 0;
+  g.cmaj = cmaj;
   g.idx32 = g.M * K < (1ll << 32) ? 1 : 0;
   static const int dbg = getenv("ACFE_CONV_DBG") ? atoi(getenv("ACFE_CONV_DBG")) : 0;
   g.dbg = dbg;
@@ -3667,7 +3685,8 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
     // 64-bit tap mask, 32-bit pixel index and < 2 GiB of input per M tile
     const long long img = (long long)g.H * g.W * g.C * 2;
     const long long span = ((256 + (long long)g.P * g.Q - 1) / ((long long)g.P * g.Q) + 1) * img;
-    if (g.C % 64 == 0 && g.K % BN == 0 && g.R * g.S <= 64 && g.R < 32 && g.M < (1ll << 31) &&
+    static const bool dbg_g = getenv("ACFE_DBG_FWD_G") && atoi(getenv("ACFE_DBG_FWD_G")) != 0;  // (A/B probe)
+    if (!dbg_g && g.C % 64 == 0 && g.K % BN == 0 && g.R * g.S <= 64 && g.R < 32 && g.M < (1ll << 31) &&
         span < (1ll << 31)) {
       // persistent: one 512-thread workgroup per CU (256 CUs), a multiple of 8
       const int ny = g.Kp / BN, tiles = (int)((g.M + 255) / 256);

@@ -69,6 +69,7 @@ struct ConvGeom {
   int s2d, s2d_C, s2d_H, s2d_W, s2d_pt, s2d_pl, s2d_fill;
   int s2d_lc, s2d_amul;     // log2(s2d_C); block position a = (ab * s2d_amul) >> 5
   float s2d_rpq, s2d_rq;    // 1 / (P Q), 1 / Q of the block grid
+  int cmaj;  // k_conv_fwd_g fp32: K-tiles chunk-major (ACFE_CONVG_CMAJ=0: tap-major, A/B)
 };
 
 // XCD-aware walk over the M tiles of a persistent grid.  Workgroups are

@@ -55,14 +55,15 @@ for w in "$@"; do
     wrnx) step wrnx_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra ;;
     infx) step infx_bench 600 python bench.py --workload infer --steps 5 --warmup 2 --no-cpu-baseline ;;
     strx) step strx_bench 600 python bench.py --workload stream --dtype fp32 --steps 3 --warmup 1 --no-cpu-baseline ;;
-    inf0) ACFE_CONVG_RIN=0 step inf0_bench 600 python bench.py --workload infer --steps 5 --warmup 2 --no-cpu-baseline ;;
-    str0) ACFE_CONVG_RIN=0 step str0_bench 600 python bench.py --workload stream --dtype fp32 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    inf0) ACFE_CONVG_CMAJ=0 step inf0_bench 600 python bench.py --workload infer --steps 5 --warmup 2 --no-cpu-baseline ;;
+    str0) ACFE_CONVG_CMAJ=0 step str0_bench 600 python bench.py --workload stream --dtype fp32 --steps 3 --warmup 1 --no-cpu-baseline ;;
     wrnp0) ACFE_DGRAD_S2D=0 step wrnp0_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wrnp0_prof -o run -- \
            python bench.py --no-cpu-baseline --no-extra --model wrn --classes 2 --steps 5 --warmup 2 ;;
     s2db) step s2db 300 python tools/s2d_bench.py && ACFE_DGRAD_S2D=0 step s2db0 300 python tools/s2d_bench.py ;;
     trwrn) step trwrn 700 bash tools/step_traffic.sh wrn_r05 --model wrn --classes 2 ;;
     trt1) step trt1 700 bash tools/step_traffic.sh t1_r05 ;;
     wrnsub0) ACFE_SUB_FUSE=0 step wrnsub0_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra ;;
+    s2dg) ACFE_DBG_FWD_G=1 step s2dg 300 python tools/s2d_bench.py ;;
     t1nx) step t1nx_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     t1f0) ACFE_BN_BWD_FUSE=0 step t1f0_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     wrnnx) step wrnnx_bench 600 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline ;;
