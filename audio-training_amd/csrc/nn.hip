@@ -140,7 +140,7 @@ __device__ __forceinline__ void slab_sum(const double* __restrict__ part, int nr
 // Requires the grid stride (gridDim.x * 256 vectors) to be a multiple of C/8,
 // so every vector a thread visits has the same channel group.
 __device__ __forceinline__ void stats8_flush(const double* a, const double* b, int cv, int C, bool active,
-                                             double* red, double* __restrict__ part) {
+                                             double* red, double* __restrict__ part, int nt = 256) {
   if (active) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -149,7 +149,7 @@ __device__ __forceinline__ void stats8_flush(const double* a, const double* b, i
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C; i += 256) part[(long long)blockIdx.x * 2 * C + i] = red[i];
+  for (int i = threadIdx.x; i < 2 * C; i += nt) part[(long long)blockIdx.x * 2 * C + i] = red[i];
 }
 
 static bool stats8_ok(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0 && C <= 2048; }
@@ -557,8 +557,15 @@ struct PoolAdd {
   int H, W, k, P, Q, pt, pl, sub;
 };
 
+// threads per workgroup of k_bn_bwd_apply8: with the channel-sum slab the grid
+// is fixed at acfe_reduce_blocks(rows) workgroups (<= 1024), so the block size
+// sets how many 16-B vectors are in flight per CU
+#ifndef ACFE_BWD_APPLY_NT
+#define ACFE_BWD_APPLY_NT 256
+#endif
+constexpr int BWD_APPLY_NT = ACFE_BWD_APPLY_NT;
 template <typename TG, typename TX, typename TO>
-__global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy, const TX* __restrict__ x,
+__global__ void __launch_bounds__(BWD_APPLY_NT) k_bn_bwd_apply8(const TG* __restrict__ dy, const TX* __restrict__ x,
                                                        unsigned nvec, int C, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int relu,
                                                        const float* __restrict__ coef, const TO* __restrict__ add,
@@ -568,7 +575,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
   extern __shared__ double smd[];
   double* red = smd;
   float* sm = reinterpret_cast<float*>(smd + (sum_part ? 2 * C : 0));
-  for (int i = threadIdx.x; i < C; i += 256) {
+  for (int i = threadIdx.x; i < C; i += BWD_APPLY_NT) {
     sm[i] = scale[i];
     sm[C + i] = shift[i];
     sm[2 * C + i] = coef[i];
@@ -582,8 +589,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
   double sa[8], sb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
-  const unsigned v0 = blockIdx.x * 256 + threadIdx.x;
-  for (unsigned v = v0; v < nvec; v += gridDim.x * 256) {
+  const unsigned v0 = blockIdx.x * BWD_APPLY_NT + threadIdx.x;
+  for (unsigned v = v0; v < nvec; v += gridDim.x * BWD_APPLY_NT) {
     const int c0 = (int)(v % CV) * 8;
     float g[8], xv[8], o[8];
     ld8(dy + (size_t)v * 8, g);
@@ -633,7 +640,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply8(const TG* __restrict__ dy
       for (int j = 0; j < 8; ++j) sa[j] += rnd(o[j], TO());  // the stored value
     }
   }
-  if (sum_part) stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, sum_part);
+  if (sum_part) stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, sum_part, BWD_APPLY_NT);
 }
 
 static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_dtype, long long rows, int C,
@@ -649,7 +656,7 @@ static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_
     const int grid = sum_part ? red_blocks(rows) : vgrid(n / 8);
     const size_t shm = 5 * C * sizeof(float) + (sum_part ? 2 * C * sizeof(double) : 0);
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
-        hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(grid), dim3(256), shm, strm(stream), (const TG*)dy,
+        hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(grid), dim3(BWD_APPLY_NT), shm, strm(stream), (const TG*)dy,
                            (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu, coef, (const TO*)add, d, (TO*)dx,
                            sum_part, pa))));
   } else {
