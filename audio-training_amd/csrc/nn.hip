@@ -564,7 +564,7 @@ struct PoolAdd {
 #define ACFE_BWD_APPLY_NT 256
 #endif
 constexpr int BWD_APPLY_NT = ACFE_BWD_APPLY_NT;
-template <typename TG, typename TX, typename TO>
+template <typename TG, typename TX, typename TO, bool REG>
 __global__ void __launch_bounds__(BWD_APPLY_NT) k_bn_bwd_apply8(const TG* __restrict__ dy, const TX* __restrict__ x,
                                                        unsigned nvec, int C, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int relu,
@@ -590,54 +590,76 @@ __global__ void __launch_bounds__(BWD_APPLY_NT) k_bn_bwd_apply8(const TG* __rest
 #pragma unroll
   for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.0;
   const unsigned v0 = blockIdx.x * BWD_APPLY_NT + threadIdx.x;
-  for (unsigned v = v0; v < nvec; v += gridDim.x * BWD_APPLY_NT) {
-    const int c0 = (int)(v % CV) * 8;
-    float g[8], xv[8], o[8];
-    ld8(dy + (size_t)v * 8, g);
-    ld8(x + (size_t)v * 8, xv);
-    if (add) ld8(add + (size_t)v * 8, o);
-    if (pa.g && pa.sub) {
-      const unsigned row = v / CV, t = row / (unsigned)pa.W;
-      const int w = (int)(row - t * (unsigned)pa.W), h = (int)(t % (unsigned)pa.H), nn = (int)(t / (unsigned)pa.H);
-      const int p = h / pa.k, q = w / pa.k;
-      if (h == p * pa.k && w == q * pa.k && p < pa.P && q < pa.Q) {
+  // With the channel-sum slab (grid = acfe_reduce_blocks, 256 % (C / 8) == 0)
+  // a thread's 8 channels are fixed across the grid-stride loop: its 5 x 8
+  // coefficients are held in registers instead of read from LDS per element
+  // (r05u, same box: 2.72 -> 2.62 ms at wr_resnet's stage-1 tensors with
+  // dropout, 385 -> 341 us at T1's 64x128, 1.57 -> 1.35 ms at 64x257x128);
+  // the many-workgroup grid without the slab keeps the LDS reads (measured
+  // level or slower with registers; its own instantiation keeps 6 waves per
+  // SIMD)
+  {
+    float kc[REG ? 5 : 1][8];
+    if constexpr (REG) {
+      const int cf = (int)(v0 % CV) * 8;
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kc[q][j] = sm[q * C + cf + j];
+    }
+    auto kcf = [&](int q, int c, int j) __attribute__((always_inline)) {
+      if constexpr (REG) return kc[q][j];
+      else return sm[q * C + c];
+    };
+    for (unsigned v = v0; v < nvec; v += gridDim.x * BWD_APPLY_NT) {
+      const int c0 = (int)(v % CV) * 8;
+      float g[8], xv[8], o[8];
+      ld8(dy + (size_t)v * 8, g);
+      ld8(x + (size_t)v * 8, xv);
+      if (add) ld8(add + (size_t)v * 8, o);
+      if (pa.g && pa.sub) {
+        const unsigned row = v / CV, t = row / (unsigned)pa.W;
+        const int w = (int)(row - t * (unsigned)pa.W), h = (int)(t % (unsigned)pa.H), nn = (int)(t / (unsigned)pa.H);
+        const int p = h / pa.k, q = w / pa.k;
+        if (h == p * pa.k && w == q * pa.k && p < pa.P && q < pa.Q) {
+          ld8(reinterpret_cast<const TO*>(pa.g) + (((size_t)nn * pa.P + p) * pa.Q + q) * C + c0, o);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = 0.f;  // (0 + r, as the materialised zero gradient adds)
+        }
+      } else if (pa.g) {
+        const unsigned row = v / CV, t = row / (unsigned)pa.W;
+        const int w = (int)(row - t * (unsigned)pa.W), h = (int)(t % (unsigned)pa.H), nn = (int)(t / (unsigned)pa.H);
+        const int p = (h + pa.pt) / pa.k, q = (w + pa.pl) / pa.k;
+        const int h0 = max(p * pa.k - pa.pt, 0), h1 = min(p * pa.k - pa.pt + pa.k, pa.H);
+        const int w0 = max(q * pa.k - pa.pl, 0), w1 = min(q * pa.k - pa.pl + pa.k, pa.W);
+        const float inv = 1.0f / (float)((h1 - h0) * (w1 - w0));
         ld8(reinterpret_cast<const TO*>(pa.g) + (((size_t)nn * pa.P + p) * pa.Q + q) * C + c0, o);
-      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = 0.f;  // (0 + r, as the materialised zero gradient adds)
+        for (int j = 0; j < 8; ++j) o[j] *= inv;
       }
-    } else if (pa.g) {
-      const unsigned row = v / CV, t = row / (unsigned)pa.W;
-      const int w = (int)(row - t * (unsigned)pa.W), h = (int)(t % (unsigned)pa.H), nn = (int)(t / (unsigned)pa.H);
-      const int p = (h + pa.pt) / pa.k, q = (w + pa.pl) / pa.k;
-      const int h0 = max(p * pa.k - pa.pt, 0), h1 = min(p * pa.k - pa.pt + pa.k, pa.H);
-      const int w0 = max(q * pa.k - pa.pl, 0), w1 = min(q * pa.k - pa.pl + pa.k, pa.W);
-      const float inv = 1.0f / (float)((h1 - h0) * (w1 - w0));
-      ld8(reinterpret_cast<const TO*>(pa.g) + (((size_t)nn * pa.P + p) * pa.Q + q) * C + c0, o);
+      const bool has_add = add || pa.g;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] *= inv;
-    }
-    const bool has_add = add || pa.g;
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        const float gj = ((relu & 1) && !(xv[j] * kcf(0, c, j) + kcf(1, c, j) > 0.f)) ? 0.f : g[j];
+        const float r = __builtin_fmaf(kcf(2, c, j), gj, __builtin_fmaf(kcf(3, c, j), xv[j], kcf(4, c, j)));
+        o[j] = has_add ? o[j] + r : r;
+        if ((relu & 2) && !(xv[j] > 0.f)) o[j] = 0.f;  // x = ReLU output upstream: its backward
+      }
+      if (drop.on) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      const float gj = ((relu & 1) && !(xv[j] * sm[c] + sm[C + c] > 0.f)) ? 0.f : g[j];
-      const float r = __builtin_fmaf(sm[2 * C + c], gj, __builtin_fmaf(sm[3 * C + c], xv[j], sm[4 * C + c]));
-      o[j] = has_add ? o[j] + r : r;
-      if ((relu & 2) && !(xv[j] > 0.f)) o[j] = 0.f;  // x = ReLU output upstream: its backward
-    }
-    if (drop.on) {
+        for (int j = 0; j < 8; ++j) o[j] = rnd(o[j], TO());
+        drop_apply8<TO>(drop, (uint64_t)v * 8, i32, o);
+      }
+      st8(dx + (size_t)v * 8, o);
+      if (sum_part) {
+        // (the slab's sum-of-squares row stays zero: only the bias gradient --
+        // the first row, acfe_channel_sum_finalize -- reads this slab, and the
+        // f64 square-sum was half of this pass's double-precision work)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = rnd(o[j], TO());
-      drop_apply8<TO>(drop, (uint64_t)v * 8, i32, o);
-    }
-    st8(dx + (size_t)v * 8, o);
-    if (sum_part) {
-      // (the slab's sum-of-squares row stays zero: only the bias gradient --
-      // the first row, acfe_channel_sum_finalize -- reads this slab, and the
-      // f64 square-sum was half of this pass's double-precision work)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sa[j] += rnd(o[j], TO());  // the stored value
+        for (int j = 0; j < 8; ++j) sa[j] += rnd(o[j], TO());  // the stored value
+      }
     }
   }
   if (sum_part) stats8_flush(sa, sb, (int)(v0 % CV), C, v0 < nvec, red, sum_part, BWD_APPLY_NT);
@@ -656,9 +678,12 @@ static int bn_bwd_apply_impl(const void* dy, int dy_dtype, const void* x, int x_
     const int grid = sum_part ? red_blocks(rows) : vgrid(n / 8);
     const size_t shm = 5 * C * sizeof(float) + (sum_part ? 2 * C * sizeof(double) : 0);
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
-        hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO>), dim3(grid), dim3(BWD_APPLY_NT), shm, strm(stream), (const TG*)dy,
-                           (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu, coef, (const TO*)add, d, (TO*)dx,
-                           sum_part, pa))));
+        if (sum_part) hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO, true>), dim3(grid), dim3(BWD_APPLY_NT), shm,
+                                         strm(stream), (const TG*)dy, (const TX*)x, (unsigned)(n / 8), C, scale, shift,
+                                         relu, coef, (const TO*)add, d, (TO*)dx, sum_part, pa);
+        else hipLaunchKernelGGL((k_bn_bwd_apply8<TG, TX, TO, false>), dim3(grid), dim3(BWD_APPLY_NT), shm,
+                                strm(stream), (const TG*)dy, (const TX*)x, (unsigned)(n / 8), C, scale, shift, relu,
+                                coef, (const TO*)add, d, (TO*)dx, sum_part, pa))));
   } else {
     if (sum_part) return ACFE_E_INVAL;
     DISPATCH1(dy_dtype, TG, DISPATCH1(x_dtype, TX, DISPATCH1(dx_dtype, TO,
