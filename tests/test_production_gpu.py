@@ -245,6 +245,47 @@ def test_strided_dgrad_wr_resnet_production(env, cuda, H, W, C, K, R, st):
     _within_ulp(dx, xr.grad.permute(0, 2, 3, 1), what="strided dgrad")
 
 
+# Randomised strided-dgrad sweep: the super-pixel GEMM (bf16, K % 64 == 0,
+# C a power of two) and the phase fallback (C = 48, 96) at "same" / "valid"
+# padding, strides 2 / 3, 3x3 / 1x1 / 2x2 / 5x5 filters, odd and even sizes
+_S2D_SWEEP = [
+    # N, H, W, C, K, R, st, padding
+    (2, 17, 30, 64, 128, 3, 2, "same"), (1, 30, 17, 32, 64, 3, 2, "valid"), (2, 25, 26, 128, 64, 3, 3, "same"),
+    (1, 19, 40, 16, 128, 3, 3, "valid"), (2, 16, 21, 64, 64, 1, 2, "valid"), (1, 23, 24, 128, 256, 1, 3, "valid"),
+    (2, 14, 18, 64, 64, 2, 2, "same"), (1, 21, 22, 32, 128, 5, 2, "same"), (1, 20, 33, 64, 128, 5, 3, "same"),
+    (2, 15, 19, 48, 64, 3, 2, "same"), (1, 18, 20, 96, 128, 3, 3, "same"), (2, 4, 5, 64, 64, 3, 2, "same"),
+]
+
+
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", _S2D_SWEEP, ids=lambda v: str(v))
+def test_strided_dgrad_sweep(env, cuda, N, H, W, C, K, R, st, pad):
+    """acfe_conv2d_dgrad at stride 2 / 3 against the float64 adjoint of the
+    padded strided conv of the same bf16 operands: every element within one
+    bf16 ulp + 1e-4, every pixel written (the tap-less positions as zeros)."""
+    ops, call, lib, ptr, stream = env
+    g = torch.Generator(device="cpu").manual_seed(H * 131 + W * 7 + C + K + R + st)
+    w = (torch.randn((K, R, R, C), generator=g) * (1.0 / (R * C ** 0.5))).to(cuda)
+    if pad == "same":
+        P, pt = ops.same_padding(H, R, st)
+        Q, pl = ops.same_padding(W, R, st)
+    else:
+        P, Q, pt, pl = ops.valid_out(H, R, st), ops.valid_out(W, R, st), 0, 0
+    dy = (torch.randn((N, P, Q, K), generator=g) * 0.5).to(BF).to(cuda)
+    wf = ops.pack_weights(w, BF, True)
+    dx = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
+    nb = lib.acfe_conv2d_dgrad_workspace(N, P, Q, K, C, R, R, st, pt, pl, H, W, 1)
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=cuda)
+    call("acfe_conv2d_dgrad", ptr(dy), N, P, Q, K, ptr(wf), C, R, R, st, pt, pl, H, W, ptr(dx), 1, ptr(ws), stream())
+    torch.cuda.synchronize()
+    wd = w.cpu().to(BF).to(F64).permute(0, 3, 1, 2)
+    gd = dy.cpu().to(F64).permute(0, 3, 1, 2)
+    xr = torch.zeros((N, C, H, W), dtype=F64, requires_grad=True)
+    xp = F.pad(xr, (pl, max(0, (Q - 1) * st + R - W - pl), pt, max(0, (P - 1) * st + R - H - pt)))
+    (F.conv2d(xp, wd, stride=st) * gd).sum().backward()
+    assert torch.isfinite(dx.float()).all()
+    _within_ulp(dx, xr.grad.permute(0, 2, 3, 1), what="strided dgrad sweep")
+
+
 def test_bird_t1_shape_eval_parity(cuda):
     """wr_resnet_bird at the T1 input (128 mels x 513 frames, 50 classes), bf16,
     eval-mode BN, 2 clips, against the bf16-storage float64 oracle
