@@ -3719,8 +3719,11 @@ static int launch_1x1(const ConvGeom& g, const void* x, const void* wp, const fl
 template <typename T>
 static int launch_fwd(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y,
                       double* stats, int grid_m, hipStream_t s) {
-  if (sizeof(T) == 2 && g.R == 1 && g.S == 1 && g.st == 1 && g.pt == 0 && g.pl == 0 && g.C % 8 == 0 &&
-      g.K % 4 == 0 && g.ldy == g.K && ((g.C <= 32 && g.K <= 128) || (g.K <= 32 && g.C <= 128))) {
+  // (k_conv1x1_reg maps output pixel m to input pixel m: P x Q must be H x W --
+  // the strided dgrad's phase convs can have one more output row / column)
+  if (sizeof(T) == 2 && g.R == 1 && g.S == 1 && g.st == 1 && g.pt == 0 && g.pl == 0 && g.P == g.H &&
+      g.Q == g.W && g.C % 8 == 0 && g.K % 4 == 0 && g.ldy == g.K &&
+      ((g.C <= 32 && g.K <= 128) || (g.K <= 32 && g.C <= 128))) {
     const int ncs = (g.C + 31) / 32, nkb = (g.K + 15) / 16;
     if (nkb >= 4 && g.K != nkb * 16) goto general;  // WIDE tile stores whole 16-channel blocks
     // dispatch on (reduction steps, 16-channel output blocks)
