@@ -63,6 +63,20 @@ CONV_CASES = [
     (2, 10, 64, 128, 128, 3, 3, 1, "same"),
     (2, 9, 128, 64, 64, 3, 3, 1, "same"),
     (1, 6, 64, 192, 128, 3, 3, 1, "same"),
+    # r05 sweep of the dispatch paths at ragged sizes: rows K = 64 / one-wave
+    # K = 128 with partial row and column tiles, c16, narrow K = 32 / 16, cw
+    # (32 -> 128, 16 -> 256), a stride-2 "valid" 3x3 and 1x1 at odd sizes,
+    # a K = 192 generic layer
+    (2, 13, 70, 64, 64, 3, 3, 1, "same"),
+    (1, 9, 130, 128, 128, 3, 3, 1, "same"),
+    (2, 7, 33, 16, 64, 3, 3, 1, "same"),
+    (2, 10, 20, 128, 32, 3, 3, 1, "same"),
+    (2, 12, 24, 256, 16, 3, 3, 1, "same"),
+    (2, 12, 24, 32, 128, 3, 3, 1, "same"),
+    (2, 6, 40, 16, 256, 3, 3, 1, "same"),
+    (1, 5, 7, 64, 64, 3, 3, 2, "valid"),
+    (2, 11, 13, 64, 128, 1, 1, 2, "valid"),
+    (2, 9, 17, 64, 192, 3, 3, 1, "same"),
     # register-weight 1x1 kernel (C or K <= 32)
     (2, 18, 30, 16, 64, 1, 1, 1, "valid"),
     (2, 11, 37, 32, 96, 1, 1, 1, "same"),
