@@ -19,7 +19,8 @@ def load(d):
     per = defaultdict(lambda: defaultdict(float))  # kernel -> dispatch -> value
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            per[r["Kernel_Name"].split("(")[0]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+            per[name][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
     return per
 
 
