@@ -4291,7 +4291,7 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
 #define WB(KB_, CW_, NR_)                                                                                       \
   hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_, NR_, true>), gr, dim3(512), 0, s, g, (const uint16_t*)x,  \
                      (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
-    if (amax || wp != 1 && !c16k64) return ACFE_E_INVAL;
+    if (amax || (wp != 1 && !c16k64)) return ACFE_E_INVAL;
     if (c16k64 && nr == 2) WB(64, 16, 2);
     else if (cw == 64 && g.K == 64 && nr == 2) WB(64, 64, 2);
     else if (cw == 64 && g.K == 32 && nr == 2) WB(32, 64, 2);
