@@ -615,7 +615,11 @@ __device__ uint2 g_store_sink[64];  // never read: target of masked-off epilogue
 __device__ u32x4 g_store_sink16[64];  // the same for 16-B stores
 
 
-template <int BN, bool S2D = false>
+// RES (acfe_conv2d_fwd_add where the row-halo kernels do not apply, e.g.
+// wr_resnet's 256-channel stage 3): z = (ReLU)(conv + g.res) in the epilogue,
+// as ops.add stores it, statistics of z; the tile's residual quads are loaded
+// at the start of its last K-tile
+template <int BN, bool S2D = false, bool RES = false>
 __global__ void __launch_bounds__(512, 1)
 k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_m,
@@ -731,6 +735,8 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   Stamps stp(g.dbg == 8);
+  uint2 rres[RES ? FM : 1][RES ? FN : 1];
+  bool rissued = false;  // RES: this step issued a stage after the residual loads
   while (ctm < walk.end) {
     stp.mark(0);
     // stage `done` landed: leave the younger stage (if issued) and stores in flight
@@ -746,6 +752,20 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     lds_barrier();
     stp.mark(2);
     pend = false;
+    if constexpr (RES) {
+      if (ckt == nkt - 1) {
+        const int pb = ctm * BM + wm * TWM + (lane & 15);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) {
+            const int pix = pb + fm * 16, c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
+            rres[fm][fn] = *reinterpret_cast<const uint2*>(
+                pix < M ? g.res + (long long)pix * g.ldy + c : reinterpret_cast<const uint16_t*>(g_zero_page));
+          }
+      }
+      rissued = itm < walk.end;
+    }
     if (itm < walk.end) issue();
     stp.mark(3);
     {
@@ -777,6 +797,10 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     if (++ckt < nkt) continue;
     // ---- epilogue of tile ctm (acc[fm][fn][jj] = channel (lane>>4)*4+jj of pixel lane&15)
     ckt = 0;
+    if constexpr (RES) {  // the residual quads (older than this step's stage, if any)
+      if (rissued) wait_vmcnt<LPS>();
+      else wait_vmcnt<0>();
+    }
     float sv[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) sv[i] = 0.f;
@@ -826,6 +850,12 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         for (int jj = 0; jj < 4; ++jj) {
           h[jj] = f2bf(acc[fm][fn][jj] + bv[fn][jj]);
           if (g.drop.on) h[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(h[jj])));
+          if constexpr (RES) {
+            const unsigned rw = jj < 2 ? rres[fm][fn].x : rres[fm][fn].y;
+            float z = bf2f(h[jj]) + __uint_as_float((jj & 1) ? (rw & 0xffff0000u) : (rw << 16));
+            if (g.res_relu) z = fmaxf(z, 0.f);
+            h[jj] = f2bf(z);
+          }
           if constexpr (!S2D) {  // (the dgrad has no statistics)
             const float f = inb ? bf2f(h[jj]) : 0.f;
             sv[fn * 4 + jj] += f;
@@ -4665,7 +4695,7 @@ ACFE_API int acfe_conv2d_rows_supported(int N, int H, int W, int C, int K, int R
 // Shapes the generic (C % 8 == 0) kernel takes with the Add in its row stores:
 // wr_resnet_bird's stage-2/3 conv2b (32 -> 128, 16 / 32 -> 256 channels).
 static bool fwd_add_generic_ok(int N, int H, int W, int C, int K, int dtype) {
-  return dtype == ACFE_DTYPE_BF16 && N > 0 && H > 0 && W > 0 && C % 8 == 0 && C % 64 != 0 && K % 128 == 0 &&
+  return dtype == ACFE_DTYPE_BF16 && N > 0 && H > 0 && W > 0 && C % 8 == 0 && K % 128 == 0 &&
          pick_bn(K) == 128 && (long long)N * H * W < (1ll << 31);
 }
 
@@ -4711,6 +4741,19 @@ ACFE_API int acfe_conv2d_fwd_add(const void* x, int N, int H, int W, int C, cons
 #undef CWA
         return launch_rc("acfe_conv2d_fwd_add(cw)");
       }
+    }
+    const long long img = (long long)H * W * C * 2;
+    const long long span = ((256 + (long long)H * W - 1) / ((long long)H * W) + 1) * img;
+    if (C % 64 == 0 && span < (1ll << 31)) {
+      // the persistent GEMM with the residual epilogue (wr_resnet's stage 3)
+      const int tiles = (int)((g.M + 255) / 256);
+      int gp = 256 / ny;
+      if (gp > tiles) gp = tiles;
+      if (gp >= 64) gp &= ~7;
+      hipLaunchKernelGGL((k_conv_fwd_p<128, false, true>), dim3(gp, ny), dim3(512), 0, strm(stream), g,
+                         (const uint16_t*)x, (const uint16_t*)wpacked, bias, (uint16_t*)y, stats_partial, tiles,
+                         acfe_conv2d_stats_rows(g.M, K));
+      return launch_rc("acfe_conv2d_fwd_add(persistent)");
     }
     hipLaunchKernelGGL((k_conv_fwd_g<uint16_t, 128, 128, 2, 2, true>), dim3(gm, ny), dim3(256), 0, strm(stream), g,
                        (const uint16_t*)x, (const uint16_t*)wpacked, bias, (uint16_t*)y, stats_partial, tiles_m);

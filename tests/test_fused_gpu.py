@@ -504,12 +504,14 @@ def test_sub_link_node(env, cuda, k):
 
 
 @pytest.mark.parametrize("relu", [False, True])
-@pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128), (32, 128), (16, 256), (32, 256), (128, 128)])
+@pytest.mark.parametrize("C,K", [(64, 64), (128, 64), (64, 128), (32, 128), (16, 256), (32, 256), (128, 128),
+                                 (256, 256), (128, 256)])
 def test_conv_add_node(env, cuda, relu, C, K):
     """(ReLU)(conv 3x3 + shortcut) with the Add in the conv epilogue
     (acfe_conv2d_fwd_add: the rows kernel -- K = C = 128: the one-wave
-    k_conv3x3_1w<3> --, or for the stage-2/3 conv2b shapes C = 16 / 32,
-    K = 128 / 256 the generic kernel with the Add in its row stores) ==
+    k_conv3x3_1w<3> --, for the stage-2/3 conv2b shapes C = 16 / 32,
+    K = 128 / 256 the generic kernel with the Add in its row stores, for
+    wr_resnet's 256-channel stage 3 the persistent GEMM k_conv_fwd_p<RES>) ==
     conv2d -> add: z bit-exact, statistics to 1e-6, gradients of x,
     w, b and the shortcut identical up to summation order."""
     ops = env[0]
