@@ -98,7 +98,7 @@ ACFE_API int acfe_plan_create(int sr, int n_fft, int hop, int n_mels, double fmi
     band[3 * m + 1] = e - s + 1;
     band[3 * m + 2] = (int)vals.size();
     for (int k = s; k <= e; ++k) vals.push_back(w_host[(size_t)m * nb + k]);
-    while (vals.size() & 7) vals.push_back(0.f);  // k_mel_w3 reads whole 8-tap groups
+    while (vals.size() & 7) vals.push_back(0.f);  // k_mel_w4 reads whole 8-tap groups
     kmin = s < kmin ? s : kmin;
     kmax = e > kmax ? e : kmax;
   }
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(1024) k_norm_stats(const float* __restrict__ x
 // norm1 with the division as a multiply by rinv = RN(1 / rng) and one FMA
 // correction (Markstein): q = RN(t rinv), e = t - rng q (exact by FMA),
 // RN(q + e rinv) = RN(t / rng) -- the correctly rounded quotient without the
-// ~10-instruction division sequence (k_mel_w3 divides every sample of every
+// ~10-instruction division sequence (k_mel_w4 divides every sample of every
 // overlapping frame; exhaustive-style check of the identity: 20 000 random
 // float32 pairs incl. all-ones-mantissa divisors, exact rational arithmetic)
 __device__ __forceinline__ float norm1r(float v, float mn, float rng, float rinv) {
@@ -504,57 +504,7 @@ __global__ void __launch_bounds__(256) k_mel(const float* __restrict__ raw, int6
   }
 }
 
-// ---- n_fft = 4096 (NC = 2048 = 16 x 16 x 8): radix-16 / 16 / 8 Stockham
-// passes with every butterfly in VGPRs (k_mel_w3 below).
-template <>
-__device__ __forceinline__ void dft<16>(float2* v) {
-  // X[k1 + 4 k2] = DFT4_{n2}( W16^{n2 k1} * DFT4_{n1}(x[4 n1 + n2])[k1] )
-  float2 a[4][4];
-#pragma unroll
-  for (int n2 = 0; n2 < 4; ++n2) {
-#pragma unroll
-    for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[4 * n1 + n2];
-    dft<4>(a[n2]);
-  }
-  const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f, h = 0.70710678118654752440f;
-  a[1][1] = cmul(a[1][1], make_float2(c1, -s1));  // W16^1
-  a[1][2] = cmul(a[1][2], make_float2(h, -h));    // W16^2
-  a[1][3] = cmul(a[1][3], make_float2(s1, -c1));  // W16^3
-  a[2][1] = cmul(a[2][1], make_float2(h, -h));    // W16^2
-  a[2][2] = mul_mi(a[2][2]);                      // W16^4
-  a[2][3] = cmul(a[2][3], make_float2(-h, -h));   // W16^6
-  a[3][1] = cmul(a[3][1], make_float2(s1, -c1));  // W16^3
-  a[3][2] = cmul(a[3][2], make_float2(-h, -h));   // W16^6
-  a[3][3] = cmul(a[3][3], make_float2(-c1, s1));  // W16^9
-#pragma unroll
-  for (int k1 = 0; k1 < 4; ++k1) {
-    float2 b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
-    dft<4>(b);
-#pragma unroll
-    for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
-  }
-}
-
-// The twiddles W^{r t} of a radix-R butterfly from W^t, W^{2t}, W^{4t}, W^{8t}
-// (at most two extra complex products each).
-template <int R>
-__device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
-  // bw = {W^t, W^2t, W^4t, W^8t}
-  w[0] = make_float2(1.f, 0.f);
-  w[1] = bw[0];
-  w[2] = bw[1];
-  w[3] = cmul(w[1], w[2]);
-  w[4] = bw[2];
-#pragma unroll
-  for (int r = 5; r < 8 && r < R; ++r) w[r] = cmul(w[4], w[r - 4]);
-  if constexpr (R == 16) {
-    w[8] = bw[3];
-#pragma unroll
-    for (int r = 9; r < 16; ++r) w[r] = cmul(w[8], w[r - 8]);
-  }
-}
-
-// ---- k_mel_w3 (n_fft = 4096): two waves (128 threads) per frame, 4 frames
+// ---- k_mel_w4 (n_fft = 4096): two waves (128 threads) per frame, 4 frames
 // per workgroup.  Frame + periodic Hann (computed, not loaded) + the 4096-point
 // real FFT as a 2048-point complex FFT of the even / odd sample pairs (radix
 // 16 / 16 / 8 Stockham passes through a 16 KB LDS frame buffer, base twiddles
@@ -563,7 +513,7 @@ __device__ __forceinline__ void twiddle_pows(const float2* bw, float2* w) {
 // band per lane, zero-padded 8-tap groups).  r04 over the r02-r03 kernel
 // (k_mel_w2: padded LDS, pass-3 results stored and re-read by the
 // post-processing, 148 VGPRs): one LDS round trip fewer, no bank conflicts,
-// 128 VGPRs (4 waves per SIMD); T1 1.16 -> 0.91 ms per 512 clips.
+// 128 VGPRs (4 waves per SIMD); T1 1.16 -> 0.91 ms per 512 clips (k_mel_w3).
 //  * LDS holds the 2048 points unpadded under the XOR swizzle msw(i) = i ^
 //    ((i >> 4) & 15): ds_write_b64 serves 16-lane groups on 32 banks (a
 //    float2 index mod 16 per lane), ds_read_b64 32-lane groups on 64 banks
@@ -603,28 +553,154 @@ __device__ __forceinline__ float2 w16(int r) {
   }
 }
 
-// real-FFT bin from the complex bins zk = Z[k], zm = Z[2048 - k] and W_4096^k
-__device__ __forceinline__ float rbin_power(float2 zk, float2 zm, float2 rt) {
-  const float2 E = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-  const float2 D = make_float2(zk.x - zm.x, zk.y + zm.y);
-  const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);
-  const float2 X = cadd(E, cmul(rt, O));
+// r05 (k_mel_w3 -> k_mel_w4): every complex value in a (re, im) register pair
+// and its arithmetic in packed f32 (v_pk_add / v_pk_mul / v_pk_fma_f32: both
+// halves per instruction, the f32 VALU's full rate -- k_mel_w3 issued one half
+// per instruction and was VALU-issue bound: 4 890 VALU per wave of 4 frames on
+// pre-normalised input, now 2 757; profiles/r05/sq_mel_r05z.md).  The products
+// by -i (swap + negate) and by a conjugate fold into VOP3P op_sel / neg
+// modifiers (inline asm: the compiler materialises the swap with moves);
+// products by compile-time twiddles use w and (-w.y, w.x) so they stay one
+// v_pk_mul + one v_pk_fma.  |X|^2 is kept as 4 |X|^2 and the band sums scaled
+// by 1/4 (|X|: 1/2) -- a power of two, so the same bits.  The normalize-on-
+// load arithmetic is the same IEEE sequence per lane (contraction off there);
+// the FFT and the band sums (two partial sums per lane, even and odd taps)
+// differ from the scalar kernel only in rounding.  The power is a template
+// parameter (k_mel_w3 evaluated the |X| square root of every bin and selected).
+typedef float v2f __attribute__((ext_vector_type(2)));
+#ifndef ACFE_MEL_CUT
+#define ACFE_MEL_CUT 0  // timing-only builds: stop each frame after pass 1 / 2 / 3 / the power spectrum
+#endif
+
+__device__ __forceinline__ v2f sp2(float x) { return v2f{x, x}; }
+// a + (-i) b = (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ v2f pk_addmi(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a - (-i) b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ v2f pk_submi(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a + conj(b), a - conj(b)
+__device__ __forceinline__ v2f pk_addc(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ v2f pk_subc(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a b: (a.x b.x, a.x b.y) then (.x - a.y b.y, .y + a.y b.x)
+__device__ __forceinline__ v2f pk_cmul(v2f a, v2f b) {
+  const v2f t = a.xx * b;
+  v2f r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=v"(r)
+      : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+// a w for a compile-time w, with wr = (-w.y, w.x)
+__device__ __forceinline__ v2f pk_cmulk(v2f a, v2f w, v2f wr) { return __builtin_elementwise_fma(a.yy, wr, a.xx * w); }
+__device__ __forceinline__ v2f w16v(int r) { const float2 w = w16(r); return v2f{w.x, w.y}; }
+__device__ __forceinline__ v2f w16k(v2f a, int r) {
+  const float2 w = w16(r);
+  return pk_cmulk(a, v2f{w.x, w.y}, v2f{-w.y, w.x});
+}
+__device__ __forceinline__ v2f pk_conj(v2f a) { return a * v2f{1.f, -1.f}; }
+
+// radix-4 DFT; MI2: v[2] enters multiplied by -i
+template <bool MI2 = false>
+__device__ __forceinline__ void pdft4(v2f* v) {
+  const v2f t0 = MI2 ? pk_addmi(v[0], v[2]) : v[0] + v[2];
+  const v2f t1 = MI2 ? pk_submi(v[0], v[2]) : v[0] - v[2];
+  const v2f t2 = v[1] + v[3], d = v[1] - v[3];
+  v[0] = t0 + t2;
+  v[2] = t0 - t2;
+  v[1] = pk_addmi(t1, d);
+  v[3] = pk_submi(t1, d);
+}
+__device__ __forceinline__ void pdft8(v2f* v) {
+  v2f e[4] = {v[0], v[2], v[4], v[6]};
+  v2f o[4] = {v[1], v[3], v[5], v[7]};
+  pdft4(e);
+  pdft4(o);
+  constexpr float c = 0.70710678118654752440f;
+  // W8^1 = c(1 - i), W8^2 = -i, W8^3 = -c(1 + i)
+  const v2f o1 = pk_cmulk(o[1], v2f{c, -c}, v2f{c, c});
+  const v2f o3 = pk_cmulk(o[3], v2f{-c, -c}, v2f{c, -c});
+  v[0] = e[0] + o[0]; v[4] = e[0] - o[0];
+  v[1] = e[1] + o1;   v[5] = e[1] - o1;
+  v[2] = pk_addmi(e[2], o[2]); v[6] = pk_submi(e[2], o[2]);
+  v[3] = e[3] + o3;   v[7] = e[3] - o3;
+}
+__device__ __forceinline__ void pdft16(v2f* v) {
+  v2f a[4][4];
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[4 * n1 + n2];
+    pdft4(a[n2]);
+  }
+  a[1][1] = w16k(a[1][1], 1);
+  a[1][2] = w16k(a[1][2], 2);
+  a[1][3] = w16k(a[1][3], 3);
+  a[2][1] = w16k(a[2][1], 2);
+  a[2][3] = w16k(a[2][3], 6);
+  a[3][1] = w16k(a[3][1], 3);
+  a[3][2] = w16k(a[3][2], 6);
+  a[3][3] = w16k(a[3][3], 9);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    v2f b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
+    if (k1 == 2)
+      pdft4<true>(b);  // a[2][2] W16^4 = -i folded into the butterfly
+    else
+      pdft4(b);
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
+  }
+}
+template <int R>
+__device__ __forceinline__ void ptwiddle_pows(const v2f* bw, v2f* w) {
+  w[0] = v2f{1.f, 0.f};
+  w[1] = bw[0];
+  w[2] = bw[1];
+  w[3] = pk_cmul(w[1], w[2]);
+  w[4] = bw[2];
+#pragma unroll
+  for (int r = 5; r < 8 && r < R; ++r) w[r] = pk_cmul(w[4], w[r - 4]);
+  if constexpr (R == 16) {
+    w[8] = bw[3];
+#pragma unroll
+    for (int r = 9; r < 16; ++r) w[r] = pk_cmul(w[8], w[r - 8]);
+  }
+}
+// 4 |X_k|^2 from zk = Z[k], zm = Z[2048 - k], rt = W_4096^k (rbin_power with
+// the halvings pulled out: 2 X = E2 + (-i) rt D)
+__device__ __forceinline__ float rbin_power4_pk(v2f zk, v2f zm, v2f rt) {  // 4 |X_k|^2
+  const v2f X = pk_addmi(pk_addc(zk, zm), pk_cmul(rt, pk_subc(zk, zm)));
   return X.x * X.x + X.y * X.y;
 }
-
-// LDS float2 at byte address a of the frame buffer
-__device__ __forceinline__ float2& lds2(float2* buf, unsigned a) {
-  return *reinterpret_cast<float2*>(reinterpret_cast<char*>(buf) + a);
+__device__ __forceinline__ v2f& lds2v(v2f* buf, unsigned a) {
+  return *reinterpret_cast<v2f*>(reinterpret_cast<char*>(buf) + a);
 }
 
+template <int POW>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
-k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restrict__ stats, int pad_mode, int power,
+k_mel_w4(const float* __restrict__ raw, int64_t cs, int n, const float* __restrict__ stats, int pad_mode, int,
          int n_frames, int fpw, int hop, const float2* __restrict__ tw, const float2* __restrict__ rtw,
          const int* __restrict__ band, const float* __restrict__ vals, int n_mels, int kmin, int kmax,
          float* __restrict__ out, int layout) {
   constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16;
-  extern __shared__ float2 wbuf[];
-  float* pw = reinterpret_cast<float*>(wbuf);
+  extern __shared__ float2 wbuf_[];
+  v2f* wbuf = reinterpret_cast<v2f*>(wbuf_);
+  float* pw = reinterpret_cast<float*>(wbuf_);
   const int nk = kmax - kmin + 1;
   const int tid = threadIdx.x;
   // XCD-aware work order: the hardware places workgroup L (x fastest) on XCD
@@ -643,148 +719,152 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
   const float rinv = __fdiv_rn(1.0f, rng);
   const int f0 = (item - b * gx) * fpw;
   const int j0 = tid, j1 = tid ? 256 - tid : 128;
-  // base twiddles held across frames: pass 2 W^{8 (t & 15) 2^q}, pass 3
-  // W^{t 2^q}, post W_4096^t; the j1 = 256 - t ones follow per frame as
-  // W^{256 2^q} conj(W^{t 2^q}) and W_16 conj(W_4096^t) (lane 0: j1 = 128)
-  float2 bw2[1][4], e0[3], rb0;
+  v2f bw2[4], e0[3], rb0;
   {
     const int t = (tid & 15) * 8;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bw2[0][q] = tw[(t << q) & (NC - 1)];
+    for (int q = 0; q < 4; ++q) {
+      const float2 w = tw[(t << q) & (NC - 1)];
+      bw2[q] = v2f{w.x, w.y};
+    }
 #pragma unroll
-    for (int q = 0; q < 3; ++q) e0[q] = tw[(j0 << q) & (NC - 1)];
-    rb0 = rtw[j0];
+    for (int q = 0; q < 3; ++q) {
+      const float2 w = tw[(j0 << q) & (NC - 1)];
+      e0[q] = v2f{w.x, w.y};
+    }
+    rb0 = v2f{rtw[j0].x, rtw[j0].y};
   }
-  // swizzled byte addresses: every access of a pass is its lane base XOR a
-  // compile-time constant (+ an immediate offset), see msw():
-  //   pass-1 rows  msw(16 j + r)            = msw(16 j) ^ r
-  //   pass-2 reads msw(j + 128 r)           = (msw(j) ^ 8 (r & 1)) + 128 r
-  //   pass-2 rows  msw(256 J + x + 16 r)    = ((256 J + x) ^ r) + 16 r
-  //   pass-3 reads msw(j + 256 r)           = msw(j) + 256 r
   const unsigned ua = (unsigned)msw(16 * tid) * 8u, ub = (unsigned)msw(tid) * 8u;
   const unsigned uc = (unsigned)(256 * (tid >> 4) + (tid & 15)) * 8u;
   const unsigned ud0 = (unsigned)msw(j0) * 8u, ud1 = (unsigned)msw(j1) * 8u;
-  // the lane's first mel band (band pairs (m, n_mels - 1 - m): wave 0 the
-  // low band, wave 1 the high one): its descriptor and first MAXG 8-tap
-  // weight groups are loaded each frame before the power vector's barrier, so
-  // their latency hides behind it (the band loop waited on them otherwise)
   constexpr int MAXG = 5;
+  // the power spectrum is kept as 4 |X|^2 (|X|^2: 2 |X|); the band sums are
+  // scaled back -- by a power of two, so bit for bit the sums of the scaled
+  // terms
+  constexpr float PSCALE = POW == 2 ? 0.25f : 0.5f;
   const int q0 = tid & 63;
+  typedef float f2a __attribute__((ext_vector_type(2), aligned(4)));
   for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
-    // (per frame: keeps the compiler from hoisting ~100 LDS addresses and
-    // twiddle products out of the loop into spilled registers)
     unsigned aa = ua, ab = ub, ac = uc, ad0 = ud0, ad1 = ud1;
     asm volatile("" : "+v"(aa), "+v"(ab), "+v"(ac), "+v"(ad0), "+v"(ad1));
-    asm volatile("" : "+v"(rb0.x), "+v"(rb0.y));
+    asm volatile("" : "+v"(rb0));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(bw2[0][q].x), "+v"(bw2[0][q].y));
+    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(bw2[q]));
 #pragma unroll
-    for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(e0[q].x), "+v"(e0[q].y));
+    for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(e0[q]));
     const int start = (pad_mode == ACFE_PAD_END) ? f * hop : f * hop - L / 2;
     const bool inb = start >= 0 && start + L <= n;
     __syncthreads();  // the previous frame's readers of pw are done
     // ---- pass 1 (radix 16, span 1) straight from memory: rows 16 t + r
     {
       const int j = tid;
-      float xa[16], xc[16], wa[16], wc[16];
-      typedef float f2a __attribute__((ext_vector_type(2), aligned(4)));
-      // periodic Hann w[n] = 0.5 - 0.5 cos(2 pi n / 4096) of samples
-      // n = 2 j + 256 r (+1): cos(theta + 2 pi r / 16) from the lane's
-      // cos / sin theta (theta_e = 2 pi j / 2048 = arg conj(W^j), theta_o =
-      // theta_e + 2 pi / 4096) -- no window loads, no window registers
-      {
-        const float ce = e0[0].x, se = -e0[0].y;
-        constexpr float c1 = 0.99999882345170190993f, s1 = 0.00153398018628476550f;  // cos / sin (2 pi / 4096)
-        const float co = ce * c1 - se * s1, so = se * c1 + ce * s1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float2 u = w16(r);  // (cos phi, -sin phi), phi = 2 pi r / 16
-          // 0.5 - 0.5 (cos t cos phi - sin t sin phi)
-          wa[r] = __builtin_fmaf(se, -0.5f * u.y, __builtin_fmaf(ce, -0.5f * u.x, 0.5f));
-          wc[r] = __builtin_fmaf(so, -0.5f * u.y, __builtin_fmaf(co, -0.5f * u.x, 0.5f));
-        }
-      }
+      v2f xv[16];
       if (inb) {
         const float* xs = xb + start + 2 * j;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const f2a x2 = *reinterpret_cast<const f2a*>(xs + 2 * r * NB0);
-          xa[r] = x2[0], xc[r] = x2[1];
-        }
+        for (int r = 0; r < 16; ++r) xv[r] = *reinterpret_cast<const f2a*>(xs + 2 * r * NB0);
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int nn = 2 * (j + r * NB0);
-          xa[r] = fetch(xb, n, start + nn, pad_mode, false, 0.f, 1.f);
-          xc[r] = fetch(xb, n, start + nn + 1, pad_mode, false, 0.f, 1.f);
+          xv[r] = v2f{fetch(xb, n, start + nn, pad_mode, false, 0.f, 1.f),
+                      fetch(xb, n, start + nn + 1, pad_mode, false, 0.f, 1.f)};
         }
       }
-      float2 v[16];
+      // periodic Hann w[n] = 0.5 - 0.5 cos(2 pi n / 4096) of the sample pair
+      // n = 2 j + 256 r (+1): cos(theta + 2 pi r / 16) from the lane's cos /
+      // sin theta (theta_e = 2 pi j / 2048 = arg conj(W^j), theta_o = theta_e +
+      // 2 pi / 4096) -- no window loads, no window registers;
+      // doubled (exactly: every rounding scales by 2) to absorb norm1r's final
+      // "* 2": (q * 2) * w == q * (2 w) bit for bit
+      const float ce = e0[0].x, se = -e0[0].y;
+      constexpr float c1 = 0.99999882345170190993f, s1 = 0.00153398018628476550f;
+      const float co = ce * c1 - se * s1, so = se * c1 + ce * s1;
+      const v2f cc = v2f{ce, co}, ss = v2f{se, so};
+      v2f v[16];
+      auto hann2 = [&](int r) __attribute__((always_inline)) {
+        const float2 u = w16(r);
+        return __builtin_elementwise_fma(ss, sp2(-u.y), __builtin_elementwise_fma(cc, sp2(-u.x), sp2(1.f)));
+      };
       if (do_norm) {
+        // norm1r per lane: the same IEEE operations, packed
+#pragma clang fp contract(off)
+        const v2f vmn = sp2(mn), vrng = sp2(rng), vri = sp2(rinv);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int nn = 2 * (j + r * NB0);
-          const bool ia = inb || in_sig(start + nn, n, pad_mode), ic = inb || in_sig(start + nn + 1, n, pad_mode);
-          v[r] = make_float2(ia ? norm1r(xa[r], mn, rng, rinv) * wa[r] : 0.f,
-                             ic ? norm1r(xc[r], mn, rng, rinv) * wc[r] : 0.f);
+          const v2f t = xv[r] - vmn;
+          const v2f q0v = t * vri;
+          const v2f e = __builtin_elementwise_fma(-q0v, vrng, t);
+          v2f q = __builtin_elementwise_fma(e, vri, q0v);
+          q = q + sp2(0.000001f);
+          q = q - sp2(0.5f);
+          v[r] = q * hann2(r);
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = make_float2(xa[r] * wa[r], xc[r] * wc[r]);
+        for (int r = 0; r < 16; ++r) {
+          const float2 u = w16(r);  // the window itself (no doubling)
+          v[r] = xv[r] * __builtin_elementwise_fma(ss, sp2(-0.5f * u.y),
+                                                   __builtin_elementwise_fma(cc, sp2(-0.5f * u.x), sp2(0.5f)));
+        }
       }
-      dft<16>(v);
+      if (do_norm && !inb) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) lds2(wbuf, aa ^ (8u * r)) = v[r];
+        for (int r = 0; r < 16; ++r) {
+          const int nn = 2 * (j + r * NB0);
+          if (!in_sig(start + nn, n, pad_mode)) v[r].x = 0.f;
+          if (!in_sig(start + nn + 1, n, pad_mode)) v[r].y = 0.f;
+        }
+      }
+      pdft16(v);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lds2v(wbuf, aa ^ (8u * r)) = v[r];
     }
     __syncthreads();
+#if ACFE_MEL_CUT == 1
+    continue;
+#endif
     // ---- pass 2 (radix 16, span 16)
     {
-      float2 v[16], w[16];
+      v2f v[16], w[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = lds2(wbuf, (ab ^ (64u * (r & 1))) + 1024u * r);
-      twiddle_pows<16>(bw2[0], w);
+      for (int r = 0; r < 16; ++r) v[r] = lds2v(wbuf, (ab ^ (64u * (r & 1))) + 1024u * r);
+      ptwiddle_pows<16>(bw2, w);
 #pragma unroll
-      for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], w[r]);
+      for (int r = 1; r < 16; ++r) v[r] = pk_cmul(v[r], w[r]);
       __syncthreads();
-      dft<16>(v);
+      pdft16(v);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) lds2(wbuf, (ac ^ (8u * r)) + 128u * r) = v[r];
+      for (int r = 0; r < 16; ++r) lds2v(wbuf, (ac ^ (8u * r)) + 128u * r) = v[r];
     }
     __syncthreads();
+#if ACFE_MEL_CUT == 2
+    continue;
+#endif
     // ---- pass 3 (radix 8, span 256): butterflies j0, j1 -> Z[j + 256 r] in registers
-    float2 z[2][8];
+    v2f z[2][8];
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const unsigned ad = p ? ad1 : ad0;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) z[p][r] = lds2(wbuf, ad + 2048u * r);
-      float2 bw[4], w[8];
+      for (int r = 0; r < 8; ++r) z[p][r] = lds2v(wbuf, ad + 2048u * r);
+      v2f bw[4], w[8];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        if (p == 0) {
-          bw[q] = e0[q];
-        } else {  // W^{(256 - t) 2^q} = W_8^{2^q} conj(W^{t 2^q}); lane 0: W^{128 2^q} = W_16^{2^q}
-          const float2 a = w16(2 << q), c = make_float2(e0[q].x, -e0[q].y);
-          bw[q] = tid ? cmul(a, c) : w16(1 << q);
-        }
-      }
-      twiddle_pows<8>(bw, w);
+      for (int q = 0; q < 3; ++q) bw[q] = p == 0 ? e0[q] : (tid ? w16k(pk_conj(e0[q]), 2 << q) : w16v(1 << q));
+      ptwiddle_pows<8>(bw, w);
 #pragma unroll
-      for (int r = 1; r < 8; ++r) z[p][r] = cmul(z[p][r], w[r]);
-      dft<8>(z[p]);
+      for (int r = 1; r < 8; ++r) z[p][r] = pk_cmul(z[p][r], w[r]);
+      pdft8(z[p]);
     }
+#if ACFE_MEL_CUT == 3
+    pw[tid] = z[0][0].x + z[0][1].x + z[0][2].x + z[0][3].x + z[0][4].x + z[0][5].x + z[0][6].x + z[0][7].x + z[1][0].x + z[1][1].x + z[1][2].x + z[1][3].x + z[1][4].x + z[1][5].x + z[1][6].x + z[1][7].x + z[0][0].y + z[1][0].y;
+    continue;
+#endif
     __syncthreads();  // every lane's pass-3 reads precede the power writes (pw aliases the FFT buffer)
-    // W_4096^{256 - t} = W_16 conj(W_4096^t); lane 0: W_4096^128 = W_32
-    const float2 rb1 = tid ? cmul(w16(1), make_float2(rb0.x, -rb0.y))
-                           : make_float2(0.98078528040323044913f, -0.19509032201612826785f);
-    // ---- real-FFT bins k = j + 256 r: the partner 2048 - k is bin 7 - r of
-    // the other butterfly (lane 0: j0 = 0 pairs with itself at (8 - r) & 7,
-    // j1 = 128 likewise at 7 - r); W_4096^k = W_4096^j W_16^r
+    const v2f rb1 = tid ? w16k(pk_conj(rb0), 1) : v2f{0.98078528040323044913f, -0.19509032201612826785f};
     {
-      int tt = tid;  // (opaque per frame: no hoisted per-bin masks / addresses)
+      int tt = tid;
       asm volatile("" : "+v"(tt));
-      // the r range of each butterfly set holding bins of [kmin, kmax]: set 0
-      // holds k = 256 r + [0, 127], set 1 k = 256 r + [128, 255]
       int rhi0 = kmax >> 8, rhi1 = kmax >= 128 ? (kmax - 128) >> 8 : -1;
       int rlo0 = kmin > 127 ? (kmin - 127 + 255) >> 8 : 0, rlo1 = kmin > 255 ? (kmin - 255 + 255) >> 8 : 0;
       asm volatile("" : "+s"(rhi0), "+s"(rhi1), "+s"(rlo0), "+s"(rlo1));
@@ -792,69 +872,91 @@ k_mel_w3(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int kb = (p ? (l0 ? 128 : 256 - tt) : tt) - kmin;
+        // bins in groups of four r (uniform skip of a group without a bin in
+        // [kmin, kmax]: T1 r >= 4); inside a group no branches, so the four
+        // dependent chains interleave (a dependent packed-f32 pair costs a
+        // wait state); bins outside the range go to the buffer's last word,
+        // which nothing reads (nk + 8 <= 2057 < 4095)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          // (uniform: no lane of this (p, r) holds a bin in [kmin, kmax] -- T1:
-          // r >= 4, half of the post-processing)
-          if (r > (p ? rhi1 : rhi0) || r < (p ? rlo1 : rlo0)) continue;
-          const float2 zm = l0 ? (p == 0 ? z[0][(8 - r) & 7] : z[1][7 - r]) : z[p ^ 1][7 - r];
-          const float2 rt = cmul(p ? rb1 : rb0, w16(r));
-          float pv = rbin_power(z[p][r], zm, rt);
-          if (power != 2) pv = sqrtf(pv);
-          const int i = kb + 256 * r;
-          if ((unsigned)i < (unsigned)nk) pw[i] = pv;
+        for (int h = 0; h < 2; ++h) {
+          if (4 * h + 3 < (p ? rlo1 : rlo0) || 4 * h > (p ? rhi1 : rhi0)) continue;
+          // stage by stage over the four bins
+          v2f ea[4], da[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = 4 * h + u;
+            const v2f zm = l0 ? (p == 0 ? z[0][(8 - r) & 7] : z[1][7 - r]) : z[p ^ 1][7 - r];
+            ea[u] = pk_addc(z[p][r], zm);
+            da[u] = pk_subc(z[p][r], zm);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) da[u] = pk_cmul(w16k(p ? rb1 : rb0, 4 * h + u), da[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) ea[u] = pk_addmi(ea[u], da[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = 4 * h + u;
+            float pv = ea[u].x * ea[u].x + ea[u].y * ea[u].y;
+            if constexpr (POW != 2) pv = sqrtf(pv);
+            const int i = kb + 256 * r;
+            pw[(unsigned)i < (unsigned)nk ? i : 2 * NC - 1] = pv;
+          }
         }
       }
     }
     if (tid == 0 && kmax == NC) {  // Nyquist bin: Z[0] with itself, W_4096^2048 = -1
-      float pv = rbin_power(z[0][0], z[0][0], make_float2(-1.f, 0.f));
-      if (power != 2) pv = sqrtf(pv);
+      float pv = rbin_power4_pk(z[0][0], z[0][0], v2f{-1.f, 0.f});
+      if constexpr (POW != 2) pv = sqrtf(pv);
       pw[NC - kmin] = pv;
     }
+#if ACFE_MEL_CUT == 4
+    continue;
+#endif
     if (tid < 8) pw[nk + tid] = 0.f;
-    int tq = tid;  // (per frame: the band registers are not held across the FFT)
+    int tq = tid;
     asm volatile("" : "+v"(tq));
     const int m0 = tq < 64 ? q0 : n_mels - 1 - q0;
     const bool b0ok = q0 < (n_mels + 1) / 2 && !(tq >= 64 && m0 == q0);
     int bs0 = 0, bp0 = 0, bo0 = 0;
     if (b0ok) bs0 = band[3 * m0], bp0 = (band[3 * m0 + 1] + 7) & ~7, bo0 = band[3 * m0 + 2];
-    float4 wv[MAXG][2];
+    float4 wg[MAXG][2];
     {
       const float4* v0 = reinterpret_cast<const float4*>(vals + bo0);
 #pragma unroll
       for (int gi = 0; gi < MAXG; ++gi) {
         const bool ok = b0ok && 8 * gi < bp0;
-        wv[gi][0] = ok ? v0[2 * gi] : make_float4(0.f, 0.f, 0.f, 0.f);
-        wv[gi][1] = ok ? v0[2 * gi + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+        wg[gi][0] = ok ? v0[2 * gi] : make_float4(0.f, 0.f, 0.f, 0.f);
+        wg[gi][1] = ok ? v0[2 * gi + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
     __syncthreads();
-    auto dot8 = [](float acc, const float4 a, const float4 c, const float* p) __attribute__((always_inline)) {
-      return acc + a.x * p[0] + a.y * p[1] + a.z * p[2] + a.w * p[3] + c.x * p[4] + c.y * p[5] + c.z * p[6] +
-             c.w * p[7];
+    auto dot8 = [](v2f acc, const float4 a, const float4 c, const float* p) __attribute__((always_inline)) {
+      acc = __builtin_elementwise_fma(v2f{a.x, a.y}, v2f{p[0], p[1]}, acc);
+      acc = __builtin_elementwise_fma(v2f{a.z, a.w}, v2f{p[2], p[3]}, acc);
+      acc = __builtin_elementwise_fma(v2f{c.x, c.y}, v2f{p[4], p[5]}, acc);
+      return __builtin_elementwise_fma(v2f{c.z, c.w}, v2f{p[6], p[7]}, acc);
     };
     if (b0ok) {
       const float* p0 = pw + (bs0 - kmin);
-      float acc = 0.f;
+      v2f acc = v2f{0.f, 0.f};
 #pragma unroll
       for (int gi = 0; gi < MAXG; ++gi)
-        if (8 * gi < bp0) acc = dot8(acc, wv[gi][0], wv[gi][1], p0 + 8 * gi);
+        if (8 * gi < bp0) acc = dot8(acc, wg[gi][0], wg[gi][1], p0 + 8 * gi);
       const float4* v0 = reinterpret_cast<const float4*>(vals + bo0);
       for (int i0 = 8 * MAXG; i0 < bp0; i0 += 8) acc = dot8(acc, v0[i0 / 4], v0[i0 / 4 + 1], p0 + i0);
       out[layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m0
-                                    : ((size_t)b * n_mels + m0) * n_frames + f] = acc;
+                                    : ((size_t)b * n_mels + m0) * n_frames + f] = (acc.x + acc.y) * PSCALE;
     }
-    // further band pairs (n_mels > 128)
     for (int q = q0 + 64; q < (n_mels + 1) / 2; q += 64) {
       const int m = tid < 64 ? q : n_mels - 1 - q;
       if (tid >= 64 && m == q) continue;
       const int s0 = band[3 * m], pl = (band[3 * m + 1] + 7) & ~7, off = band[3 * m + 2];
       const float4* v0 = reinterpret_cast<const float4*>(vals + off);
       const float* p0 = pw + (s0 - kmin);
-      float acc = 0.f;
+      v2f acc = v2f{0.f, 0.f};
       for (int i0 = 0; i0 < pl; i0 += 8) acc = dot8(acc, v0[i0 / 4], v0[i0 / 4 + 1], p0 + i0);
       out[layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m : ((size_t)b * n_mels + m) * n_frames + f] =
-          acc;
+          (acc.x + acc.y) * PSCALE;
     }
   }
 }
@@ -871,7 +973,7 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   const int T = acfe_plan_num_frames(p, n, pad_mode);
   if (p->n_fft == 4096) {
     constexpr int fpw = 4;  // frames per workgroup (2: 1.51 ms, 8: equal, r01n/r02y; r03: 2 / 8 / 16 +3 / 0 / +2 %)
-    hipLaunchKernelGGL(k_mel_w3, dim3(cdiv(T, fpw), batch), dim3(128), sizeof(float2) * 2048, strm(stream), raw, cs, n,
+    hipLaunchKernelGGL((power == 2 ? k_mel_w4<2> : k_mel_w4<1>), dim3(cdiv(T, fpw), batch), dim3(128), sizeof(float2) * 2048, strm(stream), raw, cs, n,
                        stats, pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_band, p->d_vals, p->n_mels,
                        p->kmin, p->kmax, out, layout);
     return launch_rc("acfe_mel_fwd");

@@ -397,7 +397,7 @@ def train_line(model_name, dtype, classes, batch, steps, warmup, rank, world, de
             "wgrad_tflops": round(flops_launch / (wgrad_ms * 1e-3) / 1e12, 2),
         },
         "mel_pipeline": {
-            "kernel": "k_mel_w3 (two waves per frame: frame+Hann+4096 rFFT+|X|^2+banded mel)",
+            "kernel": "k_mel_w4 (two waves per frame, packed-f32 complex arithmetic: frame+Hann+4096 rFFT+|X|^2+banded mel)",
             "avg_launch_ms": round(mel_ms, 4),
             "GBps": round(batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2),
             "hbm_frac": round(batch * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9 / MI355X_PEAK_HBM_GBS, 4),

@@ -96,7 +96,7 @@ def test_mel_streaming_windows(fe, cuda):
 @pytest.mark.parametrize("n_mels,pad_mode,norm,power", [(128, "end", True, 2), (160, "constant", True, 2),
                                                         (128, "reflect", False, 1), (40, "end", True, 2)])
 def test_mel_kernel_modes(fe, cuda, n_mels, pad_mode, norm, power):
-    """k_mel_w3 across its modes against the float64 oracle: normalise-on-load
+    """k_mel_w4 across its modes against the float64 oracle: normalise-on-load
     (stats) or raw input, the three framings (padded boundary frames), power 1
     and 2, and a plan whose bins do not fill a thread round (40 mels up to
     1.5 kHz)."""

@@ -44,7 +44,7 @@ for w in "$@"; do
              'k_conv_fwd_g<float,128,128> (wr_resnet_bird s1b0 conv21 3x3 128->128 @128x256 fp32; the 3 launches of a step: 1024 / 1024 / 351 windows, averaged)' \
              --workload stream --dtype fp32 --steps 1 --warmup 1 ;;
     e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;
-    sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w3' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w3" ;;
+    sqmel) step sqmel 400 bash -c "bash tools/pmc_sq.sh ${TAG}_mel 'k_mel_w4' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_mel k_mel_w4" ;;
     t1) bp t1 --steps 20 --warmup 5 ;;
     t1p) step t1p_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t1p_prof -o run -- \
            python bench.py --no-cpu-baseline --no-extra --steps 10 --warmup 3 ;;

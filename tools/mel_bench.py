@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Time acfe_mel_fwd (k_mel_w3: normalize-on-load, frame, Hann, 4096 rFFT,
+"""Time acfe_mel_fwd (k_mel_w4: normalize-on-load, frame, Hann, 4096 rFFT,
 |X|^2, banded mel) on the T1 batch: 512 synthetic 3 s clips at 48 kHz, 128
 mels, HIP events on the launch stream, median of --iters launches; GB/s of
 raw-in + mel-out bytes and fp32 VALU TFLOP/s (68.87 MFLOP per clip).

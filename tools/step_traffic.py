@@ -3,7 +3,7 @@
 HBM traffic table of one training step: FETCH_SIZE (KiB, doubled for the
 gfx950 wide-read undercount, MI355X_MICROARCH.md HBM section) and WRITE_SIZE
 (KiB) summed per kernel name over the profiled steps (warm-up included: the
-same work) and divided by the number of steps (k_mel_w3 dispatches, one per
+same work) and divided by the number of steps (k_mel_w4 dispatches, one per
 step); the batch generator's kernels (outside the timed step) are left out.
 usage: tools/step_traffic.py <dir> <tag> [bench args]  -> profiles/r05/step_traffic_<tag>.md"""
 import csv
@@ -28,7 +28,7 @@ def main():
     d, tag = sys.argv[1], sys.argv[2]
     args = sys.argv[3] if len(sys.argv) > 3 else ""
     fetch, write = load(f"{d}/p0"), load(f"{d}/p1")
-    steps = max(len(fetch.get("k_mel_w3", {})), 1)
+    steps = max(len(fetch.get("k_mel_w4", {})), 1)
     rows = []
     for k in set(fetch) | set(write):
         if any(s in k for s in SKIP):
