@@ -29,6 +29,7 @@ for w in "$@"; do
     testsall) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/testsall.log 2>&1
               rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
               case $rc in 0|1) ;; *) exit $rc ;; esac ;;
+    bdef) step bdef 600 python bench.py ;;
     mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
     fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r05 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
