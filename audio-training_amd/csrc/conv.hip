@@ -618,7 +618,7 @@ __device__ u32x4 g_store_sink16[64];  // the same for 16-B stores
 // RES (acfe_conv2d_fwd_add where the row-halo kernels do not apply, e.g.
 // wr_resnet's 256-channel stage 3): z = (ReLU)(conv + g.res) in the epilogue,
 // as ops.add stores it, statistics of z; the tile's residual quads are loaded
-// at the start of its last K-tile
+// two K-tiles before its epilogue
 template <int BN, bool S2D = false, bool RES = false>
 __global__ void __launch_bounds__(512, 1)
 k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
@@ -736,7 +736,17 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   Stamps stp(g.dbg == 8);
   uint2 rres[RES ? FM : 1][RES ? FN : 1];
-  bool rissued = false;  // RES: this step issued a stage after the residual loads
+  // RES: the residual quads are issued right after the stage issue of K-step
+  // rk = nkt - 3, so they have two K-steps to land (at the last K-step's
+  // start, r05: the epilogue waited on them, the conv + add 256 -> 256 ran
+  // 1.50 ms vs 1.24 ms without the add); the two step-top waits in between
+  // leave them in flight (they are younger than the stage being waited for)
+  // (reductions of fewer than 3 K-steps: issued before the last K-step's
+  // stage, as r05 did)
+  constexpr int NRES = FM * FN;
+  const bool rearly = nkt >= 3;
+  const int rk = rearly ? nkt - 3 : nkt - 1;
+  bool rfly = false, rissued = false;
   while (ctm < walk.end) {
     stp.mark(0);
     // stage `done` landed: leave the younger stage (if issued) and stores in flight
@@ -744,6 +754,9 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     if (pend) {
       if (two) wait_vmcnt<LPS + NSTORE>();
       else wait_vmcnt<NSTORE>();
+    } else if (RES && rfly) {
+      if (two) wait_vmcnt<LPS + NRES>();
+      else wait_vmcnt<NRES>();
     } else {
       if (two) wait_vmcnt<LPS>();
       else wait_vmcnt<0>();
@@ -752,21 +765,30 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     lds_barrier();
     stp.mark(2);
     pend = false;
+    auto rload = [&]() __attribute__((always_inline)) {
+      const int pb = ctm * BM + wm * TWM + (lane & 15);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int pix = pb + fm * 16, c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
+          rres[fm][fn] = *reinterpret_cast<const uint2*>(
+              pix < M ? g.res + (long long)pix * g.ldy + c : reinterpret_cast<const uint16_t*>(g_zero_page));
+        }
+    };
     if constexpr (RES) {
-      if (ckt == nkt - 1) {
-        const int pb = ctm * BM + wm * TWM + (lane & 15);
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn) {
-            const int pix = pb + fm * 16, c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
-            rres[fm][fn] = *reinterpret_cast<const uint2*>(
-                pix < M ? g.res + (long long)pix * g.ldy + c : reinterpret_cast<const uint16_t*>(g_zero_page));
-          }
+      if (!rearly && ckt == rk) {
+        rload();
+        rissued = itm < walk.end;
       }
-      rissued = itm < walk.end;
     }
     if (itm < walk.end) issue();
+    if constexpr (RES) {
+      if (rearly && ckt == rk) {
+        rload();
+        rfly = true;
+      }
+    }
     stp.mark(3);
     {
       const unsigned char* Ab = smem + cbuf * STG;
@@ -797,9 +819,17 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     if (++ckt < nkt) continue;
     // ---- epilogue of tile ctm (acc[fm][fn][jj] = channel (lane>>4)*4+jj of pixel lane&15)
     ckt = 0;
-    if constexpr (RES) {  // the residual quads (older than this step's stage, if any)
-      if (rissued) wait_vmcnt<LPS>();
-      else wait_vmcnt<0>();
+    if constexpr (RES) {
+      if (rearly) {  // the residual quads: older than every stage still in flight
+        const int younger = issued - done;
+        if (younger >= 2) wait_vmcnt<2 * LPS>();
+        else if (younger == 1) wait_vmcnt<LPS>();
+        else wait_vmcnt<0>();
+        rfly = false;
+      } else {  // older than the last K-step's stage (if issued)
+        if (rissued) wait_vmcnt<LPS>();
+        else wait_vmcnt<0>();
+      }
     }
     float sv[NV];
 #pragma unroll

@@ -77,7 +77,7 @@ for w in "$@"; do
     prob) step prob 300 bash -c "python tools/pro_bench.py && python tools/pro_bench.py 512 64 128" ;;
     resab) for v in new old new old; do
              if [ $v = new ]; then L=""; else L=$PWD/abtest/oldtree.so; fi
-             ACFE_LIB=$L step wrn_$v 300 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra
+             ACFE_LIB=$L step wrn_$v 300 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra && grep -o '"value": [0-9.]*' $O/wrn_$v.log
            done ;;
     t1nx) step t1nx_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     t1f0) ACFE_BN_BWD_FUSE=0 step t1f0_bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
