@@ -30,6 +30,10 @@ for w in "$@"; do
               rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
               case $rc in 0|1) ;; *) exit $rc ;; esac ;;
     bdef) step bdef 600 python bench.py ;;
+    libab) for r in 1 2; do for v in new ${LIBS}; do
+             if [ $v = new ]; then L=""; else L=$PWD/abtest/$v.so; fi
+             ACFE_LIB=$L step t1_$v 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra && grep -o '"value": [0-9.]*' $O/t1_$v.log
+           done; done ;;
     mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
     fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r05 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
