@@ -3203,7 +3203,14 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     const int PR = g.P / NR;  // row groups per image
     const int n = sg / (PR * QS), rem = sg - n * (PR * QS);
     const int h = (rem % PR) * NR, w0 = (rem / PR) * SEGW;
-    const T16* dyrow = dY + (((long long)n * g.P + h) * g.Q + w0) * g.K;
+    // buffer loads on the segment's image (offsets < 2^31: halo_ok); an
+    // element outside the image or the tile takes the out-of-range offset,
+    // which loads zeros -- no 64-bit address arithmetic, no branches
+    constexpr unsigned OOR = 0x80000000u;
+    const long long imgy = UNP ? (long long)n * (g.P >> 1) * (g.Q >> 1) * g.K : (long long)n * g.P * g.Q * g.K;
+    const int nby = UNP ? (g.P >> 1) * (g.Q >> 1) * g.K : g.P * g.Q * g.K;
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(dY + imgy), (short)0, nby * 2, 0x00020000);
 #pragma unroll
     for (int i = 0; i < ((part & 1) ? DPT : 0); ++i) {
       const int idx = tid + 512 * i;
@@ -3211,32 +3218,43 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       if constexpr (UNP) {
         const int ro = px / SEGW, w = w0 + px - ro * SEGW, hh = h + ro;
         const bool okd = idx < DG && w < g.Q;
-        const long long e = (((long long)n * (g.P >> 1) + (hh >> 1)) * (g.Q >> 1) + (w >> 1)) * g.K + cg * 8;
-        rd[i] = *reinterpret_cast<const u32x4*>(okd ? dY + e : zp);
-        rda[i] = *reinterpret_cast<const uint2*>(okd ? amax + e : reinterpret_cast<const uint8_t*>(zp));
+        const unsigned e = (unsigned)((((hh >> 1) * (g.Q >> 1) + (w >> 1)) * g.K) + cg * 8);
+        const __amdgpu_buffer_rsrc_t ars =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(amax + imgy), (short)0, nby, 0x00020000);
+        rd[i] = __builtin_amdgcn_raw_buffer_load_b128(yrs, okd ? e * 2u : OOR, 0, 0);
+        const auto a8 = __builtin_amdgcn_raw_buffer_load_b64(ars, okd ? e : OOR, 0, 0);
+        rda[i] = uint2{a8[0], a8[1]};
         if (i == 0) dpos = 0;
         dpos |= (unsigned)(((hh & 1) << 1) | (w & 1)) << (2 * i);
       } else {
         const int ro = px / SEGW, pw = px - ro * SEGW;  // row of the group, pixel of the segment
-        const long long eo = ((long long)ro * g.Q + pw) * g.K + cg * 8;
         const bool okd = idx < DG && w0 + pw < g.Q;
-        rd[i] = *reinterpret_cast<const u32x4*>(okd ? dyrow + eo : zp);
+        const unsigned eo = (unsigned)((((h + ro) * g.Q + w0 + pw) * g.K) + cg * 8);
+        rd[i] = __builtin_amdgcn_raw_buffer_load_b128(yrs, okd ? eo * 2u : OOR, 0, 0);
         if constexpr (BWD) {
           const long long e0 = (((long long)n * g.P + h) * g.Q + w0) * g.K;
-          rdx[i] = *reinterpret_cast<const u32x4*>(okd ? g.fb_x + e0 + eo : zp);
-          if (g.fb_add) rdr[i] = *reinterpret_cast<const u32x4*>(okd ? g.fb_add + e0 + eo : zp);
+          const __amdgpu_buffer_rsrc_t brs =
+              __builtin_amdgcn_make_buffer_rsrc((void*)(g.fb_x + imgy), (short)0, nby * 2, 0x00020000);
+          rdx[i] = __builtin_amdgcn_raw_buffer_load_b128(brs, okd ? eo * 2u : OOR, 0, 0);
+          if (g.fb_add) {
+            const __amdgpu_buffer_rsrc_t rrs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(g.fb_add + imgy), (short)0, nby * 2, 0x00020000);
+            rdr[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, okd ? eo * 2u : OOR, 0, 0);
+          }
           if (i == 0) fbase = e0, fw0 = w0;
         }
       }
     }
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(X + (long long)n * g.H * g.W * g.C), (short)0, g.H * g.W * g.C * 2, 0x00020000);
 #pragma unroll
     for (int i = 0; i < ((part & 2) ? XPT : 0); ++i) {
       const int idx = tid + 512 * i;
       const int hr = idx / (HW * XGR), r2 = idx - hr * (HW * XGR), hp = r2 / XGR, cg = r2 - hp * XGR;
       const int hin = h - g.pt + hr, win = w0 - g.pl + hp;
       const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
-      rx[i] = *reinterpret_cast<const u32x4*>(
-          ok ? X + (((long long)n * g.H + hin) * g.W + win) * g.C + cc * CW + cg * 8 : zp);
+      const unsigned ex = (unsigned)((hin * g.W + win) * g.C + cc * CW + cg * 8);
+      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? ex * 2u : OOR, 0, 0);
     }
   };
   auto sstore = [&](int buf) __attribute__((always_inline)) {
@@ -4422,6 +4440,8 @@ static int wgrad_row_halo_launch(const ConvGeom& g, const void* x, const void* d
 }
 
 static bool halo_ok(int N, int C, int K, int R, int S, int stride, int P, int Q, long long splits) {
+  // (k_wgrad3x3_halo's buffer loads address one image of x / dY in 32 bits)
+  if ((long long)P * Q * (C > K ? C : K) * 2 >= (1ll << 31)) return false;
   return R == 3 && S == 3 && stride == 1 &&
          ((C % 64 == 0 && (K == 64 || K == 128 || K == 32 || K == 256)) || (C % 64 == 0 && K == 16 && splits >= 16) ||
           ((C == 32 && (K == 128 || K == 256)) || (C == 16 && (K == 256 || (K == 64 && splits >= 16))))) &&

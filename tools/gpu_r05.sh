@@ -30,6 +30,10 @@ for w in "$@"; do
               rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
               case $rc in 0|1) ;; *) exit $rc ;; esac ;;
     bdef) step bdef 600 python bench.py ;;
+    wrnab) for r in 1 2; do for v in new ${LIBS}; do
+             if [ $v = new ]; then L=""; else L=$PWD/abtest/$v.so; fi
+             ACFE_LIB=$L step wrn_$v 300 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra && grep -o '"value": [0-9.]*' $O/wrn_$v.log
+           done; done ;;
     libab) for r in 1 2; do for v in new ${LIBS}; do
              if [ $v = new ]; then L=""; else L=$PWD/abtest/$v.so; fi
              ACFE_LIB=$L step t1_$v 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra && grep -o '"value": [0-9.]*' $O/t1_$v.log
