@@ -124,12 +124,21 @@ __device__ __forceinline__ void bldsx4s(unsigned voff, i4 desc, unsigned soff, u
 // 2x2 max-pool backward on the fly: 8 bf16 of the pooled gradient and their 8
 // argmax bytes -> the values that land on tap `pos` ((row & 1) * 2 + (col & 1)) of
 // the window, zeros elsewhere (acfe_maxpool2d_bwd_argmax's scatter, gathered).
+// Byte-parallel: the argmax bytes are window taps 0..3, so byte ^ pos is zero
+// exactly where it matches and (t | t >> 1) & 1 per byte is its "differs" bit;
+// 255 * (equal bit) is the byte mask, and v_perm doubles each byte into the
+// channel's 16-bit mask (7 VALU per 4 channels instead of 10-12 compares and
+// selects).
 __device__ __forceinline__ u32x4 unpool_mask(uint2 a, unsigned pos) {
+  const unsigned rep = pos * 0x01010101u;
   u32x4 m;
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const unsigned w = d < 2 ? a.x : a.y, sh = (d & 1) * 16;
-    m[d] = (((w >> sh) & 0xffu) == pos ? 0xFFFFu : 0u) | (((w >> (sh + 8)) & 0xffu) == pos ? 0xFFFF0000u : 0u);
+  for (int h = 0; h < 2; ++h) {
+    const unsigned t = (h ? a.y : a.x) ^ rep;
+    const unsigned eq = ~(t | (t >> 1)) & 0x01010101u;
+    const unsigned e = (eq << 8) - eq;  // 0xff per matching byte
+    m[2 * h] = __builtin_amdgcn_perm(0u, e, 0x01010000u);
+    m[2 * h + 1] = __builtin_amdgcn_perm(0u, e, 0x03030202u);
   }
   return m;
 }
