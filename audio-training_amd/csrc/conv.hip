@@ -3195,6 +3195,30 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 #pragma unroll
   for (int j = 0; j < (BWD ? 8 : 1); ++j) fs[j] = 0.f;
   // part bit 0: the dY granules, bit 1: the input halo granules
+  // lane constants of the staging granules (segment independent): dY
+  // granule i = pixel (ro, pw) of the segment, channels cg * 8; halo granule i
+  // = halo row hr, pixel hp, channels cg * 8.  A step's offsets are a scalar
+  // segment base plus these -- no per-step lane multiplies (v_mul_lo_u32 is
+  // quarter rate); granules past the tile get a row / pixel that fails the
+  // bounds test.
+  int dlo[DPT], dro[DPT], dpw[DPT];
+#pragma unroll
+  for (int i = 0; i < DPT; ++i) {
+    const int idx = tid + 512 * i;
+    const int px = idx / DGR, cg = idx - px * DGR, ro = px / SEGW, pw = px - ro * SEGW;
+    dro[i] = ro;
+    dpw[i] = idx < DG ? pw : (1 << 24);
+    dlo[i] = UNP ? (pw >> 1) * g.K + cg * 8 : (ro * g.Q + pw) * g.K + cg * 8;
+  }
+  int xlo[XPT], xhr[XPT], xhp[XPT];
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int idx = tid + 512 * i;
+    const int hr = idx / (HW * XGR), r2 = idx - hr * (HW * XGR), hp = r2 / XGR, cg = r2 - hp * XGR;
+    xhr[i] = idx < XG ? hr : (1 << 24);
+    xhp[i] = hp;
+    xlo[i] = (hr * g.W + hp) * g.C + cc * CW + cg * 8;
+  }
   auto gload = [&](int sg, int part = 3) __attribute__((always_inline)) {
     // segments walk down a 64-pixel column (row fastest): consecutive steps
     // share NR + 1 of their NR + 2 halo rows (and, UNP, their pooled dY row),
@@ -3211,35 +3235,32 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     const int nby = UNP ? (g.P >> 1) * (g.Q >> 1) * g.K : g.P * g.Q * g.K;
     const __amdgpu_buffer_rsrc_t yrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(dY + imgy), (short)0, nby * 2, 0x00020000);
+    // UNP: (h + ro) >> 1 == h >> 1 (NR <= 2, h a multiple of NR) and
+    // (w0 + pw) >> 1 == w0 / 2 + pw >> 1 (w0 a multiple of 64)
+    const int dbase = UNP ? ((h >> 1) * (g.Q >> 1) + (w0 >> 1)) * g.K : (h * g.Q + w0) * g.K;
 #pragma unroll
     for (int i = 0; i < ((part & 1) ? DPT : 0); ++i) {
-      const int idx = tid + 512 * i;
-      const int px = idx / DGR, cg = idx - px * DGR;
+      const bool okd = w0 + dpw[i] < g.Q;
+      const unsigned e = (unsigned)(dbase + dlo[i]);
       if constexpr (UNP) {
-        const int ro = px / SEGW, w = w0 + px - ro * SEGW, hh = h + ro;
-        const bool okd = idx < DG && w < g.Q;
-        const unsigned e = (unsigned)((((hh >> 1) * (g.Q >> 1) + (w >> 1)) * g.K) + cg * 8);
         const __amdgpu_buffer_rsrc_t ars =
             __builtin_amdgcn_make_buffer_rsrc((void*)(amax + imgy), (short)0, nby, 0x00020000);
         rd[i] = __builtin_amdgcn_raw_buffer_load_b128(yrs, okd ? e * 2u : OOR, 0, 0);
         const auto a8 = __builtin_amdgcn_raw_buffer_load_b64(ars, okd ? e : OOR, 0, 0);
         rda[i] = uint2{a8[0], a8[1]};
         if (i == 0) dpos = 0;
-        dpos |= (unsigned)(((hh & 1) << 1) | (w & 1)) << (2 * i);
+        dpos |= (unsigned)((((h + dro[i]) & 1) << 1) | (dpw[i] & 1)) << (2 * i);
       } else {
-        const int ro = px / SEGW, pw = px - ro * SEGW;  // row of the group, pixel of the segment
-        const bool okd = idx < DG && w0 + pw < g.Q;
-        const unsigned eo = (unsigned)((((h + ro) * g.Q + w0 + pw) * g.K) + cg * 8);
-        rd[i] = __builtin_amdgcn_raw_buffer_load_b128(yrs, okd ? eo * 2u : OOR, 0, 0);
+        rd[i] = __builtin_amdgcn_raw_buffer_load_b128(yrs, okd ? e * 2u : OOR, 0, 0);
         if constexpr (BWD) {
           const long long e0 = (((long long)n * g.P + h) * g.Q + w0) * g.K;
           const __amdgpu_buffer_rsrc_t brs =
               __builtin_amdgcn_make_buffer_rsrc((void*)(g.fb_x + imgy), (short)0, nby * 2, 0x00020000);
-          rdx[i] = __builtin_amdgcn_raw_buffer_load_b128(brs, okd ? eo * 2u : OOR, 0, 0);
+          rdx[i] = __builtin_amdgcn_raw_buffer_load_b128(brs, okd ? e * 2u : OOR, 0, 0);
           if (g.fb_add) {
             const __amdgpu_buffer_rsrc_t rrs =
                 __builtin_amdgcn_make_buffer_rsrc((void*)(g.fb_add + imgy), (short)0, nby * 2, 0x00020000);
-            rdr[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, okd ? eo * 2u : OOR, 0, 0);
+            rdr[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, okd ? e * 2u : OOR, 0, 0);
           }
           if (i == 0) fbase = e0, fw0 = w0;
         }
@@ -3247,14 +3268,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     }
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(X + (long long)n * g.H * g.W * g.C), (short)0, g.H * g.W * g.C * 2, 0x00020000);
+    const int hx = h - g.pt, wx = w0 - g.pl, xbase = (hx * g.W + wx) * g.C;
 #pragma unroll
     for (int i = 0; i < ((part & 2) ? XPT : 0); ++i) {
-      const int idx = tid + 512 * i;
-      const int hr = idx / (HW * XGR), r2 = idx - hr * (HW * XGR), hp = r2 / XGR, cg = r2 - hp * XGR;
-      const int hin = h - g.pt + hr, win = w0 - g.pl + hp;
-      const bool ok = idx < XG && (unsigned)hin < (unsigned)g.H && (unsigned)win < (unsigned)g.W;
-      const unsigned ex = (unsigned)((hin * g.W + win) * g.C + cc * CW + cg * 8);
-      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? ex * 2u : OOR, 0, 0);
+      const bool ok = (unsigned)(hx + xhr[i]) < (unsigned)g.H && (unsigned)(wx + xhp[i]) < (unsigned)g.W;
+      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? (unsigned)(xbase + xlo[i]) * 2u : OOR, 0, 0);
     }
   };
   auto sstore = [&](int buf) __attribute__((always_inline)) {

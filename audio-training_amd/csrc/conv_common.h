@@ -130,13 +130,15 @@ __device__ __forceinline__ void bldsx4s(unsigned voff, i4 desc, unsigned soff, u
 // channel's 16-bit mask (7 VALU per 4 channels instead of 10-12 compares and
 // selects).
 __device__ __forceinline__ u32x4 unpool_mask(uint2 a, unsigned pos) {
-  const unsigned rep = pos * 0x01010101u;
+  const unsigned rep = __builtin_amdgcn_perm(0u, pos, 0u);  // pos in every byte (no v_mul_lo_u32)
   u32x4 m;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const unsigned t = (h ? a.y : a.x) ^ rep;
     const unsigned eq = ~(t | (t >> 1)) & 0x01010101u;
-    const unsigned e = (eq << 8) - eq;  // 0xff per matching byte
+    unsigned e8 = eq << 8;
+    asm volatile("" : "+v"(e8));  // (kept a shift and a subtract, not a quarter-rate multiply by 255)
+    const unsigned e = e8 - eq;   // 0xff per matching byte
     m[2 * h] = __builtin_amdgcn_perm(0u, e, 0x01010000u);
     m[2 * h + 1] = __builtin_amdgcn_perm(0u, e, 0x03030202u);
   }
