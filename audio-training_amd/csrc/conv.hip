@@ -3289,9 +3289,10 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         // acfe_bn_bwd_apply_ex's arithmetic per element (k_bn_bwd_apply8):
         // g masked by the BN's ReLU, a g + b x + c, rounded to bf16, then the
         // Dropout backward of the rounded value (keep: round(v * scale))
-        const int ro = px / SEGW, pw = px - ro * SEGW;
-        const bool ok = idx < DG && fw0 + pw < g.Q;
-        const long long e = fbase + ((long long)ro * g.Q + pw) * g.K + cg * 8;
+        // (the granule's lane constants: dpw fails the column test past the
+        // tile, dlo = (ro Q + pw) K + cg 8)
+        const bool ok = fw0 + dpw[i] < g.Q;
+        const long long e = fbase + dlo[i];
         const f4* tb = reinterpret_cast<const f4*>(ftab + cg * 8);
         u32x4 v;
         // one pair hash per dword (channels 2d, 2d + 1; e is even), the four
