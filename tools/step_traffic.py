@@ -28,7 +28,8 @@ def main():
     d, tag = sys.argv[1], sys.argv[2]
     args = sys.argv[3] if len(sys.argv) > 3 else ""
     fetch, write = load(f"{d}/p0"), load(f"{d}/p1")
-    steps = max(len(fetch.get("k_mel_w4", {})), 1)
+    # one mel launch per step (the kernel name carries its template arguments)
+    steps = max(sum(len(v) for k, v in fetch.items() if k.split("<")[0].split()[-1] == "k_mel_w4"), 1)
     rows = []
     for k in set(fetch) | set(write):
         if any(s in k for s in SKIP):
