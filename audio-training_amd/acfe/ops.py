@@ -781,7 +781,8 @@ class _BNFn(torch.autograd.Function):
         ctx.mask_in = FUSE and getattr(x, "_acfe_relu_out", False)
         # x is the residual output of a _ConvAddFn whose wgrad can form this
         # BN's backward apply (acfe_conv2d_wgrad_bnbwd with `add`)
-        ctx.fold = FUSE_BN_BWD and getattr(x, "_acfe_fold_consumer", False)
+        # (the producing node opted in: conv_add(..., single_consumer=True))
+        ctx.fold = getattr(x, "_acfe_fold_consumer", None) if FUSE_BN_BWD else None
         return y
 
     @staticmethod
@@ -793,12 +794,13 @@ class _BNFn(torch.autograd.Function):
             add, pool, sub = link.take(), link.take_pool(), link.take_sub()
             if add is None and pool is None and sub is None and not link.declined:
                 raise RuntimeError("ResidualLink: the shortcut gradient was not delivered before this BN's backward")
-        if ctx.fold and pool is None and sub is None and (link is None or not link.declined):
+        if ctx.fold is not None and pool is None and sub is None and (link is None or not link.declined):
             # x's only autograd consumer is this BN (a shortcut's gradient came
             # through the link): dx is returned unwritten, its apply pending for
             # the producing conv's backward (_ConvAddFn), which forms it inside
             # its weight gradient or, failing that, runs the apply pass
             dx, dgamma, dbeta = _bn_bwd_pending(x, dy, saved, relu, training, add, ctx.mask_in, ctx.gb)
+            ctx.fold.pending = True
         else:
             dx, dgamma, dbeta = _bn_bwd(x, dy, saved, relu, training, add=add, mask_in=ctx.mask_in, pool=pool,
                                         params=ctx.gb, sub=sub)
@@ -914,7 +916,7 @@ def _bnbwd_fold_ok(x, w, u, dy, stride, pt, pl, P, Q) -> bool:
     K, R, S, _ = w.shape
     if (R, S, stride, pt, pl, P, Q) != (3, 3, 1, 1, 1, H, W) or not (x.is_contiguous() and u.is_contiguous()):
         return False
-    if u.data_ptr() % 16 or x.data_ptr() % 16:
+    if u.data_ptr() % 16 or x.data_ptr() % 16 or (dy.is_contiguous() and dy.data_ptr() % 16):
         return False
     return lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K) > 0
 
@@ -1173,7 +1175,7 @@ class _ConvAddFn(torch.autograd.Function):
     the conv output itself is never stored."""
 
     @staticmethod
-    def forward(ctx, x, w, b, sc, relu, want_stats, link):
+    def forward(ctx, x, w, b, sc, relu, want_stats, link, single):
         ctx.bias = b
         ctx.bn = bn_src(x)
         N, H, W, C = x.shape
@@ -1202,8 +1204,11 @@ class _ConvAddFn(torch.autograd.Function):
         ctx.conf = (pt, pl, relu, b is not None, link)
         if relu:
             z._acfe_relu_out = True  # a BatchNormalization reading z folds in the ReLU backward
-        if FUSE_BN_BWD:
-            z._acfe_fold_consumer = True  # its BN's backward apply may be left pending for this node
+        ctx.fold = None
+        if FUSE_BN_BWD and single:
+            # the caller guarantees z's only autograd consumer is one BN: its
+            # backward apply may be left pending for this node (_FoldToken)
+            ctx.fold = z._acfe_fold_consumer = _FoldToken()
         ctx.mark_non_differentiable(stats)
         return z, stats
 
@@ -1214,6 +1219,12 @@ class _ConvAddFn(torch.autograd.Function):
         N, H, W, C = x.shape
         K = w.shape[0]
         pend = _take_pending(g)
+        if pend is None and ctx.fold is not None and ctx.fold.pending:
+            # the BN left its dx unwritten for this node, but the gradient that
+            # arrived is another tensor: z had a second autograd consumer and
+            # autograd summed unwritten memory into it
+            raise RuntimeError("conv_add(single_consumer=True): the output fed more than one autograd consumer; "
+                               "its BatchNormalization gradient was left pending")
         if pend is not None:
             if (ctx.needs_input_grad[1] and _bnbwd_fold_ok(x, w, pend[1], g, 1, pt, pl, H, W)
                     and pend[0].data_ptr() % 16 == 0 and (pend[6] is None or pend[6].data_ptr() % 16 == 0)):
@@ -1224,8 +1235,8 @@ class _ConvAddFn(torch.autograd.Function):
                     dx, _, _ = _conv_bwd(x, w, g, 1, pt, pl, H, W, True, False, False, bias=ctx.bias, bn=ctx.bn)
                 if link is not None:
                     link.grad = g
-                    return dx, dw, db, None, None, None, None
-                return dx, dw, db, g, None, None, None
+                    return dx, dw, db, None, None, None, None, None
+                return dx, dw, db, g, None, None, None, None
             _apply_pending(g, pend)
         g = g.contiguous()
         if relu and not _tagged(g, "_acfe_relu_masked"):
@@ -1242,15 +1253,28 @@ class _ConvAddFn(torch.autograd.Function):
                                has_b and ctx.needs_input_grad[2], bias=ctx.bias, bn=ctx.bn)
         if link is not None:  # the shortcut input's gradient is added by the linked BN backward
             link.grad = g
-            return dx, dw, db, None, None, None, None
-        return dx, dw, db, g, None, None, None
+            return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, g, None, None, None, None
 
 
-def conv_add(x, w, b, sc, relu=False, want_stats=False, link=None, stride=1, padding="same"):
+class _FoldToken:
+    """Shared by a _ConvAddFn node and the BN reading its output: `pending` is
+    set when the BN's backward left its dx unwritten for the node."""
+    __slots__ = ("pending",)
+
+    def __init__(self):
+        self.pending = False
+
+
+def conv_add(x, w, b, sc, relu=False, want_stats=False, link=None, stride=1, padding="same", single_consumer=False):
     """(ReLU)(Conv2D(x) + sc) -> (z, BN statistics slab of z or empty): one node
-    when the conv epilogue covers the shape, else conv2d then add."""
+    when the conv epilogue covers the shape, else conv2d then add.
+    single_consumer: the caller guarantees z's only autograd consumer is one
+    batch_norm (the WRN blocks: the next bn2a, the shortcut's gradient through
+    its ResidualLink), so that BN's backward apply may be folded into this
+    node's weight gradient.  A second consumer then raises in the backward."""
     if _conv_add_ok(x, w, sc, stride, padding):
-        return _ConvAddFn.apply(x, w, b, sc, bool(relu), bool(want_stats), link)
+        return _ConvAddFn.apply(x, w, b, sc, bool(relu), bool(want_stats), link, bool(single_consumer))
     y, _ = conv2d(x, w, b, stride, padding)
     if want_stats:
         return add(y, sc, relu=relu, want_stats=True, link=link)

@@ -74,29 +74,51 @@ def save_checkpoint(out_dir: Path, trainer, meta: dict, history: dict | None = N
 
 
 def evaluate(trainer, dataset, multi_label, group=None):
-    """Validation loss / accuracy (Keras categorical or binary accuracy).  Under
-    data parallelism every rank evaluates its own shard and the totals are
-    summed over ranks (no rank idles inside a collective meanwhile)."""
+    """The validation pass of model.fit (audiomodel.py:550-562): the compiled
+    metrics of :859-875 (callbacks.ValMetrics: loss, accuracy, precision,
+    recall, AUC, Huber, binary focal cross-entropy) as Keras names them
+    (`val_*`).  Under data parallelism every rank evaluates its own shard and
+    the metric sums are added over ranks with one all-reduce."""
     from acfe import dp, ops
+    from callbacks import ValMetrics
 
     trainer.holder.eval()
     dev = trainer.device
-    tot = torch.zeros(3, dtype=torch.float64, device=dev)  # loss sum, correct, count
+    vm = ValMetrics(multi_label, dev)
     with torch.no_grad():
         for x, y in dp.synced_batches(dataset, group=group):
             f = trainer.frontend.forward_spec(x) if x.dim() == 3 else trainer.frontend(x)
             z = trainer.model(f)
             loss, _ = ops.loss_and_grad(z, y, trainer.loss_mode)
-            b = x.shape[0]
-            if multi_label:
-                c = ((z > 0).float() == y).float().mean(1).sum()
-            else:
-                c = (z.argmax(1) == y.argmax(1)).float().sum()
-            tot += torch.stack([loss.double().sum() * b, c.double(), torch.tensor(float(b), device=dev,
-                                                                                    dtype=torch.float64)])
+            vm.update(z, y, loss)
     trainer.holder.train()
-    loss_sum, correct, n = dp.allreduce_sums(tot.tolist(), device=dev)
-    return (loss_sum / n, correct / n) if n else (float("nan"), float("nan"))
+    logs = vm.result(torch.tensor(dp.allreduce_sums(vm.totals().tolist(), device=dev), dtype=torch.float64))
+    return logs or {"val_loss": float("nan")}
+
+
+class _Fit:
+    """What the reference's callbacks touch of keras.Model during fit: the
+    optimizer's learning rate, stop_training, and save_weights (rank 0 writes,
+    Keras *.weights.h5 layout)."""
+
+    def __init__(self, trainer, rank):
+        self.trainer, self.rank = trainer, rank
+        self.stop_training = False
+
+    @property
+    def lr(self):
+        return self.trainer.opt.lr
+
+    @lr.setter
+    def lr(self, v):
+        self.trainer.opt.lr = float(v)
+
+    def save(self, path):
+        if self.rank == 0:
+            from keras_weights import save_keras_weights
+
+            Path(path).parent.mkdir(parents=True, exist_ok=True)
+            save_keras_weights(self.trainer.model, path)
 
 
 def train_epoch(dataset, step_fn, augment, steps_per_epoch=0, mixup_fn=None, group=None):
@@ -194,9 +216,14 @@ def train_model(args):
         val_ds, _, _, _, _ = tfdataset.get_dataset(val_dir, labels, files=vfiles, record_shard=vshard,
                                                    batch_size=args.batch_size, shuffle=False, device=dev,
                                                    load_raw=load_raw)
-    history = {"loss": [], "val_loss": [], "val_accuracy": [], "clips_per_s": []}
+    history = {"loss": [], "val_loss": [], "val_accuracy": [], "clips_per_s": [], "learning_rate": []}
     out_dir = Path(args.checkpoint_dir) / args.name
-    best = float("inf")
+    import callbacks
+
+    # AudioModel.checkpoints (audiomodel.py:878-950): best-metric checkpoints,
+    # EarlyStopping(10), ReduceLROnPlateau(val_loss, mode "max"), chkpt per epoch
+    checks = callbacks.checkpoints(out_dir, multi_label=args.multi_label)
+    fit = _Fit(trainer, rank)
 
     def step(x1, y1, x2, y2, lam):
         if x2 is None:
@@ -212,21 +239,26 @@ def train_model(args):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         n_all, lsum_all = dp.allreduce_sums([n, lsum], device=dev)
-        history["loss"].append(lsum_all / max(n_all, 1))
+        logs = {"loss": lsum_all / max(n_all, 1)}
+        history["loss"].append(logs["loss"])
         history["clips_per_s"].append(n_all / dt)
         # Keras SyncOnRead MEAN of the BN moving statistics before eval / save
         dp.average_buffers(trainer.holder)
         if val_ds is not None:
-            vl, va = evaluate(trainer, val_ds, args.multi_label, ctrl)
-            history["val_loss"].append(vl)
-            history["val_accuracy"].append(va)
-            if vl < best:  # ModelCheckpoint(save_best_only) on val_loss (audiomodel.py:878-938)
-                best = vl
-                if rank == 0:
-                    save_checkpoint(out_dir / "val_loss", trainer, {}, None)
+            logs.update(evaluate(trainer, val_ds, args.multi_label, ctrl))
+            history["val_loss"].append(logs["val_loss"])
+            history["val_accuracy"].append(logs.get("val_binary_accuracy", logs.get("val_categorical_accuracy")))
+            for k, v in logs.items():
+                if k.startswith("val_") and k not in ("val_loss",):
+                    history.setdefault(k, []).append(v)
+        for cb in checks:
+            cb.on_epoch_end(epoch, logs, fit)
+        history["learning_rate"].append(logs.get("learning_rate", fit.lr))
         if rank == 0:
-            logging.info("epoch %d loss %.4f val %s %.1f clips/s (%d steps/rank)", epoch, history["loss"][-1],
-                         history["val_loss"][-1:] or "-", history["clips_per_s"][-1], steps)
+            logging.info("epoch %d loss %.4f val %s lr %g %.1f clips/s (%d steps/rank)", epoch, history["loss"][-1],
+                         history["val_loss"][-1:] or "-", fit.lr, history["clips_per_s"][-1], steps)
+        if fit.stop_training:  # EarlyStopping
+            break
     if rank == 0:
         meta_out = dict(meta)
         meta_out.update(name=args.model_name, ebird_labels=labels, labels=labels, n_mels=n_mels, fmin=fmin,
@@ -234,7 +266,7 @@ def train_model(args):
                         multi_label=args.multi_label, loss_fn="bce" if args.multi_label else "cce", load_raw=load_raw,
                         dtype=args.dtype, training_date=str(time.time()), magv2=True)
         save_checkpoint(out_dir, trainer, meta_out, history)
-        print(json.dumps({"run": args.name, "epochs": args.epochs, "final_loss": history["loss"][-1],
+        print(json.dumps({"run": args.name, "epochs": len(history["loss"]), "final_loss": history["loss"][-1],
                           "val_loss": history["val_loss"][-1:] or None, "clips_per_s": history["clips_per_s"]}))
     if world > 1:
         dist.barrier()
@@ -263,7 +295,9 @@ def parse_args(argv=None):
     p.add_argument("--shuffle", type=str2bool, default=True)
     p.add_argument("--augment", type=str2bool, default=True, help="mix_up (tfdataset.py:473-481)")
     p.add_argument("--pcen", type=str2bool, default=True)
-    p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    # the reference trains in fp32 (MIXED_PRECISION = False, audiomodel.py:55-58);
+    # bf16 is the mixed-precision policy it would otherwise set
+    p.add_argument("--dtype", choices=["bf16", "fp32"], default="fp32")
     p.add_argument("--steps-per-epoch", type=int, default=0)
     p.add_argument("--checkpoint-dir", default="checkpoints")
     p.add_argument("--seed", type=int, default=0)

@@ -24,6 +24,13 @@
 //                 weights over Cin; exact up to fp reassociation).
 #include "conv_common.h"
 
+// Timing-only ablations of the BN-fold weight gradient (they skip work and
+// compute wrong results): only in `make ablate` builds (libacfe_ablate.so)
+#if !defined(ACFE_ABLATE) && (defined(ACFE_FB_NOXFORM) || defined(ACFE_FB_NOSUM) || defined(ACFE_FB_NOSTORE) || \
+                              defined(ACFE_FB_MID))
+#error "ACFE_FB_* ablation switches belong to `make ablate` builds only"
+#endif
+
 using namespace acfe;
 
 
@@ -4088,7 +4095,9 @@ S2dPlan s2d_plan(int N, int P, int Q, int K, int C, int R, int S, int st, int pt
   const long long U = (H + pt + st - 1) / st, V = (W + pl + st - 1) / st;
   const long long img = (long long)P * Q * K * 2;
   const long long span = ((256 + (long long)P * Q - 1) / ((long long)P * Q) + 1) * img;
-  p.ok = on && dtype == ACFE_DTYPE_BF16 && st > 1 && st * st < 32 && (C & (C - 1)) == 0 && K % 64 == 0 &&
+  // st <= 4: the epilogue's block row a = (ab * ceil(32 / st)) >> 5 is exact
+  // for ab < st * st only at strides 2, 3 and 4 (stride 5: ab = 23 gives 5)
+  p.ok = on && dtype == ACFE_DTYPE_BF16 && st > 1 && st <= 4 && (C & (C - 1)) == 0 && K % 64 == 0 &&
          p.kout % p.bn == 0 && p.mr * p.ms <= 64 && (long long)N * ((H + pt + st - 1) / st) * ((W + pl + st - 1) / st) < (1 << 24) &&
          pt >= 0 && pl >= 0 && pt < st && pl < st && (long long)N * U * V < (1ll << 31) && span < (1ll << 31);
   return p;

@@ -13,6 +13,12 @@
 // and the filterbank is applied as a banded sum (1839 taps at M=128 instead
 // of the reference's dense 128x2049 batch_dot).
 #include "common.h"
+
+// ACFE_MEL_CUT stops each frame after pass N (timing only, wrong results):
+// only in `make ablate` builds (libacfe_ablate.so)
+#if !defined(ACFE_ABLATE) && defined(ACFE_MEL_CUT)
+#error "ACFE_MEL_CUT belongs to `make ablate` builds only"
+#endif
 #include <cmath>
 #include <cstdlib>
 #include <cstring>

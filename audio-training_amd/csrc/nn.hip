@@ -560,10 +560,10 @@ struct PoolAdd {
 // threads per workgroup of k_bn_bwd_apply8: with the channel-sum slab the grid
 // is fixed at acfe_reduce_blocks(rows) workgroups (<= 1024), so the block size
 // sets how many 16-B vectors are in flight per CU
-#ifndef ACFE_BWD_APPLY_NT
-#define ACFE_BWD_APPLY_NT 256
-#endif
-constexpr int BWD_APPLY_NT = ACFE_BWD_APPLY_NT;
+// (256: the REG path and stats8_flush assume each thread keeps the same 8
+// channels across its grid-stride loop, i.e. gridDim * 256 a multiple of
+// C / 8, which stats8_ok guarantees for this block size only)
+constexpr int BWD_APPLY_NT = 256;
 template <typename TG, typename TX, typename TO, bool REG>
 __global__ void __launch_bounds__(BWD_APPLY_NT) k_bn_bwd_apply8(const TG* __restrict__ dy, const TX* __restrict__ x,
                                                        unsigned nvec, int C, const float* __restrict__ scale,

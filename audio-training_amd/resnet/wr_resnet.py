@@ -54,7 +54,7 @@ class BasicBlock(nn.Module):
         sc = x if self.shortcut is None else self.shortcut(x, link=link)
         want = self.training and ops.FUSE
         z, st = ops.conv_add(y, self.conv2b.weight, self.conv2b.bias, sc, relu=True, want_stats=want,
-                             link=link if self.shortcut is None else None,
+                             single_consumer=True, link=link if self.shortcut is None else None,
                              stride=self.conv2b.strides, padding=self.conv2b.padding)
         return z, (st if want else None)
 

@@ -77,7 +77,8 @@ class BasicBlock(nn.Module):
         add_link = link if self.shortcut is None else None
         want = training and ops.FUSE
         z, st = ops.conv_add(y, self.conv2b.weight, self.conv2b.bias, sc, relu=self.relu_out, want_stats=want,
-                             link=add_link, stride=self.conv2b.strides, padding=self.conv2b.padding)
+                             single_consumer=True, link=add_link, stride=self.conv2b.strides,
+                             padding=self.conv2b.padding)
         return z, (st if want else None)
 
 

@@ -242,10 +242,13 @@ def main():
     out, _ = train_line(a.model, dtype, a.classes, a.batch, a.steps, a.warmup, rank, world, dev, dist)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps, a.model, a.classes)
-        suite = ROOT / "profiles" / "r02_cpu_baseline.json"
-        if suite.exists():  # the other workloads' CPU rows (tools/cpu_baseline.py, same host type)
+        # the other workloads' CPU rows (tools/cpu_baseline.py on a GPU box's
+        # host cores, same host type), newest round first
+        suite = next((p for p in (ROOT / "profiles" / f"r{r:02d}_cpu_baseline.json" for r in range(9, 1, -1))
+                      if p.exists()), None)
+        if suite is not None:
             try:
-                out["cpu_baseline"]["suite"] = {"source": "profiles/r02_cpu_baseline.json",
+                out["cpu_baseline"]["suite"] = {"source": f"profiles/{suite.name}",
                                                 **json.loads(suite.read_text())["rows"]}
             except (ValueError, KeyError):
                 pass
@@ -265,6 +268,16 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def active_switches():
+    """The ACFE_* environment switches of this process (A/B and diagnostic
+    flags of acfe/ops.py and the C library; empty on the default product
+    path) and the library that was loaded -- recorded in every bench line."""
+    from acfe import _lib
+
+    return {"env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("ACFE_")},
+            "library": os.path.relpath(_lib.LIB_PATH, ROOT) if hasattr(_lib, "LIB_PATH") else None}
 
 
 def _summary(o):
@@ -412,6 +425,7 @@ def train_line(model_name, dtype, classes, batch, steps, warmup, rank, world, de
                            if trainer.buckets is not None else None),
         "model_tflops_fwd_bwd": round(3 * (flops_per_clip(model) if flops_per_clip else 64.956e9) * value / 1e12, 2),
         "final_loss": round(loss_v, 5),
+        "switches": active_switches(),
     }
     return out, trainer
 
@@ -652,6 +666,7 @@ def run_inference(a, workload=None, steps=None, warmup=None, emit=True):
                      "flops_per_launch": flops_launch, "counters": counters},
         "mel_pipeline": {"avg_launch_ms": round(mel_ms, 4),
                          "GBps": round(avg_clips * FRONTEND_BYTES_PER_CLIP / (mel_ms * 1e-3) / 1e9, 2)},
+        "switches": active_switches(),
     }
     return out
 

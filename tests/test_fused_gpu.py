@@ -540,6 +540,53 @@ def test_conv_add_node(env, cuda, relu, C, K):
         assert rel(outs[1][i], outs[0][i]) < 1e-3, (i, rel(outs[1][i], outs[0][i]))
 
 
+@pytest.mark.parametrize("mode", ["single", "opt_out", "second_consumer"])
+def test_conv_add_bn_fold_consumers(env, cuda, mode):
+    """The BN-backward fold into conv_add's weight gradient is opt-in
+    (single_consumer=True): with one BN consumer the folded
+    gradients equal the unfused chain; without the opt-in a second consumer of
+    z (a BN and another op) gets correct gradients; opted in while z has a
+    second consumer, the backward raises instead of reading unwritten memory."""
+    ops = env[0]
+    N, H, W, C, K = 2, 14, 128, 64, 64
+    g = torch.Generator(device="cpu").manual_seed(43)
+    x0 = torch.randn((N, H, W, C), generator=g).to(torch.bfloat16).to(cuda)
+    s0 = torch.randn((N, H, W, K), generator=g).to(torch.bfloat16).to(cuda)
+    w0 = (torch.randn((K, 3, 3, C), generator=g) * 0.05).to(cuda)
+    b0 = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    gy = torch.randn((N, H, W, K), generator=g).to(torch.bfloat16).to(cuda)
+    gamma0 = (1 + 0.2 * torch.randn(K, generator=g)).to(cuda)
+    beta0 = (0.1 * torch.randn(K, generator=g)).to(cuda)
+
+    def run(fused, single, second):
+        x = x0.clone().requires_grad_(True)
+        w, b = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        gamma, beta = gamma0.clone().requires_grad_(True), beta0.clone().requires_grad_(True)
+        mm, mv = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
+        if fused:
+            z, st = ops.conv_add(x, w, b, s0, relu=True, want_stats=True, single_consumer=single)
+        else:
+            y, _ = ops.conv2d(x, w, b)
+            z, st = ops.add(y, s0, relu=True, want_stats=True)
+        out = ops.batch_norm(z, gamma, beta, mm, mv, True, relu=True, stats=st)
+        loss = (out.float() * gy.float()).sum()
+        if second:
+            loss = loss + (z.float() * 0.5).sum()
+        loss.backward()
+        return [x.grad, w.grad, b.grad, gamma.grad, beta.grad]
+
+    if mode == "second_consumer":
+        with pytest.raises(RuntimeError, match="pending"):
+            run(True, True, True)
+        return
+    second = mode == "opt_out"
+    ref = run(False, False, second)
+    got = run(True, mode == "single", second)
+    for i, (a, r) in enumerate(zip(got, ref)):
+        assert torch.isfinite(a).all()
+        assert rel(a, r) < 2e-3, (i, rel(a, r))
+
+
 @pytest.mark.parametrize("W", [66, 67])
 @pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32], ids=["bf16", "f32"])

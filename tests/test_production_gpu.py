@@ -254,6 +254,10 @@ _S2D_SWEEP = [
     (1, 19, 40, 16, 128, 3, 3, "valid"), (2, 16, 21, 64, 64, 1, 2, "valid"), (1, 23, 24, 128, 256, 1, 3, "valid"),
     (2, 14, 18, 64, 64, 2, 2, "same"), (1, 21, 22, 32, 128, 5, 2, "same"), (1, 20, 33, 64, 128, 5, 3, "same"),
     (2, 15, 19, 48, 64, 3, 2, "same"), (1, 18, 20, 96, 128, 3, 3, "same"), (2, 4, 5, 64, 64, 3, 2, "same"),
+    # stride 4 takes the super-pixel GEMM; stride 5 must fall back to the
+    # phase path (its block-row multiply is not exact: ADVICE r05)
+    (2, 21, 26, 64, 64, 3, 4, "same"), (1, 17, 23, 64, 64, 3, 4, "valid"), (2, 26, 27, 64, 64, 3, 5, "same"),
+    (1, 23, 31, 64, 64, 5, 5, "valid"),
 ]
 
 

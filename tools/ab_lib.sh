@@ -12,7 +12,7 @@ case $1 in
     cd $ROOT/audio-training_amd/csrc
     for f in *.hip; do
       extra=""; { [ $f = pool1w.hip ] || [ $f = frontend.hip ]; } && extra=-fno-slp-vectorize
-      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $flags $extra -c $f -o $out/${f%.hip}.o &
+      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -DACFE_ABLATE $flags $extra -c $f -o $out/${f%.hip}.o &
     done
     wait
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $ROOT/abtest/$name.so $out/*.o

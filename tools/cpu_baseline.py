@@ -16,7 +16,7 @@ faithful CPU restatement (oracle/: kind "port"):
   * config P   -- 256-clip synthetic 2-class TFRecord set (build.py), read by
                   tfdataset.AudioDataset, wr_resnet training at batch 8.
 Medians over the timed repetitions; the sample of each row is stated.
-usage: python tools/cpu_baseline.py [--out profiles/r02_cpu_baseline.json] [--quick]"""
+usage: python tools/cpu_baseline.py [--out profiles/r06_cpu_baseline.json] [--quick]"""
 import argparse
 import json
 import os
@@ -73,7 +73,7 @@ def model_params(kind, classes):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=str(ROOT / "profiles" / "r02_cpu_baseline.json"))
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r06_cpu_baseline.json"))
     ap.add_argument("--quick", action="store_true", help="small samples (smoke run)")
     a = ap.parse_args()
     from oracle import frontend as of
