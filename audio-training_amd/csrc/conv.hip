@@ -3779,6 +3779,11 @@ static int launch_fwd_t(const ConvGeom& g, const void* x, const void* wp, const 
           const int rc = launch_plain1w(g, x, wp, bias, y, stats, grid_m, s, "acfe_conv2d_fwd", 0);
           if (rc != ACFE_E_INVAL) return rc;
         }
+        if constexpr (BN == 64) {
+          // the epilogue beside the next tile's MFMAs (rows64.hip)
+          const int rc = launch_r64(g, x, wp, bias, y, stats, grid_m, s, "acfe_conv2d_fwd", g.drop.on ? 4 : 0);
+          if (rc != ACFE_E_INVAL) return rc;
+        }
 #define ROWS(TR_, PM_, ...)                                                                                   \
   hipLaunchKernelGGL((k_conv3x3_rows<BN, TR_, PM_, ##__VA_ARGS__>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x, \
                      (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, grid_m, nullptr)
@@ -4629,6 +4634,11 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
     return launch_rows_tr<KB, PM, 4, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
   } else {
     static_assert(KB == 64, "rows kernels: K in {64, 128}");
+    if constexpr (PM == 0 || PM == 3 || PM == 4) {
+      // the epilogue beside the next tile's MFMAs (rows64.hip)
+      const int rc = launch_r64(g, x, wp, bias, y, stats, srows, s, what, PM);
+      if (rc != ACFE_E_INVAL) return rc;
+    }
     if constexpr (PM != 2) {
       // BatchNormalization prologue (acfe_conv2d_bn_prologue_supported)
       if (g.pro_sc) return launch_rows_tr<KB, PM, 8, true, true>(g, x, wp, bias, y, stats, srows, amax, s, what);
@@ -4672,6 +4682,8 @@ ACFE_API int acfe_conv2d_dgrad_bn(const void* dy, int N, int P, int Q, int K, co
   g.bn_mu = mean;
   g.bn_is = invstd;
   g.bn_relu = relu ? 1 : 0;
+  const int rc = launch_r64(g, dy, wflip, nullptr, dx, part, rows, strm(stream), "acfe_conv2d_dgrad_bn", 5);
+  if (rc != ACFE_E_INVAL) return rc;
   return launch_rows_tr<64, 5, 8, true>(g, dy, wflip, nullptr, dx, part, rows, nullptr, strm(stream),
                                         "acfe_conv2d_dgrad_bn");
 }

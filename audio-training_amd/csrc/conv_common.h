@@ -176,6 +176,11 @@ int launch_pool1w(const ConvGeom& g, const void* x, const void* wp, const float*
 // (pm 0: plain / dropout / BN sums; pm 3: + the residual g.res (+ReLU) of acfe_conv2d_fwd_add)
 int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                    int srows, hipStream_t s, const char* what, int pm);
+// the K = 64 row-halo convolutions with the epilogue between the next tile's
+// MFMA groups (rows64.hip): pm 0 plain / BN sums, 4 + dropout, 3 + residual,
+// 5 the dgrad with the BN backward reduce; ACFE_E_INVAL when not its case
+int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
+               int srows, hipStream_t s, const char* what, int pm);
 // acfe_conv2d_dgrad_unpool at K = C = 128 on the same kernel (PM 2)
 int launch_unpool1w(const ConvGeom& g, const void* dyp, const void* wflip, void* dx, uint8_t* amax, hipStream_t s,
                     const char* what);

@@ -234,6 +234,14 @@ int acfe_conv2d_dgrad_bn(const void* dy, int N, int P, int Q, int K, const void*
                          int stride, int pad_top, int pad_left, int H, int W, void* dx, int dtype,
                          const void* x_bn, const float* scale, const float* shift, const float* mean,
                          const float* invstd, int relu, double* part, int part_rows, void* stream);
+/* Kernel-variant switch for A/B checks and the parity tests: 1 (default, or
+ * the ACFE_R64 environment variable) runs the K = 64 row-halo convolutions
+ * (acfe_conv2d_fwd / _dropout / _bn / _add / _add_bn, acfe_conv2d_dgrad at
+ * stride 1, acfe_conv2d_dgrad_bn) on the kernel that overlaps each tile's
+ * epilogue with the next tile's MFMAs; 0 on the previous kernel (identical
+ * results).  Returns the previous setting.  Not stream-ordered: set it
+ * between launches. */
+int acfe_conv_r64_enable(int on);
 /* float count of the wgrad split-K workspace. */
 long long acfe_conv2d_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q);
 /* dW (fp32 KRSC) = beta*dW + sum_pixels dY (x) im2col(X). */

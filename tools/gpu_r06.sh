@@ -30,6 +30,9 @@ for w in "$@"; do
               rc=$?; echo "== testsall rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/testsall.log | tail -30
               case $rc in 0|1) ;; *) exit $rc ;; esac ;;
     bdef) step bdef 600 python bench.py ;;
+    r64t) step r64t 300 python -u -m pytest tests/test_r64_gpu.py -x -v --timeout 120 --timeout-method thread ;;
+    t1x) step t1x_bench 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
+    wrnq) step wrnq_bench 300 python bench.py --model wrn --classes 2 --steps 8 --warmup 3 --no-cpu-baseline --no-extra ;;
     bench2) step bench2 600 python -u -m pytest tests/test_bench_gpu.py -x -v --timeout 420 --timeout-method thread ;;
     cpub) step cpub 900 python tools/cpu_baseline.py ;;
     wrnab) for r in 1 2; do for v in new ${LIBS}; do
