@@ -43,6 +43,13 @@
 
 using namespace acfe;
 
+#ifdef ACFE_R64_STAMPS
+// diagnostic build (make stamps): per-wave s_memtime totals of the step
+// segments (groups of rs = 0 / 1 / 2, the closing wait + barrier of each, the
+// restage + pack), read back by acfe_debug_r64_stamps (tools/r64_stamps.py)
+__device__ unsigned long long g_r64_stamps[4096 * 8];
+#endif
+
 template <int PM, int NCH, bool PRO, bool ST>
 __global__ void __launch_bounds__(512, 1)
 k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
@@ -255,14 +262,18 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
   u32x4 eld[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) eld[i] = u32x4{0u, 0u, 0u, 0u};
-  // (bitwise, not short-circuit: no branches inside an MFMA group)
+  // unit u's pixel: tile row 2 wp + u / 4 (wave-uniform: scalar), column
+  // (u % 4) * 16 + l16; the lane parts of its byte offset and of its dropout
+  // Weyl term are formed once (no per-unit multiplies; mod 2^32 like the
+  // direct form).  Bitwise, not short-circuit: no branches inside an MFMA group.
+  const unsigned lane_o = ((unsigned)l16 * (unsigned)g.ldy + (unsigned)c0) * 2u;
+  const unsigned lane_h = ((unsigned)l16 * (unsigned)(KB / 2) + (unsigned)(c0 >> 1)) * 0x9E3779B1u;
   auto unit_px = [&](int u, int tm, bool live, int& n, unsigned& o, bool& inb) __attribute__((always_inline)) {
     int hb, wb;
     tile_of(tm, n, hb, wb);
-    const int p = wp * (TR * 16) + u * 16;
-    const int hh = hb * TR + p / SEGW, ww = wb * SEGW + (p % SEGW) + l16;
-    inb = live & (hh < g.P) & (ww < g.Q);
-    o = ((unsigned)(hh * g.Q + ww) * (unsigned)g.ldy + c0) * 2u;
+    const int hh = hb * TR + 2 * wp + (u >> 2), wc = wb * SEGW + (u & 3) * 16;
+    inb = live & (hh < g.P) & (wc + l16 < g.Q);
+    o = (unsigned)(hh * g.Q + wc) * (unsigned)g.ldy * 2u + lane_o;
   };
   auto unit_load = [&](int u, int tm, bool live) __attribute__((always_inline)) {
     if constexpr (PM == 3 || PM == 5) {
@@ -297,9 +308,9 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
       // the first pair advanced by a constant (M * K < 2^32: launcher)
       int hb, wb;
       tile_of(tm, n, hb, wb);
-      const int p = wp * (TR * 16) + u * 16;
-      const unsigned pix = ((unsigned)n * g.P + hb * TR + p / SEGW) * g.Q + wb * SEGW + (p % SEGW) + l16;
-      const uint32_t hw0 = ((pix * (unsigned)KB + c0) >> 1) * 0x9E3779B1u + (uint32_t)g.drop.seed;
+      const unsigned spix = ((unsigned)n * g.P + hb * TR + 2 * wp + (u >> 2)) * g.Q + wb * SEGW + (u & 3) * 16;
+      // ((pix K + c0) >> 1) W + seed with pix = spix + l16 (K = 64, c0 even)
+      const uint32_t hw0 = spix * (unsigned)(KB / 2) * 0x9E3779B1u + lane_h + (uint32_t)g.drop.seed;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const uint32_t hsh = hash_u32_lo_w(g.drop.seed, hw0 + (uint32_t)d * 0x9E3779B1u);
@@ -312,6 +323,9 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Y + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{w8[0], w8[1], w8[2], w8[3]}, orr, inb ? o : 0x80000000u, 0, 0);
+    // pixels outside the image: their (dropped) values count as zeros in the sums
+#pragma unroll
+    for (int d = 0; d < 4; ++d) w8[d] = inb ? w8[d] : 0u;
     if constexpr (PM == 5) {
       // acfe_bn_bwd_reduce's terms of the stored dX: gm = dX masked by the BN's
       // ReLU, summed as gm and gm * (x - mean) * invstd
@@ -339,7 +353,7 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const unsigned wv = w8[e >> 1];
-        const float f = inb ? __uint_as_float((e & 1) ? (wv & 0xffff0000u) : (wv << 16)) : 0.f;
+        const float f = __uint_as_float((e & 1) ? (wv & 0xffff0000u) : (wv << 16));
         sv[e] += f;
         sv[8 + e] += f * f;
       }
@@ -382,6 +396,16 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     return n;
   };
 
+#ifdef ACFE_R64_STAMPS
+  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stl = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int i) __attribute__((always_inline)) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    stv[i] += t - stl;
+    stl = t;
+  };
+#else
+  auto stamp = [](int) __attribute__((always_inline)) {};
+#endif
   int wpar = 0;  // weight buffer of the current step (NS may be odd)
   // ---- one tile: NS steps (chunk cc = cst / 3, filter row rs = cst % 3) with
   // the previous tile's epilogue in steps 0 / 1
@@ -417,21 +441,44 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
           wf[fn] = *reinterpret_cast<const uint4*>(Wl + s * KB * 128 + (wrb[fn] ^ (kk << 6)));
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) xf[fm] = *reinterpret_cast<const uint4*>(Xl + xoff[fm] + s * XRB + kk * 64);
+        auto mfmas = [&]() __attribute__((always_inline)) {
 #pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
+          for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-          for (int fn = 0; fn < FN; ++fn) {
-            // a tile's first MFMA of an accumulator takes C = 0
-            const f4 cin = (cst == 0 && grp == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn];
-            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, wf[fn]),
-                                                                  __builtin_bit_cast(bf8, xf[fm]), cin, 0, 0, 0);
+            for (int fn = 0; fn < FN; ++fn) {
+              // a tile's first MFMA of an accumulator takes C = 0
+              const f4 cin = (cst == 0 && grp == 0) ? f4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn];
+              acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, wf[fn]),
+                                                                    __builtin_bit_cast(bf8, xf[fm]), cin, 0, 0, 0);
+            }
+        };
+#ifdef ACFE_R64_STAGGER
+        // the two waves of a SIMD (wid, wid + 4: channel halves wk 0 / 1) in
+        // complementary order: wk 0 MFMAs then the epilogue unit, wk 1 the
+        // unit (its fragment reads in flight) then the MFMAs
+        constexpr bool HAS_UNIT = cst == 0 || (cst == 1 && grp < 3);
+        if (HAS_UNIT && wk) {
+          epi_slot(std::integral_constant<int, cst>{}, std::integral_constant<int, grp>{}, ptm, live);
+          __builtin_amdgcn_sched_barrier(0);
+          mfmas();
+        } else {
+          mfmas();
+          if constexpr (HAS_UNIT) {
+            __builtin_amdgcn_sched_barrier(0);
+            epi_slot(std::integral_constant<int, cst>{}, std::integral_constant<int, grp>{}, ptm, live);
           }
+        }
+#else
+        mfmas();
         epi_slot(std::integral_constant<int, cst>{}, std::integral_constant<int, grp>{}, ptm, live);
+#endif
         __builtin_amdgcn_sched_barrier(0);
       });
       wpar ^= 1;
+      stamp(rs);
       if constexpr (rs == 2) {
         __syncthreads();  // every wave has finished reading the chunk's rows
+        stamp(5);
         sstore();
         if constexpr (cst == NS - 1) {
           // the finished tile packed (after the restage: its rows and the
@@ -443,11 +490,14 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
 #pragma unroll
           for (int u = 0; u < 3; ++u) unit_load(u, tm, true);
         }
+        stamp(6);
         wait_vmcnt<NLATE>();  // next step's weight pieces landed
         __syncthreads();
+        stamp(7);
       } else {
         wait_vmcnt<NLATE>();
         __syncthreads();
+        stamp(3 + rs);
       }
     });
   };
@@ -475,6 +525,10 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     for (int u = 0; u < FM; ++u) unit(u, tm, true);
     unit_stats();
   }
+#ifdef ACFE_R64_STAMPS
+  if (lane == 0 && blockIdx.x * 8 + wid < 4096)
+    for (int i = 0; i < 8; ++i) g_r64_stamps[(blockIdx.x * 8 + wid) * 8 + i] = stv[i];
+#endif
   wait_vmcnt<0>();
   __syncthreads();
   if (SUMS && stats) {
@@ -574,3 +628,10 @@ ACFE_API int acfe_conv_r64_enable(int on) {
   acfe::g_r64.store(on ? 1 : 0, std::memory_order_relaxed);
   return prev;
 }
+
+#ifdef ACFE_R64_STAMPS
+ACFE_API int acfe_debug_r64_stamps(unsigned long long* host, int n) {
+  if (n > 4096 * 8) n = 4096 * 8;
+  return hip_rc(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_r64_stamps), sizeof(unsigned long long) * n), "stamps");
+}
+#endif

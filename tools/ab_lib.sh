@@ -11,7 +11,7 @@ case $1 in
     out=$ROOT/abtest/$name; mkdir -p $out
     cd $ROOT/audio-training_amd/csrc
     for f in *.hip; do
-      extra=""; { [ $f = pool1w.hip ] || [ $f = frontend.hip ]; } && extra=-fno-slp-vectorize
+      extra=""; { [ $f = pool1w.hip ] || [ $f = frontend.hip ] || [ $f = rows64.hip ]; } && extra=-fno-slp-vectorize
       /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -DACFE_ABLATE $flags $extra -c $f -o $out/${f%.hip}.o &
     done
     wait

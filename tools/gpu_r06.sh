@@ -33,6 +33,10 @@ for w in "$@"; do
     r64t) step r64t 300 python -u -m pytest tests/test_r64_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     t1x) step t1x_bench 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     wrnq) step wrnq_bench 300 python bench.py --model wrn --classes 2 --steps 8 --warmup 3 --no-cpu-baseline --no-extra ;;
+    sqr64) BENCH_ARGS='--model wrn --classes 2' step sqr64 400 bash -c "bash tools/pmc_sq.sh ${TAG}_r64 'k_conv3x3_r64' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_r64 'k_conv3x3_r64<4' 'k_conv3x3_r64<3' 'k_conv3x3_r64<5'" ;;
+    r64st) step r64st 300 python tools/r64_stamps.py 512 ;;
+    sq3r64) BENCH_ARGS='--model wrn --classes 2' step sq3r64 300 bash tools/pmc_sq3.sh ${TAG}_r64mix 'k_conv3x3_r64' ;;
+    bnprobe) step bnprobe 300 python tools/bn_moving_probe.py ;;
     bench2) step bench2 600 python -u -m pytest tests/test_bench_gpu.py -x -v --timeout 420 --timeout-method thread ;;
     cpub) step cpub 900 python tools/cpu_baseline.py ;;
     wrnab) for r in 1 2; do for v in new ${LIBS}; do
@@ -51,10 +55,10 @@ for w in "$@"; do
     evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r06 'k_conv3x3_1w<1, 2, true, true, false>' 5905580032 \
              'k_conv3x3_1w<1,2,true,true> (wr_resnet_bird s1b0 branch21 3x3 128->128 @128x256 + 2x2 max-pool + dropout + BN sums, batch 512)' \
              --steps 3 --warmup 1 ;;
-    evinfer) SELECT=7:3 step evinfer 900 bash tools/pmc_evidence.sh infer_fp32 r06 'k_conv_fwd_g<float, 128, 64' 8606859264 \
+    evinfer) SELECT=7:3 step evinfer 600 bash tools/pmc_evidence.sh infer_fp32 r06 'k_conv_fwd_g<float, 128, 64' 8606859264 \
              'k_conv_fwd_g<float,128,64> (wr_resnet b1.conv2a 3x3 64->64 @128x513 fp32, batch 256)' \
              --workload infer --steps 2 --warmup 1 ;;
-    evstream) SELECT=12:1 step evstream 900 bash tools/pmc_evidence.sh stream_fp32 r06 'k_conv_fwd_g<float, 128, 128' 26832360789 \
+    evstream) SELECT=12:1 step evstream 600 bash tools/pmc_evidence.sh stream_fp32 r06 'k_conv_fwd_g<float, 128, 128' 26832360789 \
              'k_conv_fwd_g<float,128,128> (wr_resnet_bird s1b0 conv21 3x3 128->128 @128x256 fp32; the 3 launches of a step: 1024 / 1024 / 351 windows, averaged)' \
              --workload stream --dtype fp32 --steps 1 --warmup 1 ;;
     e2e) step e2e 900 python bench.py --workload e2e --clips 8192 --steps 20 --warmup 4 ;;

@@ -12,7 +12,7 @@ i=0
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
            "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES"; do
   timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "$RX" \
-      --output-format csv -d $O/p$i -o pmc -- python bench.py --no-cpu-baseline --steps 2 --warmup 1 > $O/p$i.log 2>&1
+      --output-format csv -d $O/p$i -o pmc -- python bench.py --no-cpu-baseline --no-extra --steps 2 --warmup 1 ${BENCH_ARGS:-} > $O/p$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then
     echo "pass $i rc=$rc -- stopping"; tail -5 $O/p$i.log; exit $rc
