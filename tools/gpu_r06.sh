@@ -37,6 +37,7 @@ for w in "$@"; do
     r64st) step r64st 300 python tools/r64_stamps.py 512 ;;
     sq3r64) BENCH_ARGS='--model wrn --classes 2' step sq3r64 300 bash tools/pmc_sq3.sh ${TAG}_r64mix 'k_conv3x3_r64' ;;
     bnprobe) step bnprobe 300 python tools/bn_moving_probe.py ;;
+    settle) step settle 400 python tools/learn_settle.py && step settle32 400 python tools/learn_settle.py fp32 ;;
     bench2) step bench2 600 python -u -m pytest tests/test_bench_gpu.py -x -v --timeout 420 --timeout-method thread ;;
     cpub) step cpub 900 python tools/cpu_baseline.py ;;
     wrnab) for r in 1 2; do for v in new ${LIBS}; do
