@@ -1,4 +1,6 @@
-"""The device training step learns, in bf16 and fp32.
+"""The device training step learns, in bf16 and fp32,
+and the trained model classifies through the real eval path (VERDICT r05
+next #7).
 
 A synthetic 4-class task in which each class is a chirp in its own frequency
 band (build.synth_clip's generator restricted to one band per class, at a
@@ -7,26 +9,26 @@ resnet/wr_resnet_bird.py) trains through acfe.train.Trainer -- raw clips ->
 normalize -> STFT / mel -> PCEN -> model -> CCE -> backward -> Keras Adam,
 the reference fit loop's step (audiomodel.py:550-562, loss / optimizer
 :1206-1240) -- with mix_up off, from the same initial weights in bf16 (T1's
-precision) and fp32 (the reference default).  Held-out clips are classified by
-Trainer.predict (eval-mode BN).  This is the behavioural check that the whole
-bf16 training-mode path (every BN backward, dropout, the fused nodes) moves the
-model the way fp32 does, which the per-block tests cannot show.
+precision) and fp32 (the reference default).
 
-Evaluation: Keras's moving statistics (momentum 0.99) still lag the weights
-after a few hundred steps (tools/bn_moving_probe.py, tools/learn_probe.py:
-held-out accuracy at chance with them, 99-100 % with current statistics), so
-before predicting, one training-mode forward over 128 training clips with
-momentum 0 sets every BatchNormalization's moving statistics to the current
-batch statistics ("BN recalibration"; the reference fit loop instead runs many
-epochs).
+Evaluation through Trainer.predict (eval mode: Keras's moving statistics,
+momentum 0.99, no recalibration).  After the 300 steps at lr 1e-3 the moving
+statistics still lag the weights (held-out accuracy at chance with them:
+tools/learn_settle.py, profiles/r06/learn_settle_r06g.txt); the reference fit
+loop lowers the learning rate on a plateau (ReduceLROnPlateau, factor 0.1,
+audiomodel.py:914-917) and runs many epochs, and so does the test: SETTLE
+more steps at lr 1e-4 and 1e-5, after which the moving statistics have
+caught up (probe: bf16 1.00, fp32 0.94 after 200 steps at 1e-5; the test uses
+300).  The recalibrated accuracy (one training-mode forward over 128 training
+clips with momentum 0) is checked as well, right after the lr 1e-3 phase.
 
-Bounds: held-out accuracy >= 90 % for both; the bf16 loss, averaged over each
-25-step window, within LOSS_BAND of the fp32 one in the same window or a
-neighbouring one.  When each run leaves the ln(4) plateau is chaotic (any
-change of summation order moves it by tens of steps: 0.27 apart at worst in the
-probe, 0.48 in r05q when the fp32 convolutions' K-tile order changed, with the
-bf16 curve one window behind), so the curves are compared up to a 25-step
-shift, not step for step.
+Loss-curve bound: the bf16 loss, averaged over each 25-step window, against
+the fp32 one in the same or a neighbouring window (when each run leaves the
+ln(4) plateau is chaotic: any change of summation order moves it by tens of
+steps).  The band is derived from two fp32 runs that differ only in the
+summation order -- the rows of every batch permuted (BN statistics, loss and
+gradient sums taken in another order) -- as 1.5 x their largest window
+difference (floor 0.05).
 """
 import numpy as np
 import pytest
@@ -38,7 +40,8 @@ SR = 48000
 N = 3 * SR
 BANDS = [(600.0, 1400.0), (1800.0, 3200.0), (4000.0, 6000.0), (7000.0, 10500.0)]
 B, STEPS, TRAIN, HELD = 32, 300, 512, 128
-LOSS_BAND = 0.4  # |mean bf16 loss - mean fp32 loss| over each 25-step window
+SETTLE = ((1e-4, 200), (1e-5, 300))  # (lr, steps) after the lr 1e-3 phase
+BAND_FACTOR, BAND_FLOOR = 1.5, 0.05
 
 
 def band_clip(rng, k):
@@ -70,7 +73,10 @@ def data(cuda):
             torch.from_numpy(xte).to(cuda), yte)
 
 
-def train(dtype, data, cuda):
+def train(dtype, data, cuda, permute=False, settle=True):
+    """STEPS steps at lr 1e-3 (losses), the recalibrated held-out accuracy,
+    then (settle) the SETTLE phase and the held-out accuracy through
+    Trainer.predict with the moving statistics as training left them."""
     from acfe import ops
     from acfe.train import FrontEnd, Trainer
     from resnet.wr_resnet_bird import WRResNet
@@ -83,38 +89,71 @@ def train(dtype, data, cuda):
     tr = Trainer(model, fe, lr=1e-3, loss="cce", device=cuda)
     ops._seed_counter = itertools.count()
     order = np.random.default_rng(3)
+    perm = np.random.default_rng(11)
     losses = []
     eye = torch.eye(len(BANDS), device=cuda)
-    for _ in range(STEPS):
-        idx = torch.from_numpy(order.choice(TRAIN, B, replace=False)).to(cuda)
+
+    def step():
+        idx = order.choice(TRAIN, B, replace=False)
+        if permute:  # the same batch, its rows in another order
+            idx = idx[perm.permutation(B)]
+        idx = torch.from_numpy(idx).to(cuda)
         loss, _ = tr.step(xtr[idx].contiguous(), eye[ytr[idx]])
-        losses.append(float(loss))
+        return float(loss)
+
+    for _ in range(STEPS):
+        losses.append(step())
     torch.cuda.synchronize()
+
+    def held_out():
+        pred = [tr.predict(xte[i:i + 64].contiguous()).float().argmax(1).cpu().numpy() for i in range(0, HELD, 64)]
+        return float((np.concatenate(pred) == yte).mean())
+
+    # recalibrated statistics on a copy of the moving buffers (restored after)
     bns = [m for m in model.modules() if hasattr(m, "moving_mean")]
+    saved = [(m.moving_mean.clone(), m.moving_variance.clone(), m.momentum) for m in bns]
     for m in bns:
-        m.momentum, m._m = 0.0, m.momentum
+        m.momentum = 0.0
     with torch.no_grad():
         model.train()
         model(fe(xtr[:128].contiguous()))
-    for m in bns:
-        m.momentum = m._m
-    pred = []
-    for i in range(0, HELD, 64):
-        pred.append(tr.predict(xte[i:i + 64].contiguous()).float().argmax(1).cpu().numpy())
-    acc = float((np.concatenate(pred) == yte).mean())
-    return np.array(losses), acc
+    acc_recal = held_out()
+    for m, (mm, mv, mo) in zip(bns, saved):
+        m.moving_mean.copy_(mm)
+        m.moving_variance.copy_(mv)
+        m.momentum = mo
+    acc_moving = None
+    if settle:
+        for lr, n in SETTLE:
+            tr.opt.lr = lr
+            for _ in range(n):
+                step()
+        acc_moving = held_out()
+    return np.array(losses), acc_recal, acc_moving
+
+
+def windows(l):
+    return [l[s - 25:s].mean() for s in range(25, STEPS + 1, 25)]
+
+
+def max_shift_diff(a, b):
+    """max over windows i of min over j in {i-1, i, i+1} |a[i] - b[j]|"""
+    return max(min(abs(x - y) for y in b[max(i - 1, 0):i + 2]) for i, x in enumerate(a))
 
 
 def test_training_learns_bf16_and_fp32(data, cuda):
-    l16, a16 = train(torch.bfloat16, data, cuda)
-    l32, a32 = train(torch.float32, data, cuda)
-    w16 = [l16[s - 25:s].mean() for s in range(25, STEPS + 1, 25)]
-    w32 = [l32[s - 25:s].mean() for s in range(25, STEPS + 1, 25)]
-    print("loss bf16", np.round(w16, 4), "acc", a16)
-    print("loss fp32", np.round(w32, 4), "acc", a32)
-    assert np.isfinite(l16).all() and np.isfinite(l32).all()
+    l32, r32, m32 = train(torch.float32, data, cuda)
+    l32p, _, _ = train(torch.float32, data, cuda, permute=True, settle=False)
+    l16, r16, m16 = train(torch.bfloat16, data, cuda)
+    w16, w32, w32p = windows(l16), windows(l32), windows(l32p)
+    band = max(BAND_FLOOR, BAND_FACTOR * max(max_shift_diff(w32p, w32), max_shift_diff(w32, w32p)))
+    print("loss bf16     ", np.round(w16, 4), "acc recalibrated", r16, "moving", m16)
+    print("loss fp32     ", np.round(w32, 4), "acc recalibrated", r32, "moving", m32)
+    print("loss fp32 perm", np.round(w32p, 4), "band", round(band, 4),
+          "bf16 vs fp32", round(max_shift_diff(w16, w32), 4))
+    assert np.isfinite(l16).all() and np.isfinite(l32).all() and np.isfinite(l32p).all()
     assert w32[-1] < 0.2 * w32[0] and w16[-1] < 0.2 * w16[0]
-    assert a32 >= 0.9 and a16 >= 0.9, (a16, a32)
-    for i, a in enumerate(w16):
-        near = w32[max(i - 1, 0):i + 2]
-        assert min(abs(a - b) for b in near) <= LOSS_BAND, (i, w16, w32)
+    assert r32 >= 0.9 and r16 >= 0.9, (r16, r32)
+    # the real eval path: Trainer.predict with the moving statistics
+    assert m32 >= 0.9 and m16 >= 0.9, (m16, m32)
+    assert max_shift_diff(w16, w32) <= band, (w16, w32, band)

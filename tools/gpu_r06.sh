@@ -38,6 +38,7 @@ for w in "$@"; do
     sq3r64) BENCH_ARGS='--model wrn --classes 2' step sq3r64 300 bash tools/pmc_sq3.sh ${TAG}_r64mix 'k_conv3x3_r64' ;;
     bnprobe) step bnprobe 300 python tools/bn_moving_probe.py ;;
     settle) step settle 400 python tools/learn_settle.py && step settle32 400 python tools/learn_settle.py fp32 ;;
+    learn) step learn 400 python -u -m pytest tests/test_learning_gpu.py -x -v -s --timeout 380 --timeout-method thread ;;
     bench2) step bench2 600 python -u -m pytest tests/test_bench_gpu.py -x -v --timeout 420 --timeout-method thread ;;
     cpub) step cpub 900 python tools/cpu_baseline.py ;;
     wrnab) for r in 1 2; do for v in new ${LIBS}; do
