@@ -406,6 +406,9 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
 #else
   auto stamp = [](int) __attribute__((always_inline)) {};
 #endif
+#ifdef ACFE_R64_PRIO
+  if (wk) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half (A/B)
+#endif
   int wpar = 0;  // weight buffer of the current step (NS may be odd)
   // ---- one tile: NS steps (chunk cc = cst / 3, filter row rs = cst % 3) with
   // the previous tile's epilogue in steps 0 / 1
@@ -468,6 +471,10 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
             epi_slot(std::integral_constant<int, cst>{}, std::integral_constant<int, grp>{}, ptm, live);
           }
         }
+#elif defined(ACFE_R64_VFIRST)
+        // the unit's VALU first (the group's fragment reads in flight), then the MFMAs
+        epi_slot(std::integral_constant<int, cst>{}, std::integral_constant<int, grp>{}, ptm, live);
+        mfmas();
 #else
         mfmas();
         epi_slot(std::integral_constant<int, cst>{}, std::integral_constant<int, grp>{}, ptm, live);

@@ -39,6 +39,7 @@ for w in "$@"; do
     bnprobe) step bnprobe 300 python tools/bn_moving_probe.py ;;
     settle) step settle 400 python tools/learn_settle.py && step settle32 400 python tools/learn_settle.py fp32 ;;
     learn) step learn 400 python -u -m pytest tests/test_learning_gpu.py -x -v -s --timeout 380 --timeout-method thread ;;
+    r64ab) for v in base ${LIBS}; do if [ $v = base ]; then L=$PWD/audio-training_amd/acfe/libacfe_stamps.so; else L=$PWD/abtest/$v.so; fi; echo "== $v"; ACFE_LIB=$L step r64ab_$v 300 python tools/r64_stamps.py 512 && grep -E 'ms,' $O/r64ab_$v.log; done ;;
     bench2) step bench2 600 python -u -m pytest tests/test_bench_gpu.py -x -v --timeout 420 --timeout-method thread ;;
     cpub) step cpub 900 python tools/cpu_baseline.py ;;
     wrnab) for r in 1 2; do for v in new ${LIBS}; do
