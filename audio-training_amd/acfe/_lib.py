@@ -60,6 +60,12 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_wgrad_bnbwd_rows": [I32] * 5,
     "acfe_conv2d_wgrad_bnbwd": [P, I32, I32, I32, I32, P, P, I32, P, P, I32, P, P, F32, C.c_uint64, P, P, F32, P, P,
                                 P],
+    "acfe_conv2d_dropout_keep_supported": [I32] * 6,
+    "acfe_conv2d_fwd_dropout_keep": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, P, F32, C.c_uint64, P, P],
+    "acfe_conv2d_fwd_bn_keep": [P, I32, I32, I32, I32, P, I32, I32, I32, P, P, P, F32, C.c_uint64, P, P, I32, P, P,
+                                I32, P],
+    "acfe_conv2d_wgrad_bnbwd_keep": [P, I32, I32, I32, I32, P, P, I32, P, P, I32, P, F32, C.c_uint64, P, P, P, F32,
+                                     P, P, P],
     "acfe_stem_blocks": [I32, I32, I32],
     "acfe_stem_fold_weights": [P, I32, I32, I32, I32, P, P],
     "acfe_stem_fwd": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P, P, I32, P, P],

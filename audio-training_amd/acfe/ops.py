@@ -44,6 +44,9 @@ STEM_BN_FUSE = os.environ.get("ACFE_STEM_BN_FUSE", "1") != "0"
 # runs the BN backward apply as its own pass instead of inside the conv's
 # weight gradient (acfe_conv2d_wgrad_bnbwd) (A/B, tests)
 FUSE_BN_BWD = FUSE and os.environ.get("ACFE_BN_BWD_FUSE", "1") != "0"
+# ACFE_KEEP_BITS=0: the BN-fold weight gradient regenerates the dropout mask
+# from the pair hashes instead of reading the forward's keep bits (A/B)
+KEEP_BITS = os.environ.get("ACFE_KEEP_BITS", "1") != "0"
 # ACFE_SUB_FUSE=0: a 1x1 "valid" stride-k conv shortcut hands its full-resolution
 # dX (zero off the (k p, k q) pixels) to the BN backward instead of the P x Q
 # values for acfe_bn_bwd_apply_sub (A/B, tests)
@@ -171,13 +174,27 @@ class _Timed:
 
 
 # ------------------------------------------------------------------ conv
-def _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats, drop=None):
+def keep_bits_ok(x, w, stride, pt, pl, P, Q, drop, want_stats) -> bool:
+    """Can the dropout forward write its keep bits for the BN-fold weight
+    gradient (acfe_conv2d_fwd_*_keep -> acfe_conv2d_wgrad_bnbwd_keep)?"""
+    if not (KEEP_BITS and FUSE_BN_BWD and want_stats and drop is not None and drop[0] > 0.0
+            and x.dtype == torch.bfloat16):
+        return False
+    N, H, W, C = x.shape
+    K, R, S, _ = w.shape
+    src = _pending(x)[0] if _pending(x) is not None else x  # (the BN input the prologue reads)
+    return ((R, S, stride, pt, pl, P, Q) == (3, 3, 1, 1, 1, H, W) and src.is_contiguous()
+            and src.data_ptr() % 16 == 0 and bool(lib.acfe_conv2d_dropout_keep_supported(N, H, W, C, K, 1)))
+
+
+def _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats, drop=None, keep=None):
     """acfe_conv2d_fwd[_dropout] -> (y, stats_partial); a pending BN output x
-    (bn_prologue_ok's shapes) is convolved through the BN prologue."""
+    (bn_prologue_ok's shapes) is convolved through the BN prologue.  keep: a
+    uint8 [N, P, Q, K / 8] buffer for the dropout keep bits (keep_bits_ok)."""
     if _pending(x) is not None:
         if stride == 1 and (P, Q, pt, pl) == (x.shape[1], x.shape[2], 1, 1) and \
                 bn_prologue_ok(x.shape, x.dtype, w):
-            return _conv_fwd_bn(x, w, b, want_stats, drop)
+            return _conv_fwd_bn(x, w, b, want_stats, drop, keep)
         materialize(x)
     N, H, W, C = x.shape
     K, R, S, Cw = w.shape
@@ -192,7 +209,10 @@ def _conv_fwd(x, w, b, stride, pt, pl, P, Q, want_stats, drop=None):
     args = (ptr(x), N, H, W, C, ptr(wp), K, R, S, stride, pt, pl, P, Q, ptr(b), ptr(y), dt,
             ptr(stats) if want_stats else None)
     with _Timed(w, "fwd"):
-        if drop is not None and drop[0] > 0.0:
+        if keep is not None:
+            call("acfe_conv2d_fwd_dropout_keep", ptr(x), N, H, W, C, ptr(wp), K, pt, pl, ptr(b), ptr(y), ptr(stats),
+                 float(drop[0]), int(drop[1]), ptr(keep), stream())
+        elif drop is not None and drop[0] > 0.0:
             call("acfe_conv2d_fwd_dropout", *args, float(drop[0]), int(drop[1]), stream())
         else:
             call("acfe_conv2d_fwd", *args, stream())
@@ -659,7 +679,7 @@ def _prologue_args(xb):
     return x, scale, shift, relu
 
 
-def _conv_fwd_bn(xb, w, b, want_stats, drop):
+def _conv_fwd_bn(xb, w, b, want_stats, drop, keep=None):
     """_conv_fwd of a pending BN output xb: acfe_conv2d_fwd_bn (3x3 "same" stride 1)."""
     N, H, W, C = xb.shape
     K = w.shape[0]
@@ -671,9 +691,14 @@ def _conv_fwd_bn(xb, w, b, want_stats, drop):
         stats = _empty((lib.acfe_conv2d_stats_rows(N * H * W, K), 2, wp.shape[0]), F64, xb.device)
     rate, seed = drop if drop is not None and drop[0] > 0.0 else (0.0, 0)
     with _Timed(w, "fwd"):
-        call("acfe_conv2d_fwd_bn", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y),
-             ptr(stats) if want_stats else None, float(rate), int(seed), ptr(scale), ptr(shift), int(relu), ptr(xb),
-             dtype_code(xb.dtype), stream())
+        if keep is not None:
+            call("acfe_conv2d_fwd_bn_keep", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y), ptr(stats),
+                 float(rate), int(seed), ptr(scale), ptr(shift), int(relu), ptr(xb), ptr(keep), dtype_code(xb.dtype),
+                 stream())
+        else:
+            call("acfe_conv2d_fwd_bn", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y),
+                 ptr(stats) if want_stats else None, float(rate), int(seed), ptr(scale), ptr(shift), int(relu),
+                 ptr(xb), dtype_code(xb.dtype), stream())
     return y, stats
 
 
@@ -886,7 +911,12 @@ class _ConvDropBNFn(torch.autograd.Function):
         stride, pt, pl, P, Q, rate, seed, training, relu, eps, momentum, defer = conf
         drop = (rate, seed) if training and rate > 0.0 else None
         ctx.bn = bn_src(x)
-        u, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, training, drop)
+        keep = None
+        if keep_bits_ok(x, w, stride, pt, pl, P, Q, drop, training) and any(ctx.needs_input_grad):
+            # the dropout keep bits for the BN-fold weight gradient (1/16 of u)
+            keep = _empty((x.shape[0], P, Q, w.shape[0] // 8), torch.uint8, x.device)
+        ctx.keep = keep
+        u, stats = _conv_fwd(x, w, b, stride, pt, pl, P, Q, training, drop, keep)
         y, saved = _bn_fwd(u, gamma, beta, stats if training else None, mmean, mvar, training, relu, eps, momentum,
                            u.dtype, defer, any(ctx.needs_input_grad))
         ctx.save_for_backward(x, w, u, *saved)
@@ -921,10 +951,11 @@ def _bnbwd_fold_ok(x, w, u, dy, stride, pt, pl, P, Q) -> bool:
     return lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K) > 0
 
 
-def _wgrad_bnbwd(x, w, g, pend, need_db, bias, rate=0.0, seed=0):
+def _wgrad_bnbwd(x, w, g, pend, need_db, bias, rate=0.0, seed=0, keep=None):
     """acfe_conv2d_wgrad_bnbwd: dW (and the bias gradient from its channel
     sums) of conv(x, w) whose output gradient g it forms and writes from the
-    BN backward apply `pend` = (dy, x_bn, scale, shift, flags, coef, add)."""
+    BN backward apply `pend` = (dy, x_bn, scale, shift, flags, coef, add);
+    keep: the forward's dropout keep bits (acfe_conv2d_wgrad_bnbwd_keep)."""
     N, H, W, C = x.shape
     K = w.shape[0]
     dev = x.device
@@ -936,9 +967,14 @@ def _wgrad_bnbwd(x, w, g, pend, need_db, bias, rate=0.0, seed=0):
     srows = lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K)
     sums = _empty((srows, 2, K), F64, dev)
     with _Timed(w, "wgrad"):
-        call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(scale), ptr(shift), int(flags),
-             ptr(coef), ptr(add), float(rate), int(seed), ptr(g), ptr(dwt), 1.0 if tgt is not None else 0.0, ptr(ws),
-             ptr(sums), s)
+        if keep is not None and add is None and rate > 0.0:
+            call("acfe_conv2d_wgrad_bnbwd_keep", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(scale), ptr(shift),
+                 int(flags), ptr(coef), float(rate), int(seed), ptr(keep), ptr(g), ptr(dwt),
+                 1.0 if tgt is not None else 0.0, ptr(ws), ptr(sums), s)
+        else:
+            call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(scale), ptr(shift),
+                 int(flags), ptr(coef), ptr(add), float(rate), int(seed), ptr(g), ptr(dwt),
+                 1.0 if tgt is not None else 0.0, ptr(ws), ptr(sums), s)
     if flags & 2:
         _tag(g, "_acfe_relu_masked", True)
     # g's channel sums: the bias gradient here and of any other conv receiving
@@ -986,7 +1022,7 @@ def _conv_bn_bwd_fold(ctx, x, w, u, dy, saved, relu, training):
     g = _empty(u.shape, u.dtype, dev)  # the conv output gradient
     rate, seed = ctx.drop if ctx.drop is not None else (0.0, 0)
     dw, db = _wgrad_bnbwd(x, w, g, (dy, u, scale, shift, int(relu), coef, None),
-                          ctx.has_b and ctx.needs_input_grad[2], ctx.bias, rate, seed)
+                          ctx.has_b and ctx.needs_input_grad[2], ctx.bias, rate, seed, getattr(ctx, "keep", None))
     dx = None
     if ctx.needs_input_grad[0]:
         dx, _, _ = _conv_bwd(x, w, g, 1, 1, 1, H, W, True, False, False, bias=ctx.bias, bn=ctx.bn)

@@ -3138,11 +3138,15 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 // dgrad reads it next) and sums it per channel (the conv bias gradient) -- the
 // BN backward apply pass over the tensor is gone.  Each dY element is staged
 // by one workgroup of chunk 0 (the others only read it).
-template <int KB, bool UNP, int CW = 64, int NR = 1, bool BWD = false>
+template <int KB, bool UNP, int CW = 64, int NR = 1, bool BWD = false, bool KEEP = false>
 __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
                 float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
   static_assert(!(BWD && UNP), "BN backward fold: plain dY");
+  // KEEP: the dropout keep bits of the forward (g.keep_in, one byte per 8-channel
+  // granule) instead of the regenerated pair hashes (9 quarter-rate multiplies
+  // per granule)
+  static_assert(!KEEP || BWD, "keep bits: the BN-fold wgrad");
 #ifndef ACFE_FB_MID
 #define ACFE_FB_MID 0
 #endif
@@ -3196,6 +3200,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   // element index and column, and the lane's channel sums (its 8 channels
   // cg * 8 + j are fixed: 512 is a multiple of DGR)
   u32x4 rdx[BWD ? DPT : 1], rdr[BWD ? DPT : 1];  // BN input x, residual gradient
+  unsigned rkb[KEEP ? DPT : 1];                  // KEEP: the granules' keep-bit bytes
   long long fbase = 0;
   int fw0 = 0;
   float fs[BWD ? 8 : 1];
@@ -3269,6 +3274,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
                 __builtin_amdgcn_make_buffer_rsrc((void*)(g.fb_add + imgy), (short)0, nby * 2, 0x00020000);
             rdr[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, okd ? e * 2u : OOR, 0, 0);
           }
+          if constexpr (KEEP) {  // byte e / 8 of the image's [P Q][K / 8] keep bits (e: a granule start)
+            const __amdgpu_buffer_rsrc_t krs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(g.keep_in + imgy / 8), (short)0, nby / 8, 0x00020000);
+            rkb[i] = __builtin_amdgcn_raw_buffer_load_b8(krs, okd ? e >> 3 : OOR, 0, 0);
+          }
           if (i == 0) fbase = e0, fw0 = w0;
         }
       }
@@ -3305,7 +3315,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         // one pair hash per dword (channels 2d, 2d + 1; e is even), the four
         // from one Weyl multiply when the indices fit 32 bits
         uint32_t hl[4] = {0u, 0u, 0u, 0u};
-        if (g.drop.on) {
+        if (!KEEP && g.drop.on) {
           if (g.idx32) {
             hash_u32_lo_run<4>(g.drop.seed, (uint32_t)((uint64_t)e >> 1), hl);
           } else {
@@ -3333,7 +3343,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
             if (g.fb_add) o += __uint_as_float(hf ? (rdr[i][d] & 0xffff0000u) : (rdr[i][d] << 16));
             if ((g.fb_relu & 2) && !(xv > 0.f)) o = 0.f;  // x = a ReLU output upstream: its backward
             o = bf2f(f2bf(o));
-            if (g.drop.on) o = ((hf ? hh >> 16 : hh & 0xFFFFu) >= g.drop.thr) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
+            if constexpr (KEEP) {
+              o = ((rkb[i] >> j) & 1u) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
+            } else {
+              if (g.drop.on) o = ((hf ? hh >> 16 : hh & 0xFFFFu) >= g.drop.thr) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
+            }
             o = ok ? o : 0.f;
 #ifndef ACFE_FB_NOSUM
             fs[j] += o;
@@ -3725,6 +3739,8 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
   g.fb_relu = 0;
   g.fb_out = nullptr;
   g.fb_sums = nullptr;
+  g.keep_out = nullptr;
+  g.keep_in = nullptr;
   g.s2d = g.s2d_C = g.s2d_H = g.s2d_W = g.s2d_pt = g.s2d_pl = g.s2d_fill = g.s2d_lc = g.s2d_amul = 0;
   g.s2d_rpq = g.s2d_rq = 0.f;
   static const int cmaj = !getenv("ACFE_CONVG_CMAJ") || atoi(getenv("ACFE_CONVG_CMAJ")) != 0;
@@ -4399,11 +4415,14 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   const bool c16k64 = hp.c16k64, k16c64 = hp.k16c64;
   const dim3 gr(nchunk * sp);
   if (g.fb_sc) {  // acfe_conv2d_wgrad_bnbwd: the BN backward formed while staging dY
-#define WB(KB_, CW_, NR_)                                                                                       \
-  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_, NR_, true>), gr, dim3(512), 0, s, g, (const uint16_t*)x,  \
-                     (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
+#define WB(KB_, CW_, NR_, ...)                                                                                  \
+  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_, NR_, true, ##__VA_ARGS__>), gr, dim3(512), 0, s, g,      \
+                     (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
     if (amax || (wp != 1 && !c16k64)) return ACFE_E_INVAL;
+    // keep bits: the stage-1 K = 64 fold only (the forward that writes them: k_conv3x3_r64 PM 4)
+    if (g.keep_in && !(cw == 64 && g.K == 64 && nr == 2 && !c16k64 && g.drop.on)) return ACFE_E_INVAL;
     if (c16k64 && nr == 2) WB(64, 16, 2);
+    else if (cw == 64 && g.K == 64 && nr == 2 && g.keep_in) WB(64, 64, 2, true);
     else if (cw == 64 && g.K == 64 && nr == 2) WB(64, 64, 2);
     else if (cw == 64 && g.K == 32 && nr == 2) WB(32, 64, 2);
     else return ACFE_E_INVAL;
@@ -4554,10 +4573,35 @@ ACFE_API int acfe_conv2d_wgrad_bnbwd_rows(int N, int H, int W, int C, int K) {
   return ok ? hp.nchunk * hp.sp : 0;
 }
 
+static int wgrad_bnbwd_impl(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn, int K,
+                            const float* scale, const float* shift, int relu, const float* coef, const void* add,
+                            float drop_rate, unsigned long long seed, const uint8_t* keep, void* dy, float* dw,
+                            float beta, float* workspace, double* sums, void* stream);
+
 ACFE_API int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn,
                                      int K, const float* scale, const float* shift, int relu, const float* coef,
                                      const void* add, float drop_rate, unsigned long long seed, void* dy, float* dw,
                                      float beta, float* workspace, double* sums, void* stream) {
+  return wgrad_bnbwd_impl(x, N, H, W, C, gy, u_bn, K, scale, shift, relu, coef, add, drop_rate, seed, nullptr, dy,
+                          dw, beta, workspace, sums, stream);
+}
+
+// the same with the dropout mask read from the forward's keep bits
+// (acfe_conv2d_fwd_*_keep) instead of regenerated: identical results
+ACFE_API int acfe_conv2d_wgrad_bnbwd_keep(const void* x, int N, int H, int W, int C, const void* gy,
+                                          const void* u_bn, int K, const float* scale, const float* shift, int relu,
+                                          const float* coef, float drop_rate, unsigned long long seed,
+                                          const uint8_t* keep, void* dy, float* dw, float beta, float* workspace,
+                                          double* sums, void* stream) {
+  if (!keep || drop_rate <= 0.f) return ACFE_E_INVAL;
+  return wgrad_bnbwd_impl(x, N, H, W, C, gy, u_bn, K, scale, shift, relu, coef, nullptr, drop_rate, seed, keep, dy,
+                          dw, beta, workspace, sums, stream);
+}
+
+static int wgrad_bnbwd_impl(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn, int K,
+                            const float* scale, const float* shift, int relu, const float* coef, const void* add,
+                            float drop_rate, unsigned long long seed, const uint8_t* keep, void* dy, float* dw,
+                            float beta, float* workspace, double* sums, void* stream) {
   if (!x || !gy || !u_bn || !scale || !shift || !coef || !dy || !dw || !workspace || !sums || drop_rate < 0.f ||
       drop_rate >= 1.f || (add && drop_rate > 0.f))
     return ACFE_E_INVAL;
@@ -4577,6 +4621,7 @@ ACFE_API int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, 
   g.fb_relu = relu & 3;
   g.fb_out = (uint16_t*)dy;
   g.fb_sums = sums;
+  g.keep_in = keep;
   int used = 0;
   int rc = wgrad_halo_launch(g, x, gy, nullptr, workspace, splits, strm(stream), &used);
   if (rc) return rc;
@@ -4899,6 +4944,55 @@ ACFE_API int acfe_conv2d_fwd_bn(const void* x, int N, int H, int W, int C, const
                               "acfe_conv2d_fwd_bn");
   return launch_rows<64, 0>(g, x, wpacked, bias, y, stats_partial, srows, nullptr, strm(stream),
                             "acfe_conv2d_fwd_bn");
+}
+
+// ---- dropout keep bits (the K = 64 stage-1 Conv2D -> Dropout -> BN nodes,
+// resnet/wr_resnet.py:58-71, resnet/wr_resnet_bird.py:136-161): the forward
+// writes one bit per element, [N][H][W][K / 8] bytes, the BN-fold weight
+// gradient reads them instead of regenerating the pair hashes
+ACFE_API int acfe_conv2d_dropout_keep_supported(int N, int H, int W, int C, int K, int dtype) {
+  const int nch = C / 64;
+  return acfe::r64_enabled() && dtype == ACFE_DTYPE_BF16 && N > 0 && H > 0 && W > 0 && K == 64 && C % 64 == 0 &&
+         (nch == 1 || nch == 2 || nch == 4) && (long long)H * W * C * 2 < (1ll << 31) &&
+         (long long)H * W * K * 2 < (1ll << 31) && (long long)N * H * W * K < (1ll << 32) &&
+         (long long)N * ((H + 7) / 8) * ((W + 63) / 64) < (1ll << 31);
+}
+
+static int keep_launch(ConvGeom& g, const void* x, const void* wpacked, const float* bias, void* y,
+                       double* stats, uint8_t* keep, hipStream_t s, const char* what) {
+  if (!keep || !g.drop.on || !acfe_conv2d_dropout_keep_supported(g.N, g.H, g.W, g.C, g.K, ACFE_DTYPE_BF16))
+    return ACFE_E_INVAL;
+  g.keep_out = keep;
+  return launch_r64(g, x, wpacked, bias, y, stats, grid_m_for(g.M, 1), s, what, 4);
+}
+
+ACFE_API int acfe_conv2d_fwd_dropout_keep(const void* x, int N, int H, int W, int C, const void* wpacked, int K,
+                                          int pad_top, int pad_left, const float* bias, void* y, double* stats_partial,
+                                          float drop_rate, unsigned long long seed, uint8_t* keep, void* stream) {
+  if (!x || !wpacked || !y || drop_rate <= 0.f || drop_rate >= 1.f || pad_top != 1 || pad_left != 1 ||
+      ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
+    return ACFE_E_INVAL;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
+  g.drop = make_drop(drop_rate, seed);
+  return keep_launch(g, x, wpacked, bias, y, stats_partial, keep, strm(stream), "acfe_conv2d_fwd_dropout_keep");
+}
+
+ACFE_API int acfe_conv2d_fwd_bn_keep(const void* x, int N, int H, int W, int C, const void* wpacked, int K,
+                                     int pad_top, int pad_left, const float* bias, void* y, double* stats_partial,
+                                     float drop_rate, unsigned long long seed, const float* bn_scale,
+                                     const float* bn_shift, int bn_relu, void* x_bn_out, uint8_t* keep, int dtype,
+                                     void* stream) {
+  if (!x || !wpacked || !y || dtype != ACFE_DTYPE_BF16 || !acfe_conv2d_bn_prologue_supported(N, H, W, C, K, dtype) ||
+      !pro_args_ok(bn_scale, bn_shift, x_bn_out) || ((uintptr_t)x & 15) || drop_rate <= 0.f || drop_rate >= 1.f ||
+      pad_top != 1 || pad_left != 1)
+    return ACFE_E_INVAL;
+  ConvGeom g = make_geom(N, H, W, C, K, 3, 3, 1, pad_top, pad_left, H, W, 64, K);
+  g.drop = make_drop(drop_rate, seed);
+  g.pro_sc = bn_scale;
+  g.pro_sh = bn_shift;
+  g.pro_relu = bn_relu ? 1 : 0;
+  g.pro_out = (uint16_t*)x_bn_out;
+  return keep_launch(g, x, wpacked, bias, y, stats_partial, keep, strm(stream), "acfe_conv2d_fwd_bn_keep");
 }
 
 ACFE_API int acfe_conv2d_fwd_add_bn(const void* x, int N, int H, int W, int C, const void* wpacked, int K,

@@ -70,6 +70,12 @@ struct ConvGeom {
   int s2d_lc, s2d_amul;     // log2(s2d_C); block position a = (ab * s2d_amul) >> 5
   float s2d_rpq, s2d_rq;    // 1 / (P Q), 1 / Q of the block grid
   int cmaj;  // k_conv_fwd_g fp32: K-tiles chunk-major (ACFE_CONVG_CMAJ=0: tap-major, A/B)
+  // Dropout keep bits [M][K / 8] (bit j of byte (m, c / 8) = element (m, 8 (c / 8) + j)
+  // kept): written by the K = 64 dropout forward (k_conv3x3_r64 PM 4,
+  // acfe_conv2d_fwd_*_keep), read by the BN-fold weight gradient
+  // (acfe_conv2d_wgrad_bnbwd_keep) instead of regenerating the pair hashes
+  uint8_t* keep_out;
+  const uint8_t* keep_in;
 };
 
 // XCD-aware walk over the M tiles of a persistent grid.  Workgroups are
@@ -181,6 +187,7 @@ int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float
 // 5 the dgrad with the BN backward reduce; ACFE_E_INVAL when not its case
 int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                int srows, hipStream_t s, const char* what, int pm);
+bool r64_enabled();
 // acfe_conv2d_dgrad_unpool at K = C = 128 on the same kernel (PM 2)
 int launch_unpool1w(const ConvGeom& g, const void* dyp, const void* wflip, void* dx, uint8_t* amax, hipStream_t s,
                     const char* what);

@@ -268,12 +268,15 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
   // direct form).  Bitwise, not short-circuit: no branches inside an MFMA group.
   const unsigned lane_o = ((unsigned)l16 * (unsigned)g.ldy + (unsigned)c0) * 2u;
   const unsigned lane_h = ((unsigned)l16 * (unsigned)(KB / 2) + (unsigned)(c0 >> 1)) * 0x9E3779B1u;
-  auto unit_px = [&](int u, int tm, bool live, int& n, unsigned& o, bool& inb) __attribute__((always_inline)) {
+  const unsigned lane_k = (unsigned)l16 * (KB / 8) + (unsigned)(c0 >> 3);  // keep-bit byte of the lane
+  auto unit_px = [&](int u, int tm, bool live, int& n, unsigned& o, bool& inb, unsigned* spx = nullptr)
+                     __attribute__((always_inline)) {
     int hb, wb;
     tile_of(tm, n, hb, wb);
     const int hh = hb * TR + 2 * wp + (u >> 2), wc = wb * SEGW + (u & 3) * 16;
     inb = live & (hh < g.P) & (wc + l16 < g.Q);
     o = (unsigned)(hh * g.Q + wc) * (unsigned)g.ldy * 2u + lane_o;
+    if (spx) *spx = (unsigned)(hh * g.Q + wc);  // the unit's first pixel in its image (scalar)
   };
   auto unit_load = [&](int u, int tm, bool live) __attribute__((always_inline)) {
     if constexpr (PM == 3 || PM == 5) {
@@ -288,9 +291,9 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
   };
   auto unit = [&](int u, int tm, bool live) __attribute__((always_inline)) {
     int n;
-    unsigned o;
+    unsigned o, spx;
     bool inb;
-    unit_px(u, tm, live, n, o, inb);
+    unit_px(u, tm, live, n, o, inb, &spx);
     unsigned w8[4] = {pk[u][0], pk[u][1], pk[u][2], pk[u][3]};
     if constexpr (PM == 3) {
       // z = (ReLU)(conv + residual), rounded to bf16 (ops.add's values)
@@ -311,14 +314,23 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
       const unsigned spix = ((unsigned)n * g.P + hb * TR + 2 * wp + (u >> 2)) * g.Q + wb * SEGW + (u & 3) * 16;
       // ((pix K + c0) >> 1) W + seed with pix = spix + l16 (K = 64, c0 even)
       const uint32_t hw0 = spix * (unsigned)(KB / 2) * 0x9E3779B1u + lane_h + (uint32_t)g.drop.seed;
+      unsigned kbits = 0;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const uint32_t hsh = hash_u32_lo_w(g.drop.seed, hw0 + (uint32_t)d * 0x9E3779B1u);
-        const float lo = (hsh & 0xFFFFu) >= g.drop.thr ? bf2f(f2bf(__uint_as_float(w8[d] << 16) * g.drop.scl)) : 0.f;
-        const float hi =
-            (hsh >> 16) >= g.drop.thr ? bf2f(f2bf(__uint_as_float(w8[d] & 0xffff0000u) * g.drop.scl)) : 0.f;
+        const bool klo = (hsh & 0xFFFFu) >= g.drop.thr, khi = (hsh >> 16) >= g.drop.thr;
+        const float lo = klo ? bf2f(f2bf(__uint_as_float(w8[d] << 16) * g.drop.scl)) : 0.f;
+        const float hi = khi ? bf2f(f2bf(__uint_as_float(w8[d] & 0xffff0000u) * g.drop.scl)) : 0.f;
         w8[d] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+        kbits |= (klo ? 1u : 0u) << (2 * d);
+        kbits |= (khi ? 1u : 0u) << (2 * d + 1);
       }
+      // the keep bits of channels c0 .. c0 + 7: one byte at (pixel, c0 / 8) of
+      // [M][K / 8] (g.keep_out; a null buffer drops the store)
+      const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(g.keep_out + (long long)n * g.P * g.Q * (KB / 8)), (short)0,
+          g.keep_out ? g.P * g.Q * (KB / 8) : 0, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)kbits, kr, inb ? spx * (KB / 8) + lane_k : 0x80000000u, 0, 0);
     }
     const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Y + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
@@ -385,13 +397,13 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     if constexpr (cst == 1 && grp == 2) unit_stats();
   };
   // VMEM operations a step issues after its last weight piece (group 2's) and
-  // leaves in flight at its closing wait: step 0 the stores of units 3..5 and
-  // the loads of units 6, 7; rs == 1 the next chunk's halo loads (groups
+  // leaves in flight at its closing wait: step 0 the stores of units 3..5 (and
+  // their keep-bit bytes) and the loads of units 6, 7; rs == 1 the next chunk's halo loads (groups
   // 3..5); the last step the loads of the next epilogue's units 0..2
   constexpr bool ELD = PM == 3 || PM == 5;
   auto late_ops = [](int cst) constexpr {
     int n = (cst % 3 == 1) ? XPT : 0;
-    if (cst == 0) n += 3 + (ELD ? 2 : 0);
+    if (cst == 0) n += 3 * (DROP ? 2 : 1) + (ELD ? 2 : 0);  // (DROP: + the keep-bit byte stores)
     if (cst == NS - 1 && ELD) n += 3;
     return n;
   };
@@ -571,6 +583,8 @@ static bool r64_on() {
   return v != 0;
 }
 
+bool r64_enabled() { return r64_on(); }
+
 int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                int srows, hipStream_t s, const char* what, int pm) {
   // 3x3 stride 1 "same"-shaped halo (pads 0..2), K = 64, C in {64, 128, 256},
@@ -586,6 +600,7 @@ int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bi
   if (pro && (pm == 5 || !g.pro_sh || g.pt != 1 || g.pl != 1 || ((uintptr_t)g.pro_out & 15) || !g.pro_out))
     return ACFE_E_INVAL;
   if ((pm == 3 || pm == 5) && (!g.res || ((uintptr_t)g.res & 15))) return ACFE_E_INVAL;
+  if (g.keep_out && (pm != 4 || !g.drop.on)) return ACFE_E_INVAL;
   if (pm == 5 && (!stats || !g.bn_sc || !g.bn_sh || !g.bn_mu || !g.bn_is)) return ACFE_E_INVAL;
   const int tiles_h = (g.P + 7) / 8, tiles_w = (g.Q + 63) / 64;
   const long long nt = (long long)g.N * tiles_h * tiles_w;

@@ -268,6 +268,29 @@ int acfe_conv2d_wgrad_bnbwd(const void* x, int N, int H, int W, int C, const voi
                             const float* scale, const float* shift, int relu, const float* coef, const void* add,
                             float drop_rate, unsigned long long seed, void* dy, float* dw, float beta,
                             float* workspace, double* sums, void* stream);
+/* Dropout keep bits of the K = 64 stage-1 Conv2D -> Dropout (-> BN) nodes
+ * (resnet/wr_resnet.py:58-71's conv2a -> Dropout; the reference's Keras
+ * Dropout mask, realised here by the pair-hash mask of acfe_dropout): the
+ * forward writes one bit per output element, keep [N][H][W][K / 8] bytes (bit j
+ * of byte (pixel, c / 8) = element (pixel, 8 (c / 8) + j) kept), and the BN-fold
+ * weight gradient reads them instead of regenerating the mask -- identical
+ * values.  _supported: the shapes (3x3 stride 1 "same", K = 64, C / 64 in
+ * {1, 2, 4}, bf16) on which the forward can write them.  fwd_dropout_keep /
+ * fwd_bn_keep = acfe_conv2d_fwd_dropout (pads 1, stats_partial required) /
+ * acfe_conv2d_fwd_bn plus the keep output; wgrad_bnbwd_keep =
+ * acfe_conv2d_wgrad_bnbwd (no residual `add`) with the mask from keep. */
+int acfe_conv2d_dropout_keep_supported(int N, int H, int W, int C, int K, int dtype);
+int acfe_conv2d_fwd_dropout_keep(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                                 int pad_left, const float* bias, void* y, double* stats_partial, float drop_rate,
+                                 unsigned long long seed, uint8_t* keep, void* stream);
+int acfe_conv2d_fwd_bn_keep(const void* x, int N, int H, int W, int C, const void* wpacked, int K, int pad_top,
+                            int pad_left, const float* bias, void* y, double* stats_partial, float drop_rate,
+                            unsigned long long seed, const float* bn_scale, const float* bn_shift, int bn_relu,
+                            void* x_bn_out, uint8_t* keep, int dtype, void* stream);
+int acfe_conv2d_wgrad_bnbwd_keep(const void* x, int N, int H, int W, int C, const void* gy, const void* u_bn, int K,
+                                 const float* scale, const float* shift, int relu, const float* coef, float drop_rate,
+                                 unsigned long long seed, const uint8_t* keep, void* dy, float* dw, float beta,
+                                 float* workspace, double* sums, void* stream);
 
 /* Stem convolution with one (folded) input channel and 16 outputs ("same",
  * stride 1, R = S = 5 (wr_resnet_bird) or 3 (wr_resnet)): the three identical

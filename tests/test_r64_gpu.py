@@ -174,3 +174,79 @@ def test_r64_dgrad(env, cuda, N, H, W, Kd, relu):
     ref = torch.stack([gm.sum(0), (gm * (xv - mu.cpu().to(F64)) * inv.cpu().to(F64)).sum(0)])
     s = b[2].sum(0).cpu()
     assert ((s - ref).abs() <= 1e-5 * ref.abs().clamp_min(1.0) + 1e-2).all()
+
+
+@pytest.mark.parametrize("C,pro", [(64, False), (64, True), (128, True)], ids=["c64", "c64-bn", "c128-bn"])
+def test_keep_bits(env, cuda, C, pro):
+    """The dropout keep bits (acfe_conv2d_fwd_dropout_keep / _bn_keep): the
+    forward's outputs are bit-identical to the forward without them, the bits
+    are acfe_dropout's mask of the same (rate, seed, element index), and the
+    BN-fold weight gradient reading them (acfe_conv2d_wgrad_bnbwd_keep) is
+    bit-identical to the one regenerating the mask -- dY, dW and the slab."""
+    ops, call, lib, ptr, stream = env
+    N, H, W, K = 6, 13, 100, 64
+    assert lib.acfe_conv2d_dropout_keep_supported(N, H, W, C, K, 1)
+    g = torch.Generator(device="cpu").manual_seed(C + pro)
+    x = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
+    w = (torch.randn((K, 3, 3, C), generator=g) * (1.0 / (3 * C ** 0.5))).to(cuda)
+    b = (torch.randn((K,), generator=g) * 0.1).to(cuda)
+    sc, sh = (torch.rand(C, generator=g) + 0.5).to(cuda), (torch.randn(C, generator=g) * 0.3).to(cuda)
+    wp = ops.pack_weights(w, BF, False)
+    rows = lib.acfe_conv2d_stats_rows(N * H * W, K)
+    rate, seed = 0.1, 4242
+
+    def fwd(keep):
+        y = torch.full((N, H, W, K), float("nan"), dtype=BF, device=cuda)
+        st = torch.zeros((rows, 2, wp.shape[0]), dtype=F64, device=cuda)
+        xb = torch.empty_like(x)
+        if pro:
+            if keep is None:
+                call("acfe_conv2d_fwd_bn", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y), ptr(st), rate, seed,
+                     ptr(sc), ptr(sh), 1, ptr(xb), 1, stream())
+            else:
+                call("acfe_conv2d_fwd_bn_keep", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y), ptr(st), rate,
+                     seed, ptr(sc), ptr(sh), 1, ptr(xb), ptr(keep), 1, stream())
+        else:
+            if keep is None:
+                call("acfe_conv2d_fwd_dropout", ptr(x), N, H, W, C, ptr(wp), K, 3, 3, 1, 1, 1, H, W, ptr(b), ptr(y),
+                     1, ptr(st), rate, seed, stream())
+            else:
+                call("acfe_conv2d_fwd_dropout_keep", ptr(x), N, H, W, C, ptr(wp), K, 1, 1, ptr(b), ptr(y), ptr(st),
+                     rate, seed, ptr(keep), stream())
+        torch.cuda.synchronize()
+        return y, st
+    keep = torch.full((N, H, W, K // 8), 0xAA, dtype=torch.uint8, device=cuda)
+    y0, st0 = fwd(None)
+    y1, st1 = fwd(keep)
+    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16)) and torch.equal(st1, st0)
+    ones = torch.ones((N, H, W, K), dtype=BF, device=cuda)
+    m = torch.empty_like(ones)
+    call("acfe_dropout", ptr(ones), ones.numel(), rate, seed, ptr(m), 1, stream())
+    torch.cuda.synchronize()
+    mask = (m != 0).reshape(N, H, W, K // 8, 8).to(torch.int32)
+    bits = sum(mask[..., j] << j for j in range(8)).to(torch.uint8)
+    assert torch.equal(keep, bits)
+    # the fold wgrad: BN backward apply (+ReLU mask) -> dropout backward inside the wgrad staging
+    dy = torch.randn((N, H, W, K), generator=g).to(BF).to(cuda)
+    u = y1
+    bsc, bsh = (torch.rand(K, generator=g) + 0.5).to(cuda), (torch.randn(K, generator=g) * 0.2).to(cuda)
+    coef = (torch.randn(3 * K, generator=g) * 0.3).to(cuda)
+    brows = lib.acfe_conv2d_wgrad_bnbwd_rows(N, H, W, C, K)
+    assert brows > 0
+    ws = torch.empty((lib.acfe_conv2d_wgrad_workspace(N, H, W, C, K, 3, 3, H, W),), device=cuda)
+
+    def fold(kp):
+        gout = torch.full((N, H, W, K), float("nan"), dtype=BF, device=cuda)
+        dw = torch.empty((K, 3, 3, C), device=cuda)
+        sums = torch.empty((brows, 2, K), dtype=F64, device=cuda)
+        if kp is None:
+            call("acfe_conv2d_wgrad_bnbwd", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(bsc), ptr(bsh), 1, ptr(coef),
+                 None, rate, seed, ptr(gout), ptr(dw), 0.0, ptr(ws), ptr(sums), stream())
+        else:
+            call("acfe_conv2d_wgrad_bnbwd_keep", ptr(x), N, H, W, C, ptr(dy), ptr(u), K, ptr(bsc), ptr(bsh), 1,
+                 ptr(coef), rate, seed, ptr(kp), ptr(gout), ptr(dw), 0.0, ptr(ws), ptr(sums), stream())
+        torch.cuda.synchronize()
+        return gout, dw, sums
+    a, bb = fold(None), fold(keep)
+    assert torch.equal(a[0].view(torch.int16), bb[0].view(torch.int16)), "dY"
+    assert torch.equal(a[1], bb[1]) and torch.equal(a[2], bb[2])
