@@ -184,7 +184,7 @@ def test_keep_bits(env, cuda, C, pro):
     BN-fold weight gradient reading them (acfe_conv2d_wgrad_bnbwd_keep) is
     bit-identical to the one regenerating the mask -- dY, dW and the slab."""
     ops, call, lib, ptr, stream = env
-    N, H, W, K = 6, 13, 100, 64
+    N, H, W, K = 6, 14, 100, 64  # (the fold wgrad takes row pairs: even H; a partial 64-column tile)
     assert lib.acfe_conv2d_dropout_keep_supported(N, H, W, C, K, 1)
     g = torch.Generator(device="cpu").manual_seed(C + pro)
     x = torch.randn((N, H, W, C), generator=g).to(BF).to(cuda)
