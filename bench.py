@@ -400,7 +400,7 @@ def train_line(model_name, dtype, classes, batch, steps, warmup, rank, world, de
                 if dtype != torch.bfloat16 else
                 "(k_conv3x3_1w<1,2,true>: 4 rows x 64 px x 128 ch per workgroup of 4 waves, one per SIMD with 128 accumulators each, chunk-resident halo rows; 2x2 max-pool + dropout + BN sums of the previous tile between this tile's MFMA groups)"
                 if bird else
-                "(k_conv3x3_rows<64,8,4,true,true>: bn2a + ReLU applied while staging the input rows, dropout + BN sums epilogue; 8 rows x 64 px x 64 ch per workgroup of 8 waves)"),
+                "(k_conv3x3_r64<4,1,true,true>: bn2a + ReLU applied while staging the input rows, dropout (+ keep bits) + BN sums of the previous tile between this tile's MFMA groups; persistent, 8 rows x 64 px x 64 ch per tile, 8 waves)"),
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
             "avg_launch_ms": round(fwd_ms, 4), "flops_per_launch": flops_launch,

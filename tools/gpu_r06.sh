@@ -34,6 +34,7 @@ for w in "$@"; do
     t1x) step t1x_bench 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra ;;
     wrnq) step wrnq_bench 300 python bench.py --model wrn --classes 2 --steps 8 --warmup 3 --no-cpu-baseline --no-extra ;;
     sqr64) BENCH_ARGS='--model wrn --classes 2' step sqr64 400 bash -c "bash tools/pmc_sq.sh ${TAG}_r64 'k_conv3x3_r64' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_r64 'k_conv3x3_r64<4' 'k_conv3x3_r64<3' 'k_conv3x3_r64<5'" ;;
+    fwdps) step fwdps 300 python tools/fwdp_stamps.py ;;
     r64st) step r64st 300 python tools/r64_stamps.py 512 ;;
     sq3r64) BENCH_ARGS='--model wrn --classes 2' step sq3r64 300 bash tools/pmc_sq3.sh ${TAG}_r64mix 'k_conv3x3_r64' ;;
     bnprobe) step bnprobe 300 python tools/bn_moving_probe.py ;;
@@ -52,8 +53,8 @@ for w in "$@"; do
            done; done ;;
     mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
     fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
-    evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r06 'k_conv3x3_rows<64, 8, 4, true, true>' 12910141440 \
-             'k_conv3x3_rows<64,8,4,true,true> (wr_resnet b1/b2 conv2a 3x3 64->64 @128x513 with the BN prologue + dropout + BN sums, batch 512)' \
+    evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r06 'k_conv3x3_r64<4, 1, true, true>' 12910141440 \
+             'k_conv3x3_r64<4,1,true,true> (wr_resnet b1/b2 conv2a 3x3 64->64 @128x513 with the BN prologue + dropout + BN sums, batch 512)' \
              --model wrn --classes 2 --steps 2 --warmup 1 ;;
     evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r06 'k_conv3x3_1w<1, 2, true, true, false>' 5905580032 \
              'k_conv3x3_1w<1,2,true,true> (wr_resnet_bird s1b0 branch21 3x3 128->128 @128x256 + 2x2 max-pool + dropout + BN sums, batch 512)' \
