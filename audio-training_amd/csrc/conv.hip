@@ -620,6 +620,7 @@ struct Stamps {
 
 __device__ uint2 g_store_sink[64];  // never read: target of masked-off epilogue stores
 __device__ u32x4 g_store_sink16[64];  // the same for 16-B stores
+__device__ __attribute__((aligned(16))) uint16_t g_store_sink_rows[64 * 64];  // the same, one 128-B row per lane
 
 
 // RES (acfe_conv2d_fwd_add where the row-halo kernels do not apply, e.g.
@@ -842,6 +843,7 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
 #pragma unroll
     for (int i = 0; i < NV; ++i) sv[i] = 0.f;
     const int pbase = ctm * BM + wm * TWM + (lane & 15);
+    const int c0 = n0 + wn * TWN + (lane >> 4) * 4;  // the lane's first channel (fn = 0)
     // S2D: per fragment column fn, the lane's channel quad c -> block position
     // (a, b) and channel cc (s2d_C a power of two, a = ab * amul >> 5 for the
     // st^2 < 32 positions), as an element offset from the block origin
@@ -849,7 +851,7 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     if constexpr (S2D) {
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const int c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
+        const int c = c0 + fn * 16;
         const int ab = g.s2d_fill ? 0 : c >> g.s2d_lc, cc = c & (g.s2d_C - 1);
         const int a = (ab * g.s2d_amul) >> 5, b = ab - a * g.s2d;
         s2a[fn] = a;
@@ -857,61 +859,94 @@ k_conv_fwd_p(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         s2o[fn] = (a * g.s2d_W + b) * g.s2d_C + cc;
       }
     }
+    // The tile's values as bf16 words (two channels each, pk_bf2 = f2bf's
+    // rounding), Dropout by acfe_dropout's pair hashes -- one per channel pair,
+    // from a Weyl term advanced by constants when every index is < 2^32 (the
+    // per-element 64-bit hash cost 4 quarter-rate multiplies per value, r06l)
+    // -- then the residual add, the statistics of the stored values and one
+    // 8-byte store per fragment through a per-row pointer (fn: immediate offset).
+    auto epi = [&](auto drop_c) __attribute__((always_inline)) {
+      constexpr bool DROP = decltype(drop_c)::value;
+      const bool w32 = DROP && g.idx32;
+      const uint32_t hwl = (((uint32_t)pbase * (uint32_t)g.K + (uint32_t)c0) >> 1) * 0x9E3779B1u +
+                           (uint32_t)g.drop.seed;
+      const uint32_t hwm = (uint32_t)(8 * g.K) * 0x9E3779B1u;  // + 16 pixels (pair index + 8 K)
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
-      const int pix = pbase + fm * 16;
-      const bool inb = pix < M;
-      // super-pixel store (g.s2d): this pixel's dX block origin (sn, sh, sw),
-      // the divisions by P Q and Q through a float reciprocal (pix < 2^24) and
-      // one correction step
-      int sh = 0, sw = 0;
-      long long sbase = 0;
-      if constexpr (S2D) {
-        const int pp = inb ? pix : 0;
-        int sn = (int)((float)pp * g.s2d_rpq);
-        sn -= sn * PQ > pp ? 1 : 0;
-        sn += (sn + 1) * PQ <= pp ? 1 : 0;
-        const int rem = pp - sn * PQ;
-        int u = (int)((float)rem * g.s2d_rq);
-        u -= u * g.Q > rem ? 1 : 0;
-        u += (u + 1) * g.Q <= rem ? 1 : 0;
-        sh = u * g.s2d - g.s2d_pt;
-        sw = (rem - u * g.Q) * g.s2d - g.s2d_pl;
-        sbase = (((long long)sn * g.s2d_H + sh) * g.s2d_W + sw) * g.s2d_C;
-      }
+      for (int fm = 0; fm < FM; ++fm) {
+        const int pix = pbase + fm * 16;
+        const bool inb = pix < M;
+        // super-pixel store (g.s2d): this pixel's dX block origin (sn, sh, sw),
+        // the divisions by P Q and Q through a float reciprocal (pix < 2^24) and
+        // one correction step
+        int sh = 0, sw = 0;
+        long long sbase = 0;
+        if constexpr (S2D) {
+          const int pp = inb ? pix : 0;
+          int sn = (int)((float)pp * g.s2d_rpq);
+          sn -= sn * PQ > pp ? 1 : 0;
+          sn += (sn + 1) * PQ <= pp ? 1 : 0;
+          const int rem = pp - sn * PQ;
+          int u = (int)((float)rem * g.s2d_rq);
+          u -= u * g.Q > rem ? 1 : 0;
+          u += (u + 1) * g.Q <= rem ? 1 : 0;
+          sh = u * g.s2d - g.s2d_pt;
+          sw = (rem - u * g.Q) * g.s2d - g.s2d_pl;
+          sbase = (((long long)sn * g.s2d_H + sh) * g.s2d_W + sw) * g.s2d_C;
+        }
+        uint16_t* rowp = inb ? Y + (long long)pix * g.ldy + c0 : g_store_sink_rows + lane * 64;
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int c = n0 + wn * TWN + fn * 16 + (lane >> 4) * 4;
-        uint16_t h[4];
+        for (int fn = 0; fn < FN; ++fn) {
+          unsigned wv[2];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          h[jj] = f2bf(acc[fm][fn][jj] + bv[fn][jj]);
-          if (g.drop.on) h[jj] = f2bf(drop_apply<T>(g.drop, (uint64_t)pix * g.K + c + jj, bf2f(h[jj])));
+          for (int p = 0; p < 2; ++p)
+            wv[p] = pk_bf2(acc[fm][fn][2 * p] + bv[fn][2 * p], acc[fm][fn][2 * p + 1] + bv[fn][2 * p + 1]);
+          if constexpr (DROP) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+              const uint32_t hsh =
+                  w32 ? hash_u32_lo_w(g.drop.seed, hwl + (uint32_t)fm * hwm + (uint32_t)(8 * fn + p) * 0x9E3779B1u)
+                      : hash_u32(g.drop.seed, ((uint64_t)pix * g.K + c0 + fn * 16 + 2 * p) >> 1);
+              const bool klo = (hsh & 0xFFFFu) >= g.drop.thr, khi = (hsh >> 16) >= g.drop.thr;
+              const float lo = klo ? bf2f(f2bf(__uint_as_float(wv[p] << 16) * g.drop.scl)) : 0.f;
+              const float hi = khi ? bf2f(f2bf(__uint_as_float(wv[p] & 0xffff0000u) * g.drop.scl)) : 0.f;
+              wv[p] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+            }
+          }
           if constexpr (RES) {
-            const unsigned rw = jj < 2 ? rres[fm][fn].x : rres[fm][fn].y;
-            float z = bf2f(h[jj]) + __uint_as_float((jj & 1) ? (rw & 0xffff0000u) : (rw << 16));
-            if (g.res_relu) z = fmaxf(z, 0.f);
-            h[jj] = f2bf(z);
+            const unsigned rw[2] = {rres[fm][fn].x, rres[fm][fn].y};
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+              float lo = __uint_as_float(wv[p] << 16) + __uint_as_float(rw[p] << 16);
+              float hi = __uint_as_float(wv[p] & 0xffff0000u) + __uint_as_float(rw[p] & 0xffff0000u);
+              if (g.res_relu) lo = fmaxf(lo, 0.f), hi = fmaxf(hi, 0.f);
+              wv[p] = pk_bf2(lo, hi);
+            }
           }
           if constexpr (!S2D) {  // (the dgrad has no statistics)
-            const float f = inb ? bf2f(h[jj]) : 0.f;
-            sv[fn * 4 + jj] += f;
-            sv[FN * 4 + fn * 4 + jj] += f * f;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const unsigned w = wv[jj >> 1];
+              const float f = inb ? __uint_as_float((jj & 1) ? (w & 0xffff0000u) : (w << 16)) : 0.f;
+              sv[fn * 4 + jj] += f;
+              sv[FN * 4 + fn * 4 + jj] += f * f;
+            }
           }
+          uint2 v;
+          v.x = wv[0];
+          v.y = wv[1];
+          uint2* dst = reinterpret_cast<uint2*>(rowp + fn * 16);
+          if constexpr (S2D) {
+            dst = (inb && (unsigned)(sh + s2a[fn]) < (unsigned)g.s2d_H && (unsigned)(sw + s2b[fn]) < (unsigned)g.s2d_W)
+                      ? reinterpret_cast<uint2*>(Y + sbase + s2o[fn])
+                      : &g_store_sink[lane];
+          }
+          *dst = v;
+          acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
         }
-        uint2 v;
-        v.x = (unsigned)h[0] | ((unsigned)h[1] << 16);
-        v.y = (unsigned)h[2] | ((unsigned)h[3] << 16);
-        uint2* dst = inb ? reinterpret_cast<uint2*>(Y + (long long)pix * g.ldy + c) : &g_store_sink[lane];
-        if constexpr (S2D) {
-          dst = (inb && (unsigned)(sh + s2a[fn]) < (unsigned)g.s2d_H && (unsigned)(sw + s2b[fn]) < (unsigned)g.s2d_W)
-                    ? reinterpret_cast<uint2*>(Y + sbase + s2o[fn])
-                    : &g_store_sink[lane];
-        }
-        *dst = v;
-        acc[fm][fn] = f4{0.f, 0.f, 0.f, 0.f};
       }
-    }
+    };
+    if (g.drop.on) epi(std::true_type{});
+    else epi(std::false_type{});
     pend = true;
     if (stats) {
       // butterfly reduce-scatter over the 16 lanes of equal lane>>4, partners

@@ -16,6 +16,13 @@ typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t T16;
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+// two floats -> one word of two bf16 (lo in bits 0-15), f2bf's RNE rounding
+// in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ unsigned pk_bf2(float lo, float hi) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f2v){lo, hi}, b2v));
+}
 
 struct ConvGeom {
   int N, H, W, C;    // input

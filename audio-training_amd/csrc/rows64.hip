@@ -72,8 +72,6 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   float* pss = reinterpret_cast<float*>(smem + SMEM0);
   float* bnt = reinterpret_cast<float*>(smem + SMEMP);
-  typedef float f2v __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, q = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = wid >> 2, wp = wid & 3;

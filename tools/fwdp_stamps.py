@@ -44,7 +44,7 @@ def run(tag, fn, flops):
         print(f"    {n:9s} {100 * t[:, i].mean() / tot:5.1f} %")
 
 
-def conv(H, W, C, K, R, S, st, stats):
+def conv(H, W, C, K, R, S, st, stats, drop=None):
     x = (torch.randn((N, H, W, C), device=dev) * 0.5).to(BF)
     w = torch.randn((K, R, S, C), device=dev) / (R * S * C) ** 0.5
     b = torch.zeros((K,), device=dev)
@@ -52,13 +52,13 @@ def conv(H, W, C, K, R, S, st, stats):
     Q, pl = ops.same_padding(W, S, st)
     fl = 2.0 * N * P * Q * K * R * S * C
     lbl = f"{R}x{S}/{st} {C}->{K} @{H}x{W}"
-    run(f"fwd   {lbl}", lambda: ops._conv_fwd(x, w, b, st, pt, pl, P, Q, stats), fl)
+    run(f"fwd   {lbl}" + (" + dropout" if drop else ""), lambda: ops._conv_fwd(x, w, b, st, pt, pl, P, Q, stats, drop), fl)
     dy = (torch.randn((N, P, Q, K), device=dev) * 0.5).to(BF)
     run(f"dgrad {lbl}", lambda: ops._conv_bwd(x, w, dy, st, pt, pl, P, Q, True, False, False), fl)
 
 
-conv(128, 513, 64, 128, 3, 3, 2, True)    # stage-2 transition conv (b3.conv2a)
+conv(128, 513, 64, 128, 3, 3, 2, True, (0.1, 7))    # stage-2 transition conv (b3.conv2a)
 conv(128, 513, 64, 128, 1, 1, 2, False)   # its 1x1 shortcut
-conv(64, 257, 128, 256, 3, 3, 2, True)    # stage-3 transition conv
-conv(64, 257, 128, 256, 1, 1, 2, False)
-conv(32, 129, 256, 256, 3, 3, 1, True)    # stage-3 3x3 (reference point: 36 K-tiles)
+conv(64, 257, 128, 256, 3, 3, 3, True, (0.1, 7))    # stage-3 transition conv (stride 3)
+conv(64, 257, 128, 256, 1, 1, 3, False)
+conv(22, 86, 256, 256, 3, 3, 1, True)     # stage-3 3x3 (reference point: 36 K-tiles)
