@@ -57,6 +57,7 @@ SIGNATURES: dict[str, list] = {
     "acfe_conv2d_wgrad_workspace": [I32, I32, I32, I32, I32, I32, I32, I32, I32],
     "acfe_conv2d_wgrad": [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, F32, I32, P, P],
     "acfe_conv_r64_enable": [I32],
+    "acfe_mel_w5_frames": [I32],
     "acfe_conv2d_wgrad_bnbwd_rows": [I32] * 5,
     "acfe_conv2d_wgrad_bnbwd": [P, I32, I32, I32, I32, P, P, I32, P, P, I32, P, P, F32, C.c_uint64, P, P, F32, P, P,
                                 P],

@@ -20,6 +20,7 @@
 #error "ACFE_MEL_CUT belongs to `make ablate` builds only"
 #endif
 #include <cmath>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -967,6 +968,278 @@ k_mel_w4(const float* __restrict__ raw, int64_t cs, int n, const float* __restri
   }
 }
 
+// ---- k_mel_w5 (n_fft = 4096): ONE wave per frame.
+// The 2048-point complex FFT of k_mel_w4 with each lane running two of its
+// 128 threads (virtual threads j = lane + 64 h, h = 0 / 1: the same radix
+// 16 / 16 / 8 Stockham passes, the same swizzled 16 KB frame buffer, the same
+// per-instruction address patterns, so the same conflict-free LDS accesses),
+// every pass ordered by the wave's own in-order LDS queue instead of the six
+// workgroup barriers per frame: a workgroup is one wave walking fpw frames,
+// each wave's frame buffer its own.  Pass 1 issues both halves' 32 sample
+// loads before the first DFT; pass 2 reads both halves before it writes (the
+// in-place Stockham step); pass 3 holds the four butterflies j, 256 - j of both
+// halves, then forms the power spectrum from registers as k_mel_w4.  Band m
+// and its mirror n_mels - 1 - m per lane (balanced lengths).  Arithmetic per
+// value identical to k_mel_w4 (same functions, same order): bit-identical.
+#ifndef MEL_W5_WAVES
+#define MEL_W5_WAVES 3
+#endif
+template <int POW>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MEL_W5_WAVES)))
+k_mel_w5(const float* __restrict__ raw, int64_t cs, int n, const float* __restrict__ stats, int pad_mode,
+         int n_frames, int fpw, int hop, const float2* __restrict__ tw, const float2* __restrict__ rtw,
+         const int* __restrict__ band, const float* __restrict__ vals, int n_mels, int kmin, int kmax,
+         float* __restrict__ out, int layout) {
+  constexpr int NC = 2048, L = 2 * NC, NB0 = NC / 16;
+  extern __shared__ float2 wbuf_[];
+  v2f* wbuf = reinterpret_cast<v2f*>(wbuf_);
+  float* pw = reinterpret_cast<float*>(wbuf_);
+  const int nk = kmax - kmin + 1;
+  const int t0 = threadIdx.x;
+  const int gx = gridDim.x, nwg = gx * gridDim.y, lin = blockIdx.x + gx * blockIdx.y;
+  const int item = nwg % 8 == 0 ? (lin % 8) * (nwg / 8) + lin / 8 : lin;  // XCD-contiguous (k_mel_w4)
+  const int b = item / gx;
+  const float* xb = raw + (int64_t)b * cs;
+  const bool do_norm = stats != nullptr;
+  const float mn = do_norm ? stats[2 * b] : 0.f, rng = do_norm ? stats[2 * b + 1] : 1.f;
+  const float rinv = __fdiv_rn(1.0f, rng);
+  const int f0 = (item - b * gx) * fpw;
+  v2f bw2[4], e0[2][3], rb0[2];
+  {
+    const int tb = (t0 & 15) * 8;  // (lane + 64) & 15 == lane & 15: shared by both halves
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float2 w = tw[(tb << q) & (NC - 1)];
+      bw2[q] = v2f{w.x, w.y};
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = t0 + 64 * h;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const float2 w = tw[(j << q) & (NC - 1)];
+        e0[h][q] = v2f{w.x, w.y};
+      }
+      rb0[h] = v2f{rtw[j].x, rtw[j].y};
+    }
+  }
+  constexpr float PSCALE = POW == 2 ? 0.25f : 0.5f;
+  typedef float f2a __attribute__((ext_vector_type(2), aligned(4)));
+  for (int f = f0; f < f0 + fpw && f < n_frames; ++f) {
+    // the base twiddles opaque per frame: their powers, the Hann terms and the
+    // addresses are recomputed each frame instead of hoisted (k_mel_w4)
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(bw2[q]));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      asm volatile("" : "+v"(rb0[h]));
+#pragma unroll
+      for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(e0[h][q]));
+    }
+    const int start = (pad_mode == ACFE_PAD_END) ? f * hop : f * hop - L / 2;
+    const bool inb = start >= 0 && start + L <= n;
+    // ---- pass 1 (radix 16, span 1) straight from memory, both halves' loads first
+    {
+      v2f xv[2][16];
+      if (inb) {
+        const float* xs = xb + start + 2 * t;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xv[h][r] = *reinterpret_cast<const f2a*>(xs + 128 * h + 2 * r * NB0);
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int nn = 2 * (t + 64 * h + r * NB0);
+            xv[h][r] = v2f{fetch(xb, n, start + nn, pad_mode, false, 0.f, 1.f),
+                           fetch(xb, n, start + nn + 1, pad_mode, false, 0.f, 1.f)};
+          }
+      }
+      // the previous frame's band reads of pw precede this frame's stores
+      // (in-order LDS queue of the wave; compiler ordering only)
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = t + 64 * h;
+        const float ce = e0[h][0].x, se = -e0[h][0].y;
+        constexpr float c1 = 0.99999882345170190993f, s1 = 0.00153398018628476550f;
+        const float co = ce * c1 - se * s1, so = se * c1 + ce * s1;
+        const v2f cc = v2f{ce, co}, ss = v2f{se, so};
+        v2f v[16];
+        auto hann2 = [&](int r) __attribute__((always_inline)) {
+          const float2 u = w16(r);
+          return __builtin_elementwise_fma(ss, sp2(-u.y), __builtin_elementwise_fma(cc, sp2(-u.x), sp2(1.f)));
+        };
+        if (do_norm) {
+#pragma clang fp contract(off)
+          const v2f vmn = sp2(mn), vrng = sp2(rng), vri = sp2(rinv);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const v2f tt = xv[h][r] - vmn;
+            const v2f q0v = tt * vri;
+            const v2f e = __builtin_elementwise_fma(-q0v, vrng, tt);
+            v2f q = __builtin_elementwise_fma(e, vri, q0v);
+            q = q + sp2(0.000001f);
+            q = q - sp2(0.5f);
+            v[r] = q * hann2(r);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float2 u = w16(r);
+            v[r] = xv[h][r] * __builtin_elementwise_fma(ss, sp2(-0.5f * u.y),
+                                                        __builtin_elementwise_fma(cc, sp2(-0.5f * u.x), sp2(0.5f)));
+          }
+        }
+        if (do_norm && !inb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int nn = 2 * (j + r * NB0);
+            if (!in_sig(start + nn, n, pad_mode)) v[r].x = 0.f;
+            if (!in_sig(start + nn + 1, n, pad_mode)) v[r].y = 0.f;
+          }
+        }
+        pdft16(v);
+        const unsigned ua = (unsigned)msw(16 * j) * 8u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lds2v(wbuf, ua ^ (8u * r)) = v[r];
+        __builtin_amdgcn_sched_barrier(0);  // one half at a time (registers)
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- pass 2 (radix 16, span 16): every read of the pass before its writes
+    {
+      v2f v[2][16], w[16];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const unsigned ub = (unsigned)msw(t + 64 * h) * 8u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[h][r] = lds2v(wbuf, (ub ^ (64u * (r & 1))) + 1024u * r);
+      }
+      ptwiddle_pows<16>(bw2, w);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int r = 1; r < 16; ++r) v[h][r] = pk_cmul(v[h][r], w[r]);
+        pdft16(v[h]);
+        const int j = t + 64 * h;
+        const unsigned uc = (unsigned)(256 * (j >> 4) + (j & 15)) * 8u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lds2v(wbuf, (uc ^ (8u * r)) + 128u * r) = v[h][r];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- pass 3 (radix 8, span 256): butterflies j, 256 - j of both halves
+    v2f z[2][2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = t + 64 * h;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const unsigned ad = (unsigned)msw(p ? (j ? 256 - j : 128) : j) * 8u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) z[h][p][r] = lds2v(wbuf, ad + 2048u * r);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // all pass-3 reads before the power writes (pw aliases the buffer)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = t + 64 * h;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        v2f bw[4], w[8];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bw[q] = p == 0 ? e0[h][q] : (j ? w16k(pk_conj(e0[h][q]), 2 << q) : w16v(1 << q));
+        ptwiddle_pows<8>(bw, w);
+#pragma unroll
+        for (int r = 1; r < 8; ++r) z[h][p][r] = pk_cmul(z[h][p][r], w[r]);
+        pdft8(z[h][p]);
+      }
+      const v2f rb1 = j ? w16k(pk_conj(rb0[h]), 1) : v2f{0.98078528040323044913f, -0.19509032201612826785f};
+      int rhi0 = kmax >> 8, rhi1 = kmax >= 128 ? (kmax - 128) >> 8 : -1;
+      int rlo0 = kmin > 127 ? (kmin - 127 + 255) >> 8 : 0, rlo1 = kmin > 255 ? (kmin - 255 + 255) >> 8 : 0;
+      asm volatile("" : "+s"(rhi0), "+s"(rhi1), "+s"(rlo0), "+s"(rlo1));
+      const bool l0 = j == 0;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int kb = (p ? (l0 ? 128 : 256 - j) : j) - kmin;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          if (4 * hh + 3 < (p ? rlo1 : rlo0) || 4 * hh > (p ? rhi1 : rhi0)) continue;
+          v2f ea[4], da[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = 4 * hh + u;
+            const v2f zm = l0 ? (p == 0 ? z[h][0][(8 - r) & 7] : z[h][1][7 - r]) : z[h][p ^ 1][7 - r];
+            ea[u] = pk_addc(z[h][p][r], zm);
+            da[u] = pk_subc(z[h][p][r], zm);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) da[u] = pk_cmul(w16k(p ? rb1 : rb0[h], 4 * hh + u), da[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) ea[u] = pk_addmi(ea[u], da[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = 4 * hh + u;
+            float pv = ea[u].x * ea[u].x + ea[u].y * ea[u].y;
+            if constexpr (POW != 2) pv = sqrtf(pv);
+            const int i = kb + 256 * r;
+            pw[(unsigned)i < (unsigned)nk ? i : 2 * NC - 1] = pv;
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t == 0 && kmax == NC) {  // Nyquist bin: Z[0] with itself, W_4096^2048 = -1
+      float pv = rbin_power4_pk(z[0][0][0], z[0][0][0], v2f{-1.f, 0.f});
+      if constexpr (POW != 2) pv = sqrtf(pv);
+      pw[NC - kmin] = pv;
+    }
+    if (t < 8) pw[nk + t] = 0.f;
+    __builtin_amdgcn_wave_barrier();
+    // ---- banded mel: bands q and n_mels - 1 - q per lane
+    auto dot8 = [](v2f acc, const float4 a, const float4 c, const float* p) __attribute__((always_inline)) {
+      acc = __builtin_elementwise_fma(v2f{a.x, a.y}, v2f{p[0], p[1]}, acc);
+      acc = __builtin_elementwise_fma(v2f{a.z, a.w}, v2f{p[2], p[3]}, acc);
+      acc = __builtin_elementwise_fma(v2f{c.x, c.y}, v2f{p[4], p[5]}, acc);
+      return __builtin_elementwise_fma(v2f{c.z, c.w}, v2f{p[6], p[7]}, acc);
+    };
+    for (int q = t; q < (n_mels + 1) / 2; q += 64) {
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int m = side ? n_mels - 1 - q : q;
+        if (side && m == q) continue;
+        const int s0 = band[3 * m], pl = (band[3 * m + 1] + 7) & ~7, off = band[3 * m + 2];
+        const float4* v0 = reinterpret_cast<const float4*>(vals + off);
+        const float* p0 = pw + (s0 - kmin);
+        v2f acc = v2f{0.f, 0.f};
+        for (int i0 = 0; i0 < pl; i0 += 8) acc = dot8(acc, v0[i0 / 4], v0[i0 / 4 + 1], p0 + i0);
+        out[layout == ACFE_LAYOUT_BTM ? ((size_t)b * n_frames + f) * n_mels + m
+                                      : ((size_t)b * n_mels + m) * n_frames + f] = (acc.x + acc.y) * PSCALE;
+      }
+    }
+  }
+}
+
+// n_fft = 4096 kernel choice: 0 = k_mel_w4 (two waves per frame), f > 0 =
+// k_mel_w5 with f frames per wave; initial value from ACFE_MEL_W5
+static std::atomic<int> g_mel_w5{[] {
+  const char* e = getenv("ACFE_MEL_W5");
+  return e ? atoi(e) : 0;
+}()};
+ACFE_API int acfe_mel_w5_frames(int fpw) {
+  if (fpw < 0 || fpw > 64) return ACFE_E_INVAL;
+  const int prev = g_mel_w5.load();
+  g_mel_w5.store(fpw);
+  return prev;
+}
+
 ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch, int n,
                           const float* stats, int pad_mode, int power, float* out, int layout,
                           void* stream) {
@@ -978,6 +1251,13 @@ ACFE_API int acfe_mel_fwd(acfe_plan_t p, const float* raw, int64_t cs, int batch
   if (batch == 0) return ACFE_OK;
   const int T = acfe_plan_num_frames(p, n, pad_mode);
   if (p->n_fft == 4096) {
+    const int w5 = g_mel_w5.load(std::memory_order_relaxed);
+    if (w5 > 0) {  // one wave per frame, w5 frames per wave
+      hipLaunchKernelGGL((power == 2 ? k_mel_w5<2> : k_mel_w5<1>), dim3(cdiv(T, w5), batch), dim3(64),
+                         sizeof(float2) * 2048, strm(stream), raw, cs, n, stats, pad_mode, T, w5, p->hop, p->d_tw,
+                         p->d_rtw, p->d_band, p->d_vals, p->n_mels, p->kmin, p->kmax, out, layout);
+      return launch_rc("acfe_mel_fwd");
+    }
     constexpr int fpw = 4;  // frames per workgroup (2: 1.51 ms, 8: equal, r01n/r02y; r03: 2 / 8 / 16 +3 / 0 / +2 %)
     hipLaunchKernelGGL((power == 2 ? k_mel_w4<2> : k_mel_w4<1>), dim3(cdiv(T, fpw), batch), dim3(128), sizeof(float2) * 2048, strm(stream), raw, cs, n,
                        stats, pad_mode, power, T, fpw, p->hop, p->d_tw, p->d_rtw, p->d_band, p->d_vals, p->n_mels,

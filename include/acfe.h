@@ -139,6 +139,11 @@ int acfe_copy_rows(const float* src, int64_t src_stride, int64_t src_rows, const
 int acfe_mel_fwd(acfe_plan_t plan, const float* raw, int64_t clip_stride, int batch, int n,
                  const float* stats, int pad_mode, int power, float* out, int layout,
                  void* stream);
+/* n_fft = 4096 kernel of acfe_mel_fwd: 0 = two waves per frame (k_mel_w4),
+ * f in 1..64 = one wave per frame walking f frames (k_mel_w5, bit-identical
+ * output).  Initial value from the environment (ACFE_MEL_W5, default see
+ * DESIGN.md); returns the previous setting, ACFE_E_INVAL out of range. */
+int acfe_mel_w5_frames(int frames_per_wave);
 
 /* Stored-spectrogram path (load_raw=False): mel = W . S^power of the magnitude
  * spectrogram each record holds, S = |librosa.stft| [n_bins][T] fp32 (clip b at

@@ -270,3 +270,37 @@ def test_normalize_reference_golden_bitexact(fe, cuda):
     a = plan.mel(x1, fe.normalize_stats(x1))
     b = plan.mel(fe.normalize(x1), None)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("fpw", [1, 3, 4, 8])
+@pytest.mark.parametrize("n_mels,pad_mode,norm,power,n", [(128, "end", True, 2, 144000), (160, "constant", True, 2, 144000),
+                                                          (128, "reflect", False, 1, 144000), (40, "end", True, 2, 144000),
+                                                          (128, "end", False, 2, 5000), (96, "constant", False, 1, 9000)])
+def test_mel_one_wave_per_frame(fe, cuda, fpw, n_mels, pad_mode, norm, power, n):
+    """k_mel_w5 (one wave per frame, acfe_mel_w5_frames(f)) is bit-identical to
+    k_mel_w4 -- same arithmetic per value, only the thread mapping and the
+    synchronisation differ -- across framings, normalise-on-load, power 1 / 2,
+    a 40-mel 1.5 kHz plan, short clips and frame counts that leave the last
+    wave's walk partial; and within the 2e-5 bound of the float64 oracle."""
+    from acfe._lib import lib
+
+    raw = synth_clips(3, n=n, seed=23)
+    plan = _plan(fe, n_mels=n_mels, fmax=11000 if n_mels != 40 else 1500)
+    x = torch.from_numpy(raw).to(cuda)
+    st = fe.normalize_stats(x) if norm else None
+    prev = lib.acfe_mel_w5_frames(0)
+    try:
+        ref4 = plan.mel(x, st, pad_mode=pad_mode, power=power, layout="btm").cpu().numpy()
+        lib.acfe_mel_w5_frames(fpw)
+        out5 = plan.mel(x, st, pad_mode=pad_mode, power=power, layout="btm").cpu().numpy()
+        out5t = plan.mel(x, st, pad_mode=pad_mode, power=power, layout="bmt").cpu().numpy()
+    finally:
+        lib.acfe_mel_w5_frames(prev)
+    np.testing.assert_array_equal(out5, ref4)
+    np.testing.assert_array_equal(out5t, out5.transpose(0, 2, 1))
+    src = of.normalize(raw) if norm else raw.astype(np.float64)
+    if pad_mode == "end":
+        ref = of.raw_to_mel(src, plan.weights, 4096, 281, power=power)
+    else:
+        ref = of.get_spect(src, plan.weights, 4096, 281, power, pad_mode)
+    _rel_close(out5, ref.transpose(0, 2, 1), 2e-5)

@@ -51,6 +51,7 @@ for w in "$@"; do
              if [ $v = new ]; then L=""; else L=$PWD/abtest/$v.so; fi
              ACFE_LIB=$L step t1_$v 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra && grep -o '"value": [0-9.]*' $O/t1_$v.log
            done; done ;;
+    melw5) step melt 300 python -u -m pytest tests/test_frontend_gpu.py -x -v --timeout 120 --timeout-method thread && for v in 0 1 2 4 8 0 4; do step mel_$v 120 python tools/mel_bench.py --iters 15 --prenorm --w5 $v && grep ms $O/mel_$v.log; done ;;
     mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
     fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r06 'k_conv3x3_r64<4, 1, true, true>' 12910141440 \

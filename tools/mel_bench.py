@@ -13,13 +13,17 @@ sys.path[:0] = [str(ROOT / "audio-training_amd"), str(ROOT)]
 import torch  # noqa: E402
 
 from acfe import frontend as fe  # noqa: E402
+from acfe._lib import lib  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--iters", type=int, default=9)
+ap.add_argument("--w5", type=int, default=None, help="acfe_mel_w5_frames(f): 0 = k_mel_w4, f = one wave per frame")
 ap.add_argument("--prenorm", action="store_true",
                 help="clips normalised beforehand (acfe.train.FrontEnd's path): no normalize-on-load")
 a = ap.parse_args()
+if a.w5 is not None:
+    lib.acfe_mel_w5_frames(a.w5)
 dev = torch.device("cuda", 0)
 g = torch.Generator(device="cpu").manual_seed(3)
 x = (torch.rand((a.batch, 144000), generator=g) * 2 - 1).to(dev)
@@ -41,5 +45,5 @@ for _ in range(a.iters):
 t = sorted(ts)[len(ts) // 2]
 T = out.shape[1]
 byts = a.batch * (144000 * 4 + T * 128 * 4)
-print(f"mel {a.batch} clips{' (pre-normalised)' if a.prenorm else ''}: {t:.3f} ms  {byts / t / 1e6:.1f} GB/s  {a.batch * 68.87e6 / t / 1e9:.2f} TFLOP/s "
+print(f"[w5={a.w5}] mel {a.batch} clips{' (pre-normalised)' if a.prenorm else ''}: {t:.3f} ms  {byts / t / 1e6:.1f} GB/s  {a.batch * 68.87e6 / t / 1e9:.2f} TFLOP/s "
       f"({a.batch * 68.87e6 / t / 1e9 / 157.3 * 100:.1f} % of fp32 VALU peak)", flush=True)
