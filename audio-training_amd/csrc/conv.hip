@@ -3227,6 +3227,15 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     for (int i = tid; i < KB; i += 512) fsum[i] = 0.0;
     __syncthreads();  // (read by the first sstore)
   }
+  // BWD: this thread's 8 channels are fixed (cg = tid % DGR: 512 is a multiple
+  // of DGR), so their 5 x 8 coefficients stay in registers across the walk
+  // instead of 10 LDS reads per staged granule
+  f4 fcv[BWD ? 10 : 1];
+  if constexpr (BWD) {
+    const f4* tb = reinterpret_cast<const f4*>(ftab + (tid % (KB / 8)) * 8);
+#pragma unroll
+    for (int q5 = 0; q5 < 5; ++q5) fcv[2 * q5] = tb[q5 * (KB / 4)], fcv[2 * q5 + 1] = tb[q5 * (KB / 4) + 1];
+  }
 
   u32x4 rd[DPT], rx[XPT];
   uint2 rda[UNP ? DPT : 1];  // UNP: argmax bytes + window taps, applied at the LDS store
@@ -3345,7 +3354,6 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
         // tile, dlo = (ro Q + pw) K + cg 8)
         const bool ok = fw0 + dpw[i] < g.Q;
         const long long e = fbase + dlo[i];
-        const f4* tb = reinterpret_cast<const f4*>(ftab + cg * 8);
         u32x4 v;
         // one pair hash per dword (channels 2d, 2d + 1; e is even), the four
         // from one Weyl multiply when the indices fit 32 bits
@@ -3358,38 +3366,61 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
             for (int d = 0; d < 4; ++d) hl[d] = hash_u32(g.drop.seed, ((uint64_t)e >> 1) + d);
           }
         }
+        // straight-line, one channel pair per packed-f32 op (r06: the
+        // per-element select of the dropout arm compiled to 16 exec-mask
+        // branches per step): the pair's words and masks are selected
+        // bitwise, the roundings are v_cvt_pk_bf16_f32 of the pair -- the
+        // same values element by element
+        const unsigned okm = ok ? ~0u : 0u;
+        const bool relu1 = (g.fb_relu & 1) != 0, relu2 = (g.fb_relu & 2) != 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-          const f4 sc = tb[d >> 1], sh = tb[KB / 4 + (d >> 1)], ca = tb[2 * (KB / 4) + (d >> 1)],
-                   cb = tb[3 * (KB / 4) + (d >> 1)], c0 = tb[4 * (KB / 4) + (d >> 1)];
-          const uint32_t hh = hl[d];
-          unsigned pk = 0;
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-            const int jj = (d & 1) * 2 + hf, j = 2 * d + hf;
-            const float xv = __uint_as_float(hf ? (rdx[i][d] & 0xffff0000u) : (rdx[i][d] << 16));
-            const float gv = __uint_as_float(hf ? (rd[i][d] & 0xffff0000u) : (rd[i][d] << 16));
-            const float gj = ((g.fb_relu & 1) && !(__builtin_fmaf(xv, sc[jj], sh[jj]) > 0.f)) ? 0.f : gv;
+          const f4 sc = fcv[d >> 1], sh = fcv[2 + (d >> 1)], ca = fcv[4 + (d >> 1)], cb = fcv[6 + (d >> 1)],
+                   c0 = fcv[8 + (d >> 1)];
+          const int jj = (d & 1) * 2;
+          const unsigned xw = rdx[i][d], gw = rd[i][d];
+          const f2v xv = {__uint_as_float(xw << 16), __uint_as_float(xw & 0xffff0000u)};
+          const f2v gv = {__uint_as_float(gw << 16), __uint_as_float(gw & 0xffff0000u)};
+          const f2v t = __builtin_elementwise_fma(xv, (f2v){sc[jj], sc[jj + 1]}, (f2v){sh[jj], sh[jj + 1]});
+          const f2v gj = {(relu1 && !(t.x > 0.f)) ? 0.f : gv.x, (relu1 && !(t.y > 0.f)) ? 0.f : gv.y};
 #ifdef ACFE_FB_NOXFORM
-            float o = gv;
+          f2v o = gv;
 #else
-            float o = __builtin_fmaf(ca[jj], gj, __builtin_fmaf(cb[jj], xv, c0[jj]));
+          f2v o = __builtin_elementwise_fma(
+              (f2v){ca[jj], ca[jj + 1]}, gj,
+              __builtin_elementwise_fma((f2v){cb[jj], cb[jj + 1]}, xv, (f2v){c0[jj], c0[jj + 1]}));
 #endif
-            if (g.fb_add) o += __uint_as_float(hf ? (rdr[i][d] & 0xffff0000u) : (rdr[i][d] << 16));
-            if ((g.fb_relu & 2) && !(xv > 0.f)) o = 0.f;  // x = a ReLU output upstream: its backward
-            o = bf2f(f2bf(o));
-            if constexpr (KEEP) {
-              o = ((rkb[i] >> j) & 1u) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
-            } else {
-              if (g.drop.on) o = ((hf ? hh >> 16 : hh & 0xFFFFu) >= g.drop.thr) ? bf2f(f2bf(o * g.drop.scl)) : 0.f;
-            }
-            o = ok ? o : 0.f;
-#ifndef ACFE_FB_NOSUM
-            fs[j] += o;
-#endif
-            pk |= hf ? (__float_as_uint(o) & 0xffff0000u) : (__float_as_uint(o) >> 16);
+          if (g.fb_add) {
+            const unsigned rw = rdr[i][d];
+            o += (f2v){__uint_as_float(rw << 16), __uint_as_float(rw & 0xffff0000u)};
           }
-          v[d] = pk;
+          // x = a ReLU output upstream: its backward
+          o.x = (relu2 && !(xv.x > 0.f)) ? 0.f : o.x;
+          o.y = (relu2 && !(xv.y > 0.f)) ? 0.f : o.y;
+          unsigned w = pk_bf2(o.x, o.y);
+          unsigned km = okm;
+          if (KEEP || g.drop.on) {
+            // the rounded pair times the keep scale, rounded again; the keep
+            // bits (bit 2d / 2d + 1 of the granule's byte, or the pair hash's
+            // halves against the threshold) as a 16-bit-per-element mask
+            const f2v r = (f2v){__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)} * g.drop.scl;
+            w = pk_bf2(r.x, r.y);
+            unsigned klo, khi;
+            if constexpr (KEEP) {
+              klo = (unsigned)((int)(rkb[i] << (31 - 2 * d)) >> 31);
+              khi = (unsigned)((int)(rkb[i] << (30 - 2 * d)) >> 31);
+            } else {
+              klo = (hl[d] & 0xFFFFu) >= g.drop.thr ? ~0u : 0u;
+              khi = (hl[d] >> 16) >= g.drop.thr ? ~0u : 0u;
+            }
+            km &= (klo & 0x0000ffffu) | (khi & 0xffff0000u);
+          }
+          w &= km;
+#ifndef ACFE_FB_NOSUM
+          fs[2 * d] += __uint_as_float(w << 16);
+          fs[2 * d + 1] += __uint_as_float(w & 0xffff0000u);
+#endif
+          v[d] = w;
         }
         if (idx < DG) *reinterpret_cast<u32x4*>(Ds + px * LDD + cg * 8) = v;
 #ifndef ACFE_FB_NOSTORE

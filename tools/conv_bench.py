@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time the acfe convolution kernels on the wr_resnet_bird T1 layer shapes
-(batch 512, bf16) with HIP events on the launch stream.  Prints TFLOP/s per
+and wr_resnet's stride-1 3x3 stages (batch 512, bf16) with HIP events on the launch stream.  Prints TFLOP/s per
 (layer, pass).  usage: python tools/conv_bench.py [--batch 512] [--iters 5]"""
 import argparse
 import sys
@@ -20,6 +20,10 @@ LAYERS = [
     ("s1b1.conv21 3x3 64->64", 64, 128, 64, 64, 3, 3),
     ("s2b1.conv21 3x3 128->32", 32, 64, 128, 32, 3, 3),
     ("head (4,10) 256->128", 16, 32, 256, 128, 4, 10),
+    # wr_resnet (resnet/wr_resnet.py) stage 1 / 2 / 3 stride-1 3x3 convs
+    ("wrn s1 3x3 64->64", 128, 513, 64, 64, 3, 3),
+    ("wrn s2 3x3 128->128", 64, 257, 128, 128, 3, 3),
+    ("wrn s3 3x3 256->256", 22, 86, 256, 256, 3, 3),
 ]
 
 

@@ -35,6 +35,8 @@ for w in "$@"; do
     wrnq) step wrnq_bench 300 python bench.py --model wrn --classes 2 --steps 8 --warmup 3 --no-cpu-baseline --no-extra ;;
     sqr64) BENCH_ARGS='--model wrn --classes 2' step sqr64 400 bash -c "bash tools/pmc_sq.sh ${TAG}_r64 'k_conv3x3_r64' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_r64 'k_conv3x3_r64<4' 'k_conv3x3_r64<3' 'k_conv3x3_r64<5'" ;;
     fwdps) step fwdps 300 python tools/fwdp_stamps.py ;;
+    cbw) step cbw 300 python tools/conv_bench.py --layers ${CBL:-6,7,8} --iters 5 ;;
+    sqs3) step sqs3 400 bash -c "bash tools/pmc_sq_cmd.sh ${TAG}_s3 'k_conv_fwd_p' tools/conv_bench.py --layers 8 --passes fwd,dgrad --iters 2 && python tools/sq_summary.py gpurun_out/pmc_${TAG}_s3 'k_conv_fwd_p<128'" ;;
     r64st) step r64st 300 python tools/r64_stamps.py 512 ;;
     sq3r64) BENCH_ARGS='--model wrn --classes 2' step sq3r64 300 bash tools/pmc_sq3.sh ${TAG}_r64mix 'k_conv3x3_r64' ;;
     bnprobe) step bnprobe 300 python tools/bn_moving_probe.py ;;
