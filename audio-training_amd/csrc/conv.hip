@@ -3173,10 +3173,17 @@ k_conv_wgrad(ConvGeom g, const T* __restrict__ X, const T* __restrict__ dY, floa
 // dgrad reads it next) and sums it per channel (the conv bias gradient) -- the
 // BN backward apply pass over the tensor is gone.  Each dY element is staged
 // by one workgroup of chunk 0 (the others only read it).
-template <int KB, bool UNP, int CW = 64, int NR = 1, bool BWD = false, bool KEEP = false>
+// SEGW: segment width -- 64 (NR rows x 64 pixels), or 16 (4 NR rows x 16
+// pixels) for the Q % 64 pixels left of each row, launched separately over
+// qs segment columns from column wofs, with the same grid, adding (wadd) its
+// partial slabs and BWD channel-sum rows into the first launch's (wr_resnet's
+// 513- / 257-wide stages otherwise run a whole 64-pixel segment per row group
+// for the last pixel).
+template <int KB, bool UNP, int CW = 64, int NR = 1, bool BWD = false, bool KEEP = false, int SEGW = 64>
 __global__ void __launch_bounds__(512, 1)
 k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY,
-                float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax) {
+                float* __restrict__ ws, int nchunk, int nseg, int segs_per_split, const uint8_t* __restrict__ amax,
+                int qs = 0, int wofs = 0, int wadd = 0) {
   static_assert(!(BWD && UNP), "BN backward fold: plain dY");
   // KEEP: the dropout keep bits of the forward (g.keep_in, one byte per 8-channel
   // granule) instead of the regenerated pair hashes (9 quarter-rate multiplies
@@ -3186,7 +3193,9 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 #define ACFE_FB_MID 0
 #endif
   constexpr int FBMID = ACFE_FB_MID < 2 * NR ? ACFE_FB_MID : 0;
-  constexpr int SEGW = 64, HW = SEGW + 2, HR = NR + 2;
+  static_assert(SEGW == 64 || SEGW == 16, "segment width");
+  // ROWS output rows per segment (SEGW 16: four times NR, the same 64 NR pixels)
+  constexpr int ROWS = SEGW == 64 ? NR : 4 * NR, HW = SEGW + 2, HR = ROWS + 2;
   // CW-channel chunks (C = 16 / 32 layers: the stage-2/3 branch2b): the 8 waves
   // are WC = CW / 16 channel blocks x WK = 8 / WC slices of K; a wave's nine
   // blocks are the nine taps of its channel block (CW = 64: 2 K halves x 4
@@ -3200,12 +3209,13 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   constexpr int WC = CW == 64 ? 4 : CW / 16;
   constexpr int WK = 8 / WC < KB / 16 ? 8 / WC : KB / 16, WP = 8 / (WC * WK);
   static_assert(WC * WK * WP == 8 && (2 * NR) % WP == 0, "wave split");
+  static_assert(SEGW == 64 || (WP == 1 && !UNP), "16-pixel segments: one pixel group, plain dY");
   constexpr int LDD = KB + 16, LDX = CW + 16;
-  constexpr int DS = NR * SEGW * LDD, XS = HR * HW * LDX;
+  constexpr int DS = ROWS * SEGW * LDD, XS = HR * HW * LDX;
   constexpr int FM = KB / (16 * WK), FN = 9;
   static_assert(FM >= 1, "K slice");
   constexpr int XGR = CW / 8;
-  constexpr int DGR = KB / 8, DG = NR * SEGW * DGR, XG = HR * HW * XGR;
+  constexpr int DGR = KB / 8, DG = ROWS * SEGW * DGR, XG = HR * HW * XGR;
   constexpr int DPT = (DG + 511) / 512, XPT = (XG + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (DS + XS)];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -3216,7 +3226,8 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   const int cc = bi % nchunk, split = (bi / nchunk) * 8 + xcd;
   const int sbeg = split * segs_per_split;
   const int send = sbeg + segs_per_split < nseg ? sbeg + segs_per_split : nseg;
-  const int QS = (g.Q + SEGW - 1) / SEGW;  // the last segment of a row may be partial
+  // segment columns (the last one may be partial)
+  const int QS = qs > 0 ? qs : (g.Q + SEGW - 1) / SEGW;
   const T16* zp = reinterpret_cast<const T16*>(g_zero_page);
   // BWD: [scale | shift | a | b | c][KB] and the channel sums of this workgroup
   __shared__ float ftab[BWD ? 5 * KB : 1];
@@ -3280,9 +3291,9 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     // share NR + 1 of their NR + 2 halo rows (and, UNP, their pooled dY row),
     // so the overlap is re-read from L2 one step later instead of a whole
     // image row later (r03v: 9.8 GB of HBM reads per launch vs 5.9 GB algorithmic)
-    const int PR = g.P / NR;  // row groups per image
+    const int PR = g.P / ROWS;  // row groups per image
     const int n = sg / (PR * QS), rem = sg - n * (PR * QS);
-    const int h = (rem % PR) * NR, w0 = (rem / PR) * SEGW;
+    const int h = (rem % PR) * ROWS, w0 = wofs + (rem / PR) * SEGW;
     // buffer loads on the segment's image (offsets < 2^31: halo_ok); an
     // element outside the image or the tile takes the out-of-range offset,
     // which loads zeros -- no 64-bit address arithmetic, no branches
@@ -3502,8 +3513,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
           if (more) sstore(buf ^ 1);
         }
       }
-      const int rb = ro * SEGW + kc * 32;  // dY pixel row of this half
-      const int xr = kc * 32;              // its pixel offset in the halo rows (tap row + ro below)
+      const int rb = kq * 32;  // dY pixel row of this half (SEGW 64: row ro, pixels kc 32 ..)
+      // its first pixel's halo offset (tap offsets in boff) and that of its
+      // second 16 pixels (SEGW 64: the same row, 16 on; 16: the next row)
+      const int xr = SEGW == 64 ? ro * HW + kc * 32 : 2 * kq * HW;
+      constexpr int XH = SEGW == 64 ? 16 : HW;
       bf8 af[FM];
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
@@ -3516,11 +3530,11 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
       }
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const uint16_t* xb = Xh + boff[fn] + ro * HW * LDX + 4 * pp;
+        const uint16_t* xb = Xh + boff[fn] + 4 * pp;
         const bf4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
             (lp)(reinterpret_cast<const __bf16*>(xb + (xr + 4 * grp + q) * LDX)));
         const bf4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lp)(reinterpret_cast<const __bf16*>(xb + (xr + 16 + 4 * grp + q) * LDX)));
+            (lp)(reinterpret_cast<const __bf16*>(xb + (xr + XH + 4 * grp + q) * LDX)));
         const bf8 bv = bf8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
@@ -3542,8 +3556,10 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     fflush();
     __syncthreads();
     for (int c = tid; c < KB; c += 512) {
-      g.fb_sums[((long long)blockIdx.x * 2 + 0) * KB + c] = cc == 0 ? fsum[c] : 0.0;
-      g.fb_sums[((long long)blockIdx.x * 2 + 1) * KB + c] = 0.0;
+      double* fr = g.fb_sums + (long long)blockIdx.x * 2 * KB;
+      const double v = cc == 0 ? fsum[c] : 0.0;
+      fr[c] = wadd ? fr[c] + v : v;
+      if (!wadd) fr[KB + c] = 0.0;
     }
   }
   // slab write: D[k][c] -> ws[split][k][tap * C + cc * 64 + c]
@@ -3557,7 +3573,8 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int k = wk * (KB / WK) + fm * 16 + (lane >> 4) * 4 + jj;
-        ws[((long long)(split * WP + wp) * g.K + k) * kd + col] = acc[fm][fn][jj];
+        float* o = ws + ((long long)(split * WP + wp) * g.K + k) * kd + col;
+        *o = wadd ? *o + acc[fm][fn][jj] : acc[fm][fn][jj];
       }
     }
 }
@@ -4431,6 +4448,11 @@ static int launch_wgrad_t(const ConvGeom& g, const void* x, const void* dy, floa
 struct HaloPlan {
   int cw, nr, wp, nchunk, nseg, sp, per;
   bool c16k64, k16c64;
+  // the Q % 64 remainder columns as 16-pixel segments (4 nr rows each) by a
+  // second launch over the same grid (plain K = 64 / 128 and the K = 64 BN
+  // fold): qs whole 64-pixel segment columns, then qse 16-pixel ones from wofs
+  bool edge;
+  int qs, qse, wofs, nsege, pere;
 };
 static HaloPlan halo_plan(const ConvGeom& g, bool amax, long long splits) {
   HaloPlan hp;
@@ -4455,7 +4477,11 @@ static HaloPlan halo_plan(const ConvGeom& g, bool amax, long long splits) {
   const bool k16c64 = cw == 64 && g.K == 16;
   const int nr = ((cw == 64 || c16k64) && g.P % 2 == 0 && (g.K == 64 || (g.K == 32 && !amax))) ? 2 : 1;
   const int wp = (c16k64 || k16c64) ? 2 : 1;
-  const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * ((g.Q + 63) / 64));
+  const int rem = g.Q >= 64 ? g.Q % 64 : 0;
+  const bool edge = rem && wp == 1 && !amax && cw == 64 && g.P % (4 * nr) == 0 &&
+                    ((g.K == 64 && nr == 2) || (g.K == 128 && nr == 1));
+  const int qs = edge ? g.Q / 64 : (g.Q + 63) / 64;
+  const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * qs);
   // c16k64: 75 KB of LDS and 114 VGPRs -> two workgroups per CU
   int sp = (c16k64 || k16c64 ? 512 : 256) / nchunk;
   if (sp > splits / wp) sp = (int)(splits / wp);
@@ -4471,6 +4497,12 @@ static HaloPlan halo_plan(const ConvGeom& g, bool amax, long long splits) {
   hp.per = (nseg + sp - 1) / sp;
   hp.c16k64 = c16k64;
   hp.k16c64 = k16c64;
+  hp.edge = edge;
+  hp.qs = qs;
+  hp.qse = edge ? (rem + 15) / 16 : 0;
+  hp.wofs = g.Q - rem;
+  hp.nsege = edge ? (int)((long long)g.N * (g.P / (4 * nr)) * hp.qse) : 0;
+  hp.pere = edge ? (hp.nsege + sp - 1) / sp : 0;
   return hp;
 }
 
@@ -4480,25 +4512,34 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   const int cw = hp.cw, nr = hp.nr, wp = hp.wp, nchunk = hp.nchunk, nseg = hp.nseg, sp = hp.sp, per = hp.per;
   const bool c16k64 = hp.c16k64, k16c64 = hp.k16c64;
   const dim3 gr(nchunk * sp);
+  const int qs = hp.qs, qse = hp.qse, wofs = hp.wofs, nsege = hp.nsege, pere = hp.pere;
   if (g.fb_sc) {  // acfe_conv2d_wgrad_bnbwd: the BN backward formed while staging dY
-#define WB(KB_, CW_, NR_, ...)                                                                                  \
-  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_, NR_, true, ##__VA_ARGS__>), gr, dim3(512), 0, s, g,      \
-                     (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
+#define WB(KB_, CW_, NR_, KP_)                                                                                  \
+  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_, NR_, true, KP_>), gr, dim3(512), 0, s, g,                 \
+                     (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr, qs, 0, 0)
+#define WBE(KB_, CW_, NR_, KP_)                                                                                 \
+  hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_, NR_, true, KP_, 16>), gr, dim3(512), 0, s, g,             \
+                     (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nsege, pere, nullptr, qse, wofs, 1)
     if (amax || (wp != 1 && !c16k64)) return ACFE_E_INVAL;
     // keep bits: the stage-1 K = 64 fold only (the forward that writes them: k_conv3x3_r64 PM 4)
     if (g.keep_in && !(cw == 64 && g.K == 64 && nr == 2 && !c16k64 && g.drop.on)) return ACFE_E_INVAL;
-    if (c16k64 && nr == 2) WB(64, 16, 2);
-    else if (cw == 64 && g.K == 64 && nr == 2 && g.keep_in) WB(64, 64, 2, true);
-    else if (cw == 64 && g.K == 64 && nr == 2) WB(64, 64, 2);
-    else if (cw == 64 && g.K == 32 && nr == 2) WB(32, 64, 2);
+    if (c16k64 && nr == 2) WB(64, 16, 2, false);
+    else if (cw == 64 && g.K == 64 && nr == 2 && g.keep_in) {
+      WB(64, 64, 2, true);
+      if (hp.edge) WBE(64, 64, 2, true);
+    } else if (cw == 64 && g.K == 64 && nr == 2) {
+      WB(64, 64, 2, false);
+      if (hp.edge) WBE(64, 64, 2, false);
+    } else if (cw == 64 && g.K == 32 && nr == 2) WB(32, 64, 2, false);
     else return ACFE_E_INVAL;
+#undef WBE
 #undef WB
     *used = sp * wp;
     return launch_rc("acfe_conv2d_wgrad_bnbwd");
   }
 #define WH(KB_, U_)                                                                                              \
   hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, U_>), gr, dim3(512), 0, s, g, (const uint16_t*)x, (const uint16_t*)dy, \
-                     ws, nchunk, nseg, per, amax)
+                     ws, nchunk, nseg, per, amax, qs, 0, 0)
 #define WHC(KB_, CW_)                                                                                              \
   hipLaunchKernelGGL((k_wgrad3x3_halo<KB_, false, CW_>), gr, dim3(512), 0, s, g, (const uint16_t*)x,               \
                      (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr)
@@ -4516,16 +4557,25 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   } else if (cw == 16) {  // stage 3 (16 -> 256)
     WHC(256, 16);
   } else if (g.K == 128) {
-    if (amax) WH(128, true); else WH(128, false);
+    if (amax) WH(128, true);
+    else {
+      WH(128, false);
+      if (hp.edge)
+        hipLaunchKernelGGL((k_wgrad3x3_halo<128, false, 64, 1, false, false, 16>), gr, dim3(512), 0, s, g,
+                           (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nsege, pere, nullptr, qse, wofs, 1);
+    }
   } else if (g.K == 64) {
     if (amax && nr == 2)
       hipLaunchKernelGGL((k_wgrad3x3_halo<64, true, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
-                         (const uint16_t*)dy, ws, nchunk, nseg, per, amax);
+                         (const uint16_t*)dy, ws, nchunk, nseg, per, amax, qs, 0, 0);
     else if (amax) WH(64, true);
-    else if (nr == 2)
+    else if (nr == 2) {
       hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
-                         (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);
-    else WH(64, false);
+                         (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr, qs, 0, 0);
+      if (hp.edge)
+        hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 64, 2, false, false, 16>), gr, dim3(512), 0, s, g,
+                           (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nsege, pere, nullptr, qse, wofs, 1);
+    } else WH(64, false);
   } else if (nr == 2) {  // the stage-2 branch21 (128 -> 32): 36 MFMAs per wave per two-row step
     hipLaunchKernelGGL((k_wgrad3x3_halo<32, false, 64, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
                        (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);

@@ -1575,11 +1575,17 @@ __global__ void k_axis_pool(const T* __restrict__ x, long long outer, int L, int
     const int in = (int)(i % inner);
     const T* xp = x + o * (long long)L * inner + in;
     if (mode == 0) {
+      // tfp.math.reduce_logmeanexp(s x) / s: s x rounded once (no fp
+      // contraction: a fused fma(s, x, -m) left the max element's rounding
+      // residual in the exponent, expf(+256) = inf at |s x| ~ 5e9), shifted by
+      // its max -- by 0 when the max is not finite, as reduce_logsumexp does
+#pragma clang fp contract(off)
       float m = -INFINITY;
-      for (int l = 0; l < L; ++l) m = fmaxf(m, s * ld(xp, (long long)l * inner));
+      for (int l = 0; l < L; ++l) m = fmaxf(m, __fmul_rn(s, ld(xp, (long long)l * inner)));
+      const float sh = isfinite(m) ? m : 0.f;
       float acc = 0.f;
-      for (int l = 0; l < L; ++l) acc += expf(s * ld(xp, (long long)l * inner) - m);
-      y[i] = (m + logf(acc) - logf((float)L)) / s;
+      for (int l = 0; l < L; ++l) acc += expf(__fmul_rn(s, ld(xp, (long long)l * inner)) - sh);
+      y[i] = (sh + logf(acc) - logf((float)L)) / s;
     } else {
       float acc = 0.f;
       for (int l = 0; l < L; ++l) acc += ld(xp, (long long)l * inner);
@@ -1598,14 +1604,17 @@ __global__ void k_axis_pool_bwd(const T* __restrict__ x, const float* __restrict
     const long long base = o * (long long)L * inner + in;
     const float g = dy[i];
     if (mode == 0) {
+      // (the forward's rounding of s x and its shift)
+#pragma clang fp contract(off)
       float m = -INFINITY;
-      for (int l = 0; l < L; ++l) m = fmaxf(m, s * ld(x, base + (long long)l * inner));
+      for (int l = 0; l < L; ++l) m = fmaxf(m, __fmul_rn(s, ld(x, base + (long long)l * inner)));
+      const float sh = isfinite(m) ? m : 0.f;
       float acc = 0.f;
-      for (int l = 0; l < L; ++l) acc += expf(s * ld(x, base + (long long)l * inner) - m);
+      for (int l = 0; l < L; ++l) acc += expf(__fmul_rn(s, ld(x, base + (long long)l * inner)) - sh);
       const float inv = 1.f / acc;
       for (int l = 0; l < L; ++l) {
         const long long j = base + (long long)l * inner;
-        st(dx, j, g * expf(s * ld(x, j) - m) * inv);
+        st(dx, j, g * expf(__fmul_rn(s, ld(x, j)) - sh) * inv);
       }
     } else {
       for (int l = 0; l < L; ++l) st(dx, base + (long long)l * inner, g / (float)L);

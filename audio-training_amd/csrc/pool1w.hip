@@ -49,11 +49,15 @@ using namespace acfe;
 // segments, read back by acfe_debug_pool1w_stamps (tools/pool1w_stamps.py)
 __device__ unsigned long long g_p1w_stamps[4096 * 8];
 #endif
-template <int PM, int NCH, bool DROP, bool ST = true, bool PRO = false>
+// SEGW: tile width -- 64 (4 rows x 64 pixels), or 16 (16 rows x 16 pixels,
+// PM 0 / 3) for the Q % 64 pixels left of each row, launched separately from
+// column wofs (wr_resnet's 257-wide stage 2 ran a whole 64-pixel tile per 4
+// rows for its last pixel); srow0: the first statistics slab row it writes.
+template <int PM, int NCH, bool DROP, bool ST = true, bool PRO = false, int SEGW = 64>
 __global__ void __launch_bounds__(256, 1)
 k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
-             int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax) {
+             int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax, int wofs = 0, int srow0 = 0) {
   static_assert(NCH % 2 == 0, "even step count per tile: weight buffer parity is static");
   static_assert(PM == 0 || PM == 1 || ((PM == 2 || PM == 3) && !DROP), "modes");
   // PRO: the BatchNormalization (+ReLU) of the input applied while staging it
@@ -62,9 +66,10 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   // bf16 (acfe_bn_apply's values); the tile's own pixels of x' also go to
   // pro_out for the weight gradient
   static_assert(!PRO || PM == 0 || PM == 3, "prologue: plain / residual forward");
+  static_assert(SEGW == 64 || (SEGW == 16 && (PM == 0 || PM == 3)), "16-pixel tiles: the dense modes");
   constexpr bool CPERM = PM != 1;     // weights x pixels operand order (PM 0 / 2 / 3)
   constexpr bool DENSE = PM == 0 || PM == 3;  // full-resolution output with bias (PM 3: + residual)
-  constexpr int KB = 128, TR = 4, FM = 4, FN = 4, NH = 2, NF = NH * FN, SEGW = 64, HWX = SEGW + 2, XRB = 160;
+  constexpr int KB = 128, TR = 256 / SEGW, FM = 4, FN = 4, NH = 2, NF = NH * FN, HWX = SEGW + 2, XRB = 160;
   constexpr int NT = 256, NS = 3 * NCH;                          // threads, steps per tile
   constexpr int XROWS = TR + 2, XBYTES = XROWS * HWX * XRB;      // 63 360 B
   constexpr int WBYTES = 3 * KB * 128, WBASE = XBYTES;           // 2 x 49 152 B
@@ -201,7 +206,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     const int tm = walk.tm + tl * walk.step;
     int n, hb, wb;
     tile_of(tm, n, hb, wb);
-    const int sh0 = hb * TR - g.pt, sw0 = wb * SEGW - g.pl;
+    const int sh0 = hb * TR - g.pt, sw0 = wofs + wb * SEGW - g.pl;
     int t0 = tid;
     asm volatile("" : "+v"(t0));  // (per tile, not hoisted)
     cmask = 0;
@@ -317,8 +322,9 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       const int a = wp * 8 + (fm & 1) * 4 + (qq ^ (qq >> 1));
       xoff[fm] = (((fm >> 1) * 2 + (j >> 1)) * HWX + 2 * a + (j & 1)) * XRB + q * 16;
     } else {
-      // B columns = pixels wp * 64 + fm * 16 + l16 (tile row wp)
-      xoff[fm] = (wp * HWX + fm * 16 + l16) * XRB + q * 16;
+      // B columns = tile pixels wp * 64 + fm * 16 + l16 (SEGW 64: tile row wp)
+      const int p0 = wp * 64 + fm * 16;
+      xoff[fm] = ((p0 / SEGW) * HWX + p0 % SEGW + l16) * XRB + q * 16;
     }
   }
 #pragma unroll
@@ -481,7 +487,8 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   auto dx_unit = [&](int fm, int h, int tm, bool live) __attribute__((always_inline)) {
     int n, hb, wb;
     tile_of(tm, n, hb, wb);
-    const int hh = hb * TR + wp, ww = wb * SEGW + fm * 16 + l16;
+    // tile pixels wp * 64 + fm * 16 + l16: SEGW 64 row wp, 16 row 4 wp + fm
+    const int hh = hb * TR + (SEGW == 64 ? wp : 4 * wp + fm), ww = wofs + wb * SEGW + (SEGW == 64 ? fm * 16 : 0) + l16;
     const bool inb = live && hh < g.P && ww < g.Q;
     const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Y + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
@@ -505,7 +512,8 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   auto res_load = [&](int u, int fm, int h, int tm, bool live) __attribute__((always_inline)) {
     int n, hb, wb;
     tile_of(tm, n, hb, wb);
-    const int hh = hb * TR + wp, ww = wb * SEGW + fm * 16 + l16;
+    // tile pixels wp * 64 + fm * 16 + l16: SEGW 64 row wp, 16 row 4 wp + fm
+    const int hh = hb * TR + (SEGW == 64 ? wp : 4 * wp + fm), ww = wofs + wb * SEGW + (SEGW == 64 ? fm * 16 : 0) + l16;
     const bool inb = live && hh < g.P && ww < g.Q;
     const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(g.res + (long long)n * g.P * g.Q * g.ldy), (short)0, g.P * g.Q * g.ldy * 2, 0x00020000);
@@ -516,7 +524,8 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   auto dense_unit = [&](int fm, int h, int tm, bool live, int u = 0) __attribute__((always_inline)) {
     int n, hb, wb;
     tile_of(tm, n, hb, wb);
-    const int hh = hb * TR + wp, ww = wb * SEGW + fm * 16 + l16;
+    // tile pixels wp * 64 + fm * 16 + l16: SEGW 64 row wp, 16 row 4 wp + fm
+    const int hh = hb * TR + (SEGW == 64 ? wp : 4 * wp + fm), ww = wofs + wb * SEGW + (SEGW == 64 ? fm * 16 : 0) + l16;
     const bool inb = live && hh < g.P && ww < g.Q;
     const int c0 = h * 64 + 16 * q;
     unsigned w8[8];
@@ -770,11 +779,14 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
           stats[((long long)blockIdx.x * 2 + idx / FN) * g.Kp + h * 64 + FN * l16 + idx % FN] = v;
         } else {
           const int idx = ((l16 >> 3) & 1) * 16 + ((l16 >> 2) & 1) * 8 + ((l16 >> 1) & 1) * 4 + (l16 & 1) * 2 + k;
-          stats[((long long)blockIdx.x * 2 + idx / 16) * g.Kp + h * 64 + 16 * q + idx % 16] = v;
+          stats[((long long)(srow0 + blockIdx.x) * 2 + idx / 16) * g.Kp + h * 64 + 16 * q + idx % 16] = v;
         }
       }
     }
-    for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
+    // (the first launch zeroes every row past its own; the remainder-column
+    // launch writes its rows afterwards)
+    if (srow0 == 0)
+      for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
       for (int c = tid; c < 2 * KB; c += NT) stats[((long long)rr * 2 + (c / KB)) * g.Kp + (c % KB)] = 0.0;
   }
 }
@@ -816,17 +828,41 @@ int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float
   if (g.K != 128 || g.C != 128 || g.R != 3 || g.S != 3 || g.st != 1 || g.ldy != 128 ||
       (long long)g.P * g.Q * g.ldy * 2 >= (1ll << 31) || (g.drop.on && !g.idx32) || ((uintptr_t)y & 15))
     return ACFE_E_INVAL;
-  int th, tw, gp;
-  long long nt;
-  grid_1w(g, stats, srows, &th, &tw, &nt, &gp);
-#define P1W_L(PM_, D, S_, ...)                                                                                \
-  hipLaunchKernelGGL((k_conv3x3_1w<PM_, 2, D, S_, ##__VA_ARGS__>), dim3(gp), dim3(256), 0, s, g,              \
-                     (const uint16_t*)x, (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows,  \
-                     nullptr)
+  if (g.pro_sc && (!g.pro_sh || !g.pro_out || ((uintptr_t)g.pro_out & 15) || ((uintptr_t)x & 15)))
+    return ACFE_E_INVAL;
+  if (pm == 3 && (!g.res || g.drop.on)) return ACFE_E_INVAL;
+  // the image's whole 64-pixel columns in 4 x 64 tiles, the Q % 64 pixels left
+  // of each row (when Q >= 64) in 16 x 16 tiles by a second launch writing the
+  // statistics slab rows after the first one's (per-pixel values unchanged:
+  // an accumulator's MFMA sequence does not depend on the tiling)
+  const int rem = g.Q >= 64 ? g.Q % 64 : 0;
+  const int th = (g.P + 3) / 4, tw = rem ? g.Q / 64 : (g.Q + 63) / 64;
+  const long long nt = (long long)g.N * th * tw;
+  const int the = (g.P + 15) / 16, twe = (rem + 15) / 16;
+  const long long nte = rem ? (long long)g.N * the * twe : 0;
+  if (nt >= (1ll << 31) || nte >= (1ll << 31)) return ACFE_E_INVAL;
+  auto grid_for = [&](long long n, int rows_left) {
+    int gp = 256;
+    if (gp > n) gp = (int)n;
+    if (gp >= 64) gp &= ~7;
+    if (stats && gp > rows_left) gp = rows_left;  // one statistics slab row per workgroup
+    return gp;
+  };
+  // (small slabs: leave the second launch up to half of the rows)
+  const int gp = grid_for(nt, nte && stats ? srows - (int)(srows / 2 < nte ? srows / 2 : nte) : srows);
+  const int gpe = nte ? grid_for(nte, srows - gp) : 0;
+  if (nte && gpe <= 0) return ACFE_E_INVAL;
+#define P1W_L(PM_, D, S_, PRO_)                                                                                  \
+  do {                                                                                                          \
+    hipLaunchKernelGGL((k_conv3x3_1w<PM_, 2, D, S_, PRO_, 64>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)x, \
+                       (const uint16_t*)wp, bias, (uint16_t*)y, stats, th, tw, (int)nt, srows, nullptr, 0, 0);   \
+    if (nte)                                                                                                    \
+      hipLaunchKernelGGL((k_conv3x3_1w<PM_, 2, D, S_, PRO_, 16>), dim3(gpe), dim3(256), 0, s, g,                \
+                         (const uint16_t*)x, (const uint16_t*)wp, bias, (uint16_t*)y, stats, the, twe, (int)nte,  \
+                         srows, nullptr, g.Q - rem, gp);                                                         \
+  } while (0)
   if (g.pro_sc) {  // BN prologue (acfe_conv2d_fwd_bn / fwd_add_bn)
-    if (!g.pro_sh || !g.pro_out || ((uintptr_t)g.pro_out & 15) || ((uintptr_t)x & 15)) return ACFE_E_INVAL;
     if (pm == 3) {
-      if (!g.res || g.drop.on) return ACFE_E_INVAL;
       if (stats) P1W_L(3, false, true, true);
       else P1W_L(3, false, false, true);
     } else if (g.drop.on) {
@@ -837,15 +873,14 @@ int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float
       P1W_L(0, false, false, true);
     }
   } else if (pm == 3) {
-    if (!g.res || g.drop.on) return ACFE_E_INVAL;
-    if (stats) P1W_L(3, false, true);
-    else P1W_L(3, false, false);
+    if (stats) P1W_L(3, false, true, false);
+    else P1W_L(3, false, false, false);
   } else if (g.drop.on) {
-    P1W_L(0, true, true);
+    P1W_L(0, true, true, false);
   } else if (stats) {
-    P1W_L(0, false, true);
+    P1W_L(0, false, true, false);
   } else {
-    P1W_L(0, false, false);
+    P1W_L(0, false, false, false);
   }
 #undef P1W_L
   return launch_rc(what);

@@ -50,18 +50,24 @@ using namespace acfe;
 __device__ unsigned long long g_r64_stamps[4096 * 8];
 #endif
 
-template <int PM, int NCH, bool PRO, bool ST>
+// SEGW: tile width -- 64 (8 rows x 64 pixels) for the image's whole 64-pixel
+// columns, 16 (32 rows x 16 pixels) for the Q % 64 pixels left of a row
+// (wofs: the first column of tile column 0), so that wr_resnet's 513-wide
+// stage 1 does not run a whole 64-pixel tile per 8 rows for its last pixel;
+// srow0: the first statistics slab row of this launch.
+template <int PM, int NCH, bool PRO, bool ST, int SEGW = 64>
 __global__ void __launch_bounds__(512, 1)
 k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
               const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
-              int tiles_w, int ntiles, int srows) {
+              int tiles_w, int ntiles, int srows, int wofs, int srow0) {
   static_assert(PM == 0 || PM == 3 || PM == 4 || PM == 5, "modes");
+  static_assert(SEGW == 64 || SEGW == 16, "tile width");
   static_assert(!PRO || PM != 5, "prologue: forwards");
   constexpr bool DROP = PM == 4;
   constexpr bool SUMS = ST || PM == 5;
-  constexpr int KB = 64, TR = 8, FM = 8, FN = 2, SEGW = 64, HWX = SEGW + 2, XRB = 160, NT = 512;
+  constexpr int KB = 64, TR = 512 / SEGW, FM = 8, FN = 2, HWX = SEGW + 2, XRB = 160, NT = 512;
   constexpr int NS = 3 * NCH;                                   // steps per tile
-  constexpr int XROWS = TR + 2, XBYTES = XROWS * HWX * XRB;     // 105 600 B
+  constexpr int XROWS = TR + 2, XBYTES = XROWS * HWX * XRB;     // 105 600 B (SEGW 16: 97 920 B)
   constexpr int WBYTES = 3 * KB * 128, WBASE = XBYTES;          // 2 x 24 576 B
   constexpr int XG = XROWS * HWX * 8, XPT = (XG + NT - 1) / NT;  // 16-B halo granules: 11 per thread
   constexpr int WPW = 3 * KB * 8 / 64 / 8;                       // 3 weight pieces per wave per step
@@ -143,7 +149,7 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     const int tm = walk.tm + tl * walk.step;
     int n, hb, wb;
     tile_of(tm, n, hb, wb);
-    const int sh0 = hb * TR - g.pt, sw0 = wb * SEGW - g.pl;
+    const int sh0 = hb * TR - g.pt, sw0 = wofs + wb * SEGW - g.pl;
     int t0 = tid;
     asm volatile("" : "+v"(t0));  // (per tile, not hoisted)
     tbase = (sh0 * g.W + sw0) * CB;
@@ -217,7 +223,7 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
   int xoff[FM], wrb[FN];
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm) {
-    const int p = wp * (TR * 16) + fm * 16;
+    const int p = wp * 128 + fm * 16;
     xoff[fm] = ((p / SEGW) * HWX + (p % SEGW) + l16) * XRB + q * 16;
   }
 #pragma unroll
@@ -271,7 +277,9 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
                      __attribute__((always_inline)) {
     int hb, wb;
     tile_of(tm, n, hb, wb);
-    const int hh = hb * TR + 2 * wp + (u >> 2), wc = wb * SEGW + (u & 3) * 16;
+    // the unit's 16 pixels: tile pixels wp * 128 + u * 16 + l16
+    // (SEGW 64: row 2 wp + u / 4, column (u % 4) 16; SEGW 16: row 8 wp + u)
+    const int hh = hb * TR + (SEGW == 64 ? 2 * wp + (u >> 2) : 8 * wp + u), wc = wofs + wb * SEGW + (SEGW == 64 ? (u & 3) * 16 : 0);
     inb = live & (hh < g.P) & (wc + l16 < g.Q);
     o = (unsigned)(hh * g.Q + wc) * (unsigned)g.ldy * 2u + lane_o;
     if (spx) *spx = (unsigned)(hh * g.Q + wc);  // the unit's first pixel in its image (scalar)
@@ -307,9 +315,8 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
     if constexpr (DROP) {
       // acfe_dropout's mask: one pair hash per channel pair, the Weyl term of
       // the first pair advanced by a constant (M * K < 2^32: launcher)
-      int hb, wb;
-      tile_of(tm, n, hb, wb);
-      const unsigned spix = ((unsigned)n * g.P + hb * TR + 2 * wp + (u >> 2)) * g.Q + wb * SEGW + (u & 3) * 16;
+      // ((n P + hh) Q + wc): the unit's first pixel (spx) plus the image's
+      const unsigned spix = (unsigned)n * (unsigned)(g.P * g.Q) + spx;
       // ((pix K + c0) >> 1) W + seed with pix = spix + l16 (K = 64, c0 even)
       const uint32_t hw0 = spix * (unsigned)(KB / 2) * 0x9E3779B1u + lane_h + (uint32_t)g.drop.seed;
       unsigned kbits = 0;
@@ -560,9 +567,12 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
 #pragma unroll
       for (int w = 0; w < 4; ++w) v += red[(wk * 4 + w) * 64 + lane];
       // lane l16 keeps value l16 of [sums | squares][8 channels c0 + ..]
-      stats[((long long)blockIdx.x * 2 + (l16 >> 3)) * g.Kp + c0 + (l16 & 7)] = v;
+      stats[((long long)(srow0 + blockIdx.x) * 2 + (l16 >> 3)) * g.Kp + c0 + (l16 & 7)] = v;
     }
-    for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
+    // (the first launch zeroes every row past its own; a remainder-column
+    // launch writes its rows afterwards)
+    if (srow0 == 0)
+      for (int rr = blockIdx.x + gridDim.x; rr < srows; rr += gridDim.x)
       for (int c = tid; c < 2 * KB; c += NT) stats[((long long)rr * 2 + (c / KB)) * g.Kp + (c % KB)] = 0.0;
   }
 }
@@ -600,22 +610,44 @@ int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bi
   if ((pm == 3 || pm == 5) && (!g.res || ((uintptr_t)g.res & 15))) return ACFE_E_INVAL;
   if (g.keep_out && (pm != 4 || !g.drop.on)) return ACFE_E_INVAL;
   if (pm == 5 && (!stats || !g.bn_sc || !g.bn_sh || !g.bn_mu || !g.bn_is)) return ACFE_E_INVAL;
-  const int tiles_h = (g.P + 7) / 8, tiles_w = (g.Q + 63) / 64;
-  const long long nt = (long long)g.N * tiles_h * tiles_w;
-  if (nt >= (1ll << 31)) return ACFE_E_INVAL;
-  int gp = 256;
-  if (gp > nt) gp = (int)nt;
-  if (gp >= 64) gp &= ~7;
-  if (stats && gp > srows) gp = srows;  // one statistics slab row per workgroup
+  if (pm != 0 && pm != 3 && pm != 4 && pm != 5) return ACFE_E_INVAL;
+  if (pm == 4 && !stats) return ACFE_E_INVAL;
   const bool st = stats != nullptr;
-#define R64L(PM_, NCH_, PRO_, ST_)                                                                           \
-  hipLaunchKernelGGL((k_conv3x3_r64<PM_, NCH_, PRO_, ST_>), dim3(gp), dim3(512), 0, s, g, (const uint16_t*)x, \
-                     (const uint16_t*)wp, bias, (uint16_t*)y, stats, tiles_h, tiles_w, (int)nt, srows)
-#define R64N(PM_, PRO_, ST_)                         \
-  do {                                               \
-    if (nch == 1) R64L(PM_, 1, PRO_, ST_);           \
-    else if (nch == 2) R64L(PM_, 2, PRO_, ST_);      \
-    else R64L(PM_, 4, PRO_, ST_);                    \
+  // the image's whole 64-pixel columns in 8 x 64 tiles, the Q % 64 pixels
+  // left of each row (when Q >= 64) in 32 x 16 tiles by a second launch that
+  // writes the statistics slab rows after the first one's (the per-pixel
+  // values are the same either way: each accumulator's MFMA sequence does not
+  // depend on the tiling)
+  const int rem = g.Q >= 64 ? g.Q % 64 : 0;
+  const int tiles_h = (g.P + 7) / 8, tiles_w = rem ? g.Q / 64 : (g.Q + 63) / 64;
+  const long long nt = (long long)g.N * tiles_h * tiles_w;
+  const int tiles_he = (g.P + 31) / 32, tiles_we = (rem + 15) / 16;
+  const long long nte = rem ? (long long)g.N * tiles_he * tiles_we : 0;
+  if (nt >= (1ll << 31) || nte >= (1ll << 31)) return ACFE_E_INVAL;
+  auto grid_for = [&](long long n, int rows_left) {
+    int gp = 256;
+    if (gp > n) gp = (int)n;
+    if (gp >= 64) gp &= ~7;
+    if (stats && gp > rows_left) gp = rows_left;  // one statistics slab row per workgroup
+    return gp;
+  };
+  // (small slabs: leave the second launch up to half of the rows)
+  const int gp = grid_for(nt, nte && stats ? srows - (int)(srows / 2 < nte ? srows / 2 : nte) : srows);
+  const int gpe = nte ? grid_for(nte, srows - gp) : 0;
+  if (nte && gpe <= 0) return ACFE_E_INVAL;
+#define R64L(SW_, PM_, NCH_, PRO_, ST_, G_, TH_, TW_, NT_, WO_, SR_)                                              \
+  hipLaunchKernelGGL((k_conv3x3_r64<PM_, NCH_, PRO_, ST_, SW_>), dim3(G_), dim3(512), 0, s, g, (const uint16_t*)x, \
+                     (const uint16_t*)wp, bias, (uint16_t*)y, stats, TH_, TW_, (int)(NT_), srows, WO_, SR_)
+#define R64N(PM_, PRO_, ST_)                                                                                   \
+  do {                                                                                                         \
+    if (nch == 1) R64L(64, PM_, 1, PRO_, ST_, gp, tiles_h, tiles_w, nt, 0, 0);                                 \
+    else if (nch == 2) R64L(64, PM_, 2, PRO_, ST_, gp, tiles_h, tiles_w, nt, 0, 0);                            \
+    else R64L(64, PM_, 4, PRO_, ST_, gp, tiles_h, tiles_w, nt, 0, 0);                                          \
+    if (nte) {                                                                                                 \
+      if (nch == 1) R64L(16, PM_, 1, PRO_, ST_, gpe, tiles_he, tiles_we, nte, g.Q - rem, gp);                  \
+      else if (nch == 2) R64L(16, PM_, 2, PRO_, ST_, gpe, tiles_he, tiles_we, nte, g.Q - rem, gp);             \
+      else R64L(16, PM_, 4, PRO_, ST_, gpe, tiles_he, tiles_we, nte, g.Q - rem, gp);                           \
+    }                                                                                                          \
   } while (0)
   switch (pm) {
     case 0:
@@ -623,7 +655,6 @@ int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bi
       else { if (st) R64N(0, false, true); else R64N(0, false, false); }
       break;
     case 4:
-      if (!st) return ACFE_E_INVAL;
       if (pro) R64N(4, true, true); else R64N(4, false, true);
       break;
     case 3:
@@ -633,8 +664,6 @@ int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bi
     case 5:
       R64N(5, false, true);
       break;
-    default:
-      return ACFE_E_INVAL;
   }
 #undef R64N
 #undef R64L

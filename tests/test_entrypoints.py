@@ -88,7 +88,7 @@ def test_train_checkpoint_predict(tmp_path, cuda, load_raw):
     p = predict.Predictor(ck)
     r = p.predict_file(tmp_path / "rec.wav", stride=1.0, batch_size=4)
     assert r["windows"] == 8
-    assert set(r["mean"]) == {"bird", "noise"} and all(0 <= v <= 1 for v in r["mean"].values())
+    assert set(r["mean"]) == {"bird", "noise"} and all(0 <= v <= 1 for v in r["mean"].values()), (r, hist)
     # track mode gathers windows on the host: the same windows read in place
     # by the fused front end give the same probabilities
     wins = np.stack([rec[k * 48000:(k + 3) * 48000] for k in range(8)])

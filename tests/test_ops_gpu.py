@@ -294,6 +294,30 @@ def test_dense_backward_batch_sizes(ops, cuda, B, I, O):
     assert rel(wd.grad, wr.grad) < 1e-6 and rel(bd.grad, br.grad) < 1e-6 and rel(xd.grad, xr.grad) < 1e-6
 
 
+def test_lme_large_and_nonfinite(ops, cuda):
+    """logmeanexp at the magnitudes an eval forward reaches with the Keras
+    moving statistics still near their initial values (|x| ~ 1e9, found as a
+    run-to-run NaN in test_train_checkpoint_predict[raw]: a contracted
+    fma(s, x, -max) kept the max element's rounding residual in the exponent,
+    expf(~256) = inf), and tfp.math.reduce_logsumexp's handling of an infinite
+    max (shift by 0: +inf stays +inf, an all -inf row gives -inf, no NaN)."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand((4, 16, 7, 3), generator=g, dtype=torch.float64) * 2 - 1) * 1.2e9
+    x = x.float().double()  # the fp32 values the kernel sees
+    ref = ref_lme(x, 1)
+    y = ops.logmeanexp(x.float().to(cuda), 1).double().cpu()
+    assert torch.isfinite(y).all()
+    assert ((y - ref).abs() <= 1e-6 * ref.abs() + 1.0).all()
+    xg = x.float().to(cuda).requires_grad_(True)
+    ops.logmeanexp(xg, 1).sum().backward()
+    xr = x.clone().requires_grad_(True)
+    ref_lme(xr, 1).sum().backward()
+    assert torch.isfinite(xg.grad).all() and (xg.grad.double().cpu() - xr.grad).abs().max() < 1e-5
+    z = torch.tensor([[1.0, float("inf"), -2.0], [float("-inf")] * 3, [float("inf"), float("-inf"), 0.0]])
+    yz = ops.logmeanexp(z.to(cuda), 1).cpu()
+    assert yz[0] == float("inf") and yz[1] == float("-inf") and yz[2] == float("inf"), yz
+
+
 def test_lme_dense_loss_adam(ops, cuda):
     from oracle.models import keras_adam, keras_loss
 
