@@ -3291,7 +3291,9 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     // share NR + 1 of their NR + 2 halo rows (and, UNP, their pooled dY row),
     // so the overlap is re-read from L2 one step later instead of a whole
     // image row later (r03v: 9.8 GB of HBM reads per launch vs 5.9 GB algorithmic)
-    const int PR = g.P / ROWS;  // row groups per image
+    // row groups per image (SEGW 16: the last may be partial, its rows past
+    // P loading zeros -- the plain kernels only; launcher)
+    const int PR = SEGW == 64 ? g.P / ROWS : (g.P + ROWS - 1) / ROWS;
     const int n = sg / (PR * QS), rem = sg - n * (PR * QS);
     const int h = (rem % PR) * ROWS, w0 = wofs + (rem / PR) * SEGW;
     // buffer loads on the segment's image (offsets < 2^31: halo_ok); an
@@ -3307,7 +3309,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
     const int dbase = UNP ? ((h >> 1) * (g.Q >> 1) + (w0 >> 1)) * g.K : (h * g.Q + w0) * g.K;
 #pragma unroll
     for (int i = 0; i < ((part & 1) ? DPT : 0); ++i) {
-      const bool okd = w0 + dpw[i] < g.Q;
+      const bool okd = (w0 + dpw[i] < g.Q) && (SEGW == 64 || h + dro[i] < g.P);
       const unsigned e = (unsigned)(dbase + dlo[i]);
       if constexpr (UNP) {
         const __amdgpu_buffer_rsrc_t ars =
@@ -4478,8 +4480,12 @@ static HaloPlan halo_plan(const ConvGeom& g, bool amax, long long splits) {
   const int nr = ((cw == 64 || c16k64) && g.P % 2 == 0 && (g.K == 64 || (g.K == 32 && !amax))) ? 2 : 1;
   const int wp = (c16k64 || k16c64) ? 2 : 1;
   const int rem = g.Q >= 64 ? g.Q % 64 : 0;
-  const bool edge = rem && wp == 1 && !amax && cw == 64 && g.P % (4 * nr) == 0 &&
-                    ((g.K == 64 && nr == 2) || (g.K == 128 && nr == 1));
+  // (the BN fold writes its dY rows: whole 4 nr row groups only, and the
+  // plain K = 64 kernel splits exactly as the fold does, so that their dW
+  // stay bit-identical; K = 128 / 256 mask the rows of a partial last group)
+  const bool edge = rem && wp == 1 && !amax &&
+                    ((cw == 64 && g.K == 64 && nr == 2 && g.P % 8 == 0) ||
+                     (!g.fb_sc && ((cw == 64 && g.K == 128 && nr == 1) || (cw == 32 && g.K == 256 && nr == 1))));
   const int qs = edge ? g.Q / 64 : (g.Q + 63) / 64;
   const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * qs);
   // c16k64: 75 KB of LDS and 114 VGPRs -> two workgroups per CU
@@ -4501,7 +4507,7 @@ static HaloPlan halo_plan(const ConvGeom& g, bool amax, long long splits) {
   hp.qs = qs;
   hp.qse = edge ? (rem + 15) / 16 : 0;
   hp.wofs = g.Q - rem;
-  hp.nsege = edge ? (int)((long long)g.N * (g.P / (4 * nr)) * hp.qse) : 0;
+  hp.nsege = edge ? (int)((long long)g.N * ((g.P + 4 * nr - 1) / (4 * nr)) * hp.qse) : 0;
   hp.pere = edge ? (hp.nsege + sp - 1) / sp : 0;
   return hp;
 }
@@ -4552,8 +4558,15 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
       hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 16, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
                          (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);
     else WHC(64, 16);
-  } else if (cw == 32) {  // the stage-2/3 branch2b (32 -> 128 / 256)
-    if (g.K == 128) WHC(128, 32); else WHC(256, 32);
+  } else if (cw == 32) {  // the stage-2/3 branch2b (32 -> 128 / 256); wr_resnet's stage 3 (256 -> 256)
+    if (g.K == 128) WHC(128, 32);
+    else {
+      hipLaunchKernelGGL((k_wgrad3x3_halo<256, false, 32>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
+                         (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr, qs, 0, 0);
+      if (hp.edge)
+        hipLaunchKernelGGL((k_wgrad3x3_halo<256, false, 32, 1, false, false, 16>), gr, dim3(512), 0, s, g,
+                           (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nsege, pere, nullptr, qse, wofs, 1);
+    }
   } else if (cw == 16) {  // stage 3 (16 -> 256)
     WHC(256, 16);
   } else if (g.K == 128) {

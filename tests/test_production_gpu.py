@@ -583,10 +583,11 @@ def test_model_stem_bn_fusion(env, cuda):
 @pytest.mark.parametrize("C,K,H,W", [(128, 32, 32, 64), (32, 128, 32, 64), (32, 256, 16, 32), (16, 256, 16, 32),
                                      (64, 64, 64, 128), (128, 64, 64, 128), (64, 64, 14, 100), (256, 256, 22, 86),
                                      (256, 16, 16, 32), (128, 16, 16, 40), (16, 64, 64, 100), (16, 64, 15, 70),
-                                     (64, 16, 20, 70)],
+                                     (64, 16, 20, 70), (128, 128, 22, 100), (64, 64, 10, 150)],
                          ids=["s2-21", "s2-2b", "s3-2b-b6", "s3-2b", "k64-rowpair", "k64-rowpair-2chunks",
                               "k64-rowpair-partial", "wrn-s3-256", "s3-21-k16", "k16-1chunk-partial",
-                              "wrn-s1-2a-c16", "c16-k64-oddrows", "k16-c64-chunks"])
+                              "wrn-s1-2a-c16", "c16-k64-oddrows", "k16-c64-chunks", "k128-rem-oddrows",
+                              "k64-rem-2cols"])
 def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
     """k_wgrad3x3_halo for the stage-2/3 layers whose channel count is the
     feature height: K = 32 (branch21 128 -> 32) and the 16 / 32-channel
@@ -598,7 +599,9 @@ def test_wgrad_halo_narrow(env, cuda, C, K, H, W):
     channel chunks with two pixel groups when C = 64 * odd) and
     wr_resnet's stage-1 16 -> 64 (two pixel groups of waves writing separate
     split slabs; two rows per step, one for an odd row count), at 32 clips and
-    the production split count, against float64."""
+    the production split count, against float64.  Widths past a multiple of
+    64 run their last Q % 64 pixels as 16-pixel segments (r06; a partial last
+    row group at 22 / 10 rows, two remainder columns at W = 150)."""
     ops, call, lib, ptr, stream = env
     N = 32
     x, w, b, g = _data(N, H, W, C, K, 307, cuda)
