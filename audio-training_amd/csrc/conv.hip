@@ -4831,9 +4831,17 @@ static int launch_rows(const ConvGeom& g, const void* x, const void* wp, const f
 // same sums in the one-wave K = C = 128 dgrad's units (r04p) cost more issue
 // time than the separate reduce pass (+0.85 ms vs 0.75 ms per wr_resnet stage-2
 // call): that kernel is issue-bound, the reduce runs at the copy rate.
+// ACFE_DGRADBN128=0: the K = C = 128 dgrads keep the separate reduce pass (A/B)
+static bool rows_pm5_128_enabled() {
+  static const int v = getenv("ACFE_DGRADBN128") ? atoi(getenv("ACFE_DGRADBN128")) : 1;
+  return v != 0;
+}
+
 ACFE_API int acfe_conv2d_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int dtype) {
+  // C = 64: the K = 64 row-halo kernels (rows64.hip PM 5); C = K = 128: the
+  // one-wave kernel (pool1w.hip PM 5, wr_resnet's stage 2)
   if (dtype != ACFE_DTYPE_BF16 || N <= 0 || H <= 0 || W <= 0 || stride != 1 || R != 3 || S != 3 || K <= 0 ||
-      C != 64 || K % 64 != 0 ||
+      !((C == 64 && K % 64 == 0) || (C == 128 && K == 128 && rows_pm5_128_enabled())) ||
       (long long)N * ((H + 3) / 4) * ((W + 63) / 64) >= (1ll << 31) || (long long)H * W * C * 2 >= (1ll << 31))
     return 0;
   return grid_m_for((long long)N * H * W, 1);
@@ -4849,13 +4857,14 @@ ACFE_API int acfe_conv2d_dgrad_bn(const void* dy, int N, int P, int Q, int K, co
       ((uintptr_t)dx & 15) || ((uintptr_t)x_bn & 15))
     return ACFE_E_INVAL;
   // the dgrad as a forward conv of dY with the flipped weights (acfe_conv2d_dgrad)
-  ConvGeom g = make_geom(N, P, Q, K, C, R, S, 1, R - 1 - pad_top, S - 1 - pad_left, H, W, 64, 64);
+  ConvGeom g = make_geom(N, P, Q, K, C, R, S, 1, R - 1 - pad_top, S - 1 - pad_left, H, W, 64, C == 128 ? 128 : 64);
   g.res = (const uint16_t*)x_bn;
   g.bn_sc = scale;
   g.bn_sh = shift;
   g.bn_mu = mean;
   g.bn_is = invstd;
   g.bn_relu = relu ? 1 : 0;
+  if (C == 128) return launch_dgradbn1w(g, dy, wflip, dx, part, rows, strm(stream), "acfe_conv2d_dgrad_bn");
   const int rc = launch_r64(g, dy, wflip, nullptr, dx, part, rows, strm(stream), "acfe_conv2d_dgrad_bn", 5);
   if (rc != ACFE_E_INVAL) return rc;
   return launch_rows_tr<64, 5, 8, true>(g, dy, wflip, nullptr, dx, part, rows, nullptr, strm(stream),

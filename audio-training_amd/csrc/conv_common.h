@@ -195,6 +195,9 @@ int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float
 int launch_r64(const ConvGeom& g, const void* x, const void* wp, const float* bias, void* y, double* stats,
                int srows, hipStream_t s, const char* what, int pm);
 bool r64_enabled();
+// acfe_conv2d_dgrad_bn at K = C = 128 on the same kernel (PM 5: dX + the BN backward reduce sums)
+int launch_dgradbn1w(const ConvGeom& g, const void* dy, const void* wflip, void* dx, double* part, int srows,
+                     hipStream_t s, const char* what);
 // acfe_conv2d_dgrad_unpool at K = C = 128 on the same kernel (PM 2)
 int launch_unpool1w(const ConvGeom& g, const void* dyp, const void* wflip, void* dx, uint8_t* amax, hipStream_t s,
                     const char* what);

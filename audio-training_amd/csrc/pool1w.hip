@@ -59,16 +59,21 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
              const float* __restrict__ bias, uint16_t* __restrict__ Y, double* __restrict__ stats, int tiles_h,
              int tiles_w, int ntiles, int srows, uint8_t* __restrict__ amax, int wofs = 0, int srow0 = 0) {
   static_assert(NCH % 2 == 0, "even step count per tile: weight buffer parity is static");
-  static_assert(PM == 0 || PM == 1 || ((PM == 2 || PM == 3) && !DROP), "modes");
+  // PM 5: the stride-1 dgrad whose dX is a BatchNormalization's output
+  // gradient, with acfe_bn_bwd_reduce's sums of the stored dX in the epilogue
+  // (g.res = the BN input, g.bn_*; wr_resnet's stage-2 conv dgrads, rows64.hip
+  // PM 5's K = 128 counterpart)
+  static_assert(PM == 0 || PM == 1 || ((PM == 2 || PM == 3 || PM == 5) && !DROP), "modes");
   // PRO: the BatchNormalization (+ReLU) of the input applied while staging it
   // (acfe_conv2d_fwd_bn / fwd_add_bn at K = C = 128: wr_resnet's stage-2
   // bn2a / bn2b -> conv2a / conv2b), x' = (ReLU)(x * pro_sc + pro_sh) rounded to
   // bf16 (acfe_bn_apply's values); the tile's own pixels of x' also go to
   // pro_out for the weight gradient
   static_assert(!PRO || PM == 0 || PM == 3, "prologue: plain / residual forward");
-  static_assert(SEGW == 64 || (SEGW == 16 && (PM == 0 || PM == 3)), "16-pixel tiles: the dense modes");
+  static_assert(SEGW == 64 || (SEGW == 16 && (PM == 0 || PM == 3 || PM == 5)), "16-pixel tiles: the dense modes");
   constexpr bool CPERM = PM != 1;     // weights x pixels operand order (PM 0 / 2 / 3)
-  constexpr bool DENSE = PM == 0 || PM == 3;  // full-resolution output with bias (PM 3: + residual)
+  constexpr bool DENSE = PM == 0 || PM == 3 || PM == 5;  // full-resolution output with bias (PM 3: + residual)
+  constexpr bool RLD = PM == 3 || PM == 5;                // per-unit words of g.res (residual / BN input)
   constexpr int KB = 128, TR = 256 / SEGW, FM = 4, FN = 4, NH = 2, NF = NH * FN, HWX = SEGW + 2, XRB = 160;
   constexpr int NT = 256, NS = 3 * NCH;                          // threads, steps per tile
   constexpr int XROWS = TR + 2, XBYTES = XROWS * HWX * XRB;      // 63 360 B
@@ -76,8 +81,10 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
   constexpr int XG = XROWS * HWX * 8, XPT = (XG + NT - 1) / NT;  // 16-B input granules
   constexpr int WPW = 3 * KB * 8 / 64 / (NT / 64);               // 12 weight pieces per wave per step
   constexpr int WPG = 4;                                         // pieces per MFMA group (groups 0..2)
-  constexpr int SMEMP = XBYTES + 2 * WBYTES + (DENSE ? KB * 4 : 0);  // (PM 0 / 3: bias table)
-  constexpr int SMEM = SMEMP + (PRO ? 2 * 64 * NCH * 4 : 0);          // (PRO: scale / shift of the C channels)
+  constexpr bool BTAB = PM == 0 || PM == 3;                          // (PM 5: the dgrad has no bias)
+  constexpr int SMEMP = XBYTES + 2 * WBYTES + (BTAB ? KB * 4 : 0);   // (PM 0 / 3: bias table)
+  constexpr int SMEMB = SMEMP + (PRO ? 2 * 64 * NCH * 4 : 0);         // (PRO: scale / shift of the C channels)
+  constexpr int SMEM = SMEMB + (PM == 5 ? 4 * KB * 4 : 0);            // (PM 5: [scale | shift | mean | invstd][KB])
   static_assert(SMEM <= 163840, "LDS");
   static_assert(XPT * NT - XG <= 2 * XROWS * HWX, "spare granules fit the pixel pads");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
@@ -114,9 +121,13 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     bch[h] = (PM == 1 && bias) ? *reinterpret_cast<const f4*>(bias + h * 64 + 4 * l16) : f4{0.f, 0.f, 0.f, 0.f};
   float* btab = reinterpret_cast<float*>(smem + XBYTES + 2 * WBYTES);
   float* pss = reinterpret_cast<float*>(smem + SMEMP);  // PRO: scale[C], shift[C]
+  float* bnt = reinterpret_cast<float*>(smem + SMEMB);  // PM 5: the BN's scale, shift, mean, invstd
+  if constexpr (PM == 5)
+    for (int i = tid; i < KB; i += NT)
+      bnt[i] = g.bn_sc[i], bnt[KB + i] = g.bn_sh[i], bnt[2 * KB + i] = g.bn_mu[i], bnt[3 * KB + i] = g.bn_is[i];
   if constexpr (PRO)
     for (int i = tid; i < 64 * NCH; i += NT) pss[i] = g.pro_sc[i], pss[64 * NCH + i] = g.pro_sh[i];
-  if constexpr (DENSE)
+  if constexpr (BTAB)
     if (tid < KB) btab[tid] = bias ? bias[tid] : 0.f;
 
   // ---- weight pieces (LDS-DMA, 1 KB each, 48 per step).  The lane part of a
@@ -362,8 +373,10 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
     for (int j = 0; j < NF; ++j) prev[i][j] = u32x2{0u, 0u};
   auto pack1 = [&](int fm, int n) __attribute__((always_inline)) {
     f4 b4;
-    if constexpr (DENSE) {  // channels h * 64 + 16 q + 4 fn + j
+    if constexpr (BTAB) {  // channels h * 64 + 16 q + 4 fn + j
       b4 = *reinterpret_cast<const f4*>(btab + (n / FN) * 64 + 16 * q + 4 * (n % FN));
+    } else if constexpr (PM == 5) {
+      b4 = f4{0.f, 0.f, 0.f, 0.f};
     } else {
       const float b = bch[n / FN][n % FN];
       b4 = f4{b, b, b, b};
@@ -543,7 +556,33 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
         w8[pr] = __builtin_bit_cast(unsigned, pk);
       }
     }
-    if constexpr (DROP || ST) {
+    if constexpr (PM == 5) {
+      // acfe_bn_bwd_reduce's terms of the stored dX: gm = dX masked by the BN's
+      // ReLU (x * scale + shift > 0), summed as gm and gm * (x - mean) * invstd
+      // (the table's pair reads from a per-unit opaque base: not hoisted into
+      // 64 live registers)
+      const bool norelu = g.bn_relu == 0;
+      unsigned bo = (unsigned)(c0 * 4);
+      asm volatile("" : "+v"(bo));
+      const unsigned char* tb = reinterpret_cast<const unsigned char*>(bnt) + bo;
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) {
+        const unsigned xw = rres[u][pr >> 2][pr & 3];
+        const f2v csc = *reinterpret_cast<const f2v*>(tb + 8 * pr), csh = *reinterpret_cast<const f2v*>(tb + KB * 4 + 8 * pr),
+                  cmu = *reinterpret_cast<const f2v*>(tb + 2 * KB * 4 + 8 * pr),
+                  cis = *reinterpret_cast<const f2v*>(tb + 3 * KB * 4 + 8 * pr);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int j = 2 * pr + e;
+          const float xf = __uint_as_float(e ? (xw & 0xffff0000u) : (xw << 16));
+          const float gf = __uint_as_float(e ? (w8[pr] & 0xffff0000u) : (w8[pr] << 16));
+          const bool on = inb && (norelu || xf * csc[e] + csh[e] > 0.f);
+          const float gm = on ? gf : 0.f;
+          ds[j] += gm;
+          dq[j] += gm * ((xf - cmu[e]) * cis[e]);
+        }
+      }
+    } else if constexpr (DROP || ST) {
       const unsigned pix = ((unsigned)n * g.P + hh) * g.Q + ww;  // (M * K < 2^32: launcher)
       // the Weyl term of the first pair; the other pairs add a constant (one
       // quarter-rate multiply instead of eight)
@@ -609,7 +648,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       // units (fm, h) with h = cst >> 1, fm = 2 (cst & 1) + (grp == 3) in
       // groups 1 / 3 (PM 3: their residual loads in group 0); half h's
       // statistics in group 5 of steps 1 / 3
-      if constexpr (PM == 3 && grp == 0) {
+      if constexpr (RLD && grp == 0) {
         res_load(0, 2 * (cst & 1), cst >> 1, ptm, live);
         res_load(1, 2 * (cst & 1) + 1, cst >> 1, ptm, live);
       }
@@ -746,7 +785,7 @@ k_conv3x3_1w(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __restr
       for (int h = 0; h < NH; ++h) {
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {
-          if constexpr (PM == 3) res_load(0, fm, h, tm, true);
+          if constexpr (RLD) res_load(0, fm, h, tm, true);
           dense_unit(fm, h, tm, true, 0);
         }
         dense_stats(h);
@@ -883,6 +922,38 @@ int launch_plain1w(const ConvGeom& g, const void* x, const void* wp, const float
     P1W_L(0, false, false, false);
   }
 #undef P1W_L
+  return launch_rc(what);
+}
+
+int launch_dgradbn1w(const ConvGeom& g, const void* dy, const void* wflip, void* dx, double* part, int srows,
+                     hipStream_t s, const char* what) {
+  // acfe_conv2d_dgrad_bn at K = C = 128 (PM 5), tiled as launch_plain1w
+  if (g.K != 128 || g.C != 128 || g.R != 3 || g.S != 3 || g.st != 1 || g.ldy != 128 || !part || !g.res ||
+      !g.bn_sc || !g.bn_sh || !g.bn_mu || !g.bn_is || (long long)g.P * g.Q * g.ldy * 2 >= (1ll << 31) ||
+      ((uintptr_t)dx & 15) || ((uintptr_t)g.res & 15))
+    return ACFE_E_INVAL;
+  const int rem = g.Q >= 64 ? g.Q % 64 : 0;
+  const int th = (g.P + 3) / 4, tw = rem ? g.Q / 64 : (g.Q + 63) / 64;
+  const long long nt = (long long)g.N * th * tw;
+  const int the = (g.P + 15) / 16, twe = (rem + 15) / 16;
+  const long long nte = rem ? (long long)g.N * the * twe : 0;
+  if (nt >= (1ll << 31) || nte >= (1ll << 31)) return ACFE_E_INVAL;
+  auto grid_for = [&](long long n, int rows_left) {
+    int gp = 256;
+    if (gp > n) gp = (int)n;
+    if (gp >= 64) gp &= ~7;
+    if (gp > rows_left) gp = rows_left;
+    return gp;
+  };
+  const int gp = grid_for(nt, nte ? srows - (int)(srows / 2 < nte ? srows / 2 : nte) : srows);
+  const int gpe = nte ? grid_for(nte, srows - gp) : 0;
+  if (gp <= 0 || (nte && gpe <= 0)) return ACFE_E_INVAL;
+  hipLaunchKernelGGL((k_conv3x3_1w<5, 2, false, true, false, 64>), dim3(gp), dim3(256), 0, s, g, (const uint16_t*)dy,
+                     (const uint16_t*)wflip, nullptr, (uint16_t*)dx, part, th, tw, (int)nt, srows, nullptr, 0, 0);
+  if (nte)
+    hipLaunchKernelGGL((k_conv3x3_1w<5, 2, false, true, false, 16>), dim3(gpe), dim3(256), 0, s, g,
+                       (const uint16_t*)dy, (const uint16_t*)wflip, nullptr, (uint16_t*)dx, part, the, twe, (int)nte,
+                       srows, nullptr, g.Q - rem, gp);
   return launch_rc(what);
 }
 

@@ -838,11 +838,13 @@ def test_model_bn_reduce_fusion_matches_unfused(env, cuda, model_name):
 
 
 @pytest.mark.parametrize("N,H,W,C,K,relu", [(4, 128, 513, 64, 64, True), (2, 21, 70, 64, 128, True),
-                                              (3, 9, 64, 64, 64, False)])
+                                              (3, 9, 64, 64, 64, False), (4, 64, 257, 128, 128, True),
+                                              (3, 22, 100, 128, 128, False)])
 def test_conv_dgrad_bn_reduce_fused(env, cuda, N, H, W, C, K, relu):
     """acfe_conv2d_dgrad_bn (wr_resnet's 64-channel bn2a / bn2b -> conv dgrads,
     resnet/wr_resnet.py:56-80, at the stage-1 128 x 513 shape; partial row /
-    column tiles; no ReLU) against acfe_conv2d_dgrad ->
+    column tiles; no ReLU; and the stage-2 128 -> 128 dgrads at 64 x 257 on
+    the one-wave kernel, r06) against acfe_conv2d_dgrad ->
     acfe_bn_bwd_reduce: dX bit-identical, the reduce slab's per-channel column
     sums within 1e-6 of each other and 1e-5 of a float64 sum (relative to the
     largest sum)."""
@@ -860,7 +862,7 @@ def test_conv_dgrad_bn_reduce_fused(env, cuda, N, H, W, C, K, relu):
     brows = lib.acfe_conv2d_dgrad_bn_rows(N, H, W, C, K, 3, 3, 1, 1)
     assert brows > 0
     assert lib.acfe_conv2d_dgrad_bn_rows(N, H, W, 32, K, 3, 3, 1, 1) == 0  # uncovered: C = 32
-    assert lib.acfe_conv2d_dgrad_bn_rows(N, H, W, 128, 128, 3, 3, 1, 1) == 0  # uncovered: C = 128
+    assert lib.acfe_conv2d_dgrad_bn_rows(N, H, W, 128, 64, 3, 3, 1, 1) == 0  # uncovered: C = 128, K = 64
     dx0 = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
     dx1 = torch.full((N, H, W, C), float("nan"), dtype=BF, device=cuda)
     nrows = lib.acfe_reduce_blocks(rows)

@@ -36,6 +36,10 @@ for w in "$@"; do
     sqr64) BENCH_ARGS='--model wrn --classes 2' step sqr64 400 bash -c "bash tools/pmc_sq.sh ${TAG}_r64 'k_conv3x3_r64' && python tools/sq_summary.py gpurun_out/pmc_${TAG}_r64 'k_conv3x3_r64<4' 'k_conv3x3_r64<3' 'k_conv3x3_r64<5'" ;;
     fwdps) step fwdps 300 python tools/fwdp_stamps.py ;;
     epp) step epp 400 python -u tools/ep_probe.py ${EPN:-8} && grep -c '"nan": 0, "inf": 0, "n": [0-9]*}}' $O/epp.log ;;
+    envab) for r in 1 2 3; do for v in on off; do
+             if [ $v = off ]; then export $ABVAR=0; else unset $ABVAR; fi
+             step wrn_${ABVAR}_$v 300 python bench.py --model wrn --classes 2 --steps 10 --warmup 3 --no-cpu-baseline --no-extra && grep -o '"value": [0-9.]*' $O/wrn_${ABVAR}_$v.log
+           done; done; unset $ABVAR ;;
     cbw) step cbw 300 python tools/conv_bench.py --layers ${CBL:-6,7,8} --iters 5 ;;
     sqs3) step sqs3 400 bash -c "bash tools/pmc_sq_cmd.sh ${TAG}_s3 'k_conv_fwd_p' tools/conv_bench.py --layers 8 --passes fwd,dgrad --iters 2 && python tools/sq_summary.py gpurun_out/pmc_${TAG}_s3 'k_conv_fwd_p<128'" ;;
     r64st) step r64st 300 python tools/r64_stamps.py 512 ;;
