@@ -61,10 +61,10 @@ for w in "$@"; do
     melw5) step melt 300 python -u -m pytest tests/test_frontend_gpu.py -x -v --timeout 120 --timeout-method thread && for v in 0 1 2 4 8 0 4; do step mel_$v 120 python tools/mel_bench.py --iters 15 --prenorm --w5 $v && grep ms $O/mel_$v.log; done ;;
     mel) step mel 300 python tools/mel_bench.py --iters 15 && step melpre 300 python tools/mel_bench.py --iters 15 --prenorm ;;
     fetests) step fetests 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
-    evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r06 'k_conv3x3_r64<4, 1, true, true>' 12910141440 \
+    evwrn) step evwrn 900 bash tools/pmc_evidence.sh wrn r06 'k_conv3x3_r64<4, 1, true, true, 64>' 12910141440 \
              'k_conv3x3_r64<4,1,true,true> (wr_resnet b1/b2 conv2a 3x3 64->64 @128x513 with the BN prologue + dropout + BN sums, batch 512)' \
              --model wrn --classes 2 --steps 2 --warmup 1 ;;
-    evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r06 'k_conv3x3_1w<1, 2, true, true, false>' 5905580032 \
+    evt1) step evt1 900 bash tools/pmc_evidence.sh t1 r06 'k_conv3x3_1w<1, 2, true, true, false, 64>' 5905580032 \
              'k_conv3x3_1w<1,2,true,true> (wr_resnet_bird s1b0 branch21 3x3 128->128 @128x256 + 2x2 max-pool + dropout + BN sums, batch 512)' \
              --steps 3 --warmup 1 ;;
     evinfer) SELECT=7:3 step evinfer 600 bash tools/pmc_evidence.sh infer_fp32 r06 'k_conv_fwd_g<float, 128, 64' 8606859264 \
