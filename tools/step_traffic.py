@@ -5,7 +5,7 @@ gfx950 wide-read undercount, MI355X_MICROARCH.md HBM section) and WRITE_SIZE
 (KiB) summed per kernel name over the profiled steps (warm-up included: the
 same work) and divided by the number of steps (k_mel_w4 dispatches, one per
 step); the batch generator's kernels (outside the timed step) are left out.
-usage: tools/step_traffic.py <dir> <tag> [bench args]  -> profiles/r05/step_traffic_<tag>.md"""
+usage: tools/step_traffic.py <dir> <tag> [bench args]  -> profiles/r06/step_traffic_<tag>.md"""
 import csv
 import glob
 import sys
@@ -53,7 +53,7 @@ def main():
         if t < 0.05:
             continue
         out.append(f"| `{k[:90]}` | {n:.0f} | {rd:.2f} | {wr:.2f} | {t:.2f} | {100 * t / tot:.1f} % |")
-    p = root / "profiles" / "r05" / f"step_traffic_{tag}.md"
+    p = root / "profiles" / "r06" / f"step_traffic_{tag}.md"
     p.parent.mkdir(parents=True, exist_ok=True)
     p.write_text("\n".join(out) + "\n")
     print("\n".join(out[:16]))
