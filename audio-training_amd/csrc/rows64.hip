@@ -319,17 +319,23 @@ k_conv3x3_r64(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __rest
       const unsigned spix = (unsigned)n * (unsigned)(g.P * g.Q) + spx;
       // ((pix K + c0) >> 1) W + seed with pix = spix + l16 (K = 64, c0 even)
       const uint32_t hw0 = spix * (unsigned)(KB / 2) * 0x9E3779B1u + lane_h + (uint32_t)g.drop.seed;
-      unsigned kbits = 0;
+      // per dword (channel pair): both values times the keep scale, rounded
+      // by one v_cvt_pk_bf16_f32, then ANDed with the pair's 16-bit keep
+      // masks; the keep bits gathered from the masks (bit 2 d <- bit 0,
+      // bit 2 d + 1 <- bit 16) -- the same words as rounding each kept value
+      // separately and zeroing the dropped ones (r06: 16 -> ~10 VALU per pair)
+      unsigned kacc = 0;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const uint32_t hsh = hash_u32_lo_w(g.drop.seed, hw0 + (uint32_t)d * 0x9E3779B1u);
-        const bool klo = (hsh & 0xFFFFu) >= g.drop.thr, khi = (hsh >> 16) >= g.drop.thr;
-        const float lo = klo ? bf2f(f2bf(__uint_as_float(w8[d] << 16) * g.drop.scl)) : 0.f;
-        const float hi = khi ? bf2f(f2bf(__uint_as_float(w8[d] & 0xffff0000u) * g.drop.scl)) : 0.f;
-        w8[d] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
-        kbits |= (klo ? 1u : 0u) << (2 * d);
-        kbits |= (khi ? 1u : 0u) << (2 * d + 1);
+        const unsigned m = ((hsh & 0xFFFFu) >= g.drop.thr ? 0x0000ffffu : 0u) |
+                           ((hsh >> 16) >= g.drop.thr ? 0xffff0000u : 0u);
+        const float lo = __uint_as_float(w8[d] << 16) * g.drop.scl;
+        const float hi = __uint_as_float(w8[d] & 0xffff0000u) * g.drop.scl;
+        w8[d] = pk_bf2(lo, hi) & m;
+        kacc |= (m & 0x00010001u) << (2 * d);
       }
+      const unsigned kbits = (kacc | (kacc >> 15)) & 0xffu;
       // the keep bits of channels c0 .. c0 + 7: one byte at (pixel, c0 / 8) of
       // [M][K / 8] (g.keep_out; a null buffer drops the store)
       const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
