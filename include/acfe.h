@@ -233,7 +233,9 @@ int acfe_conv2d_dgrad(const void* dy, int N, int P, int Q, int K, const void* wf
  * acfe_bn_finalize outputs, part = [part_rows][2][C] for
  * acfe_bn_bwd_finalize_ex (nrows = part_rows).  _rows returns the slab rows,
  * or 0 when the fused form does not cover the shape (then: acfe_conv2d_dgrad +
- * acfe_bn_bwd_reduce). */
+ * acfe_bn_bwd_reduce).  Covered: C = 64 (any K % 64 == 0) and, since r06,
+ * C = K = 128 (wr_resnet's stage-2 dgrads; environment ACFE_DGRADBN128=0
+ * reports it uncovered, for A/B runs). */
 int acfe_conv2d_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int stride, int dtype);
 int acfe_conv2d_dgrad_bn(const void* dy, int N, int P, int Q, int K, const void* wflip, int C, int R, int S,
                          int stride, int pad_top, int pad_left, int H, int W, void* dx, int dtype,
