@@ -3209,7 +3209,7 @@ k_wgrad3x3_halo(ConvGeom g, const uint16_t* __restrict__ X, const uint16_t* __re
   constexpr int WC = CW == 64 ? 4 : CW / 16;
   constexpr int WK = 8 / WC < KB / 16 ? 8 / WC : KB / 16, WP = 8 / (WC * WK);
   static_assert(WC * WK * WP == 8 && (2 * NR) % WP == 0, "wave split");
-  static_assert(SEGW == 64 || (WP == 1 && !UNP), "16-pixel segments: one pixel group, plain dY");
+  static_assert(SEGW == 64 || !UNP, "16-pixel segments: plain dY");
   constexpr int LDD = KB + 16, LDX = CW + 16;
   constexpr int DS = ROWS * SEGW * LDD, XS = HR * HW * LDX;
   constexpr int FM = KB / (16 * WK), FN = 9;
@@ -4483,9 +4483,11 @@ static HaloPlan halo_plan(const ConvGeom& g, bool amax, long long splits) {
   // (the BN fold writes its dY rows: whole 4 nr row groups only, and the
   // plain K = 64 kernel splits exactly as the fold does, so that their dW
   // stay bit-identical; K = 128 / 256 mask the rows of a partial last group)
-  const bool edge = rem && wp == 1 && !amax &&
-                    ((cw == 64 && g.K == 64 && nr == 2 && g.P % 8 == 0) ||
-                     (!g.fb_sc && ((cw == 64 && g.K == 128 && nr == 1) || (cw == 32 && g.K == 256 && nr == 1))));
+  // (C = 16 -> K = 64, two pixel groups of waves: the same rule as K = 64)
+  const bool edge = rem && !amax &&
+                    ((((cw == 64 && wp == 1) || c16k64) && g.K == 64 && nr == 2 && g.P % 8 == 0) ||
+                     (!g.fb_sc && wp == 1 &&
+                      ((cw == 64 && g.K == 128 && nr == 1) || (cw == 32 && g.K == 256 && nr == 1))));
   const int qs = edge ? g.Q / 64 : (g.Q + 63) / 64;
   const int nchunk = g.C / cw, nseg = (int)((long long)g.N * (g.P / nr) * qs);
   // c16k64: 75 KB of LDS and 114 VGPRs -> two workgroups per CU
@@ -4529,8 +4531,10 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
     if (amax || (wp != 1 && !c16k64)) return ACFE_E_INVAL;
     // keep bits: the stage-1 K = 64 fold only (the forward that writes them: k_conv3x3_r64 PM 4)
     if (g.keep_in && !(cw == 64 && g.K == 64 && nr == 2 && !c16k64 && g.drop.on)) return ACFE_E_INVAL;
-    if (c16k64 && nr == 2) WB(64, 16, 2, false);
-    else if (cw == 64 && g.K == 64 && nr == 2 && g.keep_in) {
+    if (c16k64 && nr == 2) {
+      WB(64, 16, 2, false);
+      if (hp.edge) WBE(64, 16, 2, false);
+    } else if (cw == 64 && g.K == 64 && nr == 2 && g.keep_in) {
       WB(64, 64, 2, true);
       if (hp.edge) WBE(64, 64, 2, true);
     } else if (cw == 64 && g.K == 64 && nr == 2) {
@@ -4554,10 +4558,13 @@ static int wgrad_halo_launch(const ConvGeom& g, const void* x, const void* dy, c
   } else if (k16c64) {
     WHC(16, 64);
   } else if (c16k64) {
-    if (nr == 2)
+    if (nr == 2) {
       hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 16, 2>), gr, dim3(512), 0, s, g, (const uint16_t*)x,
-                         (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr);
-    else WHC(64, 16);
+                         (const uint16_t*)dy, ws, nchunk, nseg, per, nullptr, qs, 0, 0);
+      if (hp.edge)
+        hipLaunchKernelGGL((k_wgrad3x3_halo<64, false, 16, 2, false, false, 16>), gr, dim3(512), 0, s, g,
+                           (const uint16_t*)x, (const uint16_t*)dy, ws, nchunk, nsege, pere, nullptr, qse, wofs, 1);
+    } else WHC(64, 16);
   } else if (cw == 32) {  // the stage-2/3 branch2b (32 -> 128 / 256); wr_resnet's stage 3 (256 -> 256)
     if (g.K == 128) WHC(128, 32);
     else {
